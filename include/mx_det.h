@@ -1,0 +1,168 @@
+/* mx_det.h — C ABI of libmx_det.so, the MI355X (gfx950) hot path of the Faster R-CNN
+ * R50-FPN v2 train/eval step, corruption augmentation and U-Net restoration pre-pass of
+ * ysbbin/Robust-Object-Detection.
+ *
+ * The reference has no plugin API of its own: its hot path is reached through
+ * torchvision / OpenCV calls made from its scripts. Each entry point below names the reference call
+ * site and the third-party operator it replaces, so a maintainer can bind it (ctypes stub in
+ * INTEGRATION.md; the package robust-object-detection_amd/mx_det is that binding).
+ *
+ * Conventions
+ *  - Every pointer argument is a device pointer owned by the caller; the library never allocates
+ *    or frees on these paths. Scratch comes from a caller workspace sized by *_workspace().
+ *  - Work is enqueued on `stream` (a hipStream_t) and is stream-ordered; nothing synchronises.
+ *  - Return 0 on success, negative MX_E* on error; mx_last_error() gives the message (thread-local).
+ *  - Activations are NHWC; conv weights are KRSC (Cout, kh, kw, Cin); dtype codes below.
+ */
+#ifndef MX_DET_H
+#define MX_DET_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MX_OK 0
+#define MX_EINVAL -1
+#define MX_EUNSUPPORTED -2
+#define MX_EHIP -3
+
+#define MX_F32 0
+#define MX_BF16 1
+
+typedef void* mx_stream_t; /* hipStream_t */
+
+int mx_version(void);
+const char* mx_last_error(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Anchor assignment: torchvision box_iou + Matcher (+ label/target construction), fused.
+ * Replaces RegionProposalNetwork.assign_targets_to_anchors / RoIHeads.assign_targets_to_proposals
+ * (reached from train_frcnn_baseline.py:171, model(images, targets)).
+ *   gt[G,4], boxes[A,4] xyxy f32. matches[A] int64: gt index, -1 below low, -2 between.
+ *   mode 0: matches only.
+ *   mode 1 (RPN):  labels_f32[A] = 1 / 0 / -1 ; targets[A,4] = encode(gt[max(m,0)], boxes, w)
+ *   mode 2 (RoI):  labels_i64[A] = gt_labels[max(m,0)] / 0 (below) / -1 (between); targets as mode 1
+ *   G == 0 is allowed (all background, matches = -1, zero targets), as the empty-target path of
+ *   coco_detection_dataset.py:44-48 requires.
+ * ------------------------------------------------------------------------------------------- */
+size_t mx_match_workspace(int64_t G, int64_t A);
+int mx_match_assign(const float* gt, const int64_t* gt_labels, int64_t G, const float* boxes, int64_t A,
+                    float high, float low, int allow_low_quality, int mode, const float* enc_weights4_host,
+                    int64_t* matches, void* labels, float* targets, void* ws, size_t ws_bytes, mx_stream_t stream);
+
+/* torchvision.ops.box_iou -> out[n,m] (test/diagnostic entry). */
+int mx_box_iou(const float* b1, int64_t n, const float* b2, int64_t m, float* out, mx_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * NMS: torchvision.ops.nms / batched_nms (boxes.py), CPU semantics: stable score-descending order,
+ * suppress when IoU > thr. Replaces RegionProposalNetwork.filter_proposals' batched_nms(level) and
+ * RoIHeads.postprocess_detections' batched_nms(label) (eval_all.py:111).
+ *   idxs == NULL -> plain nms. mode: 0 = CPU dispatch rule (4*n > 4000 -> per-class, else
+ *   coordinate-offset trick), 1 = per-class, 2 = coordinate trick.
+ *   group (nullable, int32[n]): output is ordered by (group asc, score desc) instead of score desc,
+ *   so several images can share one call.
+ *   keep[n] int64 receives kept indices; *num_keep (device int64) the count.
+ *   max_seg: upper bound on the number of boxes that share one idx value (n is always safe).
+ * ------------------------------------------------------------------------------------------- */
+size_t mx_nms_workspace(int64_t n, int64_t max_seg);
+int mx_batched_nms(const float* boxes, const float* scores, const int64_t* idxs, const int32_t* group, int64_t n,
+                   int64_t max_seg, double iou_threshold, int mode, int64_t* keep, int64_t* num_keep, void* ws,
+                   size_t ws_bytes, mx_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * RoIAlign (torchvision::roi_align / _roi_align_backward, aligned flag honoured), NHWC features.
+ * Multi-scale form = MultiScaleRoIAlign(['0'..'3'], 7, 2) with its LevelMapper
+ * (floor(4 + log2(sqrt(area)/224) + 1e-6) clamped to [k_min, k_max]) — replaces
+ * RoIHeads.box_roi_pool reached from train_frcnn_baseline.py:171 / eval_all.py:111.
+ *   feats[l]: NHWC [N, H[l], W[l], C] of dtype; rois[K,5] f32 (batch, x1,y1,x2,y2).
+ *   out: [K, PH, PW, C] dtype.  Backward: grad_feats[l] NHWC f32, zero-initialised by the caller,
+ *   accumulated with float atomics (order-dependent in the last bits).
+ * ------------------------------------------------------------------------------------------- */
+int mx_roi_align_fwd(const void* feat, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, const float* rois,
+                     int64_t K, float spatial_scale, int PH, int PW, int sampling, int aligned, void* out,
+                     mx_stream_t stream);
+int mx_roi_align_bwd(const void* grad_out, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, const float* rois,
+                     int64_t K, float spatial_scale, int PH, int PW, int sampling, int aligned, float* grad_feat,
+                     mx_stream_t stream);
+int mx_multiscale_roi_align_fwd(const void* const* feats_host, const int64_t* H_host, const int64_t* W_host,
+                                const float* scales_host, int nlev, int k_min, int dtype, int64_t C,
+                                const float* rois, int64_t K, int PH, int PW, int sampling, void* out,
+                                int32_t* levels_out, mx_stream_t stream);
+int mx_multiscale_roi_align_bwd(const void* grad_out, int dtype, float* const* grad_feats_host,
+                                const int64_t* H_host, const int64_t* W_host, const float* scales_host, int nlev,
+                                int64_t C, const float* rois, const int32_t* levels, int64_t K, int PH, int PW,
+                                int sampling, mx_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Anchors and box coder (torchvision AnchorGenerator / BoxCoder, anchor_utils.py, _utils.py).
+ * ------------------------------------------------------------------------------------------- */
+/* One FPN level: cell anchors round([-ws,-hs,ws,hs]/2) for `size` and ratios, shifted by
+ * arange*stride; order (y, x, ratio). out[gh*gw*nr, 4]. */
+int mx_anchors_level(float size, const float* ratios_host, int nr, int64_t gh, int64_t gw, int64_t stride_h,
+                     int64_t stride_w, float* out, mx_stream_t stream);
+/* decode_single: rel[n, ncls*4] against boxes[n,4] -> out[n, ncls*4]; weights (wx,wy,ww,wh);
+ * dw/dh clamped at `clip`. clip_hw (nullable, int64 per-box image id into img_hw[2*i]) applies
+ * clip_boxes_to_image. */
+int mx_box_decode(const float* rel, const float* boxes, int64_t n, int64_t ncls, const float* weights4_host,
+                  float clip, float* out, mx_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Corruption augmentation (scripts/augmentations.py:14-56, RandomCorruption :60-74), uint8 HWC.
+ *   op: 0 identity, 1 noise (sigma, Philox seed; or `noise` field f32 if non-NULL), 2 motion blur
+ *   (k=9, angle 0), 3 low-res (INTER_AREA x factor, INTER_LINEAR back). Batched form takes one op
+ *   per image; images are [B, H, W, 3] contiguous. tmp: >= B*nh*nw*3 bytes for op 3.
+ * ------------------------------------------------------------------------------------------- */
+int mx_corrupt_u8(const uint8_t* img, int64_t B, int64_t H, int64_t W, int64_t C, const int32_t* ops_host,
+                  float sigma, uint64_t seed, const float* noise, double factor, uint8_t* tmp, uint8_t* out,
+                  mx_stream_t stream);
+/* GeneralizedRCNNTransform (normalize, zero-pad to /32) fused with ToDtype(scale=True):
+ * u8 HWC [B,H,W,3] -> NHWC [B, Hp, Wp, Cp] dtype, (x/255 - mean)/std, zero padding; Cp >= 3 (extra
+ * channels zero, for the conv stem's 8-channel gather). */
+int mx_normalize_pad(const uint8_t* img, int64_t B, int64_t H, int64_t W, const float* mean3_host,
+                     const float* std3_host, int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out,
+                     mx_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Convolution (implicit GEMM on MFMA, bf16 in / f32 accumulate), NHWC x KRSC.
+ * Replaces the cuDNN convs of ResNet-50 / FPN / RPN head / box head (torchvision model reached at
+ * train_frcnn_baseline.py:171) and the U-Net convs (restoration_net.py:17-30, restore_testsets.py:68).
+ *   fwd:   y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]) (+bias[K] f32, nullable), output dtype
+ *          ydtype; stats (nullable) receives per-block column partial sums for train-mode
+ *          BatchNorm: stats[2][mblocks][K] f32 (sum, sum of squares) of the f32 accumulators.
+ *   dgrad: dx[N,H,W,C] = conv_transpose(dy[N,Ho,Wo,K], w)   (bf16)
+ *   wgrad: dw[K,R,S,C] f32 = sum over N,Ho,Wo dy (x) x      (split-K with f32 atomics; dw zeroed
+ *          by the caller)
+ *   C % 8 == 0 is required (the stem input is padded to 8 channels).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+  int64_t N, H, W, C, K, R, S, Ho, Wo;
+  int32_t stride_h, stride_w, pad_h, pad_w;
+} mx_conv_shape;
+int64_t mx_conv_mblocks(const mx_conv_shape* s);
+int mx_conv2d_fwd(const mx_conv_shape* s, const uint16_t* x, const uint16_t* w, const float* bias, void* y,
+                  int ydtype, float* stats, mx_stream_t stream);
+int mx_conv2d_dgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
+                    mx_stream_t stream);
+int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw, mx_stream_t stream);
+
+/* Train-mode BatchNorm2d around the conv (torch.nn.BatchNorm2d semantics, momentum 0.1,
+ * unbiased running_var). finalize: reduce stats partials -> mean/invstd (f64 accumulation), fold
+ * into scale/shift, update running stats. apply: y = act(x*scale + shift (+ residual)), act 0 none,
+ * 1 relu, 2 leaky relu(0.2). bwd_reduce + bwd_apply: BN backward through the activation mask. */
+int mx_bn_finalize(const float* stats, int64_t mblocks, int64_t K, int64_t count, const float* gamma,
+                   const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                   float* mean_out, float* invstd_out, float* scale_out, float* shift_out, mx_stream_t stream);
+int mx_bn_apply(const void* x, int xdtype, int64_t M, int64_t K, const float* scale, const float* shift,
+                const uint16_t* residual, int act, uint16_t* y, mx_stream_t stream);
+int mx_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
+                     const float* mean, const float* invstd, float* sums /*[2][K] zeroed*/, mx_stream_t stream);
+int mx_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
+                    const float* mean, const float* invstd, const float* gamma, const float* sums,
+                    uint16_t* dx, uint16_t* dres /*nullable: grad of residual = masked dy*/,
+                    mx_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

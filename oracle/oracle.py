@@ -1,0 +1,173 @@
+"""numpy front-end for the CPU restatement in mx_oracle.c.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, as the checker. The product package (robust-object-detection_amd/mx_det) never imports it.
+Each wrapper names the reference call site the restated algorithm serves (see mx_oracle.h).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+F32 = ctypes.POINTER(ctypes.c_float)
+I64 = ctypes.POINTER(ctypes.c_int64)
+U8 = ctypes.POINTER(ctypes.c_uint8)
+i64 = ctypes.c_int64
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        _lib = ctypes.CDLL(_SO)
+        _lib.orc_nms.restype = ctypes.c_int64
+        _lib.orc_batched_nms.restype = ctypes.c_int64
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def box_iou(b1, b2):
+    b1, b2 = _f32(b1).reshape(-1, 4), _f32(b2).reshape(-1, 4)
+    out = np.empty((len(b1), len(b2)), np.float32)
+    lib().orc_box_iou(_p(b1, F32), i64(len(b1)), _p(b2, F32), i64(len(b2)), _p(out, F32))
+    return out
+
+
+def matcher(q, high, low, allow_low_quality):
+    """rpn.py / roi_heads.py Matcher (train_frcnn_baseline.py:171 reaches it)."""
+    q = _f32(q)
+    G, A = q.shape
+    out = np.empty(A, np.int64)
+    lib().orc_matcher(_p(q, F32), i64(G), i64(A), ctypes.c_float(high), ctypes.c_float(low),
+                      ctypes.c_int(int(allow_low_quality)), _p(out, I64))
+    return out
+
+
+def nms(boxes, scores, thr):
+    boxes, scores = _f32(boxes).reshape(-1, 4), _f32(scores)
+    keep = np.empty(len(scores), np.int64)
+    n = lib().orc_nms(_p(boxes, F32), _p(scores, F32), i64(len(scores)), ctypes.c_double(thr), _p(keep, I64))
+    return keep[:n]
+
+
+def batched_nms(boxes, scores, idxs, thr):
+    boxes, scores = _f32(boxes).reshape(-1, 4), _f32(scores)
+    idxs = np.ascontiguousarray(idxs, dtype=np.int64)
+    keep = np.empty(len(scores), np.int64)
+    n = lib().orc_batched_nms(_p(boxes, F32), _p(scores, F32), _p(idxs, I64), i64(len(scores)),
+                              ctypes.c_double(thr), _p(keep, I64))
+    return keep[:n]
+
+
+def roi_align(feat_nchw, rois, scale, out_hw=(7, 7), sampling=2, aligned=False):
+    f = _f32(feat_nchw)
+    r = _f32(rois).reshape(-1, 5)
+    N, C, H, W = f.shape
+    out = np.empty((len(r), C, out_hw[0], out_hw[1]), np.float32)
+    lib().orc_roi_align_fwd(_p(f, F32), i64(N), i64(C), i64(H), i64(W), _p(r, F32), i64(len(r)),
+                            ctypes.c_float(scale), out_hw[0], out_hw[1], sampling, int(aligned), _p(out, F32))
+    return out
+
+
+def roi_align_backward(grad_out, rois, scale, nchw, sampling=2, aligned=False):
+    g = _f32(grad_out)
+    r = _f32(rois).reshape(-1, 5)
+    N, C, H, W = nchw
+    gi = np.zeros((N, C, H, W), np.float32)
+    lib().orc_roi_align_bwd(_p(g, F32), i64(N), i64(C), i64(H), i64(W), _p(r, F32), i64(len(r)),
+                            ctypes.c_float(scale), g.shape[2], g.shape[3], sampling, int(aligned), _p(gi, F32))
+    return gi
+
+
+def anchors_level(size, ratios, gh, gw, stride_h, stride_w):
+    ratios = _f32(ratios)
+    out = np.empty((gh * gw * len(ratios), 4), np.float32)
+    lib().orc_anchors_level(ctypes.c_float(size), _p(ratios, F32), len(ratios), i64(gh), i64(gw),
+                            i64(stride_h), i64(stride_w), _p(out, F32))
+    return out
+
+
+def box_decode(rel, boxes, weights, clip=float(np.log(1000.0 / 16))):
+    boxes = _f32(boxes).reshape(-1, 4)
+    rel = _f32(rel).reshape(len(boxes), -1)
+    ncls = rel.shape[1] // 4
+    w = _f32(weights)
+    out = np.empty_like(rel)
+    lib().orc_box_decode(_p(rel, F32), _p(boxes, F32), i64(len(boxes)), i64(ncls), _p(w, F32),
+                         ctypes.c_float(clip), _p(out, F32))
+    return out
+
+
+def box_encode(gt, prop, weights):
+    gt, prop = _f32(gt).reshape(-1, 4), _f32(prop).reshape(-1, 4)
+    w = _f32(weights)
+    out = np.empty_like(gt)
+    lib().orc_box_encode(_p(gt, F32), _p(prop, F32), i64(len(gt)), _p(w, F32), _p(out, F32))
+    return out
+
+
+def noise_u8(img, noise):
+    img = np.ascontiguousarray(img, np.uint8)
+    noise = _f32(noise)
+    out = np.empty_like(img)
+    lib().orc_noise_u8(_p(img, U8), _p(noise, F32), i64(img.size), _p(out, U8))
+    return out
+
+
+def blur_u8(img):
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W, C = img.shape
+    out = np.empty_like(img)
+    lib().orc_blur_h9_u8(_p(img, U8), i64(H), i64(W), i64(C), _p(out, U8))
+    return out
+
+
+def lowres_u8(img, factor=0.5):
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W, C = img.shape
+    nw, nh = max(1, int(W * factor)), max(1, int(H * factor))
+    tmp = np.empty((nh, nw, C), np.uint8)
+    out = np.empty_like(img)
+    lib().orc_lowres_u8(_p(img, U8), i64(H), i64(W), i64(C), ctypes.c_double(factor), _p(tmp, U8), _p(out, U8))
+    return out
+
+
+def resize_area_u8(img, dh, dw):
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W, C = img.shape
+    out = np.empty((dh, dw, C), np.uint8)
+    lib().orc_resize_area_u8(_p(img, U8), i64(H), i64(W), i64(C), _p(out, U8), i64(dh), i64(dw))
+    return out
+
+
+def resize_linear_u8(img, dh, dw):
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W, C = img.shape
+    out = np.empty((dh, dw, C), np.uint8)
+    lib().orc_resize_linear_u8(_p(img, U8), i64(H), i64(W), i64(C), _p(out, U8), i64(dh), i64(dw))
+    return out
+
+
+def reflect_pad_u8(img, ph, pw):
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W, C = img.shape
+    out = np.empty((H + ph, W + pw, C), np.uint8)
+    lib().orc_reflect_pad_u8(_p(img, U8), i64(H), i64(W), i64(C), i64(ph), i64(pw), _p(out, U8))
+    return out

@@ -1,0 +1,273 @@
+// mx_elementwise.hip — anchors, box decode, corruption augmentation, normalize+pad (gfx950).
+// Built -ffp-contract=off: every f32 op rounds once, as the restated torch / OpenCV code does.
+#include "mx_common.h"
+
+namespace mx {
+
+// ---- AnchorGenerator (torchvision anchor_utils.py; oracle orc_anchors_level) -------------------
+__global__ void anchors_kernel(float4 b0, float4 b1, float4 b2, int nr, int64_t gh, int64_t gw, int64_t sh, int64_t sw,
+                               float4* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = gh * gw * nr;
+  if (i >= total) return;
+  int r = (int)(i % nr);
+  int64_t loc = i / nr;
+  int64_t y = loc / gw, x = loc % gw;
+  float4 b = r == 0 ? b0 : (r == 1 ? b1 : b2);
+  float sx = (float)(x * sw), sy = (float)(y * sh);
+  out[i] = make_float4(sx + b.x, sy + b.y, sx + b.z, sy + b.w);
+}
+
+// ---- BoxCoder.decode_single (torchvision _utils.py; oracle orc_box_decode) ------------------------
+__global__ void decode_kernel(const float4* __restrict__ rel, const float4* __restrict__ boxes, int64_t n, int64_t ncls,
+                              float4 w, float clip, float4* __restrict__ out) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * ncls) return;
+  int64_t i = t / ncls;
+  float4 b = boxes[i];
+  float widths = b.z - b.x, heights = b.w - b.y;
+  float cx = b.x + 0.5f * widths, cy = b.y + 0.5f * heights;
+  float4 r = rel[t];
+  float dx = r.x / w.x, dy = r.y / w.y, dw = r.z / w.z, dh = r.w / w.w;
+  dw = dw > clip ? clip : dw;
+  dh = dh > clip ? clip : dh;
+  float pcx = dx * widths + cx, pcy = dy * heights + cy;
+  float pw = expf(dw) * widths, ph = expf(dh) * heights;
+  float hw = 0.5f * pw, hh = 0.5f * ph;
+  out[t] = make_float4(pcx - hw, pcy - hh, pcx + hw, pcy + hh);
+}
+
+// ---- corruption (scripts/augmentations.py:30-45) --------------------------------------------
+// Philox4x32-10 counter RNG + Box-Muller: N(0, sigma) per element (the on-device replacement of
+// np.random.normal, which cannot be matched bit for bit; parity tests pass the field explicitly).
+__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ float gauss(uint64_t seed, uint64_t idx) {
+  uint4 r = philox(make_uint4((uint32_t)idx, (uint32_t)(idx >> 32), 0x5eedu, 0u), make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+  float u1 = ((float)(r.x >> 8) + 1.0f) * (1.0f / 16777217.0f);
+  float u2 = (float)(r.y >> 8) * (1.0f / 16777216.0f);
+  return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+}
+
+// apply_noise: clip(f32(img) + f32(noise), 0, 255).astype(uint8) (truncation)
+__global__ void noise_kernel(const uint8_t* __restrict__ img, const float* __restrict__ noise, float sigma, uint64_t seed,
+                             int64_t n, uint8_t* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float nz = noise ? noise[i] : sigma * gauss(seed, (uint64_t)i);
+  float v = (float)img[i] + nz;
+  v = v < 0.f ? 0.f : (v > 255.f ? 255.f : v);
+  out[i] = (uint8_t)v;
+}
+
+__device__ __forceinline__ int64_t refl101(int64_t i, int64_t n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) {
+    if (i < 0) i = -i;
+    if (i >= n) i = 2 * n - 2 - i;
+  }
+  return i;
+}
+
+// filter2D with the angle-0 9x9 motion kernel: only row 4 is non-zero (float(1/9) each), so the
+// filter is a 1x9 horizontal box over BORDER_REFLECT_101, summed in f32, rounded half-to-even.
+__global__ void blur_kernel(const uint8_t* __restrict__ img, int64_t H, int64_t W, int64_t C, uint8_t* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= H * W * C) return;
+  int64_t c = i % C, x = (i / C) % W, y = i / (C * W);
+  const float k = 1.0f / 9.0f;
+  float s = 0.f;
+#pragma unroll
+  for (int t = -4; t <= 4; ++t) s += k * (float)img[(y * W + refl101(x + t, W)) * C + c];
+  float r = rintf(s);
+  r = r < 0.f ? 0.f : (r > 255.f ? 255.f : r);
+  out[i] = (uint8_t)r;
+}
+
+// OpenCV computeResizeAreaTab for one destination index: up to 3 (src, alpha) entries
+__device__ int area_entries(int64_t ssize, int64_t d, double scale, int64_t* si, float* al) {
+  int k = 0;
+  double fs1 = d * scale, fs2 = fs1 + scale;
+  double cell = scale < (ssize - fs1) ? scale : (ssize - fs1);
+  int64_t s1 = (int64_t)ceil(fs1), s2 = (int64_t)floor(fs2);
+  if (s2 > ssize - 1) s2 = ssize - 1;
+  if (s1 > s2) s1 = s2;
+  if (s1 - fs1 > 1e-3) { si[k] = s1 - 1; al[k++] = (float)((s1 - fs1) / cell); }
+  for (int64_t s = s1; s < s2 && k < 7; ++s) { si[k] = s; al[k++] = (float)(1.0 / cell); }
+  if (fs2 - s2 > 1e-3 && k < 8) {
+    double dd = fs2 - s2;
+    if (dd > 1.) dd = 1.;
+    if (dd > cell) dd = cell;
+    si[k] = s2; al[k++] = (float)(dd / cell);
+  }
+  return k;
+}
+
+// INTER_AREA general path: out = sat(sum_y beta_y * (sum_x alpha_x * S)) in f32, same order as OpenCV
+__global__ void area_kernel(const uint8_t* __restrict__ src, int64_t sh, int64_t sw, int64_t C, uint8_t* __restrict__ dst,
+                            int64_t dh, int64_t dw) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= dh * dw * C) return;
+  int64_t c = i % C, dx = (i / C) % dw, dy = i / (C * dw);
+  int64_t xs[8], ys[8];
+  float xa[8], ya[8];
+  int nx = area_entries(sw, dx, (double)sw / dw, xs, xa);
+  int ny = area_entries(sh, dy, (double)sh / dh, ys, ya);
+  float sum = 0.f;
+  for (int j = 0; j < ny; ++j) {
+    const uint8_t* S = src + ys[j] * sw * C;
+    float buf = 0.f;
+    for (int k = 0; k < nx; ++k) buf = buf + (float)S[xs[k] * C + c] * xa[k];
+    sum = j == 0 ? ya[j] * buf : sum + ya[j] * buf;
+  }
+  float r = rintf(sum);
+  dst[i] = (uint8_t)(r < 0.f ? 0.f : (r > 255.f ? 255.f : r));
+}
+
+__device__ __forceinline__ void lin_coef(int64_t ssize, int64_t dsize, int64_t d, int64_t* s_out, int* a0, int* a1) {
+  double scale = 1.0 / ((double)dsize / ssize);
+  float f = (float)((d + 0.5) * scale - 0.5);
+  int64_t s = (int64_t)floorf(f);
+  f -= (float)s;
+  if (s < 0) { f = 0.f; s = 0; }
+  if (s >= ssize - 1) { f = 0.f; s = ssize - 1; }
+  *s_out = s;
+  *a0 = (int)rintf((1.f - f) * 2048.f);
+  *a1 = (int)rintf(f * 2048.f);
+}
+
+// INTER_LINEAR 8U, 11-bit fixed point; vertical combine as OpenCV's SIMD path (see oracle)
+__global__ void linear_kernel(const uint8_t* __restrict__ src, int64_t sh, int64_t sw, int64_t C, uint8_t* __restrict__ dst,
+                              int64_t dh, int64_t dw) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= dh * dw * C) return;
+  int64_t c = i % C, x = (i / C) % dw, y = i / (C * dw);
+  int64_t r0, c0;
+  int b0, b1, a0, a1;
+  lin_coef(sh, dh, y, &r0, &b0, &b1);
+  lin_coef(sw, dw, x, &c0, &a0, &a1);
+  int64_t r1 = r0 + 1 < sh ? r0 + 1 : sh - 1, c1 = c0 + 1 < sw ? c0 + 1 : sw - 1;
+  int S0 = src[(r0 * sw + c0) * C + c] * a0 + src[(r0 * sw + c1) * C + c] * a1;
+  int S1 = src[(r1 * sw + c0) * C + c] * a0 + src[(r1 * sw + c1) * C + c] * a1;
+  int v = ((((S0 >> 4) * b0) >> 16) + (((S1 >> 4) * b1) >> 16) + 2) >> 2;
+  dst[i] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+// ToDtype(float32, scale=True) -> x * float(1/255); GeneralizedRCNNTransform.normalize (x-mean)/std;
+// batch_images zero padding; NHWC with Cp channels (channels >= 3 zero).
+template <typename T>
+__global__ void normalize_pad_kernel(const uint8_t* __restrict__ img, int64_t B, int64_t H, int64_t W, float3 mean, float3 stdv,
+                                     int64_t Hp, int64_t Wp, int64_t Cp, T* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * Hp * Wp) return;
+  int64_t x = i % Wp, y = (i / Wp) % Hp, b = i / (Wp * Hp);
+  float v[3] = {0.f, 0.f, 0.f};
+  if (y < H && x < W) {
+    const uint8_t* p = img + ((b * H + y) * W + x) * 3;
+    const float inv = (float)(1.0 / 255.0);
+    v[0] = ((float)p[0] * inv - mean.x) / stdv.x;
+    v[1] = ((float)p[1] * inv - mean.y) / stdv.y;
+    v[2] = ((float)p[2] * inv - mean.z) / stdv.z;
+  }
+  T* o = out + i * Cp;
+  for (int64_t c = 0; c < Cp; ++c) io<T>::st(o + c, c < 3 ? v[c] : 0.f);
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+extern "C" int mx_anchors_level(float size, const float* ratios, int nr, int64_t gh, int64_t gw, int64_t sh, int64_t sw,
+                                float* out, mx_stream_t stream) {
+  MX_CHECK_ARG(nr >= 1 && nr <= 3, "mx_anchors_level: 1..3 ratios supported");
+  float4 b[3];
+  for (int r = 0; r < nr; ++r) {
+    // generate_anchors on the host, same f32 ops (it is a 3-element table)
+    float hr = sqrtf(ratios[r]);
+    float wr = 1.f / hr;
+    float ws = wr * size, hs = hr * size;
+    b[r] = make_float4(rintf(-ws / 2.f), rintf(-hs / 2.f), rintf(ws / 2.f), rintf(hs / 2.f));
+  }
+  for (int r = nr; r < 3; ++r) b[r] = b[0];
+  int64_t total = gh * gw * nr;
+  if (total == 0) return MX_OK;
+  anchors_kernel<<<(unsigned)cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(b[0], b[1], b[2], nr, gh, gw, sh, sw,
+                                                                               (float4*)out);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" int mx_box_decode(const float* rel, const float* boxes, int64_t n, int64_t ncls, const float* w, float clip,
+                             float* out, mx_stream_t stream) {
+  MX_CHECK_ARG(n >= 0 && ncls >= 1, "mx_box_decode: bad sizes");
+  if (n == 0) return MX_OK;
+  decode_kernel<<<(unsigned)cdiv(n * ncls, 256), 256, 0, (hipStream_t)stream>>>(
+      (const float4*)rel, (const float4*)boxes, n, ncls, make_float4(w[0], w[1], w[2], w[3]), clip, (float4*)out);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" int mx_corrupt_u8(const uint8_t* img, int64_t B, int64_t H, int64_t W, int64_t C, const int32_t* ops, float sigma,
+                             uint64_t seed, const float* noise, double factor, uint8_t* tmp, uint8_t* out,
+                             mx_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  MX_CHECK_ARG(B >= 0 && H > 0 && W > 0 && C > 0, "mx_corrupt_u8: bad shape");
+  int64_t nw = (int64_t)(W * factor), nh = (int64_t)(H * factor);
+  if (nw < 1) nw = 1;
+  if (nh < 1) nh = 1;
+  const int64_t per = H * W * C;
+  for (int64_t b = 0; b < B; ++b) {
+    const uint8_t* src = img + b * per;
+    uint8_t* dst = out + b * per;
+    switch (ops[b]) {
+      case 0:
+        if (src != dst) MX_HIP(hipMemcpyAsync(dst, src, per, hipMemcpyDeviceToDevice, s));
+        break;
+      case 1:
+        noise_kernel<<<(unsigned)cdiv(per, 256), 256, 0, s>>>(src, noise ? noise + b * per : nullptr, sigma,
+                                                             seed + 0x9E3779B97F4A7C15ull * (uint64_t)b, per, dst);
+        break;
+      case 2:
+        MX_CHECK_ARG(src != dst, "mx_corrupt_u8: blur cannot run in place");
+        blur_kernel<<<(unsigned)cdiv(per, 256), 256, 0, s>>>(src, H, W, C, dst);
+        break;
+      case 3: {
+        MX_CHECK_ARG(tmp != nullptr, "mx_corrupt_u8: low-res needs tmp");
+        uint8_t* t = tmp + b * nh * nw * C;
+        area_kernel<<<(unsigned)cdiv(nh * nw * C, 256), 256, 0, s>>>(src, H, W, C, t, nh, nw);
+        linear_kernel<<<(unsigned)cdiv(per, 256), 256, 0, s>>>(t, nh, nw, C, dst, H, W);
+        break;
+      }
+      default:
+        MX_CHECK_ARG(false, "mx_corrupt_u8: bad op %d", ops[b]);
+    }
+    MX_LAUNCH_CHECK();
+  }
+  return MX_OK;
+}
+
+extern "C" int mx_normalize_pad(const uint8_t* img, int64_t B, int64_t H, int64_t W, const float* mean, const float* stdv,
+                                int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out, mx_stream_t stream) {
+  MX_CHECK_ARG(Hp >= H && Wp >= W && Cp >= 3, "mx_normalize_pad: bad padded shape");
+  int64_t n = B * Hp * Wp;
+  if (n == 0) return MX_OK;
+  float3 m = make_float3(mean[0], mean[1], mean[2]), sd = make_float3(stdv[0], stdv[1], stdv[2]);
+  if (dtype == MX_F32)
+    normalize_pad_kernel<float><<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(img, B, H, W, m, sd, Hp, Wp, Cp,
+                                                                                          (float*)out);
+  else
+    normalize_pad_kernel<uint16_t><<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(img, B, H, W, m, sd, Hp, Wp,
+                                                                                             Cp, (uint16_t*)out);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}

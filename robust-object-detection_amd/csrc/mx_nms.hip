@@ -1,0 +1,288 @@
+// mx_nms.hip — torchvision nms / batched_nms with CPU semantics, segmented, on gfx950.
+//
+// Restates torchvision 0.20.1 (oracle/mx_oracle.c orc_nms / orc_batched_nms):
+//   nms: stable score-descending order; keep i unless suppressed; suppress j (later) when
+//        inter/((area_i + area_j) - inter) > thr (f32 IoU compared in double).
+//   batched_nms: CPU rule 4n > 4000 -> per-class ("vanilla"), else coordinate trick
+//        boxes + idx*(max(boxes) + 1); result ordered by score descending.
+// Serves RegionProposalNetwork.filter_proposals (batched over levels) and
+// RoIHeads.postprocess_detections (batched over labels), reached from train_frcnn_baseline.py:171
+// and eval_all.py:111.
+//
+// Design: one radix sort by (class, score desc, index) makes every class a contiguous segment;
+// a 64x64 bitmask tile kernel (one lane per row, 64 columns per tile) fills only tiles inside a
+// segment; one wave per segment then resolves the suppression scan 64 rows at a time: the
+// in-tile dependency chain runs on the diagonal word in registers (v_readlane per step), the
+// survivors' rows are OR-ed into the LDS "removed" bitmap lane-parallel over words. A second
+// stable radix sort orders survivors by (group, score desc, index).
+#include <hipcub/hipcub.hpp>
+
+#include "mx_common.h"
+
+namespace mx {
+
+__device__ __forceinline__ uint32_t ord_f32(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ uint32_t ord_i32(int64_t v) { return ((uint32_t)(int32_t)v) ^ 0x80000000u; }
+
+__global__ void nms_max_kernel(const float* __restrict__ b, int64_t n4, uint32_t* __restrict__ out) {
+  uint32_t m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)
+    m = max(m, ord_f32(b[i]));
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+__device__ __forceinline__ float unord_f32(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+// keys for the segment sort; offset boxes for the coordinate trick
+__global__ void nms_keys_kernel(const float4* __restrict__ boxes, const float* __restrict__ scores,
+                                const int64_t* __restrict__ idxs, int64_t n, int trick, const uint32_t* __restrict__ maxbits,
+                                uint64_t* __restrict__ keys, int32_t* __restrict__ vals, float4* __restrict__ obox) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float4 b = boxes[i];
+  uint32_t hi = 0;
+  if (trick) {
+    float step = unord_f32(*maxbits) + 1.0f;
+    float off = (float)idxs[i] * step;  // idxs.to(boxes) * (max_coordinate + 1)
+    b.x = b.x + off; b.y = b.y + off; b.z = b.z + off; b.w = b.w + off;
+  } else if (idxs) {
+    hi = ord_i32(idxs[i]);
+  }
+  obox[i] = b;
+  keys[i] = ((uint64_t)hi << 32) | (uint64_t)(~ord_f32(scores[i]));
+  vals[i] = (int32_t)i;
+}
+
+// gather sorted boxes, areas and segment heads
+__global__ void nms_gather_kernel(const uint64_t* __restrict__ skeys, const int32_t* __restrict__ svals,
+                                  const float4* __restrict__ obox, int64_t n, float4* __restrict__ sbox,
+                                  float* __restrict__ sarea, int32_t* __restrict__ head) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float4 b = obox[svals[i]];
+  sbox[i] = b;
+  sarea[i] = (b.z - b.x) * (b.w - b.y);
+  head[i] = (i == 0 || (skeys[i] >> 32) != (skeys[i - 1] >> 32)) ? 1 : 0;
+}
+
+// seg_id = inclusive_sum(head) - 1 ; seg_start[seg] = i for heads; nseg = seg_id[n-1]+1
+__global__ void nms_seg_kernel(const int32_t* __restrict__ head, const int32_t* __restrict__ incl, int64_t n,
+                               int32_t* __restrict__ seg_start, int32_t* __restrict__ nseg) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (head[i]) seg_start[incl[i] - 1] = (int32_t)i;
+  if (i == n - 1) {
+    *nseg = incl[i];
+    seg_start[incl[i]] = (int32_t)n;
+  }
+}
+
+// one 64-thread block per (64-row block, 64-column tile relative to the row's segment start)
+__global__ void __launch_bounds__(64) nms_mask_kernel(const float4* __restrict__ sbox, const float* __restrict__ sarea,
+                                                      const int32_t* __restrict__ incl, const int32_t* __restrict__ seg_start,
+                                                      int64_t n, int Wm, double thr, uint64_t* __restrict__ mask) {
+  int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  int cb = blockIdx.y;
+  if (i >= n) return;
+  int sid = incl[i] - 1;
+  int64_t s0 = seg_start[sid], s1 = seg_start[sid + 1];
+  int64_t c0 = s0 + (int64_t)cb * 64;
+  if (c0 >= s1) return;
+  float4 bi = sbox[i];
+  float ai = sarea[i];
+  uint64_t bits = 0;
+  int64_t cend = min<int64_t>(c0 + 64, s1);
+  for (int64_t j = max<int64_t>(c0, i + 1); j < cend; ++j) {
+    float4 bj = sbox[j];
+    float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
+    float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
+    float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
+    float inter = w * h;
+    float ovr = inter / ((ai + sarea[j]) - inter);
+    if ((double)ovr > thr) bits |= 1ull << (j - c0);
+  }
+  mask[i * Wm + cb] = bits;
+}
+
+// one wave per segment: greedy scan, 64 rows per step
+__global__ void __launch_bounds__(64) nms_scan_kernel(const uint64_t* __restrict__ mask, const int32_t* __restrict__ seg_start,
+                                                      const int32_t* __restrict__ nseg_p, const int32_t* __restrict__ svals,
+                                                      int Wm, int32_t* __restrict__ flags, int32_t* __restrict__ nkeep) {
+  extern __shared__ uint64_t removed[];
+  const int lane = threadIdx.x;
+  const int nseg = *nseg_p;
+  for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    const int64_t s0 = seg_start[seg], len = seg_start[seg + 1] - s0;
+    const int W = (int)((len + 63) / 64);
+    if (W > Wm) {  // caller's max_seg bound was violated: report, never read past the mask rows
+      if (lane == 0) atomicExch(nkeep, (int32_t)0x80000000);
+      continue;
+    }
+    for (int w = lane; w < W; w += 64) removed[w] = 0;
+    __syncthreads();
+    int kept_total = 0;
+    for (int blk = 0; blk < W; ++blk) {
+      const int64_t rbase = s0 + (int64_t)blk * 64;
+      const int cnt = (int)min<int64_t>(64, len - (int64_t)blk * 64);
+      const uint64_t diag = lane < cnt ? mask[(rbase + lane) * Wm + blk] : 0ull;
+      uint64_t cur = removed[blk];
+      uint64_t kept = 0;
+      const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
+      for (int t = 0; t < cnt; ++t) {
+        if (!((cur >> t) & 1ull)) {
+          kept |= 1ull << t;
+          uint64_t row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, t) << 32) |
+                         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, t);
+          cur |= row;
+        }
+      }
+      if (lane < cnt && ((kept >> lane) & 1ull)) flags[svals[rbase + lane]] = 1;
+      kept_total += __popcll(kept);
+      __syncthreads();
+      for (int w = blk + 1 + lane; w < W; w += 64) {
+        uint64_t acc = removed[w];
+        uint64_t k = kept;
+        while (k) {
+          int t = __ffsll((unsigned long long)k) - 1;
+          k &= k - 1;
+          acc |= mask[(rbase + t) * Wm + w];
+        }
+        removed[w] = acc;
+      }
+      __syncthreads();
+    }
+    if (lane == 0 && kept_total) atomicAdd(nkeep, kept_total);
+    __syncthreads();
+  }
+}
+
+// final order: kept first by (group, score desc, index); the rest after
+__global__ void nms_final_keys_kernel(const float* __restrict__ scores, const int32_t* __restrict__ group,
+                                      const int32_t* __restrict__ flags, int64_t n, uint64_t* __restrict__ keys,
+                                      int32_t* __restrict__ vals) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t k = ~0ull;
+  if (flags[i]) {
+    uint32_t hi = group ? ord_i32(group[i]) : 0u;
+    k = ((uint64_t)hi << 32) | (uint64_t)(~ord_f32(scores[i]));
+    if (k == ~0ull) k = ~0ull - 1;
+  }
+  keys[i] = k;
+  vals[i] = (int32_t)i;
+}
+
+__global__ void nms_out_kernel(const int32_t* __restrict__ vals, int64_t n, const int32_t* __restrict__ nk32,
+                               int64_t* __restrict__ keep, int64_t* __restrict__ num_keep) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) keep[i] = vals[i];
+  if (i == 0) *num_keep = *nk32;
+}
+
+struct NmsWs {
+  uint64_t *k0, *k1, *mask;
+  int32_t *v0, *v1, *head, *incl, *seg_start, *nseg, *flags, *nk;
+  uint32_t* maxbits;
+  float4 *obox, *sbox;
+  float* sarea;
+  void* cub;
+  size_t cub_bytes;
+};
+
+static size_t cub_bytes_needed(int64_t n) {
+  size_t a = 0, b = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (uint64_t*)nullptr, (uint64_t*)nullptr, (int32_t*)nullptr,
+                                           (int32_t*)nullptr, (int)n, 0, 64, (hipStream_t)0);
+  (void)hipcub::DeviceScan::InclusiveSum(nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, (int)n, (hipStream_t)0);
+  return a > b ? a : b;
+}
+
+static size_t carve(Carver& c, int64_t n, int Wm, NmsWs* w) {
+  int64_t m = n > 0 ? n : 1;
+  w->k0 = c.take<uint64_t>(m); w->k1 = c.take<uint64_t>(m);
+  w->v0 = c.take<int32_t>(m); w->v1 = c.take<int32_t>(m);
+  w->head = c.take<int32_t>(m); w->incl = c.take<int32_t>(m);
+  w->seg_start = c.take<int32_t>(m + 1); w->nseg = c.take<int32_t>(1);
+  w->flags = c.take<int32_t>(m); w->nk = c.take<int32_t>(1);
+  w->maxbits = c.take<uint32_t>(1);
+  w->obox = c.take<float4>(m); w->sbox = c.take<float4>(m); w->sarea = c.take<float>(m);
+  w->mask = c.take<uint64_t>((size_t)m * Wm);
+  w->cub_bytes = cub_bytes_needed(m);
+  w->cub = c.take<char>(w->cub_bytes);
+  return c.off;
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+extern "C" size_t mx_nms_workspace(int64_t n, int64_t max_seg) {
+  if (max_seg <= 0 || max_seg > n) max_seg = n;
+  if (n * 4 <= 4000) max_seg = n;  // coordinate-trick path treats all boxes as one segment
+  int Wm = (int)cdiv(max_seg > 0 ? max_seg : 1, 64);
+  Carver c(nullptr, 0);
+  NmsWs w;
+  return carve(c, n, Wm, &w);
+}
+
+extern "C" int mx_batched_nms(const float* boxes, const float* scores, const int64_t* idxs, const int32_t* group,
+                              int64_t n, int64_t max_seg, double thr, int mode, int64_t* keep, int64_t* num_keep,
+                              void* ws, size_t ws_bytes, mx_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  MX_CHECK_ARG(n >= 0 && n < (1ll << 31), "mx_batched_nms: bad n %lld", (long long)n);
+  MX_CHECK_ARG(mode >= 0 && mode <= 2, "mx_batched_nms: bad mode %d", mode);
+  if (n == 0) {
+    MX_HIP(hipMemsetAsync(num_keep, 0, sizeof(int64_t), s));
+    return MX_OK;
+  }
+  int trick = 0;
+  if (idxs) trick = (mode == 2) || (mode == 0 && n * 4 <= 4000);
+  if (!idxs || trick) max_seg = n;
+  if (max_seg <= 0 || max_seg > n) max_seg = n;
+  int Wm = (int)cdiv(max_seg, 64);
+  Carver c(ws, ws_bytes);
+  NmsWs w;
+  carve(c, n, Wm, &w);
+  MX_CHECK_ARG(c.ok(), "mx_batched_nms: workspace too small (%zu < %zu); size it with max_seg=%lld", ws_bytes, c.off,
+               (long long)max_seg);
+  MX_CHECK_ARG(Wm * 8 <= 64 * 1024, "mx_batched_nms: segment bound %lld too large", (long long)max_seg);
+  const int T = 256;
+  const int nb = (int)cdiv(n, T);
+  MX_HIP(hipMemsetAsync(w.flags, 0, sizeof(int32_t) * n, s));
+  MX_HIP(hipMemsetAsync(w.nk, 0, sizeof(int32_t), s));
+  if (trick) {
+    MX_HIP(hipMemsetAsync(w.maxbits, 0, sizeof(uint32_t), s));
+    nms_max_kernel<<<(int)std::min<int64_t>(cdiv(4 * n, T), 1024), T, 0, s>>>(boxes, 4 * n, w.maxbits);
+    MX_LAUNCH_CHECK();
+  }
+  nms_keys_kernel<<<nb, T, 0, s>>>((const float4*)boxes, scores, idxs, n, trick, w.maxbits, w.k0, w.v0, w.obox);
+  MX_LAUNCH_CHECK();
+  size_t cb = w.cub_bytes;
+  int end_bit = (idxs && !trick) ? 64 : 32;
+  MX_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.k0, w.k1, w.v0, w.v1, (int)n, 0, end_bit, s));
+  nms_gather_kernel<<<nb, T, 0, s>>>(w.k1, w.v1, w.obox, n, w.sbox, w.sarea, w.head);
+  MX_LAUNCH_CHECK();
+  cb = w.cub_bytes;
+  MX_HIP(hipcub::DeviceScan::InclusiveSum(w.cub, cb, w.head, w.incl, (int)n, s));
+  nms_seg_kernel<<<nb, T, 0, s>>>(w.head, w.incl, n, w.seg_start, w.nseg);
+  MX_LAUNCH_CHECK();
+  dim3 mg((unsigned)cdiv(n, 64), (unsigned)Wm);
+  nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask);
+  MX_LAUNCH_CHECK();
+  int sgrid = (int)std::min<int64_t>(n, 1024);
+  nms_scan_kernel<<<sgrid, 64, sizeof(uint64_t) * Wm, s>>>(w.mask, w.seg_start, w.nseg, w.v1, Wm, w.flags, w.nk);
+  MX_LAUNCH_CHECK();
+  nms_final_keys_kernel<<<nb, T, 0, s>>>(scores, group, w.flags, n, w.k0, w.v0);
+  MX_LAUNCH_CHECK();
+  cb = w.cub_bytes;
+  MX_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.k0, w.k1, w.v0, w.v1, (int)n, 0, 64, s));
+  nms_out_kernel<<<nb, T, 0, s>>>(w.v1, n, w.nk, keep, num_keep);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}

@@ -1,0 +1,99 @@
+"""ctypes binding of libmx_det.so (include/mx_det.h).
+
+The library is the product path: if it is missing or fails to load, every op raises. There is no
+CPU or eager-PyTorch fallback for the hot ops.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmx_det.so")
+
+c_i64 = ctypes.c_int64
+c_int = ctypes.c_int
+c_f = ctypes.c_float
+c_d = ctypes.c_double
+c_vp = ctypes.c_void_p
+c_sz = ctypes.c_size_t
+c_u64 = ctypes.c_uint64
+F4 = ctypes.c_float * 4
+
+
+class ConvShape(ctypes.Structure):
+    _fields_ = [("N", c_i64), ("H", c_i64), ("W", c_i64), ("C", c_i64), ("K", c_i64), ("R", c_i64), ("S", c_i64),
+                ("Ho", c_i64), ("Wo", c_i64), ("stride_h", ctypes.c_int32), ("stride_w", ctypes.c_int32),
+                ("pad_h", ctypes.c_int32), ("pad_w", ctypes.c_int32)]
+
+
+_SIGS = {
+    "mx_version": (c_int, []),
+    "mx_last_error": (ctypes.c_char_p, []),
+    "mx_match_workspace": (c_sz, [c_i64, c_i64]),
+    "mx_match_assign": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_f, c_f, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
+                                c_vp, c_sz, c_vp]),
+    "mx_box_iou": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "mx_nms_workspace": (c_sz, [c_i64, c_i64]),
+    "mx_batched_nms": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_d, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "mx_roi_align_fwd": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_f, c_int, c_int, c_int,
+                                 c_int, c_vp, c_vp]),
+    "mx_roi_align_bwd": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_f, c_int, c_int, c_int,
+                                 c_int, c_vp, c_vp]),
+    "mx_multiscale_roi_align_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_i64, c_vp, c_i64, c_int,
+                                            c_int, c_int, c_vp, c_vp, c_vp]),
+    "mx_multiscale_roi_align_bwd": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_i64,
+                                            c_int, c_int, c_int, c_vp]),
+    "mx_anchors_level": (c_int, [c_f, c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "mx_box_decode": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_f, c_vp, c_vp]),
+    "mx_corrupt_u8": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_f, c_u64, c_vp, c_d, c_vp, c_vp, c_vp]),
+    "mx_normalize_pad": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp]),
+    "mx_conv_mblocks": (c_i64, [ctypes.POINTER(ConvShape)]),
+    "mx_conv2d_fwd": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "mx_conv2d_dgrad": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp]),
+    "mx_conv2d_wgrad": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp]),
+    "mx_bn_finalize": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                               c_vp]),
+    "mx_bn_apply": (c_int, [c_vp, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "mx_bn_bwd_reduce": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "mx_bn_bwd_apply": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+}
+
+_lib = None
+
+
+class MxError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libmx_det.so (raises if absent: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        # torch first: its bundled libamdhip64 (soname libamdhip64.so.7) must be the one HIP runtime
+        # in the process; libmx_det's NEEDED entry then binds to it.
+        import torch  # noqa: F401
+        if not os.path.exists(LIB_PATH):
+            raise MxError(f"libmx_det.so not built at {LIB_PATH}; run `python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            if not hasattr(lib, name):
+                continue  # reported by call() and by tests/test_abi.py
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def declared_symbols():
+    return list(_SIGS)
+
+
+def call(name, *args):
+    lib = load()
+    if not hasattr(lib, name):
+        raise MxError(f"libmx_det.so does not export {name}")
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = load().mx_last_error().decode(errors="replace")
+        raise MxError(f"{name} failed ({rc}): {msg}")
+    return rc

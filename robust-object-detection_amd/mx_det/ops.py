@@ -1,0 +1,275 @@
+"""torch-facing wrappers of libmx_det (the HIP hot path).
+
+Mirrors the torchvision operator surface the reference reaches:
+  nms(boxes, scores, iou_threshold) / batched_nms(boxes, scores, idxs, iou_threshold)
+      torchvision/ops/boxes.py (RPN filter_proposals, RoIHeads.postprocess_detections)
+  roi_align(input, boxes, output_size, spatial_scale, sampling_ratio, aligned)
+      torchvision/ops/roi_align.py (here on NHWC features)
+  box_iou(boxes1, boxes2)                      torchvision/ops/boxes.py
+plus fused ops the build adds (match_assign, multiscale_roi_align, anchors_level, box_decode,
+corrupt_u8, normalize_pad). Errors follow torchvision's TORCH_CHECK style: RuntimeError on bad
+rank/shape/device; empty inputs give empty outputs.
+"""
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+from ._lib import call
+
+MX_F32, MX_BF16 = 0, 1
+BBOX_CLIP = math.log(1000.0 / 16)
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _check(cond, msg):
+    if not cond:
+        raise RuntimeError(msg)
+
+
+def _dev(*ts):
+    for t in ts:
+        _check(t.is_cuda, "mx_det ops take CUDA (HIP) tensors")
+
+
+def _dtype_code(t):
+    if t.dtype == torch.float32:
+        return MX_F32
+    if t.dtype == torch.bfloat16:
+        return MX_BF16
+    raise RuntimeError(f"unsupported dtype {t.dtype}")
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+# ---------------------------------------------------------------------------------------------
+def box_iou(boxes1, boxes2):
+    _dev(boxes1, boxes2)
+    b1 = boxes1.float().contiguous().view(-1, 4)
+    b2 = boxes2.float().contiguous().view(-1, 4)
+    out = torch.empty((b1.shape[0], b2.shape[0]), dtype=torch.float32, device=b1.device)
+    if out.numel():
+        call("mx_box_iou", _p(b1), b1.shape[0], _p(b2), b2.shape[0], _p(out), _stream())
+    return out
+
+
+def match_assign(gt_boxes, boxes, high, low, allow_low_quality, mode=0, gt_labels=None, weights=None):
+    """Fused box_iou + Matcher (+ labels / encoded regression targets).
+
+    mode 0 -> matches; mode 1 (RPN) -> (matches, labels f32 1/0/-1, targets);
+    mode 2 (RoI) -> (matches, labels i64, targets). See include/mx_det.h mx_match_assign.
+    """
+    _dev(gt_boxes, boxes)
+    gt = gt_boxes.float().contiguous().view(-1, 4)
+    bx = boxes.float().contiguous().view(-1, 4)
+    G, A = gt.shape[0], bx.shape[0]
+    dev = bx.device
+    matches = torch.empty(A, dtype=torch.int64, device=dev)
+    labels = None
+    if mode == 1:
+        labels = torch.empty(A, dtype=torch.float32, device=dev)
+    elif mode == 2:
+        labels = torch.empty(A, dtype=torch.int64, device=dev)
+        _check(gt_labels is not None, "mode 2 needs gt_labels")
+        gt_labels = gt_labels.to(torch.int64).contiguous()
+    targets = torch.empty((A, 4), dtype=torch.float32, device=dev) if weights is not None else None
+    w = (_lib.F4)(*weights) if weights is not None else None
+    ws = _ws(_lib.load().mx_match_workspace(G, A), dev)
+    call("mx_match_assign", _p(gt), _p(gt_labels) if mode == 2 else None, G, _p(bx), A, float(high), float(low),
+         int(bool(allow_low_quality)), int(mode), w, _p(matches), _p(labels), _p(targets), _p(ws), ws.numel(),
+         _stream())
+    if mode == 0:
+        return matches
+    return matches, labels, targets
+
+
+# ---------------------------------------------------------------------------------------------
+def batched_nms(boxes, scores, idxs, iou_threshold, group=None, max_seg=None, mode=0):
+    """torchvision.ops.batched_nms (CPU dispatch semantics). idxs=None -> plain nms.
+
+    group: optional int tensor; output ordered by (group, score desc).
+    Returns int64 indices of kept boxes.
+    """
+    _dev(boxes, scores)
+    _check(boxes.dim() == 2 and boxes.shape[-1] == 4, f"boxes should be [N,4], got {tuple(boxes.shape)}")
+    _check(scores.dim() == 1 and scores.shape[0] == boxes.shape[0], "scores should be [N]")
+    n = boxes.shape[0]
+    dev = boxes.device
+    if n == 0:
+        return torch.empty(0, dtype=torch.int64, device=dev)
+    b = boxes.float().contiguous()
+    s = scores.float().contiguous()
+    ix = idxs.to(torch.int64).contiguous() if idxs is not None else None
+    g = group.to(torch.int32).contiguous() if group is not None else None
+    ms = int(max_seg) if max_seg else n
+    keep = torch.empty(n, dtype=torch.int64, device=dev)
+    nk = torch.empty(1, dtype=torch.int64, device=dev)
+    ws = _ws(_lib.load().mx_nms_workspace(n, ms), dev)
+    call("mx_batched_nms", _p(b), _p(s), _p(ix), _p(g), n, ms, float(iou_threshold), int(mode), _p(keep), _p(nk),
+         _p(ws), ws.numel(), _stream())
+    k = int(nk.item())
+    _check(k >= 0, "batched_nms: a class segment exceeded max_seg")
+    return keep[:k]
+
+
+def nms(boxes, scores, iou_threshold):
+    """torchvision.ops.nms: kept indices sorted by decreasing score."""
+    return batched_nms(boxes, scores, None, iou_threshold)
+
+
+# ---------------------------------------------------------------------------------------------
+class _RoIAlign(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feat, rois, scale, ph, pw, sampling, aligned):
+        _dev(feat, rois)
+        _check(feat.dim() == 4, "roi_align input must be NHWC [N,H,W,C]")
+        _check(rois.dim() == 2 and rois.shape[1] == 5, f"rois must be [K,5], got {tuple(rois.shape)}")
+        f = feat.contiguous()
+        r = rois.float().contiguous()
+        N, H, W, C = f.shape
+        out = torch.empty((r.shape[0], ph, pw, C), dtype=f.dtype, device=f.device)
+        if r.shape[0]:
+            call("mx_roi_align_fwd", _p(f), _dtype_code(f), N, H, W, C, _p(r), r.shape[0], float(scale), ph, pw,
+                 sampling, int(aligned), _p(out), _stream())
+        ctx.save_for_backward(r)
+        ctx.cfg = (N, H, W, C, float(scale), ph, pw, sampling, int(aligned), f.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (r,) = ctx.saved_tensors
+        N, H, W, C, scale, ph, pw, sampling, aligned, dt = ctx.cfg
+        g = gout.contiguous()
+        gf = torch.zeros((N, H, W, C), dtype=torch.float32, device=g.device)
+        if r.shape[0]:
+            call("mx_roi_align_bwd", _p(g), _dtype_code(g), N, H, W, C, _p(r), r.shape[0], scale, ph, pw, sampling,
+                 aligned, _p(gf), _stream())
+        return gf.to(dt), None, None, None, None, None, None
+
+
+def roi_align(input, boxes, output_size, spatial_scale=1.0, sampling_ratio=2, aligned=False):
+    """torchvision.ops.roi_align on NHWC input; boxes = Tensor[K,5] (batch, x1, y1, x2, y2).
+    Returns [K, PH, PW, C]."""
+    if isinstance(output_size, int):
+        output_size = (output_size, output_size)
+    return _RoIAlign.apply(input, boxes, spatial_scale, output_size[0], output_size[1], sampling_ratio, aligned)
+
+
+class _MultiScaleRoIAlign(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, rois, scales, k_min, ph, pw, sampling, *feats):
+        _dev(rois, *feats)
+        r = rois.float().contiguous()
+        fs = [f.contiguous() for f in feats]
+        C = fs[0].shape[3]
+        dt = fs[0].dtype
+        for f in fs:
+            _check(f.dim() == 4 and f.shape[3] == C and f.dtype == dt, "features must share C and dtype")
+        n = len(fs)
+        K = r.shape[0]
+        out = torch.empty((K, ph, pw, C), dtype=dt, device=r.device)
+        levels = torch.empty(K, dtype=torch.int32, device=r.device)
+        ptrs = (ctypes.c_void_p * n)(*[f.data_ptr() for f in fs])
+        Hs = (ctypes.c_int64 * n)(*[f.shape[1] for f in fs])
+        Ws = (ctypes.c_int64 * n)(*[f.shape[2] for f in fs])
+        sc = (ctypes.c_float * n)(*scales)
+        if K:
+            call("mx_multiscale_roi_align_fwd", ptrs, Hs, Ws, sc, n, int(k_min), _dtype_code(fs[0]), C, _p(r), K, ph,
+                 pw, sampling, _p(out), _p(levels), _stream())
+        ctx.save_for_backward(r, levels)
+        ctx.cfg = ([tuple(f.shape) for f in fs], list(scales), ph, pw, sampling, dt)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        r, levels = ctx.saved_tensors
+        shapes, scales, ph, pw, sampling, dt = ctx.cfg
+        g = gout.contiguous()
+        gfs = [torch.zeros(s, dtype=torch.float32, device=g.device) for s in shapes]
+        n = len(gfs)
+        if r.shape[0]:
+            ptrs = (ctypes.c_void_p * n)(*[f.data_ptr() for f in gfs])
+            Hs = (ctypes.c_int64 * n)(*[s[1] for s in shapes])
+            Ws = (ctypes.c_int64 * n)(*[s[2] for s in shapes])
+            sc = (ctypes.c_float * n)(*scales)
+            call("mx_multiscale_roi_align_bwd", _p(g), _dtype_code(g), ptrs, Hs, Ws, sc, n, shapes[0][3], _p(r),
+                 _p(levels), r.shape[0], ph, pw, sampling, _stream())
+        return (None, None, None, None, None, None) + tuple(x.to(dt) for x in gfs)
+
+
+def multiscale_roi_align(feats, rois, scales, k_min, output_size=(7, 7), sampling_ratio=2):
+    """MultiScaleRoIAlign over NHWC feature maps with the fused LevelMapper. rois [K,5]."""
+    return _MultiScaleRoIAlign.apply(rois, list(scales), int(k_min), output_size[0], output_size[1],
+                                     sampling_ratio, *feats)
+
+
+# ---------------------------------------------------------------------------------------------
+def anchors_level(size, ratios, grid_h, grid_w, stride_h, stride_w, device):
+    nr = len(ratios)
+    out = torch.empty((grid_h * grid_w * nr, 4), dtype=torch.float32, device=device)
+    if out.numel():
+        rr = (ctypes.c_float * nr)(*ratios)
+        call("mx_anchors_level", float(size), rr, nr, grid_h, grid_w, int(stride_h), int(stride_w), _p(out),
+             _stream())
+    return out
+
+
+def box_decode(rel_codes, boxes, weights, clip=BBOX_CLIP):
+    """BoxCoder.decode_single: rel [n, ncls*4] against boxes [n,4] -> [n, ncls*4]."""
+    _dev(rel_codes, boxes)
+    b = boxes.float().contiguous().view(-1, 4)
+    n = b.shape[0]
+    r = rel_codes.float().contiguous().view(n, -1)
+    out = torch.empty_like(r)
+    if n:
+        call("mx_box_decode", _p(r), _p(b), n, r.shape[1] // 4, (_lib.F4)(*weights), float(clip), _p(out),
+             _stream())
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+CORRUPT_NONE, CORRUPT_NOISE, CORRUPT_BLUR, CORRUPT_LOWRES = 0, 1, 2, 3
+
+
+def corrupt_u8(images, ops, sigma=15.0, seed=0, noise=None, factor=0.5):
+    """augmentations.py corruption ops on uint8 [B,H,W,C] (one op code per image)."""
+    _dev(images)
+    _check(images.dtype == torch.uint8 and images.dim() == 4, "images must be uint8 [B,H,W,C]")
+    x = images.contiguous()
+    B, H, W, C = x.shape
+    out = torch.empty_like(x)
+    nw, nh = max(1, int(W * factor)), max(1, int(H * factor))
+    tmp = torch.empty((B, nh, nw, C), dtype=torch.uint8, device=x.device) if 3 in list(ops) else None
+    if noise is not None:
+        noise = noise.float().contiguous()
+        _check(noise.numel() == x.numel(), "noise field must match images")
+    arr = (ctypes.c_int32 * B)(*[int(o) for o in ops])
+    call("mx_corrupt_u8", _p(x), B, H, W, C, arr, float(sigma), ctypes.c_uint64(int(seed) & (2 ** 64 - 1)),
+         _p(noise), float(factor), _p(tmp), _p(out), _stream())
+    return out
+
+
+IMAGE_MEAN = (0.485, 0.456, 0.406)
+IMAGE_STD = (0.229, 0.224, 0.225)
+
+
+def normalize_pad(images, padded_hw, channels=3, dtype=torch.float32, mean=IMAGE_MEAN, std=IMAGE_STD):
+    """uint8 [B,H,W,3] -> NHWC [B,Hp,Wp,channels] normalized, zero-padded (GeneralizedRCNNTransform)."""
+    _dev(images)
+    x = images.contiguous()
+    B, H, W, _ = x.shape
+    Hp, Wp = padded_hw
+    out = torch.empty((B, Hp, Wp, channels), dtype=dtype, device=x.device)
+    call("mx_normalize_pad", _p(x), B, H, W, (ctypes.c_float * 3)(*mean), (ctypes.c_float * 3)(*std), Hp, Wp,
+         channels, _dtype_code(out), _p(out), _stream())
+    return out

@@ -1,0 +1,302 @@
+"""GPU parity of the libmx_det HIP ops against the CPU oracle (oracle/mx_oracle.c).
+
+Bar: bit-exact for index work (matches, NMS keep lists, anchors) and for f32 RoIAlign forward
+(same op order per element); IoU values bit-exact; exp/log-based coder outputs within 1e-5
+relative (device expf/logf vs libm may differ in the last ulp; north_star tolerance is 1e-3).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand_boxes(rng, n, H=800, W=1333, med=24.0):
+    cx = rng.uniform(0, W, n)
+    cy = rng.uniform(0, H, n)
+    w = np.clip(rng.lognormal(np.log(med), 0.8, n), 2, W)
+    h = np.clip(rng.lognormal(np.log(med), 0.8, n), 2, H)
+    b = np.stack([cx - w / 2, cy - h / 2, cx + w / 2, cy + h / 2], 1)
+    b[:, 0::2] = np.clip(b[:, 0::2], 0, W)
+    b[:, 1::2] = np.clip(b[:, 1::2], 0, H)
+    return b.astype(np.float32)
+
+
+def _anchors_np(H=800, W=1344):
+    lv = []
+    for i, s in enumerate((32, 64, 128, 256, 512)):
+        st = 4 * 2 ** i
+        gh, gw = -(-H // st), -(-W // st)
+        if i == 4:  # P6 = max_pool(P5, 1, 2)
+            gh, gw = (-(-H // 32) + 1) // 2, (-(-W // 32) + 1) // 2
+        sh, sw = H // gh, W // gw
+        lv.append(orc.anchors_level(s, [0.5, 1.0, 2.0], gh, gw, sh, sw))
+    return np.concatenate(lv)
+
+
+def test_anchors_bitexact(dev):
+    from mx_det import ops
+    ref = _anchors_np()
+    assert ref.shape[0] == 268569
+    got = []
+    for i, s in enumerate((32, 64, 128, 256, 512)):
+        st = 4 * 2 ** i
+        gh, gw = -(-800 // st), -(-1344 // st)
+        if i == 4:
+            gh, gw = 13, 21
+        got.append(ops.anchors_level(s, [0.5, 1.0, 2.0], gh, gw, 800 // gh, 1344 // gw, dev))
+    got = torch.cat(got).cpu().numpy()
+    assert np.array_equal(got, ref)
+
+
+def test_box_iou_bitexact(dev):
+    from mx_det import ops
+    rng = np.random.default_rng(0)
+    a, b = _rand_boxes(rng, 77), _rand_boxes(rng, 1500)
+    b[:10] = a[:10]  # exact duplicates -> IoU 1
+    got = ops.box_iou(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), orc.box_iou(a, b).view(np.uint32))
+
+
+@pytest.mark.parametrize("G", [0, 1, 55, 300])
+def test_rpn_matcher_bitexact(dev, G):
+    """RPN: Matcher(0.7, 0.3, allow_low_quality=True) over the real 800x1344 anchor set."""
+    from mx_det import ops
+    rng = np.random.default_rng(G + 1)
+    anchors = _anchors_np()
+    gt = _rand_boxes(rng, G)
+    if G > 3:
+        gt[1] = gt[0]  # duplicate gt -> argmax tie must pick the first index
+    m, lab, tgt = ops.match_assign(torch.from_numpy(gt).to(dev), torch.from_numpy(anchors).to(dev), 0.7, 0.3, True,
+                                   mode=1, weights=(1.0, 1.0, 1.0, 1.0))
+    m = m.cpu().numpy()
+    if G == 0:
+        assert (m == -1).all() and (lab.cpu().numpy() == 0).all()
+        return
+    ref = orc.matcher(orc.box_iou(gt, anchors), 0.7, 0.3, True)
+    assert np.array_equal(m, ref)
+    reflab = np.where(ref >= 0, 1.0, np.where(ref == -1, 0.0, -1.0)).astype(np.float32)
+    assert np.array_equal(lab.cpu().numpy(), reflab)
+    pos = ref >= 0
+    reft = orc.box_encode(gt[np.clip(ref, 0, None)][pos], anchors[pos], [1, 1, 1, 1])
+    np.testing.assert_allclose(tgt.cpu().numpy()[pos], reft, rtol=1e-5, atol=1e-5)
+
+
+def test_roi_matcher_labels(dev):
+    """RoIHeads: proposals + gt appended, Matcher(0.5, 0.5, False), labels from gt labels."""
+    from mx_det import ops
+    rng = np.random.default_rng(5)
+    gt = _rand_boxes(rng, 40)
+    props = np.concatenate([_rand_boxes(rng, 2000, med=40), gt])
+    glab = rng.integers(1, 7, 40).astype(np.int64)
+    m, lab, tgt = ops.match_assign(torch.from_numpy(gt).to(dev), torch.from_numpy(props).to(dev), 0.5, 0.5, False,
+                                   mode=2, gt_labels=torch.from_numpy(glab).to(dev), weights=(10., 10., 5., 5.))
+    ref = orc.matcher(orc.box_iou(gt, props), 0.5, 0.5, False)
+    assert np.array_equal(m.cpu().numpy(), ref)
+    reflab = np.where(ref >= 0, glab[np.clip(ref, 0, None)], 0)
+    assert np.array_equal(lab.cpu().numpy(), reflab)
+    reft = orc.box_encode(gt[np.clip(ref, 0, None)], props, [10, 10, 5, 5])
+    np.testing.assert_allclose(tgt.cpu().numpy(), reft, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("n,thr", [(1, 0.7), (50, 0.7), (999, 0.5), (2000, 0.7), (6000, 0.5)])
+def test_nms_bitexact(dev, n, thr):
+    from mx_det import ops
+    rng = np.random.default_rng(n)
+    b = _rand_boxes(rng, n, med=60)
+    b[n // 2:] = b[: n - n // 2] + rng.normal(0, 3, (n - n // 2, 4)).astype(np.float32)  # dense clusters
+    s = rng.random(n).astype(np.float32)
+    s[::7] = s[0]  # score ties -> stable order by index
+    got = ops.nms(torch.from_numpy(b).to(dev), torch.from_numpy(s).to(dev), thr).cpu().numpy()
+    assert np.array_equal(got, orc.nms(b, s, thr))
+
+
+@pytest.mark.parametrize("n,ncls", [(700, 6), (1000, 5), (1001, 5), (8819, 5), (5000, 6)])
+def test_batched_nms_paths(dev, n, ncls):
+    """CPU dispatch: 4n > 4000 -> per-class loop; else coordinate trick (both bit-exact)."""
+    from mx_det import ops
+    rng = np.random.default_rng(n + ncls)
+    b = _rand_boxes(rng, n, med=50)
+    s = rng.random(n).astype(np.float32)
+    idx = rng.integers(0, ncls, n).astype(np.int64)
+    got = ops.batched_nms(torch.from_numpy(b).to(dev), torch.from_numpy(s).to(dev), torch.from_numpy(idx).to(dev),
+                          0.7).cpu().numpy()
+    assert np.array_equal(got, orc.batched_nms(b, s, idx, 0.7))
+
+
+def test_batched_nms_grouped(dev):
+    """Two images in one call: output ordered by (image, score desc) == per-image calls."""
+    from mx_det import ops
+    rng = np.random.default_rng(9)
+    n = 3000
+    b = _rand_boxes(rng, n, med=50)
+    s = rng.random(n).astype(np.float32)
+    lvl = rng.integers(0, 5, n)
+    img = (np.arange(n) >= 1700).astype(np.int64)
+    idx = img * 5 + lvl
+    got = ops.batched_nms(torch.from_numpy(b).to(dev), torch.from_numpy(s).to(dev), torch.from_numpy(idx).to(dev),
+                          0.7, group=torch.from_numpy(img).to(dev), mode=1).cpu().numpy()
+    ref = []
+    for i in (0, 1):
+        sel = np.where(img == i)[0]
+        k = orc.batched_nms(b[sel], s[sel], lvl[sel], 0.7)
+        ref.append(sel[k])
+    assert np.array_equal(got, np.concatenate(ref))
+
+
+def test_nms_empty(dev):
+    from mx_det import ops
+    k = ops.nms(torch.zeros((0, 4), device=dev), torch.zeros(0, device=dev), 0.5)
+    assert k.shape == (0,) and k.dtype == torch.int64
+
+
+def _rois(rng, K, N, H, W, scale):
+    b = _rand_boxes(rng, K, H=H / scale, W=W / scale, med=60)
+    b[0] = [-20, -30, 5, 5]  # partially outside the map
+    b[1] = [3, 3, 3.2, 3.1]  # smaller than one pixel -> size clamped to 1
+    bi = rng.integers(0, N, K).astype(np.float32)[:, None]
+    return np.concatenate([bi, b], 1).astype(np.float32)
+
+
+def test_roi_align_fwd_f32_bitexact(dev):
+    from mx_det import ops
+    rng = np.random.default_rng(3)
+    N, C, H, W, scale = 2, 96, 50, 84, 1 / 16
+    feat = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    rois = _rois(rng, 300, N, H, W, scale)
+    ref = orc.roi_align(feat, rois, scale, (7, 7), 2, False)
+    f = torch.from_numpy(feat).to(dev).permute(0, 2, 3, 1).contiguous()
+    got = ops.roi_align(f, torch.from_numpy(rois).to(dev), (7, 7), scale, 2, False)
+    got = got.permute(0, 3, 1, 2).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_roi_align_aligned_and_bf16(dev):
+    from mx_det import ops
+    rng = np.random.default_rng(4)
+    N, C, H, W, scale = 1, 256, 40, 40, 0.25
+    feat = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    rois = _rois(rng, 64, N, H, W, scale)
+    ref = orc.roi_align(feat, rois, scale, (7, 7), 2, True)
+    f = torch.from_numpy(feat).to(dev).permute(0, 2, 3, 1).contiguous()
+    got = ops.roi_align(f, torch.from_numpy(rois).to(dev), 7, scale, 2, True).permute(0, 3, 1, 2).cpu().numpy()
+    assert np.array_equal(got, ref)
+    fb = f.bfloat16()
+    ref_b = orc.roi_align(fb.float().permute(0, 3, 1, 2).cpu().numpy(), rois, scale, (7, 7), 2, False)
+    got_b = ops.roi_align(fb, torch.from_numpy(rois).to(dev), 7, scale, 2, False).float().permute(0, 3, 1, 2)
+    np.testing.assert_allclose(got_b.cpu().numpy(), ref_b, rtol=8e-3, atol=8e-3)
+
+
+def test_roi_align_backward(dev):
+    from mx_det import ops
+    rng = np.random.default_rng(6)
+    N, C, H, W, scale = 2, 64, 30, 41, 0.125
+    feat = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    rois = _rois(rng, 120, N, H, W, scale)
+    gout = rng.standard_normal((120, C, 7, 7)).astype(np.float32)
+    ref = orc.roi_align_backward(gout, rois, scale, (N, C, H, W), 2, False)
+    f = torch.from_numpy(feat).to(dev).permute(0, 2, 3, 1).contiguous().requires_grad_(True)
+    out = ops.roi_align(f, torch.from_numpy(rois).to(dev), 7, scale, 2, False)
+    out.backward(torch.from_numpy(gout).to(dev).permute(0, 2, 3, 1))
+    got = f.grad.permute(0, 3, 1, 2).cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
+
+
+def _level_mapper_np(boxes, k_min=2, k_max=5):
+    # torchvision poolers.LevelMapper in f32 (CPU path)
+    b = torch.from_numpy(boxes)
+    s = torch.sqrt((b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1]))
+    t = torch.floor(4 + torch.log2(s / 224) + torch.tensor(1e-6, dtype=s.dtype))
+    t = torch.clamp(t, min=k_min, max=k_max)
+    return (t.to(torch.int64) - k_min).numpy()
+
+
+def test_multiscale_roi_align(dev):
+    from mx_det import ops
+    rng = np.random.default_rng(8)
+    N, C = 2, 32
+    shapes = [(200, 336), (100, 168), (50, 84), (25, 42)]
+    scales = [0.25, 0.125, 0.0625, 0.03125]
+    feats = [rng.standard_normal((N, C, h, w)).astype(np.float32) for h, w in shapes]
+    boxes = np.concatenate([_rand_boxes(rng, 200, med=30), _rand_boxes(rng, 200, med=200)])
+    bi = rng.integers(0, N, len(boxes)).astype(np.float32)[:, None]
+    rois = np.concatenate([bi, boxes], 1)
+    lv = _level_mapper_np(boxes)
+    ref = np.zeros((len(rois), C, 7, 7), np.float32)
+    for l in range(4):
+        sel = np.where(lv == l)[0]
+        if len(sel):
+            ref[sel] = orc.roi_align(feats[l], rois[sel], scales[l], (7, 7), 2, False)
+    ft = [torch.from_numpy(f).to(dev).permute(0, 2, 3, 1).contiguous().requires_grad_(True) for f in feats]
+    got = ops.multiscale_roi_align(ft, torch.from_numpy(rois).to(dev), scales, 2)
+    assert np.array_equal(got.permute(0, 3, 1, 2).detach().cpu().numpy(), ref)
+    g = rng.standard_normal(got.shape).astype(np.float32)
+    got.backward(torch.from_numpy(g).to(dev))
+    gn = torch.from_numpy(g).permute(0, 3, 1, 2).numpy()
+    for l in range(4):
+        sel = np.where(lv == l)[0]
+        r = orc.roi_align_backward(gn[sel], rois[sel], scales[l], feats[l].shape, 2, False)
+        np.testing.assert_allclose(ft[l].grad.permute(0, 3, 1, 2).cpu().numpy(), r, rtol=1e-5, atol=1e-5)
+
+
+def test_box_decode(dev):
+    from mx_det import ops
+    rng = np.random.default_rng(11)
+    boxes = _rand_boxes(rng, 4000, med=80)
+    rel = rng.normal(0, 1.5, (4000, 28)).astype(np.float32)
+    rel[0, 2] = 50.0  # exercises the dw clamp
+    ref = orc.box_decode(rel, boxes, [10, 10, 5, 5])
+    got = ops.box_decode(torch.from_numpy(rel).to(dev), torch.from_numpy(boxes).to(dev), (10., 10., 5., 5.))
+    np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=1e-5, atol=1e-3)
+
+
+def _img(rng, H=800, W=1333):
+    base = rng.integers(0, 256, (H // 8 + 1, W // 8 + 1, 3)).astype(np.float32)
+    low = np.kron(base, np.ones((8, 8, 1)))[:H, :W]
+    return np.clip(low + rng.normal(0, 25, (H, W, 3)), 0, 255).astype(np.uint8)
+
+
+def test_corruption_ops(dev):
+    from mx_det import ops
+    rng = np.random.default_rng(12)
+    img = np.stack([_img(rng, 96, 133), _img(rng, 96, 133), _img(rng, 96, 133)])
+    noise = rng.normal(0, 15, img.shape).astype(np.float32)
+    t = torch.from_numpy(img).to(dev)
+    got = ops.corrupt_u8(t, [1, 2, 3], noise=torch.from_numpy(noise).to(dev)).cpu().numpy()
+    assert np.array_equal(got[0], orc.noise_u8(img[0], noise[0]))
+    assert np.array_equal(got[1], orc.blur_u8(img[1]))
+    assert np.array_equal(got[2], orc.lowres_u8(img[2], 0.5))
+
+
+def test_noise_golden_from_reference(dev):
+    """apply_noise pinned by the reference itself (tests/golden/noise.npz, make_golden.py)."""
+    from mx_det import ops
+    d = np.load("tests/golden/noise.npz")
+    got = ops.corrupt_u8(torch.from_numpy(d["img"][None]).to(dev), [1],
+                         noise=torch.from_numpy(d["noise"][None]).to(dev)).cpu().numpy()[0]
+    assert np.array_equal(got, d["out"])
+
+
+def test_corruption_full_size_properties(dev):
+    """Full 1333x800: device Philox noise statistics; blur/lowres idempotent on flat images."""
+    from mx_det import ops
+    flat = torch.full((1, 800, 1333, 3), 117, dtype=torch.uint8, device=dev)
+    for op in (2, 3):
+        assert torch.equal(ops.corrupt_u8(flat, [op]), flat)
+    z = torch.full((1, 800, 1333, 3), 128, dtype=torch.uint8, device=dev)
+    n = ops.corrupt_u8(z, [1], sigma=15.0, seed=123).float() - 128
+    # astype(uint8) truncates: floor(128 + N(0,15)) has mean -0.5, std sqrt(225 + 1/12)
+    assert abs(n.mean().item() + 0.5) < 0.05 and abs(n.std().item() - 15.0) < 0.1
+
+
+def test_normalize_pad(dev):
+    from mx_det import ops
+    rng = np.random.default_rng(13)
+    img = np.stack([_img(rng, 50, 61), _img(rng, 50, 61)])
+    got = ops.normalize_pad(torch.from_numpy(img).to(dev), (64, 64), channels=8).cpu()
+    x = torch.from_numpy(img).float().mul_(1.0 / 255)
+    ref = (x - torch.tensor(ops.IMAGE_MEAN)) / torch.tensor(ops.IMAGE_STD)
+    assert torch.equal(got[:, :50, :61, :3], ref)
+    assert got[:, 50:].abs().sum() == 0 and got[:, :, 61:].abs().sum() == 0 and got[..., 3:].abs().sum() == 0
