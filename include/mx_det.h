@@ -144,6 +144,15 @@ int mx_conv2d_fwd(const mx_conv_shape* s, const uint16_t* x, const uint16_t* w, 
                   int ydtype, float* stats, mx_stream_t stream);
 int mx_conv2d_dgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
                     mx_stream_t stream);
+/* Hot-path forms. fwd_ex adds a fused epilogue: + residual[M][K] (bf16, nullable), then activation
+ * (0 none, 1 ReLU, 2 LeakyReLU(0.2)) — the eval-mode conv+folded-BN(+add)+act of the backbone and
+ * the U-Net. dgrad_t takes the weight pre-transposed to [C][R][S][K] by mx_conv_transpose_weight
+ * (the plain mx_conv2d_dgrad allocates that temporary itself and is not graph-capturable). */
+int mx_conv2d_fwd_ex(const mx_conv_shape* s, const uint16_t* x, const uint16_t* w, const float* bias,
+                     const uint16_t* residual, int act, void* y, int ydtype, float* stats, mx_stream_t stream);
+int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS, int64_t C, uint16_t* wt, mx_stream_t stream);
+int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx,
+                      mx_stream_t stream);
 int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw, mx_stream_t stream);
 
 /* Train-mode BatchNorm2d around the conv (torch.nn.BatchNorm2d semantics, momentum 0.1,

@@ -1,0 +1,241 @@
+"""Convolution + BatchNorm + activation on libmx_det's MFMA implicit-GEMM kernels (NHWC, bf16).
+
+Autograd functions:
+  ConvAct      conv (+bias) (+act)                      - RPN head convs, predictor / FC layers
+  ConvBNAct    conv -> train-mode BatchNorm2d (+residual) (+act) - ResNet-50 body, FPN, box head
+The parameters keep torchvision's shapes ([Cout, Cin, kh, kw] conv weights, BatchNorm affine and
+running buffers), so state_dicts load both ways; the kernels take KRSC bf16 copies
+made once per step.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import call
+
+ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
+
+
+def _s():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def out_hw(H, W, R, S, stride, pad):
+    return (H + 2 * pad[0] - R) // stride[0] + 1, (W + 2 * pad[1] - S) // stride[1] + 1
+
+
+def shape(x_nhwc, K, R, S, stride, pad):
+    N, H, W, C = x_nhwc.shape
+    Ho, Wo = out_hw(H, W, R, S, stride, pad)
+    return _lib.ConvShape(N, H, W, C, K, R, S, Ho, Wo, stride[0], stride[1], pad[0], pad[1])
+
+
+def weight_krsc(w, cin_pad=None):
+    """[K,C,R,S] f32 parameter -> [K,R,S,C'] bf16 (C' = cin_pad, zero channels appended)."""
+    k = w.detach().permute(0, 2, 3, 1)
+    if cin_pad is not None and cin_pad != k.shape[3]:
+        k = torch.nn.functional.pad(k, (0, cin_pad - k.shape[3]))
+    return k.to(torch.bfloat16).contiguous()
+
+
+def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dtype=torch.bfloat16, stats=False):
+    """x NHWC bf16, wk KRSC bf16 -> y NHWC (out_dtype); optional BN stat partials."""
+    assert x.dtype == torch.bfloat16 and wk.dtype == torch.bfloat16 and x.is_contiguous() and wk.is_contiguous()
+    K, R, S, C = wk.shape
+    assert x.shape[3] == C, (x.shape, wk.shape)
+    sh = shape(x, K, R, S, stride, pad)
+    y = torch.empty((sh.N, sh.Ho, sh.Wo, K), dtype=out_dtype, device=x.device)
+    st = None
+    if stats:
+        mb = _lib.load().mx_conv_mblocks(ctypes.byref(sh))
+        st = torch.empty((2, mb, K), dtype=torch.float32, device=x.device)
+    if residual is not None:
+        residual = residual.contiguous()
+    call("mx_conv2d_fwd_ex", ctypes.byref(sh), _p(x), _p(wk), _p(bias), _p(residual), int(act), _p(y),
+         1 if out_dtype == torch.bfloat16 else 0, _p(st), _s())
+    return (y, st) if stats else y
+
+
+def conv_dgrad(dy, wk, x_shape, stride, pad):
+    """dy NHWC bf16 [N,Ho,Wo,K], wk KRSC bf16 -> dx NHWC bf16 [N,H,W,C]."""
+    K, R, S, C = wk.shape
+    N, H, W, _ = x_shape
+    Ho, Wo = out_hw(H, W, R, S, stride, pad)
+    sh = _lib.ConvShape(N, H, W, C, K, R, S, Ho, Wo, stride[0], stride[1], pad[0], pad[1])
+    wt = torch.empty((C, R, S, K), dtype=torch.bfloat16, device=dy.device)
+    call("mx_conv_transpose_weight", _p(wk), K, R * S, C, _p(wt), _s())
+    dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=dy.device)
+    call("mx_conv2d_dgrad_t", ctypes.byref(sh), _p(dy.contiguous()), _p(wt), _p(dx), _s())
+    return dx
+
+
+def conv_wgrad(dy, x, K, R, S, stride, pad):
+    """-> dW f32 [K,R,S,C]."""
+    sh = shape(x, K, R, S, stride, pad)
+    dw = torch.zeros((K, R, S, x.shape[3]), dtype=torch.float32, device=x.device)
+    call("mx_conv2d_wgrad", ctypes.byref(sh), _p(dy.contiguous()), _p(x), _p(dw), _s())
+    return dw
+
+
+def _act_grad(g, y, act):
+    if act == ACT_RELU:
+        return g * (y > 0).to(g.dtype)
+    if act == ACT_LEAKY:
+        return g * torch.where(y > 0, 1.0, 0.2).to(g.dtype)
+    return g
+
+
+class ConvAct(torch.autograd.Function):
+    """y = act(conv(x, w) + b). x NHWC bf16; w [K,C,R,S] f32 parameter; b f32 [K] or None."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, act, out_dtype):
+        wk = weight_krsc(w, x.shape[3])
+        y = conv_fwd(x, wk, stride, pad, bias=b.detach() if b is not None else None, act=act, out_dtype=out_dtype)
+        ctx.save_for_backward(x, wk, y)
+        ctx.cfg = (stride, pad, act, w.shape, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wk, y = ctx.saved_tensors
+        stride, pad, act, wshape, has_b = ctx.cfg
+        g = _act_grad(gy, y, act).to(torch.bfloat16).contiguous()
+        K, R, S, C = wk.shape
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad(g, wk, x.shape, stride, pad)
+        if ctx.needs_input_grad[1]:
+            dwk = conv_wgrad(g, x, K, R, S, stride, pad)
+            dw = dwk[..., : wshape[1]].permute(0, 3, 1, 2)
+        if has_b and ctx.needs_input_grad[2]:
+            db = g.float().sum(dim=(0, 1, 2))
+        return dx, dw, db, None, None, None, None
+
+
+class ConvBNAct(torch.autograd.Function):
+    """y = act(BN_train(conv(x, w)) (+ residual)). Updates running stats in place."""
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, residual, rmean, rvar, stride, pad, act, eps, momentum):
+        wk = weight_krsc(w, x.shape[3])
+        z, st = conv_fwd(x, wk, stride, pad, stats=True)
+        K = wk.shape[0]
+        M = z.numel() // K
+        mean = torch.empty(K, dtype=torch.float32, device=x.device)
+        invstd, scale, shift = torch.empty_like(mean), torch.empty_like(mean), torch.empty_like(mean)
+        call("mx_bn_finalize", _p(st), st.shape[1], K, M, _p(gamma.detach()), _p(beta.detach()), float(eps),
+             float(momentum), _p(rmean), _p(rvar), _p(mean), _p(invstd), _p(scale), _p(shift), _s())
+        y = torch.empty_like(z)
+        res = residual.contiguous() if residual is not None else None
+        call("mx_bn_apply", _p(z), 1, M, K, _p(scale), _p(shift), _p(res), int(act), _p(y), _s())
+        ctx.save_for_backward(x, wk, z, y, mean, invstd, gamma)
+        ctx.cfg = (stride, pad, act, w.shape, residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wk, z, y, mean, invstd, gamma = ctx.saved_tensors
+        stride, pad, act, wshape, has_res = ctx.cfg
+        K, R, S, C = wk.shape
+        M = z.numel() // K
+        gy = gy.to(torch.bfloat16).contiguous()
+        sums = torch.zeros((2, K), dtype=torch.float32, device=z.device)
+        call("mx_bn_bwd_reduce", _p(gy), _p(y), _p(z), M, K, int(act), _p(mean), _p(invstd), _p(sums), _s())
+        dz = torch.empty_like(z)
+        dres = torch.empty_like(z) if has_res else None
+        call("mx_bn_bwd_apply", _p(gy), _p(y), _p(z), M, K, int(act), _p(mean), _p(invstd), _p(gamma.detach()),
+             _p(sums), _p(dz), _p(dres), _s())
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad(dz, wk, x.shape, stride, pad)
+        if ctx.needs_input_grad[1]:
+            dwk = conv_wgrad(dz, x, K, R, S, stride, pad)
+            dw = dwk[..., : wshape[1]].permute(0, 3, 1, 2)
+        dgamma = sums[1] if ctx.needs_input_grad[2] else None
+        dbeta = sums[0] if ctx.needs_input_grad[3] else None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None
+
+
+class Conv2d(torch.nn.Module):
+    """nn.Conv2d-compatible parameters (state_dict keys weight/bias), NHWC bf16 activations."""
+
+    def __init__(self, cin, cout, k, stride=1, padding=0, bias=True, act=ACT_NONE, out_dtype=torch.bfloat16):
+        super().__init__()
+        k = (k, k) if isinstance(k, int) else tuple(k)
+        self.stride = (stride, stride) if isinstance(stride, int) else tuple(stride)
+        self.padding = (padding, padding) if isinstance(padding, int) else tuple(padding)
+        self.weight = torch.nn.Parameter(torch.empty(cout, cin, *k))
+        self.bias = torch.nn.Parameter(torch.zeros(cout)) if bias else None
+        self.act = act
+        self.out_dtype = out_dtype
+        torch.nn.init.kaiming_uniform_(self.weight, a=5 ** 0.5)
+
+    def forward(self, x):
+        return ConvAct.apply(x, self.weight, self.bias, self.stride, self.padding, self.act, self.out_dtype)
+
+
+class BatchNorm2d(torch.nn.Module):
+    """nn.BatchNorm2d-compatible parameters/buffers (weight, bias, running_mean, running_var,
+    num_batches_tracked); the arithmetic runs inside ConvBN."""
+
+    def __init__(self, c, eps=1e-5, momentum=0.1):
+        super().__init__()
+        self.eps, self.momentum = eps, momentum
+        self.weight = torch.nn.Parameter(torch.ones(c))
+        self.bias = torch.nn.Parameter(torch.zeros(c))
+        self.register_buffer("running_mean", torch.zeros(c))
+        self.register_buffer("running_var", torch.ones(c))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+
+def conv_bn(x, conv, bn, act, residual=None):
+    """Conv2d(bias=False) + BatchNorm2d (+ residual) + activation as one fused unit. Train mode:
+    batch statistics + running-stat update (nn.BatchNorm2d semantics); eval: BN folded into the conv."""
+    if bn.training:
+        if bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+        return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
+                               conv.stride, conv.padding, act, bn.eps, bn.momentum)
+    return eval_conv_bn(x, conv, bn, act, residual)
+
+
+class ConvNormAct(torch.nn.Sequential):
+    """torchvision Conv2dNormActivation layout: child "0" = Conv2d, child "1" = BatchNorm2d (or a
+    parameter-free activation when norm is None), so state_dict keys match (e.g. fpn.inner_blocks.0.0.weight,
+    rpn.head.conv.0.0.bias)."""
+
+    def __init__(self, cin, cout, k, stride=1, padding=None, norm=True, act=ACT_RELU):
+        padding = (k - 1) // 2 if padding is None else padding
+        conv = Conv2d(cin, cout, k, stride, padding, bias=not norm, act=ACT_NONE if norm else act)
+        if norm:
+            super().__init__(conv, BatchNorm2d(cout))
+        else:
+            super().__init__(conv, torch.nn.ReLU() if act == ACT_RELU else torch.nn.Identity())
+        self.norm, self.act_code = norm, act
+
+    def forward(self, x, residual=None):
+        if self.norm:
+            return conv_bn(x, self[0], self[1], self.act_code, residual)
+        return self[0](x)
+
+
+def fold_bn(conv, bn):
+    """Eval-mode BatchNorm folded into the conv: w' = w*gamma/sqrt(var+eps), b' = beta - mean*scale."""
+    scale = bn.weight.detach() / torch.sqrt(bn.running_var + bn.eps)
+    w = conv.weight.detach() * scale.view(-1, 1, 1, 1)
+    b = bn.bias.detach() - bn.running_mean * scale
+    if conv.bias is not None:
+        b = b + conv.bias.detach() * scale
+    return w, b.float().contiguous()
+
+
+def eval_conv_bn(x, conv, bn, act, residual=None):
+    w, b = fold_bn(conv, bn)
+    wk = weight_krsc(w, x.shape[3])
+    return conv_fwd(x.contiguous(), wk, conv.stride, conv.padding, bias=b, residual=residual, act=act)

@@ -1,0 +1,125 @@
+"""GPU numerics of the MFMA implicit-GEMM conv and the BatchNorm kernels.
+
+Reference: torch fp32 conv on the same bf16-rounded operands (the kernels multiply bf16 exactly and
+accumulate in f32, so only the summation order differs): f32-output comparisons use rtol 2e-5 of
+the |x|.|w| scale; bf16 outputs add one bf16 rounding (2^-8 relative).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # N, H, W, C, K, k, stride, pad
+    (2, 17, 23, 64, 128, 3, 1, 1),
+    (2, 20, 34, 128, 128, 3, 2, 1),
+    (1, 25, 42, 256, 512, 1, 2, 0),
+    (2, 33, 41, 8, 64, 7, 2, 3),       # stem: 3 real channels padded to 8
+    (4, 1, 1, 12544 // 16, 1024, 1, 1, 0),
+    (3, 9, 11, 256, 15, 1, 1, 0),      # RPN cls+bbox head (odd K)
+    (2, 7, 7, 256, 256, 3, 1, 1),      # box head conv on RoI tiles
+]
+
+
+def _scale(x, w, k):
+    return (x.abs().amax() * w.abs().amax() * x.shape[-1] * k * k).item()
+
+
+@pytest.mark.parametrize("N,H,W,C,K,k,st,pd", CASES)
+def test_conv_fwd(dev, N, H, W, C, K, k, st, pd):
+    from mx_det import conv as mc
+    g = torch.Generator().manual_seed(N * 1000 + C + K)
+    x = torch.randn(N, H, W, C, generator=g).bfloat16()
+    w = (torch.randn(K, C, k, k, generator=g) * 0.05).bfloat16()
+    b = torch.randn(K, generator=g)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float(), b, st, pd).permute(0, 2, 3, 1)
+    wk = mc.weight_krsc(w.float()).to(dev)
+    y, stats = mc.conv_fwd(x.to(dev), wk, (st, st), (pd, pd), bias=b.to(dev), out_dtype=torch.float32, stats=True)
+    tol = 2e-5 * _scale(x.float(), w.float(), k)
+    torch.testing.assert_close(y.cpu(), ref, rtol=0, atol=tol)
+    # BN statistics partials are over the pre-bias accumulators
+    z = (ref - b).reshape(-1, K).double()
+    s = stats.cpu().double().sum(1)
+    torch.testing.assert_close(s[0], z.sum(0), rtol=1e-4, atol=tol * 10)
+    torch.testing.assert_close(s[1], (z * z).sum(0), rtol=1e-4, atol=tol * tol * 10 + 1e-3)
+    yb = mc.conv_fwd(x.to(dev), wk, (st, st), (pd, pd), bias=b.to(dev), act=mc.ACT_RELU)
+    torch.testing.assert_close(yb.float().cpu(), ref.clamp_min(0), rtol=1e-2, atol=tol + 1e-2)
+
+
+def test_conv_fwd_residual_leaky(dev):
+    from mx_det import conv as mc
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 16, 16, 64, generator=g).bfloat16()
+    w = (torch.randn(64, 64, 3, 3, generator=g) * 0.05).bfloat16()
+    r = torch.randn(2, 16, 16, 64, generator=g).bfloat16()
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float(), None, 1, 1).permute(0, 2, 3, 1) + r.float()
+    ref = F.leaky_relu(ref, 0.2)
+    y = mc.conv_fwd(x.to(dev), mc.weight_krsc(w.float()).to(dev), (1, 1), (1, 1), residual=r.to(dev),
+                    act=mc.ACT_LEAKY, out_dtype=torch.float32)
+    torch.testing.assert_close(y.cpu(), ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("N,H,W,C,K,k,st,pd", [c for c in CASES if c[3] != 8 and c[4] % 8 == 0])
+def test_conv_dgrad_wgrad(dev, N, H, W, C, K, k, st, pd):
+    from mx_det import conv as mc
+    g = torch.Generator().manual_seed(7 + C + K)
+    x = torch.randn(N, H, W, C, generator=g).bfloat16()
+    w = (torch.randn(K, C, k, k, generator=g) * 0.05).bfloat16()
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, st, pd)
+    dy = torch.randn(yr.shape, generator=g).bfloat16()
+    yr.backward(dy.float())
+    wk = mc.weight_krsc(w.float()).to(dev)
+    dyn = dy.permute(0, 2, 3, 1).contiguous().to(dev)
+    dx = mc.conv_dgrad(dyn, wk, x.shape, (st, st), (pd, pd))
+    ref_dx = xr.grad.permute(0, 2, 3, 1)
+    tol = 2e-5 * (dy.abs().amax() * w.abs().amax() * K * k * k).item()
+    torch.testing.assert_close(dx.float().cpu(), ref_dx, rtol=1e-2, atol=tol + 1e-2 * ref_dx.abs().amax().item())
+    dw = mc.conv_wgrad(dyn, x.to(dev), K, k, k, (st, st), (pd, pd))
+    ref_dw = wr.grad.permute(0, 2, 3, 1)
+    tolw = 2e-5 * (dy.abs().amax() * x.abs().amax()).item() * dy.numel() / K
+    torch.testing.assert_close(dw.cpu(), ref_dw, rtol=0, atol=tolw)
+
+
+@pytest.mark.parametrize("act", [0, 1])
+def test_conv_bn_train_matches_torch(dev, act):
+    """ConvBNAct (train-mode BN, residual) vs torch conv -> batch_norm(training) -> add -> relu."""
+    from mx_det import conv as mc
+    g = torch.Generator().manual_seed(3)
+    N, H, W, C, K = 2, 20, 24, 64, 128
+    x = torch.randn(N, H, W, C, generator=g).bfloat16()
+    w = (torch.randn(K, C, 3, 3, generator=g) * 0.05).bfloat16().float()
+    gamma = torch.rand(K, generator=g) + 0.5
+    beta = torch.randn(K, generator=g) * 0.1
+    res = torch.randn(N, H, W, K, generator=g).bfloat16()
+    # torch reference
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr, gr, br = w.clone().requires_grad_(True), gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    rr = res.float().permute(0, 3, 1, 2).requires_grad_(True)
+    rm, rv = torch.zeros(K), torch.ones(K)
+    # mx
+    xd = x.to(dev).requires_grad_(True)
+    wd, gd, bd = w.to(dev).requires_grad_(True), gamma.to(dev).requires_grad_(True), beta.to(dev).requires_grad_(True)
+    rd = res.to(dev).requires_grad_(True)
+    rmd, rvd = torch.zeros(K, device=dev), torch.ones(K, device=dev)
+    y = mc.ConvBNAct.apply(xd, wd, gd, bd, rd, rmd, rvd, (1, 1), (1, 1), act, 1e-5, 0.1)
+    z = F.conv2d(xr, wr, None, 1, 1)
+    yr = F.batch_norm(z, rm, rv, gr, br, training=True, momentum=0.1, eps=1e-5) + rr
+    if act:
+        # ReLU with the mask of the device output: elements within bf16 rounding of 0 may flip
+        # sign between the two paths; the BN-backward math is what is compared here
+        yr = yr * (y.detach().float().cpu().permute(0, 3, 1, 2) > 0)
+    dy = torch.randn(yr.shape, generator=g).bfloat16().float()
+    yr.backward(dy)
+    y.backward(dy.permute(0, 2, 3, 1).bfloat16().to(dev))
+    torch.testing.assert_close(y.float().cpu(), yr.detach().permute(0, 2, 3, 1), rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(rmd.cpu(), rm, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(rvd.cpu(), rv, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(gd.grad.cpu(), gr.grad, rtol=2e-2, atol=2e-1)
+    torch.testing.assert_close(bd.grad.cpu(), br.grad, rtol=2e-2, atol=2e-1)
+    torch.testing.assert_close(rd.grad.float().cpu(), rr.grad.permute(0, 2, 3, 1), rtol=2e-2, atol=2e-2)
+    rel = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+    assert rel(xd.grad.float().cpu(), xr.grad.permute(0, 2, 3, 1)) < 2e-2
+    assert rel(wd.grad.cpu(), wr.grad) < 2e-2
