@@ -1,0 +1,201 @@
+"""Headline benchmark: images/sec of the Faster R-CNN R50-FPN v2 train step at 1333x800, bs=2/GPU.
+
+BASELINE.json metric "images/sec FRCNN-R50-FPN train @1333x800 bs=2/GPU, 1/2/4/8 MI355X"; workload =
+configs[1] (baseline train, bs=2 per GPU, HIP conv + RoIAlign + NMS ops) — the reference's training
+step of scripts/train_frcnn_baseline.py:167-178 (forward + loss sum + zero_grad + backward + SGD
+step + loss.item()), on synthetic VisDrone-shaped uint8 images resident in HBM (no dataset offline),
+random-init weights of the same architecture, trainable_backbone_layers=3 as in the reference run.
+`--augment` adds the on-GPU 50% noise/blur/low-res corruption of configs[2].
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+One process per GPU; gradients all-reduced over RCCL (torch.distributed "nccl") by DDP buckets;
+per-GPU BatchNorm statistics (no SyncBN: each GPU sees the reference's bs=2). Rank 0 prints one
+JSON line. Weak scaling: per-GPU work is fixed.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "robust-object-detection_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+N_IMAGES_PER_RANK = 8
+
+
+def build_model(device, trainable=3, backend=None):
+    from mx_det import frcnn
+    model = frcnn.fasterrcnn_resnet50_fpn_v2(weights=None)
+    model.roi_heads.box_predictor = frcnn.FastRCNNPredictor(model.roi_heads.box_predictor.cls_score.in_features, 7)
+    frcnn.set_trainable_layers(model.backbone.body, trainable)
+    if backend is not None:
+        model.set_backend(backend)
+    return model.to(device)
+
+
+def make_optimizer(model):
+    params = [p for p in model.parameters() if p.requires_grad]
+    return torch.optim.SGD(params, lr=0.005, momentum=0.9, weight_decay=0.0005)
+
+
+def train_step(model, opt, images, targets, augment=False, gen=None):
+    if augment:
+        from mx_det import ops
+        B = images.shape[0]
+        r = torch.rand(2 * B, generator=gen).tolist()
+        codes = [0 if r[2 * i] > 0.5 else 1 + min(int(r[2 * i + 1] * 3), 2) for i in range(B)]
+        images = ops.corrupt_u8(images, codes, seed=int(torch.randint(0, 2 ** 62, (1,), generator=gen)))
+    loss_dict = model(images, targets)
+    losses = sum(loss for loss in loss_dict.values())
+    opt.zero_grad(set_to_none=True)
+    losses.backward()
+    opt.step()
+    return float(losses.item())
+
+
+def cpu_baseline(gpu_model, seconds_hint=30.0):
+    """The oracle CPU restatement (oracle/cpu_backend.py: torch-CPU fp32 dense ops + C torchvision ops)
+    timed on this host's cores for ONE train step of the same workload (bs=2, 1333x800)."""
+    from oracle.cpu_backend import CpuBackend
+    from mx_det.data import synth_batch
+    torch.manual_seed(0)
+    cores = torch.get_num_threads()
+    m = build_model("cpu", backend=CpuBackend())
+    m.load_state_dict({k: v.detach().cpu() for k, v in gpu_model.state_dict().items()})
+    m.train()
+    opt = make_optimizer(m)
+    imgs, tg = synth_batch(0, 2)
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        train_step(m, opt, imgs, tg)
+        n += 1
+        if time.perf_counter() - t0 > seconds_hint or n >= 2:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": 2 * n / dt, "unit": "images/sec", "cores": cores, "kind": "port",
+            "sample": f"{n} train step(s) x 2 images 1333x800 on {cores} CPU threads ({dt:.1f} s)"}
+
+
+def conv_roofline(model, opt, imgs, tg):
+    """Live HIP-event timing of every conv kernel launch in one train step; the dominant kernel kind
+    (largest total time) is reported against the bf16 MFMA peak with its algorithmic FLOPs."""
+    from mx_det import conv as mc
+    t = mc.KernelTimer()
+    mc.set_timer(t)
+    try:
+        train_step(model, opt, imgs, tg)
+    finally:
+        mc.set_timer(None)
+    s = t.summary()
+    dom = max(s, key=lambda k: s[k]["ms"])
+    d = s[dom]
+    achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+    allf = sum(v["flops"] for v in s.values())
+    allms = sum(v["ms"] for v in s.values())
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
+            "kernel": {"fwd128": "conv_igemm_kernel<128,0>", "fwd64": "conv_igemm_kernel<64,0>",
+                       "dgrad": "conv_igemm_kernel<*,1>", "wgrad": "conv_wgrad_kernel"}[dom],
+            "launches_per_step": d["launches"], "avg_launch_us": round(1000 * d["ms"] / d["launches"], 2),
+            "gflop_per_launch": round(d["flops"] / d["launches"] / 1e9, 3),
+            "conv_stack": {"tflops": round(allf / (allms * 1e-3) / 1e12, 2), "gflop_per_step": round(allf / 1e9, 1),
+                           "ms_per_step": round(allms, 2),
+                           "by_kind": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                                           "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
+                                       for k, v in s.items()}}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--augment", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a HIP device")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from mx_det.data import synth_batch
+    torch.manual_seed(42)
+    model = build_model(dev).train()
+    ddp = model
+    if world > 1:
+        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], broadcast_buffers=False,
+                                                        gradient_as_bucket_view=True, bucket_cap_mb=50)
+    opt = make_optimizer(model)
+    imgs, tg = synth_batch(rank * N_IMAGES_PER_RANK, N_IMAGES_PER_RANK, device=dev)
+    gen = torch.Generator().manual_seed(1234 + rank)
+
+    def step(i):
+        j = (2 * i) % N_IMAGES_PER_RANK
+        return train_step(ddp, opt, imgs[j:j + 2], tg[j:j + 2], args.augment, gen)
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    images = 2 * args.steps * world
+    rec = {
+        "metric": "images/sec FRCNN-R50-FPN train @1333x800 bs=2/GPU",
+        "value": round(images / dt, 3),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * dt / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic VisDrone-shaped uint8 1333x800 (G~Poisson(55)), random-init weights",
+        "config": {"workload": "configs[1]: FRCNN R50-FPN v2 baseline train step" + (" + 50% on-GPU corruption"
+                                                                                   if args.augment else ""),
+                   "global_batch": 2 * world, "per_gpu_batch": 2, "image": "1333x800 (padded 1344x800)",
+                   "parallelism": f"dp{world}", "trainable_backbone_layers": 3},
+    }
+    if rank == 0 and not args.no_roofline:
+        rec["roofline"] = conv_roofline(ddp, opt, imgs[0:2], tg[0:2])
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(model)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -102,8 +102,7 @@ int mx_multiscale_roi_align_bwd(const void* grad_out, int dtype, float* const* g
 int mx_anchors_level(float size, const float* ratios_host, int nr, int64_t gh, int64_t gw, int64_t stride_h,
                      int64_t stride_w, float* out, mx_stream_t stream);
 /* decode_single: rel[n, ncls*4] against boxes[n,4] -> out[n, ncls*4]; weights (wx,wy,ww,wh);
- * dw/dh clamped at `clip`. clip_hw (nullable, int64 per-box image id into img_hw[2*i]) applies
- * clip_boxes_to_image. */
+ * dw/dh clamped at `clip`. */
 int mx_box_decode(const float* rel, const float* boxes, int64_t n, int64_t ncls, const float* weights4_host,
                   float clip, float* out, mx_stream_t stream);
 
@@ -154,6 +153,21 @@ int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS, int64_t C
 int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx,
                       mx_stream_t stream);
 int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw, mx_stream_t stream);
+
+/* NHWC pooling / resampling (bf16, C % 8 == 0).
+ * maxpool: F.max_pool2d (ResNet stem k3 s2 p1 — torchvision resnet50 reached at
+ *   train_frcnn_baseline.py:139; U-Net MaxPool2d(2), restoration_net.py:39); argmax (nullable,
+ *   int32 [N,Ho,Wo,C]) feeds the gather-form backward.
+ * upsample_nearest: F.interpolate(mode="nearest", size=(Ho,Wo)) of the FPN top-down path, fused with
+ *   the lateral add (y = up(x) + add, add nullable); backward sums each source's destinations. */
+int mx_maxpool_fwd(const uint16_t* x, int64_t N, int64_t H, int64_t W, int64_t C, int k, int stride, int pad,
+                   uint16_t* y, int32_t* argmax, mx_stream_t stream);
+int mx_maxpool_bwd(const uint16_t* gy, const int32_t* argmax, int64_t N, int64_t H, int64_t W, int64_t C, int k,
+                   int stride, int pad, uint16_t* gx, mx_stream_t stream);
+int mx_upsample_nearest_fwd(const uint16_t* x, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo,
+                            const uint16_t* add, uint16_t* y, mx_stream_t stream);
+int mx_upsample_nearest_bwd(const uint16_t* gy, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo,
+                            uint16_t* gx, mx_stream_t stream);
 
 /* Train-mode BatchNorm2d around the conv (torch.nn.BatchNorm2d semantics, momentum 0.1,
  * unbiased running_var). finalize: reduce stats partials -> mean/invstd (f64 accumulation), fold

@@ -22,17 +22,17 @@ __device__ __forceinline__ float actd(float y, int act) {
   return 1.f;
 }
 
-// one block per 64 channels: 4 row-slices of the partials per channel, f64 sums
-__global__ void bn_finalize_kernel(const float* __restrict__ stats, int64_t mb, int64_t K, int64_t count,
+// block = 16 channels x 16 row-slices of the per-block partials; f64 sums; LDS tree over slices
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ stats, int64_t mb, int64_t K, int64_t count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float mom,
                                    float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ mean_o,
                                    float* __restrict__ invstd_o, float* __restrict__ scale_o, float* __restrict__ shift_o) {
-  __shared__ double ps[4][64], pq[4][64];
-  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int64_t k = (int64_t)blockIdx.x * 64 + cl;
+  __shared__ double ps[16][17], pq[16][17];
+  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int64_t k = (int64_t)blockIdx.x * 16 + cl;
   double s = 0.0, q = 0.0;
   if (k < K)
-    for (int64_t b = sl; b < mb; b += 4) {
+    for (int64_t b = sl; b < mb; b += 16) {
       s += (double)stats[b * K + k];
       q += (double)stats[(mb + b) * K + k];
     }
@@ -40,8 +40,9 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int64_t mb, 
   pq[sl][cl] = q;
   __syncthreads();
   if (sl == 0 && k < K) {
-    s = ps[0][cl] + ps[1][cl] + ps[2][cl] + ps[3][cl];
-    q = pq[0][cl] + pq[1][cl] + pq[2][cl] + pq[3][cl];
+    s = 0.0; q = 0.0;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) { s += ps[t][cl]; q += pq[t][cl]; }
     double mean = s / (double)count;
     double var = q / (double)count - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -59,19 +60,28 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int64_t mb, 
   }
 }
 
+// Thread t owns channel chunk c8 = t % K8 for its whole life (per-channel constants stay in
+// registers) and walks rows r = t / K8 + i * (T / K8): 16-B vector loads/stores, coalesced per row.
 template <typename T>
-__global__ void bn_apply_kernel(const T* __restrict__ x, int64_t M, int64_t K, const float* __restrict__ scale,
+__global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, int64_t M, int64_t K, const float* __restrict__ scale,
                                 const float* __restrict__ shift, const uint16_t* __restrict__ res, int act,
                                 uint16_t* __restrict__ y) {
   const int64_t K8 = K / 8;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M * K8; e += (int64_t)gridDim.x * blockDim.x) {
-    int64_t c0 = (e % K8) * 8;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t rstride = ((int64_t)gridDim.x * blockDim.x) / K8;
+  if (t >= rstride * K8) return;
+  const int64_t c8 = t % K8, c0 = c8 * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) { sc[q] = scale[c0 + q]; sh[q] = shift[c0 + q]; }
+  for (int64_t r = t / K8; r < M; r += rstride) {
+    const int64_t e = r * K8 + c8;
     float v[8];
     if constexpr (sizeof(T) == 2) {
       uint4 u = *(const uint4*)(x + e * 8);
       const uint16_t* h = (const uint16_t*)&u;
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] = bf2f(h[t]);
+      for (int q = 0; q < 8; ++q) v[q] = bf2f(h[q]);
     } else {
       *(float4*)&v[0] = *(const float4*)(x + e * 8);
       *(float4*)&v[4] = *(const float4*)(x + e * 8 + 4);
@@ -81,12 +91,12 @@ __global__ void bn_apply_kernel(const T* __restrict__ x, int64_t M, int64_t K, c
       uint4 u = *(const uint4*)(res + e * 8);
       const uint16_t* h = (const uint16_t*)&u;
 #pragma unroll
-      for (int t = 0; t < 8; ++t) rv[t] = bf2f(h[t]);
+      for (int q = 0; q < 8; ++q) rv[q] = bf2f(h[q]);
     }
     uint4 o;
     uint16_t* oh = (uint16_t*)&o;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) oh[t] = f2bf(actf(v[t] * scale[c0 + t] + shift[c0 + t] + rv[t], act));
+    for (int q = 0; q < 8; ++q) oh[q] = f2bf(actf(v[q] * sc[q] + sh[q] + rv[q], act));
     *(uint4*)(y + e * 8) = o;
   }
 }
@@ -134,36 +144,52 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const uint16_t* __re
   for (int64_t i = threadIdx.x; i < 2 * K; i += blockDim.x) atomicAdd(&sums[i], red[i]);
 }
 
-__global__ void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                     const uint16_t* __restrict__ x, int64_t M, int64_t K, int act,
                                     const float* __restrict__ mean, const float* __restrict__ invstd,
                                     const float* __restrict__ gamma, const float* __restrict__ sums,
                                     uint16_t* __restrict__ dx, uint16_t* __restrict__ dres) {
   const int64_t K8 = K / 8;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t rstride = ((int64_t)gridDim.x * blockDim.x) / K8;
+  if (t >= rstride * K8) return;
+  const int64_t c8 = t % K8, c0 = c8 * 8;
   const float invM = 1.0f / (float)M;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M * K8; e += (int64_t)gridDim.x * blockDim.x) {
-    int64_t c0 = (e % K8) * 8;
+  // dx = a*g + b*x + c  with a = gamma*invstd, b = -a*invstd*mean(g*xhat), c = -a*(mean(g) - mean*invstd*mean(g*xhat))
+  float A[8], Bc[8], Cc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int64_t c = c0 + q;
+    float is = invstd[c], a = (gamma ? gamma[c] : 1.f) * is;
+    float mg = sums[c] * invM, mgx = sums[K + c] * invM;
+    A[q] = a;
+    Bc[q] = -a * is * mgx;
+    Cc[q] = -a * (mg - mean[c] * is * mgx);
+  }
+  for (int64_t r = t / K8; r < M; r += rstride) {
+    const int64_t e = r * K8 + c8;
     uint4 ud = *(const uint4*)(dy + e * 8), uy = *(const uint4*)(y + e * 8), ux = *(const uint4*)(x + e * 8);
     const uint16_t *hd = (const uint16_t*)&ud, *hy = (const uint16_t*)&uy, *hx = (const uint16_t*)&ux;
     uint4 o, orr;
     uint16_t* oh = (uint16_t*)&o;
     uint16_t* orh = (uint16_t*)&orr;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      int64_t c = c0 + t;
-      float g = bf2f(hd[t]) * actd(bf2f(hy[t]), act);
-      float xh = (bf2f(hx[t]) - mean[c]) * invstd[c];
-      float gm = gamma ? gamma[c] : 1.f;
-      float d = (g - sums[c] * invM - xh * sums[K + c] * invM) * invstd[c] * gm;
-      oh[t] = f2bf(d);
-      orh[t] = f2bf(g);
+    for (int q = 0; q < 8; ++q) {
+      float g = bf2f(hd[q]) * actd(bf2f(hy[q]), act);
+      oh[q] = f2bf(A[q] * g + Bc[q] * bf2f(hx[q]) + Cc[q]);
+      orh[q] = f2bf(g);
     }
     *(uint4*)(dx + e * 8) = o;
     if (dres) *(uint4*)(dres + e * 8) = orr;
   }
 }
 
-static unsigned grid_for(int64_t n, int T = 256) { return (unsigned)std::min<int64_t>(cdiv(n, T), 256 * 16); }
+// grid for the fixed-channel-chunk kernels: ~2048 blocks of 256 threads, multiple of K8 threads
+static unsigned grid_rows(int64_t M, int64_t K8) {
+  int64_t want = std::min<int64_t>(cdiv(M * K8, 256), 2048);
+  return (unsigned)std::max<int64_t>(want, cdiv(K8, 256));
+}
+
 
 }  // namespace mx
 
@@ -174,7 +200,7 @@ extern "C" int mx_bn_finalize(const float* stats, int64_t mb, int64_t K, int64_t
                               float* invstd, float* scale, float* shift, mx_stream_t stream) {
   MX_CHECK_ARG(mb > 0 && K > 0 && count > 0, "bn_finalize: bad sizes");
   MX_CHECK_ARG((rm == nullptr) == (rv == nullptr), "bn_finalize: running mean/var must both be given or both null");
-  bn_finalize_kernel<<<(unsigned)cdiv(K, 64), 256, 0, (hipStream_t)stream>>>(stats, mb, K, count, gamma, beta, eps, momentum,
+  bn_finalize_kernel<<<(unsigned)cdiv(K, 16), 256, 0, (hipStream_t)stream>>>(stats, mb, K, count, gamma, beta, eps, momentum,
                                                                               rm, rv, mean, invstd, scale, shift);
   MX_LAUNCH_CHECK();
   return MX_OK;
@@ -185,10 +211,10 @@ extern "C" int mx_bn_apply(const void* x, int xdtype, int64_t M, int64_t K, cons
   MX_CHECK_ARG(K % 8 == 0, "bn_apply: K %% 8 != 0");
   if (M == 0) return MX_OK;
   if (xdtype == MX_BF16)
-    bn_apply_kernel<uint16_t><<<grid_for(M * K / 8), 256, 0, (hipStream_t)stream>>>((const uint16_t*)x, M, K, scale, shift,
+    bn_apply_kernel<uint16_t><<<grid_rows(M, K / 8), 256, 0, (hipStream_t)stream>>>((const uint16_t*)x, M, K, scale, shift,
                                                                                      residual, act, y);
   else
-    bn_apply_kernel<float><<<grid_for(M * K / 8), 256, 0, (hipStream_t)stream>>>((const float*)x, M, K, scale, shift,
+    bn_apply_kernel<float><<<grid_rows(M, K / 8), 256, 0, (hipStream_t)stream>>>((const float*)x, M, K, scale, shift,
                                                                                   residual, act, y);
   MX_LAUNCH_CHECK();
   return MX_OK;
@@ -211,7 +237,7 @@ extern "C" int mx_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint
                                uint16_t* dx, uint16_t* dres, mx_stream_t stream) {
   MX_CHECK_ARG(K % 8 == 0, "bn_bwd_apply: K %% 8 != 0");
   if (M == 0) return MX_OK;
-  bn_bwd_apply_kernel<<<grid_for(M * K / 8), 256, 0, (hipStream_t)stream>>>(dy, y, x, M, K, act, mean, invstd, gamma, sums,
+  bn_bwd_apply_kernel<<<grid_rows(M, K / 8), 256, 0, (hipStream_t)stream>>>(dy, y, x, M, K, act, mean, invstd, gamma, sums,
                                                                            dx, dres);
   MX_LAUNCH_CHECK();
   return MX_OK;

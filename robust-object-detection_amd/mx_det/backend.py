@@ -1,0 +1,114 @@
+"""Op backend the detection model is written against.
+
+`HipBackend` (this file) is the product path: every hot op is a libmx_det HIP kernel on NHWC bf16
+activations. The model never calls torch conv/pool/RoI ops itself; it calls `self.be.*`. (A CPU
+restatement of the same interface lives in oracle/cpu_backend.py for parity tests and the CPU
+baseline; the product never imports it.)
+"""
+import ctypes
+
+import torch
+
+from . import conv as mc
+from . import ops
+from ._lib import call
+
+
+def _s():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, st, pd):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        Ho, Wo = (H + 2 * pd - k) // st + 1, (W + 2 * pd - k) // st + 1
+        y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
+        arg = torch.empty((N, Ho, Wo, C), dtype=torch.int32, device=x.device) if x.requires_grad else None
+        call("mx_maxpool_fwd", _p(x), N, H, W, C, k, st, pd, _p(y), _p(arg), _s())
+        ctx.save_for_backward(arg)
+        ctx.cfg = (x.shape, k, st, pd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (arg,) = ctx.saved_tensors
+        (N, H, W, C), k, st, pd = ctx.cfg
+        gx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=gy.device)
+        call("mx_maxpool_bwd", _p(gy.contiguous()), _p(arg), N, H, W, C, k, st, pd, _p(gx), _s())
+        return gx, None, None, None
+
+
+class _UpsampleAdd(torch.autograd.Function):
+    """y = nearest_upsample(x, size) + add (FPN top-down)."""
+
+    @staticmethod
+    def forward(ctx, x, add, Ho, Wo):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
+        a = add.contiguous() if add is not None else None
+        call("mx_upsample_nearest_fwd", _p(x), N, H, W, C, Ho, Wo, _p(a), _p(y), _s())
+        ctx.cfg = (x.shape, Ho, Wo, add is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (N, H, W, C), Ho, Wo, has_add = ctx.cfg
+        g = gy.contiguous()
+        gx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=gy.device)
+        call("mx_upsample_nearest_bwd", _p(g), N, H, W, C, Ho, Wo, _p(gx), _s())
+        return gx, (g if has_add else None), None, None
+
+
+class HipBackend:
+    name = "hip"
+    act_dtype = torch.bfloat16
+    stem_channels = 8  # RGB padded to 8 channels for the 16-B gather of the stem conv
+
+    # ---- dense ---------------------------------------------------------------------------
+    def conv_bn(self, x, conv, bn, act, residual=None):
+        return mc.conv_bn(x, conv, bn, act, residual)
+
+    def conv(self, x, weight, bias, stride, pad, act, out_dtype=torch.bfloat16):
+        return mc.ConvAct.apply(x, weight, bias, stride, pad, act, out_dtype)
+
+    def maxpool(self, x, k, stride, pad):
+        return _MaxPool.apply(x, k, stride, pad)
+
+    def upsample_add(self, x, add, size):
+        return _UpsampleAdd.apply(x, add, size[0], size[1])
+
+    # ---- detection ops ---------------------------------------------------------------------
+    def multiscale_roi_align(self, feats, rois, scales, k_min, output_size=(7, 7), sampling_ratio=2):
+        return ops.multiscale_roi_align(feats, rois, scales, k_min, output_size, sampling_ratio)
+
+    def match_assign(self, gt, boxes, high, low, allow_lq, mode, gt_labels=None, weights=None):
+        return ops.match_assign(gt, boxes, high, low, allow_lq, mode, gt_labels, weights)
+
+    def batched_nms(self, boxes, scores, idxs, thr, group=None, max_seg=None, mode=0):
+        return ops.batched_nms(boxes, scores, idxs, thr, group=group, max_seg=max_seg, mode=mode)
+
+    def box_decode(self, rel, boxes, weights):
+        return ops.box_decode(rel, boxes, weights)
+
+    def anchors_level(self, size, ratios, gh, gw, sh, sw, device):
+        return ops.anchors_level(size, ratios, gh, gw, sh, sw, device)
+
+    def normalize_pad_u8(self, images_u8, padded_hw):
+        return ops.normalize_pad(images_u8, padded_hw, channels=self.stem_channels, dtype=self.act_dtype)
+
+
+_default = None
+
+
+def default_backend():
+    global _default
+    if _default is None:
+        _default = HipBackend()
+    return _default

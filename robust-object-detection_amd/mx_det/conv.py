@@ -21,6 +21,42 @@ def _s():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+class KernelTimer:
+    """Optional live timing of the conv kernels with HIP events on the launch stream (bench.py's
+    roofline). Records (kind, algorithmic FLOPs, start/end events) per launch."""
+
+    def __init__(self):
+        self.rec = []
+
+    def start(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def stop(self, kind, flops, e0):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.rec.append((kind, float(flops), e0, e1))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for kind, fl, a, b in self.rec:
+            d = out.setdefault(kind, {"launches": 0, "flops": 0.0, "ms": 0.0})
+            d["launches"] += 1
+            d["flops"] += fl
+            d["ms"] += a.elapsed_time(b)
+        return out
+
+
+_timer = None
+
+
+def set_timer(t):
+    global _timer
+    _timer = t
+
+
 def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -56,8 +92,11 @@ def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dty
         st = torch.empty((2, mb, K), dtype=torch.float32, device=x.device)
     if residual is not None:
         residual = residual.contiguous()
+    t0 = _timer.start() if _timer else None
     call("mx_conv2d_fwd_ex", ctypes.byref(sh), _p(x), _p(wk), _p(bias), _p(residual), int(act), _p(y),
          1 if out_dtype == torch.bfloat16 else 0, _p(st), _s())
+    if _timer:
+        _timer.stop("fwd128" if K > 64 else "fwd64", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * C, t0)
     return (y, st) if stats else y
 
 
@@ -70,7 +109,11 @@ def conv_dgrad(dy, wk, x_shape, stride, pad):
     wt = torch.empty((C, R, S, K), dtype=torch.bfloat16, device=dy.device)
     call("mx_conv_transpose_weight", _p(wk), K, R * S, C, _p(wt), _s())
     dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=dy.device)
-    call("mx_conv2d_dgrad_t", ctypes.byref(sh), _p(dy.contiguous()), _p(wt), _p(dx), _s())
+    dyc = dy.contiguous()
+    t0 = _timer.start() if _timer else None
+    call("mx_conv2d_dgrad_t", ctypes.byref(sh), _p(dyc), _p(wt), _p(dx), _s())
+    if _timer:
+        _timer.stop("dgrad", 2.0 * N * Ho * Wo * K * R * S * C, t0)
     return dx
 
 
@@ -78,7 +121,11 @@ def conv_wgrad(dy, x, K, R, S, stride, pad):
     """-> dW f32 [K,R,S,C]."""
     sh = shape(x, K, R, S, stride, pad)
     dw = torch.zeros((K, R, S, x.shape[3]), dtype=torch.float32, device=x.device)
-    call("mx_conv2d_wgrad", ctypes.byref(sh), _p(dy.contiguous()), _p(x), _p(dw), _s())
+    dyc = dy.contiguous()
+    t0 = _timer.start() if _timer else None
+    call("mx_conv2d_wgrad", ctypes.byref(sh), _p(dyc), _p(x), _p(dw), _s())
+    if _timer:
+        _timer.stop("wgrad", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * x.shape[3], t0)
     return dw
 
 
@@ -108,10 +155,15 @@ class ConvAct(torch.autograd.Function):
         g = _act_grad(gy, y, act).to(torch.bfloat16).contiguous()
         K, R, S, C = wk.shape
         dx = dw = db = None
+        K8 = (K + 7) // 8 * 8
+        gk, wkk = g, wk
+        if K8 != K:  # narrow heads (RPN cls+box 15, predictor 35): zero-pad the output channels
+            gk = torch.nn.functional.pad(g, (0, K8 - K)).contiguous()
+            wkk = torch.cat([wk, wk.new_zeros((K8 - K, R, S, C))])
         if ctx.needs_input_grad[0]:
-            dx = conv_dgrad(g, wk, x.shape, stride, pad)
+            dx = conv_dgrad(gk, wkk, x.shape, stride, pad)
         if ctx.needs_input_grad[1]:
-            dwk = conv_wgrad(g, x, K, R, S, stride, pad)
+            dwk = conv_wgrad(gk, x, K8, R, S, stride, pad)[:K]
             dw = dwk[..., : wshape[1]].permute(0, 3, 1, 2)
         if has_b and ctx.needs_input_grad[2]:
             db = g.float().sum(dim=(0, 1, 2))
@@ -176,8 +228,8 @@ class Conv2d(torch.nn.Module):
         self.out_dtype = out_dtype
         torch.nn.init.kaiming_uniform_(self.weight, a=5 ** 0.5)
 
-    def forward(self, x):
-        return ConvAct.apply(x, self.weight, self.bias, self.stride, self.padding, self.act, self.out_dtype)
+    def forward(self, x, be):
+        return be.conv(x, self.weight, self.bias, self.stride, self.padding, self.act, self.out_dtype)
 
 
 class BatchNorm2d(torch.nn.Module):
@@ -219,10 +271,11 @@ class ConvNormAct(torch.nn.Sequential):
             super().__init__(conv, torch.nn.ReLU() if act == ACT_RELU else torch.nn.Identity())
         self.norm, self.act_code = norm, act
 
-    def forward(self, x, residual=None):
+    def forward(self, x, be, residual=None):
         if self.norm:
-            return conv_bn(x, self[0], self[1], self.act_code, residual)
-        return self[0](x)
+            return be.conv_bn(x, self[0], self[1], self.act_code, residual)
+        c = self[0]
+        return be.conv(x, c.weight, c.bias, c.stride, c.padding, c.act, c.out_dtype)
 
 
 def fold_bn(conv, bn):

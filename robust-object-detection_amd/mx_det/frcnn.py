@@ -1,0 +1,608 @@
+"""Faster R-CNN ResNet-50-FPN v2 on the libmx_det HIP backend (NHWC, bf16 activations).
+
+Drop-in for what the reference builds at scripts/train_frcnn_baseline.py:139-143 and
+scripts/eval_all.py:79-87:
+    model = fasterrcnn_resnet50_fpn_v2(weights=None)
+    model.roi_heads.box_predictor = FastRCNNPredictor(model.roi_heads.box_predictor.cls_score.in_features, 7)
+    loss_dict = model(images, targets)      # train: loss_classifier, loss_box_reg, loss_objectness, loss_rpn_box_reg
+    detections = model(images)              # eval: [{"boxes", "labels", "scores"}], <= 100 per image
+The module tree, parameter shapes and state_dict keys follow torchvision 0.20.1's
+fasterrcnn_resnet50_fpn_v2 (detr_env_requirements.txt:31), so reference checkpoints
+(best.pth {"model": state_dict}) load unchanged. Semantics restated from torchvision (SURVEY.md §8
+notes): GeneralizedRCNNTransform, AnchorGenerator, RPNHead(conv_depth=2), RegionProposalNetwork,
+RoIHeads with MultiScaleRoIAlign(['0'..'3'], 7, 2), FastRCNNConvFCHead (4 conv+BN, FC 1024),
+BoxCoder weights (1,1,1,1) / (10,10,5,5), Matcher / BalancedPositiveNegativeSampler settings.
+"""
+import math
+from collections import OrderedDict
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .backend import default_backend
+from .conv import ACT_NONE, ACT_RELU, BatchNorm2d, Conv2d, ConvNormAct
+
+RPN_WEIGHTS = (1.0, 1.0, 1.0, 1.0)
+ROI_WEIGHTS = (10.0, 10.0, 5.0, 5.0)
+
+
+def _be(mod):
+    return getattr(mod, "_be", None) or default_backend()
+
+
+# ------------------------------------------------------------------------------------------ body
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = BatchNorm2d(planes)
+        self.conv2 = Conv2d(planes, planes, 3, stride, 1, bias=False)
+        self.bn2 = BatchNorm2d(planes)
+        self.conv3 = Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = BatchNorm2d(planes * 4)
+        self.downsample = downsample
+
+    def forward(self, x, be):
+        out = be.conv_bn(x, self.conv1, self.bn1, ACT_RELU)
+        out = be.conv_bn(out, self.conv2, self.bn2, ACT_RELU)
+        identity = x
+        if self.downsample is not None:
+            identity = be.conv_bn(x, self.downsample[0], self.downsample[1], ACT_NONE)
+        return be.conv_bn(out, self.conv3, self.bn3, ACT_RELU, residual=identity)
+
+
+class ResNet50Body(nn.Module):
+    """torchvision resnet50 minus avgpool/fc (IntermediateLayerGetter), nn.BatchNorm2d norm layer."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv1 = Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = BatchNorm2d(64)
+        self.inplanes = 64
+        self.layer1 = self._make(64, 3, 1)
+        self.layer2 = self._make(128, 4, 2)
+        self.layer3 = self._make(256, 6, 2)
+        self.layer4 = self._make(512, 3, 2)
+        for m in self.modules():
+            if isinstance(m, Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+
+    def _make(self, planes, blocks, stride):
+        ds = None
+        if stride != 1 or self.inplanes != planes * 4:
+            ds = nn.Sequential(Conv2d(self.inplanes, planes * 4, 1, stride, bias=False), BatchNorm2d(planes * 4))
+        layers = [Bottleneck(self.inplanes, planes, stride, ds)]
+        self.inplanes = planes * 4
+        layers += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward(self, x, be):
+        x = be.conv_bn(x, self.conv1, self.bn1, ACT_RELU)
+        x = be.maxpool(x, 3, 2, 1)
+        out = OrderedDict()
+        for i, name in enumerate(("layer1", "layer2", "layer3", "layer4")):
+            for blk in getattr(self, name):
+                x = blk(x, be)
+            out[str(i)] = x
+        return out
+
+
+class FeaturePyramidNetwork(nn.Module):
+    """torchvision.ops.FeaturePyramidNetwork(norm_layer=BatchNorm2d) + LastLevelMaxPool."""
+
+    def __init__(self, in_channels_list=(256, 512, 1024, 2048), out_channels=256):
+        super().__init__()
+        self.inner_blocks = nn.ModuleList([ConvNormAct(c, out_channels, 1, padding=0, act=ACT_NONE)
+                                           for c in in_channels_list])
+        self.layer_blocks = nn.ModuleList([ConvNormAct(out_channels, out_channels, 3, act=ACT_NONE)
+                                           for _ in in_channels_list])
+        for m in self.modules():
+            if isinstance(m, Conv2d):
+                nn.init.kaiming_uniform_(m.weight, a=1)
+                if m.bias is not None:
+                    nn.init.constant_(m.bias, 0)
+
+    def forward(self, x, be):
+        names = list(x.keys())
+        feats = list(x.values())
+        last_inner = self.inner_blocks[-1](feats[-1], be)
+        results = [self.layer_blocks[-1](last_inner, be)]
+        for idx in range(len(feats) - 2, -1, -1):
+            lat = feats[idx]
+            top_down = be.upsample_add(last_inner, None, (lat.shape[1], lat.shape[2]))
+            # inner_lateral + top_down fused into the lateral conv's BN epilogue
+            last_inner = self.inner_blocks[idx](lat, be, residual=top_down)
+            results.insert(0, self.layer_blocks[idx](last_inner, be))
+        results.append(be.maxpool(results[-1], 1, 2, 0))  # LastLevelMaxPool: max_pool2d(x, 1, 2, 0)
+        return OrderedDict(zip(names + ["pool"], results))
+
+
+class BackboneWithFPN(nn.Module):
+    def __init__(self, trainable_layers=3):
+        super().__init__()
+        self.body = ResNet50Body()
+        self.fpn = FeaturePyramidNetwork()
+        self.out_channels = 256
+        set_trainable_layers(self.body, trainable_layers)
+
+    def forward(self, x, be):
+        return self.fpn(self.body(x, be), be)
+
+
+def set_trainable_layers(body, trainable_layers):
+    """torchvision _resnet_fpn_extractor: freeze every parameter outside the last `trainable_layers`."""
+    layers = ["layer4", "layer3", "layer2", "layer1", "conv1"][:trainable_layers]
+    if trainable_layers == 5:
+        layers.append("bn1")
+    for name, p in body.named_parameters():
+        if all(not name.startswith(layer) for layer in layers):
+            p.requires_grad_(False)
+
+
+# ------------------------------------------------------------------------------------------ RPN
+class RPNHead(nn.Module):
+    def __init__(self, in_channels=256, num_anchors=3, conv_depth=2):
+        super().__init__()
+        self.conv = nn.Sequential(*[ConvNormAct(in_channels, in_channels, 3, norm=False, act=ACT_RELU)
+                                    for _ in range(conv_depth)])
+        self.cls_logits = Conv2d(in_channels, num_anchors, 1)
+        self.bbox_pred = Conv2d(in_channels, num_anchors * 4, 1)
+        for m in self.modules():
+            if isinstance(m, Conv2d):
+                nn.init.normal_(m.weight, std=0.01)
+                if m.bias is not None:
+                    nn.init.constant_(m.bias, 0)
+
+    def forward(self, feats, be):
+        A = self.cls_logits.weight.shape[0]
+        w = torch.cat([self.cls_logits.weight, self.bbox_pred.weight])
+        b = torch.cat([self.cls_logits.bias, self.bbox_pred.bias])
+        logits, deltas = [], []
+        for f in feats:
+            t = f
+            for c in self.conv:
+                t = c(t, be)
+            o = be.conv(t, w, b, (1, 1), (0, 0), ACT_NONE, out_dtype=torch.float32)  # [N,H,W,A*5]
+            N = o.shape[0]
+            logits.append(o[..., :A].reshape(N, -1))          # (h, w, a) order = torchvision permute
+            deltas.append(o[..., A:].reshape(N, -1, 4))
+        return logits, deltas
+
+
+class AnchorGenerator(nn.Module):
+    def __init__(self, sizes=((32,), (64,), (128,), (256,), (512,)), aspect_ratios=((0.5, 1.0, 2.0),) * 5):
+        super().__init__()
+        self.sizes, self.aspect_ratios = sizes, aspect_ratios
+        self._cache = {}
+
+    def num_anchors_per_location(self):
+        return [len(s) * len(a) for s, a in zip(self.sizes, self.aspect_ratios)]
+
+    def forward(self, padded_hw, grid_sizes, device, be):
+        key = (tuple(padded_hw), tuple(grid_sizes), str(device))
+        if key not in self._cache:
+            out = []
+            for (gh, gw), size, ratios in zip(grid_sizes, self.sizes, self.aspect_ratios):
+                sh, sw = padded_hw[0] // gh, padded_hw[1] // gw  # torch integer division as torchvision
+                out.append(be.anchors_level(float(size[0]), list(ratios), gh, gw, sh, sw, device))
+            self._cache = {key: torch.cat(out)}
+        return self._cache[key]
+
+
+def _smooth_l1_sum(x, y, beta):
+    return F.smooth_l1_loss(x, y, beta=beta, reduction="sum")
+
+
+class BalancedPositiveNegativeSampler:
+    def __init__(self, batch_size_per_image, positive_fraction):
+        self.batch, self.frac = batch_size_per_image, positive_fraction
+
+    def __call__(self, labels_list):
+        pos_idx, neg_idx = [], []
+        for lab in labels_list:
+            positive = torch.where(lab >= 1)[0]
+            negative = torch.where(lab == 0)[0]
+            num_pos = min(positive.numel(), int(self.batch * self.frac))
+            num_neg = min(negative.numel(), self.batch - num_pos)
+            perm1 = torch.randperm(positive.numel(), device=lab.device)[:num_pos]
+            perm2 = torch.randperm(negative.numel(), device=lab.device)[:num_neg]
+            pm = torch.zeros_like(lab, dtype=torch.bool)
+            nm = torch.zeros_like(lab, dtype=torch.bool)
+            pm[positive[perm1]] = True
+            nm[negative[perm2]] = True
+            pos_idx.append(pm)
+            neg_idx.append(nm)
+        return pos_idx, neg_idx
+
+
+class RegionProposalNetwork(nn.Module):
+    def __init__(self, anchor_generator, head, fg_iou_thresh=0.7, bg_iou_thresh=0.3, batch_size_per_image=256,
+                 positive_fraction=0.5, pre_nms_top_n=None, post_nms_top_n=None, nms_thresh=0.7,
+                 score_thresh=0.0, min_size=1e-3):
+        super().__init__()
+        self.anchor_generator = anchor_generator
+        self.head = head
+        self.fg, self.bg = fg_iou_thresh, bg_iou_thresh
+        self.fg_bg_sampler = BalancedPositiveNegativeSampler(batch_size_per_image, positive_fraction)
+        self._pre = pre_nms_top_n or dict(training=2000, testing=1000)
+        self._post = post_nms_top_n or dict(training=2000, testing=1000)
+        self.nms_thresh, self.score_thresh, self.min_size = nms_thresh, score_thresh, min_size
+
+    def pre_nms_top_n(self):
+        return self._pre["training" if self.training else "testing"]
+
+    def post_nms_top_n(self):
+        return self._post["training" if self.training else "testing"]
+
+    def filter_proposals(self, proposals, objectness, image_sizes, num_per_level, be):
+        N = proposals.shape[0]
+        dev = proposals.device
+        ob = objectness.detach()
+        pre = self.pre_nms_top_n()
+        tops, lvls, off = [], [], 0
+        for i, n in enumerate(num_per_level):
+            k = min(pre, n)
+            _, ti = ob[:, off:off + n].topk(k, dim=1)
+            tops.append(ti + off)
+            lvls.append(torch.full((k,), i, dtype=torch.int64, device=dev))
+            off += n
+        top = torch.cat(tops, 1)
+        lvl = torch.cat(lvls).unsqueeze(0).expand(N, -1)
+        bi = torch.arange(N, device=dev)[:, None]
+        prob = torch.sigmoid(ob[bi, top])
+        boxes = proposals[bi, top]
+        hw = torch.tensor(image_sizes, dtype=torch.float32, device=dev)  # (h, w) per image
+        x = torch.minimum(boxes[..., 0::2].clamp(min=0), hw[:, 1, None, None])
+        y = torch.minimum(boxes[..., 1::2].clamp(min=0), hw[:, 0, None, None])
+        boxes = torch.stack((x[..., 0], y[..., 0], x[..., 1], y[..., 1]), dim=-1)
+        ws, hs = boxes[..., 2] - boxes[..., 0], boxes[..., 3] - boxes[..., 1]
+        keep = (ws >= self.min_size) & (hs >= self.min_size) & (prob >= self.score_thresh)
+        img = bi.expand_as(lvl)
+        kb, ks, kl, ki = boxes[keep], prob[keep], lvl[keep], img[keep]
+        counts = keep.sum(1).tolist()
+        nl = len(num_per_level)
+        post = self.post_nms_top_n()
+        if min(counts) * 4 > 4000:  # CPU batched_nms rule per image -> per-level ("vanilla") path
+            kk = be.batched_nms(kb, ks, ki * nl + kl, self.nms_thresh, group=ki, max_seg=pre, mode=1)
+            per = torch.bincount(ki[kk], minlength=N).tolist()
+            outs = torch.split(kk, per)
+        else:
+            outs, start = [], 0
+            for c in counts:
+                sl = slice(start, start + c)
+                k = be.batched_nms(kb[sl], ks[sl], kl[sl], self.nms_thresh, max_seg=pre)
+                outs.append(k + start)
+                start += c
+        final_boxes, final_scores = [], []
+        for k in outs:
+            k = k[:post]
+            final_boxes.append(kb[k])
+            final_scores.append(ks[k])
+        return final_boxes, final_scores
+
+    def forward(self, images, features, targets=None, be=None):
+        feats = list(features.values())
+        logits, deltas = self.head(feats, be)
+        grid = [(f.shape[1], f.shape[2]) for f in feats]
+        anchors = self.anchor_generator(images.tensors.shape[1:3], grid, feats[0].device, be)
+        N = feats[0].shape[0]
+        num_per_level = [l.shape[1] for l in logits]
+        objectness = torch.cat(logits, 1)                 # [N, A]
+        pred_deltas = torch.cat(deltas, 1)                # [N, A, 4]
+        A = anchors.shape[0]
+        proposals = be.box_decode(pred_deltas.detach().reshape(-1, 4), anchors.repeat(N, 1), RPN_WEIGHTS)
+        proposals = proposals.view(N, A, 4)
+        boxes, scores = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
+        losses = {}
+        if self.training:
+            labels, reg_targets = [], []
+            for t in targets:
+                _, lab, tg = be.match_assign(t["boxes"], anchors, self.fg, self.bg, True, mode=1,
+                                             weights=RPN_WEIGHTS)
+                labels.append(lab)
+                reg_targets.append(tg)
+            pos_m, neg_m = self.fg_bg_sampler(labels)
+            pos = torch.where(torch.cat(pos_m))[0]
+            neg = torch.where(torch.cat(neg_m))[0]
+            sampled = torch.cat([pos, neg])
+            ob = objectness.flatten()
+            lab = torch.cat(labels)
+            rt = torch.cat(reg_targets)
+            pd = pred_deltas.reshape(-1, 4)
+            box_loss = _smooth_l1_sum(pd[pos], rt[pos], 1.0 / 9) / sampled.numel()
+            obj_loss = F.binary_cross_entropy_with_logits(ob[sampled], lab[sampled])
+            losses = {"loss_objectness": obj_loss, "loss_rpn_box_reg": box_loss}
+        return boxes, losses
+
+
+# ------------------------------------------------------------------------------------------ RoI heads
+class Linear(nn.Module):
+    """nn.Linear-compatible parameters (weight [out, in], bias); runs as a 1x1 MFMA conv."""
+
+    def __init__(self, in_features, out_features, bias=True):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features))
+        self.bias = nn.Parameter(torch.empty(out_features)) if bias else None
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if self.bias is not None:
+            bound = 1 / math.sqrt(in_features)
+            nn.init.uniform_(self.bias, -bound, bound)
+
+
+class FastRCNNPredictor(nn.Module):
+    """torchvision FastRCNNPredictor(in_channels, num_classes): cls_score + bbox_pred, fused in one
+    MFMA GEMM (N = num_classes*5) with f32 output."""
+
+    def __init__(self, in_channels, num_classes):
+        super().__init__()
+        self.cls_score = Linear(in_channels, num_classes)
+        self.bbox_pred = Linear(in_channels, num_classes * 4)
+
+    def forward(self, x, be):
+        nc = self.cls_score.out_features
+        w = torch.cat([self.cls_score.weight, self.bbox_pred.weight])[:, :, None, None]
+        b = torch.cat([self.cls_score.bias, self.bbox_pred.bias])
+        o = be.conv(x, w, b, (1, 1), (0, 0), ACT_NONE, out_dtype=torch.float32).reshape(x.shape[0], -1)
+        return o[:, :nc], o[:, nc:]
+
+
+class FastRCNNConvFCHead(nn.Sequential):
+    """FastRCNNConvFCHead((256,7,7), [256]*4, [1024], norm_layer=BatchNorm2d). FC6 runs as a valid 7x7
+    conv over the NHWC RoI tile, which is exactly torch's NCHW flatten + Linear."""
+
+    def __init__(self, in_channels=256, conv_layers=(256, 256, 256, 256), fc_layers=(1024,), hw=7):
+        blocks, prev = [], in_channels
+        for c in conv_layers:
+            blocks.append(ConvNormAct(prev, c, 3, act=ACT_RELU))
+            prev = c
+        blocks.append(nn.Flatten())
+        prev = prev * hw * hw
+        for c in fc_layers:
+            blocks.append(Linear(prev, c))
+            blocks.append(nn.ReLU(inplace=True))
+            prev = c
+        super().__init__(*blocks)
+        self.hw = hw
+        for m in self.modules():
+            if isinstance(m, Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+                if m.bias is not None:
+                    nn.init.zeros_(m.bias)
+
+    def forward(self, x, be):
+        first = True
+        for m in self:
+            if isinstance(m, ConvNormAct):
+                x = m(x, be)
+            elif isinstance(m, Linear):
+                C = x.shape[3]
+                kh = x.shape[1] if first else 1
+                w = m.weight.view(m.out_features, C, kh, kh)
+                x = be.conv(x, w, m.bias, (1, 1), (0, 0), ACT_RELU)  # Linear + ReLU
+                first = False
+        return x  # [R, 1, 1, 1024]
+
+
+class RoIHeads(nn.Module):
+    def __init__(self, box_head, box_predictor, fg_iou_thresh=0.5, bg_iou_thresh=0.5, batch_size_per_image=512,
+                 positive_fraction=0.25, score_thresh=0.05, nms_thresh=0.5, detections_per_img=100):
+        super().__init__()
+        self.box_head = box_head
+        self.box_predictor = box_predictor
+        self.fg, self.bg = fg_iou_thresh, bg_iou_thresh
+        self.fg_bg_sampler = BalancedPositiveNegativeSampler(batch_size_per_image, positive_fraction)
+        self.score_thresh, self.nms_thresh, self.detections_per_img = score_thresh, nms_thresh, detections_per_img
+        self.featmap_names = ["0", "1", "2", "3"]
+
+    def _scales(self, feats, image_sizes):
+        # MultiScaleRoIAlign._setup_scales / _infer_scale (height-based), LevelMapper k_min/k_max
+        max_h = max(s[0] for s in image_sizes)
+        scales = [2.0 ** round(math.log2(float(f.shape[1]) / float(max_h))) for f in feats]
+        return scales, int(-math.log2(scales[0]))
+
+    def forward(self, features, proposals, image_sizes, targets=None, be=None):
+        feats = [features[k] for k in self.featmap_names]
+        dev = feats[0].device
+        if self.training:
+            props, labels, tgts = [], [], []
+            for p, t in zip(proposals, targets):
+                gt = t["boxes"].float()
+                pg = torch.cat([p, gt])
+                _, lab, tg = be.match_assign(gt, pg, self.fg, self.bg, False, mode=2, gt_labels=t["labels"],
+                                             weights=ROI_WEIGHTS)
+                props.append(pg)
+                labels.append(lab)
+                tgts.append(tg)
+            pos_m, neg_m = self.fg_bg_sampler(labels)
+            for i in range(len(props)):
+                s = torch.where(pos_m[i] | neg_m[i])[0]
+                props[i], labels[i], tgts[i] = props[i][s], labels[i][s], tgts[i][s]
+            proposals = props
+        rois = torch.cat([torch.cat([torch.full((p.shape[0], 1), float(i), device=dev), p], 1)
+                          for i, p in enumerate(proposals)])
+        scales, k_min = self._scales(feats, image_sizes)
+        x = be.multiscale_roi_align(feats, rois, scales, k_min)
+        x = self.box_head(x, be)
+        class_logits, box_regression = self.box_predictor(x, be)
+        if self.training:
+            lab = torch.cat(labels)
+            rt = torch.cat(tgts)
+            loss_cls = F.cross_entropy(class_logits, lab)
+            pos = torch.where(lab > 0)[0]
+            R = class_logits.shape[0]
+            reg = box_regression.reshape(R, -1, 4)
+            loss_box = _smooth_l1_sum(reg[pos, lab[pos]], rt[pos], 1.0 / 9) / lab.numel()
+            return [], {"loss_classifier": loss_cls, "loss_box_reg": loss_box}
+        return self.postprocess_detections(class_logits, box_regression, proposals, image_sizes, be), {}
+
+    def postprocess_detections(self, class_logits, box_regression, proposals, image_sizes, be):
+        dev = class_logits.device
+        nc = class_logits.shape[-1]
+        per = [p.shape[0] for p in proposals]
+        pred = be.box_decode(box_regression, torch.cat(proposals), ROI_WEIGHTS).reshape(-1, nc, 4)
+        scores = F.softmax(class_logits, -1)
+        out = []
+        for boxes, sc, hw in zip(pred.split(per), scores.split(per), image_sizes):
+            h, w = float(hw[0]), float(hw[1])
+            boxes = torch.stack((boxes[..., 0].clamp(0, w), boxes[..., 1].clamp(0, h),
+                                 boxes[..., 2].clamp(0, w), boxes[..., 3].clamp(0, h)), -1)
+            labels = torch.arange(nc, device=dev).view(1, -1).expand_as(sc)
+            boxes, sc, labels = boxes[:, 1:].reshape(-1, 4), sc[:, 1:].reshape(-1), labels[:, 1:].reshape(-1)
+            k = torch.where(sc > self.score_thresh)[0]
+            boxes, sc, labels = boxes[k], sc[k], labels[k]
+            ws, hs = boxes[:, 2] - boxes[:, 0], boxes[:, 3] - boxes[:, 1]
+            k = torch.where((ws >= 1e-2) & (hs >= 1e-2))[0]
+            boxes, sc, labels = boxes[k], sc[k], labels[k]
+            k = be.batched_nms(boxes, sc, labels, self.nms_thresh, max_seg=max(per) if per else None)
+            k = k[: self.detections_per_img]
+            out.append({"boxes": boxes[k], "labels": labels[k], "scores": sc[k]})
+        return out
+
+
+# ------------------------------------------------------------------------------------------ transform
+class ImageList:
+    def __init__(self, tensors, image_sizes):
+        self.tensors, self.image_sizes = tensors, image_sizes
+
+
+class GeneralizedRCNNTransform(nn.Module):
+    """normalize -> resize (min 800 / max 1333, bilinear) -> zero-pad to /32, NHWC output with the stem's
+    8 channels. uint8 [B,H,W,3] device batches that need no resize take the fused HIP kernel."""
+
+    def __init__(self, min_size=800, max_size=1333, image_mean=(0.485, 0.456, 0.406),
+                 image_std=(0.229, 0.224, 0.225), size_divisible=32):
+        super().__init__()
+        self.min_size, self.max_size = min_size, max_size
+        self.image_mean, self.image_std = image_mean, image_std
+        self.size_divisible = size_divisible
+
+    def _scale(self, h, w):
+        return min(self.min_size / min(h, w), self.max_size / max(h, w))
+
+    def _padded(self, sizes):
+        sd = self.size_divisible
+        H = max(s[0] for s in sizes)
+        W = max(s[1] for s in sizes)
+        return int(math.ceil(H / sd) * sd), int(math.ceil(W / sd) * sd)
+
+    def forward(self, images, targets, be):
+        if isinstance(images, torch.Tensor) and images.dtype == torch.uint8 and images.dim() == 4:
+            B, H, W, _ = images.shape
+            if self._scale(H, W) == 1.0:
+                sizes = [(H, W)] * B
+                return ImageList(be.normalize_pad_u8(images, self._padded(sizes)), sizes), targets
+            images = [im.permute(2, 0, 1).float().div(255) for im in images]
+        dev = images[0].device
+        mean = torch.tensor(self.image_mean, dtype=torch.float32, device=dev)[:, None, None]
+        std = torch.tensor(self.image_std, dtype=torch.float32, device=dev)[:, None, None]
+        out, sizes, new_targets = [], [], []
+        for i, im in enumerate(images):
+            im = (im - mean) / std
+            h, w = im.shape[-2:]
+            s = self._scale(h, w)
+            if s != 1.0:
+                im = F.interpolate(im[None], size=None, scale_factor=s, mode="bilinear",
+                                   recompute_scale_factor=True, align_corners=False)[0]
+            nh, nw = im.shape[-2:]
+            if targets is not None:
+                t = dict(targets[i])
+                if (nh, nw) != (h, w):
+                    rh = torch.tensor(nh, dtype=torch.float32) / torch.tensor(h, dtype=torch.float32)
+                    rw = torch.tensor(nw, dtype=torch.float32) / torch.tensor(w, dtype=torch.float32)
+                    b = t["boxes"]
+                    t["boxes"] = torch.stack((b[:, 0] * rw.to(b.device), b[:, 1] * rh.to(b.device),
+                                              b[:, 2] * rw.to(b.device), b[:, 3] * rh.to(b.device)), 1)
+                new_targets.append(t)
+            out.append(im)
+            sizes.append((int(nh), int(nw)))
+        Hp, Wp = self._padded(sizes)
+        batch = torch.zeros((len(out), Hp, Wp, be.stem_channels), dtype=be.act_dtype, device=dev)
+        for i, im in enumerate(out):
+            batch[i, : im.shape[1], : im.shape[2], :3] = im.permute(1, 2, 0).to(be.act_dtype)
+        return ImageList(batch, sizes), (new_targets if targets is not None else None)
+
+    def postprocess(self, result, image_sizes, original_sizes):
+        for i, (pred, s, o) in enumerate(zip(result, image_sizes, original_sizes)):
+            if tuple(s) == tuple(o):
+                continue
+            rh = torch.tensor(o[0], dtype=torch.float32) / torch.tensor(s[0], dtype=torch.float32)
+            rw = torch.tensor(o[1], dtype=torch.float32) / torch.tensor(s[1], dtype=torch.float32)
+            b = pred["boxes"]
+            pred["boxes"] = torch.stack((b[:, 0] * rw.to(b.device), b[:, 1] * rh.to(b.device),
+                                         b[:, 2] * rw.to(b.device), b[:, 3] * rh.to(b.device)), 1)
+        return result
+
+
+# ------------------------------------------------------------------------------------------ model
+class FasterRCNN(nn.Module):
+    def __init__(self, backbone, num_classes=91, rpn_head=None, box_head=None, **kw):
+        super().__init__()
+        self.transform = GeneralizedRCNNTransform()
+        self.backbone = backbone
+        ag = AnchorGenerator()
+        self.rpn = RegionProposalNetwork(ag, rpn_head or RPNHead(backbone.out_channels,
+                                                                 ag.num_anchors_per_location()[0]))
+        box_head = box_head or FastRCNNConvFCHead()
+        self.roi_heads = RoIHeads(box_head, FastRCNNPredictor(1024, num_classes))
+        self._be = kw.get("backend")
+
+    @property
+    def be(self):
+        return _be(self)
+
+    def set_backend(self, be):
+        self._be = be
+        return self
+
+    def forward(self, images, targets=None):
+        be = self.be
+        if self.training:
+            if targets is None:
+                raise ValueError("In training mode, targets should be passed")
+            for t in targets:
+                b = t["boxes"]
+                if not (isinstance(b, torch.Tensor) and b.dim() == 2 and b.shape[-1] == 4):
+                    raise ValueError(f"Expected target boxes to be a tensor of shape [N, 4], got {b.shape}.")
+                if b.numel() and bool(((b[:, 2:] <= b[:, :2]).any())):
+                    raise ValueError("All bounding boxes should have positive height and width.")
+        if isinstance(images, torch.Tensor) and images.dim() == 4 and images.dtype == torch.uint8:
+            original = [(images.shape[1], images.shape[2])] * images.shape[0]
+        else:
+            original = [(int(im.shape[-2]), int(im.shape[-1])) for im in images]
+        il, targets = self.transform(images, targets, be)
+        features = self.backbone(il.tensors, be)
+        proposals, rpn_losses = self.rpn(il, features, targets, be)
+        detections, det_losses = self.roi_heads(features, proposals, il.image_sizes, targets, be)
+        if self.training:
+            losses = {}
+            losses.update(det_losses)
+            losses.update(rpn_losses)
+            return losses
+        return self.transform.postprocess(detections, il.image_sizes, original)
+
+
+def fasterrcnn_resnet50_fpn_v2(weights=None, progress=True, num_classes=None, weights_backbone=None,
+                               trainable_backbone_layers=None, **kwargs):
+    """torchvision.models.detection.fasterrcnn_resnet50_fpn_v2 signature.
+
+    weights: None, or a path / state_dict of a reference checkpoint (there is no network: the
+    reference's weights="DEFAULT" download is replaced by a local file). Trainable layers follow
+    torchvision's rule (5 without weights, else 3 by default)."""
+    is_trained = weights is not None or weights_backbone is not None
+    if not is_trained:
+        trainable = 5
+    else:
+        trainable = 3 if trainable_backbone_layers is None else trainable_backbone_layers
+    if kwargs.pop("force_trainable_layers", None) is not None:
+        trainable = trainable_backbone_layers
+    nc = num_classes if num_classes is not None else 91
+    model = FasterRCNN(BackboneWithFPN(trainable), num_classes=nc, **kwargs)
+    if weights is not None:
+        sd = weights if isinstance(weights, dict) else torch.load(weights, map_location="cpu", weights_only=True)
+        sd = sd.get("model", sd)
+        model.load_state_dict(sd)
+    return model

@@ -1,0 +1,119 @@
+"""End-to-end Faster R-CNN on the HIP backend: the reference's train/eval contract on MI355X, and
+agreement with the CPU restatement backend on the same weights (eval)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(dev, trainable=3):
+    from mx_det import frcnn
+    m = frcnn.fasterrcnn_resnet50_fpn_v2(weights=None)
+    m.roi_heads.box_predictor = frcnn.FastRCNNPredictor(m.roi_heads.box_predictor.cls_score.in_features, 7)
+    frcnn.set_trainable_layers(m.backbone.body, trainable)
+    return m.to(dev)
+
+
+def test_train_steps_hip(dev):
+    from mx_det.data import synth_batch
+    torch.manual_seed(0)
+    m = _model(dev).train()
+    opt = torch.optim.SGD([p for p in m.parameters() if p.requires_grad], lr=0.005, momentum=0.9, weight_decay=5e-4)
+    imgs, tg = synth_batch(0, 2, H=320, W=480, device=dev)
+    first = None
+    for _ in range(3):
+        ld = m(imgs, tg)
+        assert list(ld) == ["loss_classifier", "loss_box_reg", "loss_objectness", "loss_rpn_box_reg"]
+        loss = sum(ld.values())
+        assert torch.isfinite(loss)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        for n, p in m.named_parameters():
+            if p.requires_grad:
+                assert p.grad is not None and torch.isfinite(p.grad).all(), n
+        opt.step()
+        first = first or float(loss)
+    # float image-list input (the reference DataLoader's ToDtype(float32, scale=True) tensors)
+    ld = m([im.permute(2, 0, 1).float() / 255 for im in imgs], tg)
+    assert torch.isfinite(sum(ld.values()))
+
+
+def test_full_size_step_and_eval(dev):
+    from mx_det.data import synth_batch
+    torch.manual_seed(1)
+    m = _model(dev).train()
+    imgs, tg = synth_batch(0, 2, device=dev)
+    loss = sum(m(imgs, tg).values())
+    loss.backward()
+    assert torch.isfinite(loss)
+    m.eval()
+    with torch.no_grad():
+        out = m(imgs[:1])
+    assert len(out) == 1 and out[0]["boxes"].shape[0] <= 100
+
+
+def test_features_match_cpu_backend(dev):
+    """Backbone + FPN (train-mode BN) on the same weights and image: HIP bf16 vs the CPU fp32
+    restatement, relative L2 error per pyramid level within bf16 accumulation noise."""
+    from mx_det.data import synth_batch
+    from oracle.cpu_backend import CpuBackend
+    torch.manual_seed(2)
+    m = _model(dev, trainable=5).train()
+    mc = _model("cpu", trainable=5).train().set_backend(CpuBackend())
+    mc.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    imgs, _ = synth_batch(5, 2, H=256, W=384, device=dev)
+    with torch.no_grad():
+        il, _ = m.transform(imgs, None, m.be)
+        ilc, _ = mc.transform(imgs.cpu(), None, mc.be)
+        fg = m.backbone(il.tensors, m.be)
+        fc = mc.backbone(ilc.tensors, mc.be)
+    for k in fc:
+        a, b = fg[k].float().cpu(), fc[k]
+        rel = ((a - b).norm() / b.norm()).item()
+        assert rel < 3e-2, (k, rel)
+
+
+def test_postprocess_matches_cpu_backend(dev):
+    """RoIHeads.postprocess_detections (decode, clip, score filter, remove_small, batched_nms by label,
+    top-100) on identical logits/regressions/proposals: same detections as the CPU restatement."""
+    from oracle.cpu_backend import CpuBackend
+    from mx_det.backend import default_backend
+    g = torch.Generator().manual_seed(3)
+    m = _model("cpu")
+    R = 1000
+    ctr = torch.rand(R, 2, generator=g) * torch.tensor([1333., 800.])
+    wh = torch.rand(R, 2, generator=g) * 120 + 4
+    props = torch.cat([ctr - wh / 2, ctr + wh / 2], 1)
+    logits = torch.randn(R, 7, generator=g) * 2
+    reg = torch.randn(R, 28, generator=g) * 0.5
+    sizes = [(800, 1333)]
+    ref = m.roi_heads.postprocess_detections(logits, reg, [props], sizes, CpuBackend())[0]
+    got = m.roi_heads.postprocess_detections(logits.to(dev), reg.to(dev), [props.to(dev)], sizes,
+                                             default_backend())[0]
+    assert torch.equal(got["labels"].cpu(), ref["labels"])
+    torch.testing.assert_close(got["scores"].cpu(), ref["scores"], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(got["boxes"].cpu(), ref["boxes"], rtol=1e-5, atol=1e-3)
+
+
+def test_filter_proposals_matches_cpu_backend(dev):
+    """RPN filter_proposals (per-level top-k, sigmoid, clip, remove_small, per-level NMS, top-2000)
+    on identical decoded proposals and logits: identical proposal sets as the CPU restatement."""
+    from oracle.cpu_backend import CpuBackend
+    from mx_det.backend import default_backend
+    g = torch.Generator().manual_seed(4)
+    m = _model("cpu").train()
+    levels = [200 * 336 * 3, 100 * 168 * 3, 50 * 84 * 3, 25 * 42 * 3, 13 * 21 * 3]
+    A = sum(levels)
+    ctr = torch.rand(2, A, 2, generator=g) * torch.tensor([1400., 860.]) - 30
+    wh = torch.rand(2, A, 2, generator=g) * 200 + 0.0005
+    props = torch.cat([ctr - wh / 2, ctr + wh / 2], -1)
+    # well-separated logits (spacing >> one ulp of sigmoid), so host/device sigmoid ulp differences
+    # cannot reorder scores
+    obj = (torch.stack([torch.randperm(A, generator=g), torch.randperm(A, generator=g)]).float() / A) * 8 - 4
+    sizes = [(800, 1333), (800, 1200)]
+    rb, rs = m.rpn.filter_proposals(props, obj, sizes, levels, CpuBackend())
+    gb, gs = m.rpn.filter_proposals(props.to(dev), obj.to(dev), sizes, levels, default_backend())
+    for a, b, c, d in zip(gb, rb, gs, rs):
+        assert a.shape == b.shape
+        assert torch.equal(a.cpu(), b)
+        torch.testing.assert_close(c.cpu(), d, rtol=1e-6, atol=1e-7)  # sigmoid: device vs host libm ulp

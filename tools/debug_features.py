@@ -1,0 +1,32 @@
+"""Layer-by-layer HIP vs CPU-restatement comparison of the backbone (debug aid)."""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "robust-object-detection_amd")]
+import torch
+from mx_det import frcnn
+from mx_det.conv import ACT_RELU
+from mx_det.data import synth_batch
+from oracle.cpu_backend import CpuBackend
+
+dev = torch.device("cuda")
+torch.manual_seed(2)
+m = frcnn.fasterrcnn_resnet50_fpn_v2(weights=None).to(dev).train()
+mc = frcnn.fasterrcnn_resnet50_fpn_v2(weights=None).train().set_backend(CpuBackend())
+mc.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+imgs, _ = synth_batch(5, 2, H=800, W=1333, device=dev)
+def rel(a, b):
+    a = a.float().cpu(); return ((a - b).norm() / b.norm()).item()
+with torch.no_grad():
+    il, _ = m.transform(imgs, None, m.be)
+    ilc, _ = mc.transform(imgs.cpu(), None, mc.be)
+    print("input", rel(il.tensors[..., :3], ilc.tensors))
+    bg, bc = m.backbone.body, mc.backbone.body
+    x = m.be.conv_bn(il.tensors, bg.conv1, bg.bn1, ACT_RELU)
+    xc = mc.be.conv_bn(ilc.tensors, bc.conv1, bc.bn1, ACT_RELU)
+    print("stem", rel(x, xc))
+    x = m.be.maxpool(x, 3, 2, 1); xc = mc.be.maxpool(xc, 3, 2, 1)
+    print("pool", rel(x, xc))
+    for name in ("layer1", "layer2", "layer3", "layer4"):
+        for i, (b1, b2) in enumerate(zip(getattr(bg, name), getattr(bc, name))):
+            x = b1(x, m.be); xc = b2(xc, mc.be)
+            print(name, i, rel(x, xc), x.float().abs().mean().item(), xc.abs().mean().item())
