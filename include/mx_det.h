@@ -185,6 +185,20 @@ int mx_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, in
                     uint16_t* dx, uint16_t* dres /*nullable: grad of residual = masked dy*/,
                     mx_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Restoration pre-pass on device (scripts/restore_testsets.py:53-79, restoration_net.py:44-106).
+ *   reflect_pad_u8: cv2.copyMakeBorder(0, Hp-H, 0, Wp-W, BORDER_REFLECT), uint8 [B,H,W,C] -> [B,Hp,Wp,C]
+ *   up_concat: ConvTranspose2d(2, s2) output held as [N,H,W,4*Cu] (channel = (i, j, co)) scattered to
+ *              [N,2H,2W,Cu] and concatenated with skip [N,2H,2W,Cs] along channels (torch.cat dim=1)
+ *   restore_finish: clamp(u8/255 + residual, 0, 1) * 255 -> clip -> truncate to uint8, cropped to H x W
+ * ------------------------------------------------------------------------------------------- */
+int mx_reflect_pad_u8(const uint8_t* src, int64_t B, int64_t H, int64_t W, int64_t C, int64_t Hp, int64_t Wp,
+                      uint8_t* dst, mx_stream_t stream);
+int mx_up_concat(const uint16_t* up, const uint16_t* skip, int64_t N, int64_t H, int64_t W, int64_t Cu, int64_t Cs,
+                 uint16_t* out, mx_stream_t stream);
+int mx_restore_finish(const uint8_t* img_padded, int64_t B, int64_t Hp, int64_t Wp, const float* residual, int64_t H,
+                      int64_t W, uint8_t* out, mx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,139 @@
+"""Restoration U-Net (scripts/restoration_net.py) on the libmx_det HIP kernels, forward (eval) path.
+
+Same module tree and state_dict keys as the reference (down1.conv.block.{0,1,3,4}.*, up4.up.*,
+out_conv.*; 118 entries incl. BN buffers), so experiments/restoration/best.pth loads unchanged.
+Eval forward, NHWC bf16 activations:
+  ConvBlock  = 2 x [conv3x3 with eval-BN folded into weights+bias, LeakyReLU(0.2) fused in the epilogue]
+  MaxPool2d(2), ConvTranspose2d(2, s2) as a 1x1 MFMA conv to 4*Cout channels + fused pixel-shuffle/concat,
+  out_conv 1x1 (f32 out) + clamp(x + residual, 0, 1).
+restore_u8() is restore_testsets.py:53-79 on device: reflect-pad to /16, /255, U-Net, *255, clip,
+truncate, crop — uint8 in, uint8 out, no host round trip.
+"""
+import ctypes
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import conv as mc
+from . import ops
+from ._lib import call
+
+
+def _s():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class ConvBlock(nn.Module):
+    def __init__(self, in_ch, out_ch):
+        super().__init__()
+        self.block = nn.Sequential(
+            nn.Conv2d(in_ch, out_ch, 3, padding=1, bias=False), nn.BatchNorm2d(out_ch), nn.LeakyReLU(0.2, inplace=True),
+            nn.Conv2d(out_ch, out_ch, 3, padding=1, bias=False), nn.BatchNorm2d(out_ch), nn.LeakyReLU(0.2, inplace=True))
+
+    def forward(self, x):
+        for ci, bi in ((0, 1), (3, 4)):
+            c, b = self.block[ci], self.block[bi]
+            w, bias = mc.fold_bn(c, b)
+            x = mc.conv_fwd(x, mc.weight_krsc(w, x.shape[3]), c.stride, c.padding, bias=bias, act=mc.ACT_LEAKY)
+        return x
+
+
+def _maxpool2(x):
+    N, H, W, C = x.shape
+    y = torch.empty((N, H // 2, W // 2, C), dtype=x.dtype, device=x.device)
+    call("mx_maxpool_fwd", _p(x.contiguous()), N, H, W, C, 2, 2, 0, _p(y), None, _s())
+    return y
+
+
+class DownBlock(nn.Module):
+    def __init__(self, in_ch, out_ch):
+        super().__init__()
+        self.conv = ConvBlock(in_ch, out_ch)
+        self.pool = nn.MaxPool2d(2)
+
+    def forward(self, x):
+        feat = self.conv(x)
+        return _maxpool2(feat), feat
+
+
+class UpBlock(nn.Module):
+    def __init__(self, in_ch, skip_ch, out_ch):
+        super().__init__()
+        self.up = nn.ConvTranspose2d(in_ch, in_ch, 2, stride=2)
+        self.conv = ConvBlock(in_ch + skip_ch, out_ch)
+
+    def forward(self, x, skip):
+        N, H, W, C = x.shape
+        wt = self.up.weight.detach()                     # [Cin, Cout, 2, 2]
+        Cout = wt.shape[1]
+        w1 = wt.permute(2, 3, 1, 0).reshape(4 * Cout, C, 1, 1)  # output channel = (i, j, co)
+        b1 = self.up.bias.detach().repeat(4).float().contiguous()
+        u = mc.conv_fwd(x, mc.weight_krsc(w1), (1, 1), (0, 0), bias=b1)   # [N, H, W, 4*Cout]
+        if (2 * H, 2 * W) == (skip.shape[1], skip.shape[2]):
+            cat = torch.empty((N, 2 * H, 2 * W, Cout + skip.shape[3]), dtype=x.dtype, device=x.device)
+            call("mx_up_concat", _p(u), _p(skip.contiguous()), N, H, W, Cout, skip.shape[3], _p(cat), _s())
+        else:
+            # odd spatial size (restoration_net.py:53-55): bilinear fix-up of the upsampled map
+            up = u.view(N, H, W, 2, 2, Cout).permute(0, 1, 3, 2, 4, 5).reshape(N, 2 * H, 2 * W, Cout)
+            up = F.interpolate(up.permute(0, 3, 1, 2).float(), size=tuple(skip.shape[1:3]), mode="bilinear",
+                               align_corners=False).permute(0, 2, 3, 1).to(x.dtype)
+            cat = torch.cat([up, skip], dim=3).contiguous()
+        return self.conv(cat)
+
+
+class RestorationUNet(nn.Module):
+    def __init__(self, channels=(32, 64, 128, 256)):
+        super().__init__()
+        c1, c2, c3, c4 = channels
+        self.down1 = DownBlock(3, c1)
+        self.down2 = DownBlock(c1, c2)
+        self.down3 = DownBlock(c2, c3)
+        self.down4 = DownBlock(c3, c4)
+        self.bottleneck = ConvBlock(c4, c4)
+        self.up4 = UpBlock(c4, c4, c3)
+        self.up3 = UpBlock(c3, c3, c2)
+        self.up2 = UpBlock(c2, c2, c1)
+        self.up1 = UpBlock(c1, c1, c1)
+        self.out_conv = nn.Conv2d(c1, 3, 1)
+
+    def residual_nhwc(self, x8):
+        """x8: NHWC bf16 [N,H,W,8] (image in [0,1] in channels 0..2) -> residual f32 [N,H,W,3]."""
+        d1, s1 = self.down1(x8)
+        d2, s2 = self.down2(d1)
+        d3, s3 = self.down3(d2)
+        d4, s4 = self.down4(d3)
+        b = self.bottleneck(d4)
+        u = self.up1(self.up2(self.up3(self.up4(b, s4), s3), s2), s1)
+        oc = self.out_conv
+        return mc.conv_fwd(u, mc.weight_krsc(oc.weight.detach()), (1, 1), (0, 0), bias=oc.bias.detach().float(),
+                           out_dtype=torch.float32)
+
+    @torch.no_grad()
+    def forward(self, x):
+        """Reference contract: x [N,3,H,W] f32 in [0,1] -> clamp(x + residual, 0, 1) [N,3,H,W] f32."""
+        x8 = F.pad(x.permute(0, 2, 3, 1), (0, 5)).to(torch.bfloat16).contiguous()
+        r = self.residual_nhwc(x8)
+        return torch.clamp(x + r.permute(0, 3, 1, 2), 0.0, 1.0)
+
+    @torch.no_grad()
+    def restore_u8(self, img_u8):
+        """restore_testsets.py:53-79 on device. img_u8 [B,H,W,3] uint8 (RGB) -> restored uint8 [B,H,W,3]."""
+        B, H, W, _ = img_u8.shape
+        ph, pw = (16 - H % 16) % 16, (16 - W % 16) % 16
+        Hp, Wp = H + ph, W + pw
+        src = img_u8.contiguous()
+        if ph or pw:
+            pad = torch.empty((B, Hp, Wp, 3), dtype=torch.uint8, device=img_u8.device)
+            call("mx_reflect_pad_u8", _p(src), B, H, W, 3, Hp, Wp, _p(pad), _s())
+            src = pad
+        x8 = ops.normalize_pad(src, (Hp, Wp), channels=8, dtype=torch.bfloat16, mean=(0.0, 0.0, 0.0),
+                               std=(1.0, 1.0, 1.0))
+        r = self.residual_nhwc(x8)
+        out = torch.empty((B, H, W, 3), dtype=torch.uint8, device=img_u8.device)
+        call("mx_restore_finish", _p(src), B, Hp, Wp, _p(r), H, W, _p(out), _s())
+        return out

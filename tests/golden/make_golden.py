@@ -6,7 +6,7 @@ Run here (the container that holds /root/reference), never on the GPU box:
 
 What is pinned, and by which reference code:
   * unet_small.npz   - scripts/restoration_net.py:60-106 RestorationUNet forward (eval mode) with
-                       channels (4,8,16,32), seeded weights and randomised BN running stats/affine,
+                       channels (8,16,32,64), seeded weights and randomised BN running stats/affine,
                        on [1,3,48,64] and on odd [1,3,50,66] (exercises the bilinear fix-up :53-55).
   * unet_keys.json   - state_dict key -> shape list of the full-size RestorationUNet(32,64,128,256)
                        and its parameter count (restoration_net.py:60-86).
@@ -78,7 +78,7 @@ def make_unet():
         json.dump({"n_params": nparam, "state_dict": keys}, f, indent=0)
 
     torch.manual_seed(1234)
-    m = RestorationUNet(channels=(4, 8, 16, 32))
+    m = RestorationUNet(channels=(8, 16, 32, 64))
     g = torch.Generator().manual_seed(99)
     with torch.no_grad():
         for name, mod in m.named_modules():

@@ -28,5 +28,7 @@ with torch.no_grad():
     print("pool", rel(x, xc))
     for name in ("layer1", "layer2", "layer3", "layer4"):
         for i, (b1, b2) in enumerate(zip(getattr(bg, name), getattr(bc, name))):
+            xin = x
             x = b1(x, m.be); xc = b2(xc, mc.be)
-            print(name, i, rel(x, xc), x.float().abs().mean().item(), xc.abs().mean().item())
+            one = b2(xin.float().cpu(), mc.be)  # same input on both backends: single-block error
+            print(name, i, "accum", rel(x, xc), "single", rel(x, one))
