@@ -1,0 +1,256 @@
+"""Training / evaluation runners behind the drop-in scripts (scripts/train_frcnn_*.py, eval_*.py).
+
+Behaviour follows the reference entry points:
+  train: scripts/train_frcnn_baseline.py:110-223 / train_frcnn_augmented.py:120-216 — SGD(lr, momentum,
+    weight_decay) over trainable params, StepLR(8, 0.1) per epoch, loss = sum(loss_dict.values()),
+    epoch_loss += loss.item(); history.jsonl records {epoch, train_loss_sum, lr, mAP50, mAP50_95,
+    elapsed_sec}; last.pth {"model", "epoch"} every epoch; final COCOeval on the val split; best.pth
+    {"model", "epoch": "final", "metrics"}; a final history record with epoch "final".
+  eval: scripts/eval_all.py:97-156 — bs=1 inference, xyxy -> xywh result dicts, COCOeval bbox,
+    stats[0]/[1], per-class AP50 from precision[0, :, k, 0, 2].
+MI355X-side differences: images stay uint8 until the device (ToImage/ToDtype scaling, corruption and
+normalisation run as HIP kernels); with WORLD_SIZE > 1 (torchrun) every rank trains on its shard of
+each epoch's permutation (DistributedSampler) with RCCL gradient all-reduce, and evaluation shards
+images by rank and gathers detections to rank 0.
+"""
+import json
+import os
+import random
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+from torch.utils.data import DataLoader, DistributedSampler
+
+from . import frcnn
+from .coco import get_coco_api
+
+
+def set_seed(seed):
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    torch.cuda.manual_seed_all(seed)
+
+
+def dist_info():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def init_device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("mx_det runs its hot path on MI355X (HIP); no GPU is visible")
+    world, rank, local = dist_info()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group("nccl", device_id=dev)
+    return dev, world, rank
+
+
+def build_frcnn(num_classes=7, weights=None, trainable_backbone_layers=None):
+    """fasterrcnn_resnet50_fpn_v2(weights) + FastRCNNPredictor(in_features, num_classes)
+    (train_frcnn_baseline.py:139-143). weights: None or a local state_dict / checkpoint path
+    (stand-in for the reference's COCO "DEFAULT" download, unavailable offline)."""
+    model = frcnn.fasterrcnn_resnet50_fpn_v2(weights=None)
+    in_features = model.roi_heads.box_predictor.cls_score.in_features
+    if weights is not None:
+        sd = weights if isinstance(weights, dict) else torch.load(weights, map_location="cpu", weights_only=True)
+        sd = sd.get("model", sd)
+        pred_shape = sd.get("roi_heads.box_predictor.cls_score.weight", torch.empty(0)).shape
+        if len(pred_shape) and pred_shape[0] == num_classes:
+            model.roi_heads.box_predictor = frcnn.FastRCNNPredictor(in_features, num_classes)
+            model.load_state_dict(sd)
+        else:  # COCO-pretrained body/FPN/RPN, fresh predictor (reference: head replaced after load)
+            model.load_state_dict(sd)
+            model.roi_heads.box_predictor = frcnn.FastRCNNPredictor(in_features, num_classes)
+        trainable = 3 if trainable_backbone_layers is None else trainable_backbone_layers
+    else:
+        model.roi_heads.box_predictor = frcnn.FastRCNNPredictor(in_features, num_classes)
+        trainable = 5 if trainable_backbone_layers is None else trainable_backbone_layers
+    frcnn.set_trainable_layers(model.backbone.body, trainable)
+    return model
+
+
+class ShardSampler(torch.utils.data.Sampler):
+    """Per-image eval sharding without padding (every image evaluated exactly once across ranks)."""
+
+    def __init__(self, n, world, rank):
+        self.idx = list(range(rank, n, world))
+
+    def __iter__(self):
+        return iter(self.idx)
+
+    def __len__(self):
+        return len(self.idx)
+
+
+def _to_device_batch(images, targets, dev):
+    imgs = [im.to(dev, non_blocking=True) for im in images]
+    tgs = [{k: v.to(dev, non_blocking=True) for k, v in t.items()} for t in targets]
+    return imgs, tgs
+
+
+def _append_jsonl(path, rec):
+    with open(path, "a", encoding="utf-8") as f:
+        f.write(json.dumps(rec, ensure_ascii=False) + "\n")
+
+
+@torch.no_grad()
+def evaluate(model, loader, ann_file, dev, per_class=False):
+    """COCOeval of a model over a loader of (uint8 HWC image, target) with bs=1."""
+    world, rank, _ = dist_info()
+    COCO, COCOeval = get_coco_api()
+    model.eval()
+    results = []
+    for images, targets in loader:
+        imgs = [im.to(dev, non_blocking=True) for im in images]
+        outs = model(imgs)
+        for out, tgt in zip(outs, targets):
+            img_id = int(tgt["image_id"].item())
+            b = out["boxes"].float().cpu().numpy()
+            s = out["scores"].float().cpu().numpy()
+            lab = out["labels"].cpu().numpy()
+            for (x1, y1, x2, y2), sc, lb in zip(b.tolist(), s.tolist(), lab.tolist()):
+                results.append({"image_id": img_id, "category_id": int(lb), "bbox": [x1, y1, x2 - x1, y2 - y1],
+                                "score": float(sc)})
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, results)
+        results = [r for part in gathered for r in part]
+    if rank != 0:
+        return None
+    if not results:
+        return {"mAP50_95": 0.0, "mAP50": 0.0, **({"per_class_ap50": {}} if per_class else {})}
+    gt = COCO(ann_file)
+    ev = COCOeval(gt, gt.loadRes(results), iouType="bbox")
+    ev.evaluate()
+    ev.accumulate()
+    ev.summarize()
+    out = {"mAP50_95": float(ev.stats[0]), "mAP50": float(ev.stats[1])}
+    if per_class:
+        prec = ev.eval["precision"]
+        pc = {}
+        for k, cat_id in enumerate(gt.getCatIds()):
+            name = gt.loadCats(cat_id)[0]["name"]
+            ap = prec[0, :, k, 0, 2]
+            ap = ap[ap > -1]
+            pc[name] = float(np.mean(ap)) if len(ap) else 0.0
+        out["per_class_ap50"] = pc
+    return out
+
+
+def train_frcnn(cfg):
+    """cfg: dict with SEED, EPOCHS, BATCH_SIZE, LR, WEIGHT_DECAY, MOMENTUM, TRAIN_IMG, TRAIN_ANN, VAL_IMG,
+    VAL_ANN, OUT_DIR, AUGMENT (bool), optional WEIGHTS (checkpoint path), NUM_WORKERS."""
+    from .dataset import COCODetectionDataset, collate_fn, uint8_transform
+    from .augment import RandomCorruptionGPU
+
+    set_seed(cfg["SEED"])
+    dev, world, rank = init_device()
+    out_dir = Path(cfg["OUT_DIR"])
+    if rank == 0:
+        out_dir.mkdir(parents=True, exist_ok=True)
+        print("Device:", dev, f"(world {world})", flush=True)
+        if cfg.get("AUGMENT"):
+            print("Mode: AUGMENTED training (corruption p=0.5, on GPU)\n", flush=True)
+    train_ds = COCODetectionDataset(str(cfg["TRAIN_IMG"]), str(cfg["TRAIN_ANN"]), transforms=uint8_transform)
+    val_ds = COCODetectionDataset(str(cfg["VAL_IMG"]), str(cfg["VAL_ANN"]), transforms=uint8_transform)
+    sampler = DistributedSampler(train_ds, world, rank, shuffle=True, seed=cfg["SEED"]) if world > 1 else None
+    train_loader = DataLoader(train_ds, batch_size=cfg["BATCH_SIZE"], shuffle=sampler is None, sampler=sampler,
+                              num_workers=cfg.get("NUM_WORKERS", 0), collate_fn=collate_fn, pin_memory=True)
+    val_sampler = ShardSampler(len(val_ds), world, rank) if world > 1 else None
+    val_loader = DataLoader(val_ds, batch_size=1, shuffle=False, sampler=val_sampler,
+                            num_workers=cfg.get("NUM_WORKERS", 0), collate_fn=collate_fn, pin_memory=True)
+    model = build_frcnn(7, cfg.get("WEIGHTS"), trainable_backbone_layers=cfg.get("TRAINABLE_LAYERS")).to(dev)
+    ddp = model
+    if world > 1:
+        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index], broadcast_buffers=False,
+                                                        gradient_as_bucket_view=True)
+    params = [p for p in model.parameters() if p.requires_grad]
+    optimizer = torch.optim.SGD(params, lr=cfg["LR"], momentum=cfg["MOMENTUM"], weight_decay=cfg["WEIGHT_DECAY"])
+    sched = torch.optim.lr_scheduler.StepLR(optimizer, step_size=8, gamma=0.1)
+    corrupt = RandomCorruptionGPU(p=0.5) if cfg.get("AUGMENT") else None
+    history, best_ckpt, last_ckpt = out_dir / "history.jsonl", out_dir / "best.pth", out_dir / "last.pth"
+    t0 = time.time()
+    n_batches = len(train_loader)
+    for epoch in range(1, cfg["EPOCHS"] + 1):
+        if sampler is not None:
+            sampler.set_epoch(epoch)
+        ddp.train()
+        epoch_loss = 0.0
+        for i, (images, targets) in enumerate(train_loader):
+            imgs, tgs = _to_device_batch(images, targets, dev)
+            if corrupt is not None:
+                imgs = [corrupt(im) for im in imgs]
+            loss_dict = ddp(imgs, tgs)
+            losses = sum(loss for loss in loss_dict.values())
+            optimizer.zero_grad(set_to_none=True)
+            losses.backward()
+            optimizer.step()
+            epoch_loss += float(losses.item())
+            if rank == 0 and ((i + 1) % 100 == 0 or (i + 1) == n_batches):
+                print(f"  [Epoch {epoch:03d}] batch {i + 1}/{n_batches}", flush=True)
+        sched.step()
+        if world > 1:
+            t = torch.tensor([epoch_loss], device=dev, dtype=torch.float64)
+            dist.all_reduce(t)
+            epoch_loss = float(t.item())
+        if rank == 0:
+            _append_jsonl(history, {"epoch": epoch, "train_loss_sum": epoch_loss,
+                                    "lr": float(optimizer.param_groups[0]["lr"]), "mAP50": None, "mAP50_95": None,
+                                    "elapsed_sec": int(time.time() - t0)})
+            print(f"[Epoch {epoch:03d}/{cfg['EPOCHS']}] loss_sum={epoch_loss:.4f}", flush=True)
+            torch.save({"model": model.state_dict(), "epoch": epoch}, last_ckpt)
+    if rank == 0:
+        print("\nEvaluating on clean val set (final)...", flush=True)
+    metrics = evaluate(model, val_loader, str(cfg["VAL_ANN"]), dev)
+    if rank == 0:
+        print(f"Final | mAP50={metrics['mAP50']:.4f} mAP50-95={metrics['mAP50_95']:.4f}", flush=True)
+        torch.save({"model": model.state_dict(), "epoch": "final", "metrics": metrics}, best_ckpt)
+        _append_jsonl(history, {"epoch": "final", "train_loss_sum": None,
+                                "lr": float(optimizer.param_groups[0]["lr"]), "mAP50": metrics["mAP50"],
+                                "mAP50_95": metrics["mAP50_95"], "elapsed_sec": int(time.time() - t0)})
+        print("\nTraining done.", flush=True)
+        print("Best checkpoint:", best_ckpt.resolve(), flush=True)
+    return metrics
+
+
+def load_frcnn_checkpoint(ckpt_path, dev):
+    """eval_all.py:79-87: fasterrcnn_resnet50_fpn_v2(weights=None) + 7-class predictor + best.pth."""
+    model = build_frcnn(7)
+    ckpt = torch.load(ckpt_path, map_location="cpu", weights_only=True)
+    model.load_state_dict(ckpt["model"])
+    return model.to(dev).eval()
+
+
+def eval_frcnn_variant(model, img_dir, ann_file, dev, restorer=None):
+    """One test-set variant (eval_all.py:97-143). restorer: optional device U-Net applied to every
+    uint8 image before detection (the fused restored-eval path of eval_restored.py)."""
+    from .dataset import COCODetectionDataset, collate_fn, uint8_transform
+    world, rank, _ = dist_info()
+    ds = COCODetectionDataset(img_dir, ann_file, transforms=uint8_transform)
+    sampler = ShardSampler(len(ds), world, rank) if world > 1 else None
+    loader = DataLoader(ds, batch_size=1, shuffle=False, sampler=sampler, num_workers=0, collate_fn=collate_fn,
+                        pin_memory=True)
+    if restorer is not None:
+        loader = _RestoredLoader(loader, restorer, dev)
+    return evaluate(model, loader, ann_file, dev, per_class=True)
+
+
+class _RestoredLoader:
+    def __init__(self, loader, unet, dev):
+        self.loader, self.unet, self.dev = loader, unet, dev
+
+    def __iter__(self):
+        for images, targets in self.loader:
+            out = [self.unet.restore_u8(im.to(self.dev)[None])[0] for im in images]
+            yield out, targets
+
+    def __len__(self):
+        return len(self.loader)

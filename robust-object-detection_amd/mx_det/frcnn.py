@@ -490,12 +490,16 @@ class GeneralizedRCNNTransform(nn.Module):
         return int(math.ceil(H / sd) * sd), int(math.ceil(W / sd) * sd)
 
     def forward(self, images, targets, be):
+        if isinstance(images, (list, tuple)) and len(images) and images[0].dtype == torch.uint8:
+            same = all(im.shape == images[0].shape for im in images)
+            images = torch.stack(list(images)) if same else images
         if isinstance(images, torch.Tensor) and images.dtype == torch.uint8 and images.dim() == 4:
             B, H, W, _ = images.shape
             if self._scale(H, W) == 1.0:
                 sizes = [(H, W)] * B
                 return ImageList(be.normalize_pad_u8(images, self._padded(sizes)), sizes), targets
-            images = [im.permute(2, 0, 1).float().div(255) for im in images]
+        if len(images) and images[0].dtype == torch.uint8:  # HWC uint8 -> ToDtype(float32, scale=True)
+            images = [im.permute(2, 0, 1).float().mul_(1.0 / 255) for im in images]
         dev = images[0].device
         mean = torch.tensor(self.image_mean, dtype=torch.float32, device=dev)[:, None, None]
         std = torch.tensor(self.image_std, dtype=torch.float32, device=dev)[:, None, None]
@@ -571,8 +575,9 @@ class FasterRCNN(nn.Module):
                     raise ValueError("All bounding boxes should have positive height and width.")
         if isinstance(images, torch.Tensor) and images.dim() == 4 and images.dtype == torch.uint8:
             original = [(images.shape[1], images.shape[2])] * images.shape[0]
-        else:
-            original = [(int(im.shape[-2]), int(im.shape[-1])) for im in images]
+        else:  # float CHW (reference ToDtype output) or uint8 HWC tensors
+            original = [(int(im.shape[0]), int(im.shape[1])) if im.dtype == torch.uint8 else
+                        (int(im.shape[-2]), int(im.shape[-1])) for im in images]
         il, targets = self.transform(images, targets, be)
         features = self.backbone(il.tensors, be)
         proposals, rpn_losses = self.rpn(il, features, targets, be)

@@ -53,24 +53,44 @@ def test_full_size_step_and_eval(dev):
 
 
 def test_features_match_cpu_backend(dev):
-    """Backbone + FPN (train-mode BN) on the same weights and image: HIP bf16 vs the CPU fp32
-    restatement, relative L2 error per pyramid level within bf16 accumulation noise."""
+    """Backbone + FPN (train-mode BN) on the same weights: every stage fed the SAME input on the HIP
+    bf16 path and the CPU fp32 restatement; per-stage relative L2 error at bf16 level (< 2e-2).
+    (End-to-end errors of a random-init ResNet compound chaotically, ~x1.15 per block, so stages are
+    compared one at a time: tools/debug_features.py prints both.)"""
+    from mx_det.conv import ACT_RELU
     from mx_det.data import synth_batch
     from oracle.cpu_backend import CpuBackend
     torch.manual_seed(2)
     m = _model(dev, trainable=5).train()
     mc = _model("cpu", trainable=5).train().set_backend(CpuBackend())
     mc.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
-    imgs, _ = synth_batch(5, 2, H=256, W=384, device=dev)
+    imgs, _ = synth_batch(5, 2, H=320, W=448, device=dev)
+
+    def rel(a, b):
+        a = a.float().cpu()
+        return ((a - b).norm() / b.norm()).item()
+
     with torch.no_grad():
         il, _ = m.transform(imgs, None, m.be)
         ilc, _ = mc.transform(imgs.cpu(), None, mc.be)
-        fg = m.backbone(il.tensors, m.be)
-        fc = mc.backbone(ilc.tensors, mc.be)
-    for k in fc:
-        a, b = fg[k].float().cpu(), fc[k]
-        rel = ((a - b).norm() / b.norm()).item()
-        assert rel < 3e-2, (k, rel)
+        assert rel(il.tensors[..., :3], ilc.tensors) < 1e-2
+        bg, bc = m.backbone.body, mc.backbone.body
+        x = m.be.conv_bn(il.tensors, bg.conv1, bg.bn1, ACT_RELU)
+        assert rel(x, mc.be.conv_bn(ilc.tensors, bc.conv1, bc.bn1, ACT_RELU)) < 2e-2
+        y = m.be.maxpool(x, 3, 2, 1)
+        assert rel(y, mc.be.maxpool(x.float().cpu(), 3, 2, 1)) < 1e-2
+        x, feats = y, {}
+        for li, name in enumerate(("layer1", "layer2", "layer3", "layer4")):
+            for b1, b2 in zip(getattr(bg, name), getattr(bc, name)):
+                y = b1(x, m.be)
+                e = rel(y, b2(x.float().cpu(), mc.be))
+                assert e < 2e-2, (name, e)
+                x = y
+            feats[str(li)] = x
+        fg = m.backbone.fpn(feats, m.be)
+        fc = mc.backbone.fpn({k: v.float().cpu() for k, v in feats.items()}, mc.be)
+        for k in fc:
+            assert rel(fg[k], fc[k]) < 2e-2, k
 
 
 def test_postprocess_matches_cpu_backend(dev):
