@@ -146,12 +146,19 @@ int mx_conv2d_dgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* 
 /* Hot-path forms. fwd_ex adds a fused epilogue: + residual[M][K] (bf16, nullable), then activation
  * (0 none, 1 ReLU, 2 LeakyReLU(0.2)) — the eval-mode conv+folded-BN(+add)+act of the backbone and
  * the U-Net. dgrad_t takes the weight pre-transposed to [C][R][S][K] by mx_conv_transpose_weight
- * (the plain mx_conv2d_dgrad allocates that temporary itself and is not graph-capturable). */
+ * (the plain mx_conv2d_fwd / mx_conv2d_dgrad allocate their temporaries with hipMallocAsync; the _ex / _t
+ * forms take caller workspaces and are the graph-capturable hot path). Small grids split K: their
+ * f32 partials go to `ws` (mx_conv_workspace bytes) and a reduce kernel applies the epilogue. */
 int mx_conv2d_fwd_ex(const mx_conv_shape* s, const uint16_t* x, const uint16_t* w, const float* bias,
-                     const uint16_t* residual, int act, void* y, int ydtype, float* stats, mx_stream_t stream);
+                     const uint16_t* residual, int act, void* y, int ydtype, float* stats, void* ws, size_t ws_bytes,
+                     mx_stream_t stream);
+/* Split-K workspace for pass 0 (fwd) / 1 (dgrad): 0 when the grid fills the chip without a K split. */
+size_t mx_conv_workspace(const mx_conv_shape* s, int pass);
+/* Kernel-variant knob for A/B measurement (process-wide; 1 = direct-to-LDS staging, the default). */
+int mx_conv_set_variant(int variant);
 int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS, int64_t C, uint16_t* wt, mx_stream_t stream);
-int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx,
-                      mx_stream_t stream);
+int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx, void* ws,
+                      size_t ws_bytes, mx_stream_t stream);
 int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw, mx_stream_t stream);
 
 /* NHWC pooling / resampling (bf16, C % 8 == 0).

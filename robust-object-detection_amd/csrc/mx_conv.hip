@@ -43,6 +43,11 @@ struct ConvP {
   int out_f32;
   float* stats;  // [2][mblocks][Ncol]
   int64_t mblocks;
+  // split-K: every split writes its f32 partial tile to slab[split][M][Ncol]; a reduce kernel applies
+  // the epilogue (slab == nullptr -> single pass, epilogue fused)
+  float* slab;
+  int splits;
+  int64_t kt_per_split;
 };
 
 __device__ __forceinline__ float act_f(float v, int act) {
@@ -71,6 +76,128 @@ __device__ __forceinline__ bool gather_pos(const ConvP& p, int oh, int ow, int r
     ih = th; iw = tw;
   }
   return ih >= 0 && iw >= 0 && ih < p.IH && iw < p.IW;
+}
+
+// Epilogue shared by the fwd/dgrad kernels: BN statistics from the f32 accumulators, then the tile
+// staged through LDS (after the last K-tile's barrier) for 16-B coalesced NHWC stores with fused
+// bias / residual / activation.
+template <int BN>
+__device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[4][BN / 32], char* smem, int64_t m0, int64_t n0,
+                                              int64_t mt, int wm, int wn, int lane, int tid, int split) {
+  constexpr int WN = BN / 2, TJ = WN / 16;
+  if (p.slab) {  // split-K partial: f32 tile to the slab, epilogue deferred to the reduce kernel
+    constexpr int LD = BN + 4;
+    float* Ct = (float*)smem;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Ct[(wm * 64 + i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    float* dst = p.slab + (int64_t)split * p.M * p.Ncol;
+    constexpr int CPR = BN / 4;
+    for (int e = tid; e < BM * CPR; e += NT) {
+      int row = e / CPR, cc = (e % CPR) * 4;
+      int64_t m = m0 + row, col0 = n0 + cc;
+      if (m < p.M && col0 < p.Ncol) *(float4*)(dst + m * p.Ncol + col0) = *(const float4*)&Ct[row * LD + cc];
+    }
+    return;
+  }
+  // ---- BatchNorm batch statistics from the f32 accumulators --------------------------------
+  // C/D map (16x16): col = lane & 15, row = (lane >> 4) * 4 + reg
+  if (p.stats) {
+    float* red = (float*)smem;  // [2 wm][2 (sum,sq)][BN]
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int64_t m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+          float v = m < p.M ? acc[i][j][r] : 0.f;
+          s += v;
+          q += v * v;
+        }
+      s += __shfl_xor(s, 16); q += __shfl_xor(q, 16);
+      s += __shfl_xor(s, 32); q += __shfl_xor(q, 32);
+      if (lane < 16) {
+        int col = wn * WN + j * 16 + lane;
+        red[(wm * 2 + 0) * BN + col] = s;
+        red[(wm * 2 + 1) * BN + col] = q;
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      int64_t col = n0 + c;
+      if (col < p.Ncol) {
+        p.stats[mt * p.Ncol + col] = red[c] + red[2 * BN + c];
+        p.stats[(p.mblocks + mt) * p.Ncol + col] = red[BN + c] + red[3 * BN + c];
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- stage the f32 tile through LDS, then coalesced NHWC stores ---------------------------
+  constexpr int LD = BN + 4;  // padded row (floats), keeps 16-B alignment
+  float* Ct = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        int col = wn * WN + j * 16 + (lane & 15);
+        Ct[row * LD + col] = acc[i][j][r];
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 8-column chunks per row
+  const bool vec = (p.Ncol % 8) == 0;
+  for (int e = tid; e < BM * CPR; e += NT) {
+    int row = e / CPR, cc = (e % CPR) * 8;
+    int64_t m = m0 + row, col0 = n0 + cc;
+    if (m >= p.M || col0 >= p.Ncol) continue;
+    float v[8];
+    *(float4*)&v[0] = *(const float4*)&Ct[row * LD + cc];
+    *(float4*)&v[4] = *(const float4*)&Ct[row * LD + cc + 4];
+    if (vec) {
+      if (p.bias) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] += p.bias[col0 + t];
+      }
+      if (p.residual) {
+        uint4 rr = *(const uint4*)(p.residual + m * p.Ncol + col0);
+        const uint16_t* rh = (const uint16_t*)&rr;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] += bf2f(rh[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], p.act);
+      if (p.out_f32) {
+        float* o = (float*)p.out + m * p.Ncol + col0;
+        *(float4*)o = *(float4*)&v[0];
+        *(float4*)(o + 4) = *(float4*)&v[4];
+      } else {
+        uint4 w;
+        uint16_t* wh = (uint16_t*)&w;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) wh[t] = f2bf(v[t]);
+        *(uint4*)((uint16_t*)p.out + m * p.Ncol + col0) = w;
+      }
+    } else {
+      for (int t = 0; t < 8 && col0 + t < p.Ncol; ++t) {
+        float x = v[t];
+        if (p.bias) x += p.bias[col0 + t];
+        if (p.residual) x += bf2f(p.residual[m * p.Ncol + col0 + t]);
+        x = act_f(x, p.act);
+        if (p.out_f32) ((float*)p.out)[m * p.Ncol + col0 + t] = x;
+        else ((uint16_t*)p.out)[m * p.Ncol + col0 + t] = f2bf(x);
+      }
+    }
+  }
 }
 
 template <int BN, int MODE>
@@ -180,98 +307,165 @@ __global__ void __launch_bounds__(NT, 2) conv_igemm_kernel(ConvP p) {
     __syncthreads();
   }
 
-  // ---- BatchNorm batch statistics from the f32 accumulators --------------------------------
-  // C/D map (16x16): col = lane & 15, row = (lane >> 4) * 4 + reg
-  if (p.stats) {
-    float* red = (float*)smem;  // [2 wm][2 (sum,sq)][BN]
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int64_t m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-          float v = m < p.M ? acc[i][j][r] : 0.f;
-          s += v;
-          q += v * v;
-        }
-      s += __shfl_xor(s, 16); q += __shfl_xor(q, 16);
-      s += __shfl_xor(s, 32); q += __shfl_xor(q, 32);
-      if (lane < 16) {
-        int col = wn * WN + j * 16 + lane;
-        red[(wm * 2 + 0) * BN + col] = s;
-        red[(wm * 2 + 1) * BN + col] = q;
-      }
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      int64_t col = n0 + c;
-      if (col < p.Ncol) {
-        p.stats[mt * p.Ncol + col] = red[c] + red[2 * BN + c];
-        p.stats[(p.mblocks + mt) * p.Ncol + col] = red[BN + c] + red[3 * BN + c];
-      }
-    }
-    __syncthreads();
-  }
+  conv_epilogue<BN>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, 0);
+}
 
-  // ---- stage the f32 tile through LDS, then coalesced NHWC stores ---------------------------
-  constexpr int LD = BN + 4;  // padded row (floats), keeps 16-B alignment
-  float* Ct = (float*)smem;
+// ------------------------------------------------------------------------------------------------
+// Same GEMM as conv_igemm_kernel, staged with direct-to-LDS loads (global_load_lds_dwordx4): each
+// wave instruction lands 64 x 16 B = 8 tile rows x 128 B in LDS; the XOR swizzle moves to the
+// per-lane SOURCE address (logical chunk = physical ^ (row & 7)); padding / out-of-range lanes read a
+// zero page. No staging registers, no ds_write pass.
+__device__ uint4 g_zero_page[4];
+
+template <int BN, int MODE>
+__global__ void __launch_bounds__(NT, 2) conv_igemm_glds_kernel(ConvP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int WN = BN / 2, TJ = WN / 16;
+  constexpr int BI = BN / 32;  // B instructions per wave (BN/4 rows per wave, 8 rows each)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t ntiles_n = (p.Ncol + BN - 1) / BN;
+  const int64_t gid = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int split = (int)(gid % p.splits);
+  const int64_t bid = gid / p.splits;  // the splits of one tile run on one XCD (shared A/B lines in L2)
+  const int64_t mt = bid / ntiles_n, nt = bid % ntiles_n;
+  const int64_t m0 = mt * BM, n0 = nt * BN;
+  const int lrow = lane >> 3;
+  const int lch = (lane & 7) ^ lrow;  // logical 16-B chunk this lane fetches (rows are 8-aligned)
+  int a_n[4], a_oh[4], a_ow[4];
+  bool a_ok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int64_t m = m0 + wave * 32 + i * 8 + lrow;
+    a_ok[i] = m < p.M;
+    int64_t mm = a_ok[i] ? m : 0;
+    a_ow[i] = (int)(mm % p.OW);
+    int64_t t = mm / p.OW;
+    a_oh[i] = (int)(t % p.OH);
+    a_n[i] = (int)(t / p.OH);
+  }
+  const uint16_t* zero = (const uint16_t*)g_zero_page;
+  const int64_t nk = (p.Kdim + BK - 1) / BK;
+  auto issue = [&](int64_t kt, int buf) {
+    char* A = smem + buf * STAGE;
+    char* B = A + A_BYTES;
+    const int64_t k = kt * BK + lch * 8;
+    const bool kin = k < p.Kdim;
+    const int tap = (int)(k / p.IC);
+    const int c = (int)(k - (int64_t)tap * p.IC);
+    const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int ih, iw;
+      const uint16_t* src = zero;
+      if (kin && a_ok[i] && gather_pos<MODE>(p, a_oh[i], a_ow[i], r, s, ih, iw))
+        src = p.src + (((int64_t)a_n[i] * p.IH + ih) * p.IW + iw) * p.IC + c;
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(A + (wave * 32 + i * 8) * (BK * 2)), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int row = wave * (BN / 4) + i * 8;
+      const int64_t n = n0 + row + lrow;
+      const uint16_t* src = (kin && n < p.Ncol) ? p.wt + n * p.Kdim + k : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(B + row * (BK * 2)), 16, 0, 0);
+    }
+  };
+  f32x4 acc[4][TJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        int col = wn * WN + j * 16 + (lane & 15);
-        Ct[row * LD + col] = acc[i][j][r];
-      }
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t kbeg = (int64_t)split * p.kt_per_split;
+  const int64_t kend = min<int64_t>(nk, kbeg + p.kt_per_split);
+  issue(kbeg, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  constexpr int CPR = BN / 8;  // 8-column chunks per row
-  const bool vec = (p.Ncol % 8) == 0;
-  for (int e = tid; e < BM * CPR; e += NT) {
-    int row = e / CPR, cc = (e % CPR) * 8;
-    int64_t m = m0 + row, col0 = n0 + cc;
-    if (m >= p.M || col0 >= p.Ncol) continue;
-    float v[8];
-    *(float4*)&v[0] = *(const float4*)&Ct[row * LD + cc];
-    *(float4*)&v[4] = *(const float4*)&Ct[row * LD + cc + 4];
-    if (vec) {
-      if (p.bias) {
+  for (int64_t kt = kbeg; kt < kend; ++kt) {
+    const int buf = (int)((kt - kbeg) & 1);
+    if (kt + 1 < kend) issue(kt + 1, buf ^ 1);
+    const char* A = smem + buf * STAGE;
+    const char* B = A + A_BYTES;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] += p.bias[col0 + t];
-      }
-      if (p.residual) {
-        uint4 rr = *(const uint4*)(p.residual + m * p.Ncol + col0);
-        const uint16_t* rh = (const uint16_t*)&rr;
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 4 + (lane >> 4);
+      bf16x8 af[4], bfr[TJ];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] += bf2f(rh[t]);
+      for (int i = 0; i < 4; ++i) {
+        int row = wm * 64 + i * 16 + (lane & 15);
+        af[i] = *(const bf16x8*)(A + row * (BK * 2) + ((ch ^ (row & 7)) << 4));
       }
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], p.act);
-      if (p.out_f32) {
-        float* o = (float*)p.out + m * p.Ncol + col0;
-        *(float4*)o = *(float4*)&v[0];
-        *(float4*)(o + 4) = *(float4*)&v[4];
-      } else {
-        uint4 w;
-        uint16_t* wh = (uint16_t*)&w;
+      for (int j = 0; j < TJ; ++j) {
+        int row = wn * WN + j * 16 + (lane & 15);
+        bfr[j] = *(const bf16x8*)(B + row * (BK * 2) + ((ch ^ (row & 7)) << 4));
+      }
 #pragma unroll
-        for (int t = 0; t < 8; ++t) wh[t] = f2bf(v[t]);
-        *(uint4*)((uint16_t*)p.out + m * p.Ncol + col0) = w;
-      }
-    } else {
-      for (int t = 0; t < 8 && col0 + t < p.Ncol; ++t) {
-        float x = v[t];
-        if (p.bias) x += p.bias[col0 + t];
-        if (p.residual) x += bf2f(p.residual[m * p.Ncol + col0 + t]);
-        x = act_f(x, p.act);
-        if (p.out_f32) ((float*)p.out)[m * p.Ncol + col0 + t] = x;
-        else ((uint16_t*)p.out)[m * p.Ncol + col0 + t] = f2bf(x);
-      }
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  conv_epilogue<BN>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
+}
+
+// Split-K reduce + epilogue: block = 128 rows x 64 columns; thread = 8 columns x 4 rows.
+// Sums the splits' f32 partials, then bias / residual / activation / store and the BN statistics
+// partials of the 128-row block (same [2][mblocks][Ncol] layout as the fused epilogue).
+__global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
+  __shared__ float red[2][32][65];
+  const int tid = threadIdx.x, cl = tid & 7, rl = tid >> 3;
+  const int64_t mt = blockIdx.x, col0 = (int64_t)blockIdx.y * 64 + cl * 8;
+  const bool cok = col0 < p.Ncol;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t stride = p.M * p.Ncol;
+  for (int rr = 0; rr < 4; ++rr) {
+    const int64_t m = mt * BM + rl + 32 * rr;
+    if (!cok || m >= p.M) continue;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const float* src = p.slab + m * p.Ncol + col0;
+    for (int k = 0; k < p.splits; ++k) {
+      float4 a = *(const float4*)(src + k * stride), b = *(const float4*)(src + k * stride + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) { s[t] += v[t]; q[t] += v[t] * v[t]; }
+    if (p.bias) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] += p.bias[col0 + t];
+    }
+    if (p.residual) {
+      uint4 r4 = *(const uint4*)(p.residual + m * p.Ncol + col0);
+      const uint16_t* rh = (const uint16_t*)&r4;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] += bf2f(rh[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], p.act);
+    if (p.out_f32) {
+      float* o = (float*)p.out + m * p.Ncol + col0;
+      *(float4*)o = *(float4*)&v[0];
+      *(float4*)(o + 4) = *(float4*)&v[4];
+    } else {
+      uint4 w;
+      uint16_t* wh = (uint16_t*)&w;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) wh[t] = f2bf(v[t]);
+      *(uint4*)((uint16_t*)p.out + m * p.Ncol + col0) = w;
+    }
+  }
+  if (!p.stats) return;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) { red[0][rl][cl * 8 + t] = s[t]; red[1][rl][cl * 8 + t] = q[t]; }
+  __syncthreads();
+  if (tid < 128) {
+    const int w = tid >> 6, c = tid & 63;
+    float a = 0.f;
+    for (int r = 0; r < 32; ++r) a += red[w][r][c];
+    const int64_t col = (int64_t)blockIdx.y * 64 + c;
+    if (col < p.Ncol) p.stats[(w * p.mblocks + mt) * p.Ncol + col] = a;
   }
 }
 
@@ -429,26 +623,81 @@ static int conv_check(const mx_conv_shape* s) {
 
 extern "C" int64_t mx_conv_mblocks(const mx_conv_shape* s) { return cdiv(s->N * s->Ho * s->Wo, BM); }
 
+static int g_conv_variant = 1;  // 0: register-staged loads, 1: direct-to-LDS loads (default)
+
+// GEMM geometry of a conv pass (0 fwd, 1 dgrad) and its split-K factor: grids that would leave the
+// chip under-filled (< ~1.25 blocks per CU) split the K loop, keeping >= 4 K-tiles per split.
+struct Geo {
+  int64_t M, Ncol, Kdim, tiles, nk;
+  int splits;
+  bool narrow;
+};
+static Geo conv_geo(const mx_conv_shape* s, int pass) {
+  Geo g;
+  g.M = pass == 0 ? s->N * s->Ho * s->Wo : s->N * s->H * s->W;
+  g.Ncol = pass == 0 ? s->K : s->C;
+  g.Kdim = s->R * s->S * (pass == 0 ? s->C : s->K);
+  g.narrow = g.Ncol <= 64;
+  g.tiles = cdiv(g.M, BM) * (g.narrow ? cdiv(g.Ncol, 64) : cdiv(g.Ncol, 128));
+  g.nk = cdiv(g.Kdim, BK);
+  g.splits = 1;
+  if (g_conv_variant == 1 && g.Ncol % 8 == 0 && g.tiles < 320 && g.nk >= 8) {
+    int64_t sp = std::min<int64_t>(std::min<int64_t>(cdiv(640, g.tiles), g.nk / 4), 16);
+    g.splits = (int)std::max<int64_t>(1, sp);
+  }
+  return g;
+}
+
+extern "C" size_t mx_conv_workspace(const mx_conv_shape* s, int pass) {
+  if (!s || (pass != 0 && pass != 1)) return 0;
+  Geo g = conv_geo(s, pass);
+  return g.splits > 1 ? sizeof(float) * (size_t)g.splits * g.M * g.Ncol : 0;
+}
+
 template <int MODE>
-static int launch_igemm(ConvP& p, hipStream_t st) {
-  const bool narrow = p.Ncol <= 64;
-  int64_t tn = narrow ? cdiv(p.Ncol, 64) : cdiv(p.Ncol, 128);
-  int64_t blocks = cdiv(p.M, BM) * tn;
-  MX_CHECK_ARG(blocks < (1ll << 31), "conv: grid too large");
-  if (narrow) {
+static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipStream_t st) {
+  int64_t blocks = g.tiles;
+  MX_CHECK_ARG(blocks * g.splits < (1ll << 31), "conv: grid too large");
+  const bool glds = g_conv_variant == 1;
+  p.splits = 1;
+  p.kt_per_split = g.nk;
+  p.slab = nullptr;
+  if (g.splits > 1) {
+    size_t need = sizeof(float) * (size_t)g.splits * g.M * g.Ncol;
+    MX_CHECK_ARG(ws && ws_bytes >= need, "conv: split-K workspace of %zu bytes required (mx_conv_workspace)", need);
+    p.splits = g.splits;
+    p.kt_per_split = cdiv(g.nk, g.splits);
+    p.splits = (int)cdiv(g.nk, p.kt_per_split);
+    p.slab = (float*)ws;
+    blocks *= p.splits;
+  }
+  if (g.narrow) {
     size_t lds = std::max<size_t>(2 * (BM + 64) * BK * 2, (size_t)BM * (64 + 4) * 4);
-    conv_igemm_kernel<64, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
+    if (glds) conv_igemm_glds_kernel<64, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
+    else conv_igemm_kernel<64, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
   } else {
     size_t lds = std::max<size_t>(2 * (BM + 128) * BK * 2, (size_t)BM * (128 + 4) * 4);
-    conv_igemm_kernel<128, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
+    if (glds) conv_igemm_glds_kernel<128, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
+    else conv_igemm_kernel<128, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
   }
   MX_LAUNCH_CHECK();
+  if (p.slab) {
+    dim3 rg((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.Ncol, 64));
+    conv_splitk_reduce_kernel<<<rg, 256, 0, st>>>(p);
+    MX_LAUNCH_CHECK();
+  }
+  return MX_OK;
+}
+
+extern "C" int mx_conv_set_variant(int v) {
+  MX_CHECK_ARG(v == 0 || v == 1, "mx_conv_set_variant: 0 (register staging) or 1 (direct-to-LDS)");
+  g_conv_variant = v;
   return MX_OK;
 }
 
 extern "C" int mx_conv2d_fwd_ex(const mx_conv_shape* s, const uint16_t* x, const uint16_t* w, const float* bias,
-                                const uint16_t* residual, int act, void* y, int ydtype, float* stats,
-                                mx_stream_t stream) {
+                                const uint16_t* residual, int act, void* y, int ydtype, float* stats, void* ws,
+                                size_t ws_bytes, mx_stream_t stream) {
   int rc = conv_check(s);
   if (rc) return rc;
   MX_CHECK_ARG(s->C % 8 == 0, "conv fwd: C=%lld must be a multiple of 8 (pad the input channels)", (long long)s->C);
@@ -461,12 +710,17 @@ extern "C" int mx_conv2d_fwd_ex(const mx_conv_shape* s, const uint16_t* x, const
   p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
   p.bias = bias; p.residual = residual; p.act = act; p.out = y; p.out_f32 = ydtype == MX_F32;
   p.stats = stats; p.mblocks = cdiv(p.M, BM);
-  return launch_igemm<0>(p, (hipStream_t)stream);
+  return launch_igemm<0>(p, conv_geo(s, 0), ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int mx_conv2d_fwd(const mx_conv_shape* s, const uint16_t* x, const uint16_t* w, const float* bias, void* y,
                              int ydtype, float* stats, mx_stream_t stream) {
-  return mx_conv2d_fwd_ex(s, x, w, bias, nullptr, 0, y, ydtype, stats, stream);
+  size_t ws = mx_conv_workspace(s, 0);
+  void* buf = nullptr;
+  if (ws) MX_HIP(hipMallocAsync(&buf, ws, (hipStream_t)stream));
+  int rc = mx_conv2d_fwd_ex(s, x, w, bias, nullptr, 0, y, ydtype, stats, buf, ws, stream);
+  if (buf) MX_HIP(hipFreeAsync(buf, (hipStream_t)stream));
+  return rc;
 }
 
 extern "C" int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS, int64_t C, uint16_t* wt, mx_stream_t stream) {
@@ -479,7 +733,7 @@ extern "C" int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS
 
 // dgrad with a pre-transposed weight wt[C][R][S][K]
 extern "C" int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx,
-                                 mx_stream_t stream) {
+                                 void* ws, size_t ws_bytes, mx_stream_t stream) {
   int rc = conv_check(s);
   if (rc) return rc;
   MX_CHECK_ARG(s->K % 8 == 0, "conv dgrad: K=%lld must be a multiple of 8", (long long)s->K);
@@ -490,7 +744,7 @@ extern "C" int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, con
   p.OH = s->H; p.OW = s->W; p.IH = s->Ho; p.IW = s->Wo; p.IC = s->K;
   p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
   p.out = dx; p.out_f32 = 0; p.act = 0;
-  return launch_igemm<1>(p, (hipStream_t)stream);
+  return launch_igemm<1>(p, conv_geo(s, 1), ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int mx_conv2d_dgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
@@ -502,10 +756,14 @@ extern "C" int mx_conv2d_dgrad(const mx_conv_shape* s, const uint16_t* dy, const
   if (rc) return rc;
   uint16_t* wt = nullptr;
   size_t bytes = sizeof(uint16_t) * s->K * s->R * s->S * s->C;
+  size_t wsb = mx_conv_workspace(s, 1);
+  void* ws = nullptr;
   MX_HIP(hipMallocAsync((void**)&wt, bytes, (hipStream_t)stream));
+  if (wsb) MX_HIP(hipMallocAsync(&ws, wsb, (hipStream_t)stream));
   rc = mx_conv_transpose_weight(w, s->K, s->R * s->S, s->C, wt, stream);
-  if (!rc) rc = mx_conv2d_dgrad_t(s, dy, wt, dx, stream);
+  if (!rc) rc = mx_conv2d_dgrad_t(s, dy, wt, dx, ws, wsb, stream);
   MX_HIP(hipFreeAsync(wt, (hipStream_t)stream));
+  if (ws) MX_HIP(hipFreeAsync(ws, (hipStream_t)stream));
   return rc;
 }
 

@@ -50,9 +50,12 @@ _SIGS = {
     "mx_conv2d_fwd": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "mx_conv2d_dgrad": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp]),
     "mx_conv2d_wgrad": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp]),
-    "mx_conv2d_fwd_ex": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
+    "mx_conv2d_fwd_ex": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp,
+                                 c_sz, c_vp]),
+    "mx_conv_workspace": (c_sz, [ctypes.POINTER(ConvShape), c_int]),
+    "mx_conv_set_variant": (c_int, [c_int]),
     "mx_conv_transpose_weight": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
-    "mx_conv2d_dgrad_t": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp]),
+    "mx_conv2d_dgrad_t": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_maxpool_fwd": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "mx_maxpool_bwd": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp]),
     "mx_upsample_nearest_fwd": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),

@@ -92,9 +92,11 @@ def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dty
         st = torch.empty((2, mb, K), dtype=torch.float32, device=x.device)
     if residual is not None:
         residual = residual.contiguous()
+    wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 0)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=x.device) if wsb else None
     t0 = _timer.start() if _timer else None
     call("mx_conv2d_fwd_ex", ctypes.byref(sh), _p(x), _p(wk), _p(bias), _p(residual), int(act), _p(y),
-         1 if out_dtype == torch.bfloat16 else 0, _p(st), _s())
+         1 if out_dtype == torch.bfloat16 else 0, _p(st), _p(ws), wsb, _s())
     if _timer:
         _timer.stop("fwd128" if K > 64 else "fwd64", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * C, t0)
     return (y, st) if stats else y
@@ -110,8 +112,10 @@ def conv_dgrad(dy, wk, x_shape, stride, pad):
     call("mx_conv_transpose_weight", _p(wk), K, R * S, C, _p(wt), _s())
     dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=dy.device)
     dyc = dy.contiguous()
+    wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 1)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dy.device) if wsb else None
     t0 = _timer.start() if _timer else None
-    call("mx_conv2d_dgrad_t", ctypes.byref(sh), _p(dyc), _p(wt), _p(dx), _s())
+    call("mx_conv2d_dgrad_t", ctypes.byref(sh), _p(dyc), _p(wt), _p(dx), _p(ws), wsb, _s())
     if _timer:
         _timer.stop("dgrad", 2.0 * N * Ho * Wo * K * R * S * C, t0)
     return dx

@@ -351,8 +351,8 @@ class FastRCNNPredictor(nn.Module):
 
 
 class FastRCNNConvFCHead(nn.Sequential):
-    """FastRCNNConvFCHead((256,7,7), [256]*4, [1024], norm_layer=BatchNorm2d). FC6 runs as a valid 7x7
-    conv over the NHWC RoI tile, which is exactly torch's NCHW flatten + Linear."""
+    """FastRCNNConvFCHead((256,7,7), [256]*4, [1024], norm_layer=BatchNorm2d). FC6/FC7 run as 1x1 MFMA
+    GEMMs; FC6's weight columns are permuted from torch's NCHW flatten order to the NHWC tile order."""
 
     def __init__(self, in_channels=256, conv_layers=(256, 256, 256, 256), fc_layers=(1024,), hw=7):
         blocks, prev = [], in_channels
@@ -379,11 +379,15 @@ class FastRCNNConvFCHead(nn.Sequential):
             if isinstance(m, ConvNormAct):
                 x = m(x, be)
             elif isinstance(m, Linear):
-                C = x.shape[3]
-                kh = x.shape[1] if first else 1
-                w = m.weight.view(m.out_features, C, kh, kh)
-                x = be.conv(x, w, m.bias, (1, 1), (0, 0), ACT_RELU)  # Linear + ReLU
-                first = False
+                w = m.weight
+                if first:
+                    # torch flattens the RoI tile in (C, H, W) order; the NHWC tile flattens (H, W, C):
+                    # permute FC6's input dimension once and run it as a 1x1 GEMM over [R,1,1,H*W*C]
+                    R, H, W, C = x.shape
+                    w = w.view(m.out_features, C, H, W).permute(0, 2, 3, 1).reshape(m.out_features, H * W * C)
+                    x = x.reshape(R, 1, 1, H * W * C)
+                    first = False
+                x = be.conv(x, w[:, :, None, None], m.bias, (1, 1), (0, 0), ACT_RELU)  # Linear + ReLU
         return x  # [R, 1, 1, 1024]
 
 

@@ -19,6 +19,8 @@ CASES = [
     (4, 1, 1, 12544 // 16, 1024, 1, 1, 0),
     (3, 9, 11, 256, 15, 1, 1, 0),      # RPN cls+bbox head (odd K)
     (2, 7, 7, 256, 256, 3, 1, 1),      # box head conv on RoI tiles
+    (2, 25, 42, 1024, 256, 1, 1, 0),   # small grid -> split-K (slab + reduce epilogue)
+    (2, 13, 21, 512, 512, 3, 1, 1),    # split-K, 3x3
 ]
 
 

@@ -1,0 +1,82 @@
+"""Conv kernel micro-benchmark on the shapes that dominate the FRCNN train step (bs=2, 800x1344).
+
+    python tools/bench_conv.py [--reps 20]
+Prints per shape and pass (fwd / dgrad / wgrad) the time per launch and TFLOP/s (bf16 MFMA peak 2500).
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "robust-object-detection_amd")]
+
+import torch  # noqa: E402
+
+from mx_det import conv as mc  # noqa: E402
+
+SHAPES = [  # name, N, H, W, C, K, k, stride, pad
+    ("P2 3x3 256->256 (RPN/FPN)", 2, 200, 336, 256, 256, 3, 1, 1),
+    ("P2 1x1 256->256 (FPN inner)", 2, 200, 336, 256, 256, 1, 1, 0),
+    ("L2 1x1 128->512", 2, 100, 168, 128, 512, 1, 1, 0),
+    ("L2 3x3 128->128", 2, 100, 168, 128, 128, 3, 1, 1),
+    ("L3 3x3 256->256", 2, 50, 84, 256, 256, 3, 1, 1),
+    ("L3 1x1 1024->256", 2, 50, 84, 1024, 256, 1, 1, 0),
+    ("L4 1x1 2048->512", 2, 25, 42, 2048, 512, 1, 1, 0),
+    ("box head 3x3 on 1024 RoIs", 1024, 7, 7, 256, 256, 3, 1, 1),
+    ("FC6 as 1x1 GEMM (12544->1024)", 1024, 1, 1, 12544, 1024, 1, 1, 0),
+    ("stem 7x7 s2 (8->64)", 2, 800, 1344, 8, 64, 7, 2, 3),
+    ("L3.0 3x3 s2 128->256 (dgrad s2)", 2, 100, 168, 256, 256, 3, 2, 1),
+]
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--variants", default="1")
+    args = ap.parse_args()
+    from mx_det import _lib
+    for v in [int(x) for x in args.variants.split(",")]:
+        _lib.call("mx_conv_set_variant", v)
+        print(f"== conv variant {v}", flush=True)
+        run(args)
+
+
+def run(args):
+    dev = torch.device("cuda")
+    tot = {"fwd": [0, 0], "dgrad": [0, 0], "wgrad": [0, 0]}
+    for name, N, H, W, C, K, k, st, pd in SHAPES:
+        if args.only and args.only not in name:
+            continue
+        x = torch.randn(N, H, W, C, device=dev).bfloat16()
+        w = (torch.randn(K, C, k, k, device=dev) * 0.05)
+        wk = mc.weight_krsc(w)
+        Ho, Wo = mc.out_hw(H, W, k, k, (st, st), (pd, pd))
+        dy = torch.randn(N, Ho, Wo, K, device=dev).bfloat16()
+        fl = 2.0 * N * Ho * Wo * K * k * k * C
+        res = []
+        for kind, fn in (("fwd", lambda: mc.conv_fwd(x, wk, (st, st), (pd, pd), stats=True)),
+                         ("dgrad", lambda: mc.conv_dgrad(dy, wk, x.shape, (st, st), (pd, pd))),
+                         ("wgrad", lambda: mc.conv_wgrad(dy, x, K, k, k, (st, st), (pd, pd)))):
+            ms = timeit(fn, args.reps)
+            tot[kind][0] += fl
+            tot[kind][1] += ms
+            res.append(f"{kind} {ms * 1000:8.1f}us {fl / ms / 1e9:7.1f}TF")
+        print(f"{name:34s} {fl / 1e9:7.1f} GF | " + " | ".join(res), flush=True)
+    print("aggregate: " + " | ".join(f"{k} {v[0] / v[1] / 1e9:.1f} TF/s" for k, v in tot.items() if v[1]))
+
+
+if __name__ == "__main__":
+    main()
