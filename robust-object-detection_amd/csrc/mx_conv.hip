@@ -598,6 +598,112 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(WgP p) {
       }
 }
 
+// wgrad, direct-to-LDS: 64-pixel K-tiles (two MFMA k-steps per barrier), both operands staged by
+// global_load_lds (one wave instruction = 4 pixel rows x 256 B), the swz_w XOR applied on the source
+// chunk; fragments read transposed with ds_read_b64_tr_b16 as in conv_wgrad_kernel.
+static constexpr int BKG = 64;
+
+__global__ void __launch_bounds__(NT, 2) conv_wgrad_glds_kernel(WgP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int OPB = BKG * 256, STAGE = 2 * OPB;  // per operand / per stage bytes
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t ntn = (p.Ncol + 127) / 128;
+  const int64_t tile = blockIdx.x;
+  const int64_t mt = tile / ntn, nt = tile % ntn;
+  const int64_t k0 = mt * 128, c0 = nt * 128;
+  const int64_t pbeg = (int64_t)blockIdx.y * p.kchunk;
+  const int64_t pend = min<int64_t>(p.P, pbeg + p.kchunk);
+  if (pbeg >= pend) return;
+  const int lr = lane >> 4;                       // row within a 4-row instruction group
+  const uint16_t* zero = (const uint16_t*)g_zero_page;
+  // per instruction i (0..3): rows wave*16 + i*4 + lr; logical chunk depends on the row
+  int lcs[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) lcs[i] = swz_w(wave * 16 + i * 4 + lr, lane & 15);
+  auto issue = [&](int64_t pb, int buf) {
+    char* A = smem + buf * STAGE;
+    char* B = A + OPB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wave * 16 + i * 4;
+      const int64_t px = pb + row + lr;
+      const int lc = lcs[i];
+      const uint16_t* sa = zero;
+      const uint16_t* sb = zero;
+      if (px < pend) {
+        if (k0 + lc * 8 < p.K) sa = p.dy + px * p.K + k0 + lc * 8;
+        const int64_t col = c0 + lc * 8;
+        if (col < p.Ncol) {
+          const int tap = (int)(col / p.C);
+          const int cc = (int)(col - (int64_t)tap * p.C);
+          const int r = tap / p.S, s2 = tap - (tap / p.S) * p.S;
+          const int64_t ow = px % p.OW, t = px / p.OW;
+          const int64_t oh = t % p.OH, n = t / p.OH;
+          const int64_t ih = oh * p.st_h - p.pad_h + r, iw = ow * p.st_w - p.pad_w + s2;
+          if (ih >= 0 && iw >= 0 && ih < p.H && iw < p.W) sb = p.x + ((n * p.H + ih) * p.W + iw) * p.C + cc;
+        }
+      }
+      __builtin_amdgcn_global_load_lds((const void*)sa, (LDS_AS void*)(A + row * 256), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)sb, (LDS_AS void*)(B + row * 256), 16, 0, 0);
+    }
+  };
+  auto tr_read = [&](const char* T, int prow0, int colbase) -> s16x4 {
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    int row = prow0 + 8 * g + q;
+    int colx = colbase + 4 * pp;
+    int chunk = colx >> 3, within = (colx & 7) * 2;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(T + row * 256 + (swz_w(row, chunk) << 4) + within));
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nk = (pend - pbeg + BKG - 1) / BKG;
+  issue(pbeg, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int64_t it = 0; it < nk; ++it) {
+    const int buf = (int)(it & 1);
+    if (it + 1 < nk) issue(pbeg + (it + 1) * BKG, buf ^ 1);
+    const char* A = smem + buf * STAGE;
+    const char* B = A + OPB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s16x4 lo = tr_read(A, ks * 32, wm * 64 + i * 16), hi = tr_read(A, ks * 32 + 4, wm * 64 + i * 16);
+        short t8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = *(bf16x8*)t8;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s16x4 lo = tr_read(B, ks * 32, wn * 64 + j * 16), hi = tr_read(B, ks * 32 + 4, wn * 64 + j * 16);
+        short t8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = *(bf16x8*)t8;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        int64_t k = k0 + wm * 64 + i * 16 + (lane >> 4) * 4 + rr;
+        int64_t cl = c0 + wn * 64 + j * 16 + (lane & 15);
+        if (k < p.K && cl < p.Ncol) atomicAdd(p.dw + k * p.Ncol + cl, acc[i][j][rr]);
+      }
+}
+
 __global__ void transpose_w_kernel(const uint16_t* __restrict__ w, int64_t K, int64_t RS, int64_t C, uint16_t* __restrict__ wt) {
   // w[K][RS][C] -> wt[C][RS][K]
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -641,7 +747,7 @@ static Geo conv_geo(const mx_conv_shape* s, int pass) {
   g.tiles = cdiv(g.M, BM) * (g.narrow ? cdiv(g.Ncol, 64) : cdiv(g.Ncol, 128));
   g.nk = cdiv(g.Kdim, BK);
   g.splits = 1;
-  if (g_conv_variant == 1 && g.Ncol % 8 == 0 && g.tiles < 320 && g.nk >= 8) {
+  if (g_conv_variant >= 1 && g.Ncol % 8 == 0 && g.tiles < 320 && g.nk >= 8) {
     int64_t sp = std::min<int64_t>(std::min<int64_t>(cdiv(640, g.tiles), g.nk / 4), 16);
     g.splits = (int)std::max<int64_t>(1, sp);
   }
@@ -658,7 +764,7 @@ template <int MODE>
 static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipStream_t st) {
   int64_t blocks = g.tiles;
   MX_CHECK_ARG(blocks * g.splits < (1ll << 31), "conv: grid too large");
-  const bool glds = g_conv_variant == 1;
+  const bool glds = g_conv_variant >= 1;
   p.splits = 1;
   p.kt_per_split = g.nk;
   p.slab = nullptr;
@@ -690,7 +796,7 @@ static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipSt
 }
 
 extern "C" int mx_conv_set_variant(int v) {
-  MX_CHECK_ARG(v == 0 || v == 1, "mx_conv_set_variant: 0 (register staging) or 1 (direct-to-LDS)");
+  MX_CHECK_ARG(v >= 0 && v <= 2, "mx_conv_set_variant: 0 register staging, 1 direct-to-LDS fwd/dgrad, 2 also wgrad");
   g_conv_variant = v;
   return MX_OK;
 }
@@ -777,15 +883,18 @@ extern "C" int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const
   p.OH = s->Ho; p.OW = s->Wo; p.H = s->H; p.W = s->W; p.C = s->C;
   p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
   int64_t tiles = cdiv(p.K, 128) * cdiv(p.Ncol, 128);
-  // split the pixel axis so that the grid covers the chip ~4x, at >= 8 K-tiles per split
+  const bool glds = g_conv_variant == 2;  // direct-to-LDS wgrad: correct but slower so far (see DESIGN)
+  const int bk = glds ? BKG : BKW;
+  // split the pixel axis so that the grid covers the chip ~4x, at >= 4-8 K-tiles per split
   int64_t splits = cdiv(1024, tiles);
-  int64_t max_splits = std::max<int64_t>(1, p.P / (BKW * 8));
+  int64_t max_splits = std::max<int64_t>(1, p.P / (bk * (glds ? 4 : 8)));
   splits = std::max<int64_t>(1, std::min(splits, max_splits));
-  p.kchunk = cdiv(cdiv(p.P, splits), BKW) * BKW;
+  p.kchunk = cdiv(cdiv(p.P, splits), bk) * bk;
   splits = cdiv(p.P, p.kchunk);
   MX_CHECK_ARG(tiles < (1ll << 31) && splits < 65536, "conv wgrad: grid too large");
   dim3 grid((unsigned)tiles, (unsigned)splits);
-  conv_wgrad_kernel<<<grid, NT, 0, (hipStream_t)stream>>>(p);
+  if (glds) conv_wgrad_glds_kernel<<<grid, NT, 2 * 2 * BKG * 256, (hipStream_t)stream>>>(p);
+  else conv_wgrad_kernel<<<grid, NT, 0, (hipStream_t)stream>>>(p);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }
