@@ -105,8 +105,8 @@ def conv_roofline(model, opt, imgs, tg):
     allms = sum(v["ms"] for v in s.values())
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
-            "kernel": {"fwd128": "conv_igemm_kernel<128,0>", "fwd64": "conv_igemm_kernel<64,0>",
-                       "dgrad": "conv_igemm_kernel<*,1>", "wgrad": "conv_wgrad_kernel"}[dom],
+            "kernel": {"fwd128": "conv_igemm_pipe_kernel<128,0,*>", "fwd64": "conv_igemm_pipe_kernel<64,0,*>",
+                       "dgrad": "conv_igemm_pipe_kernel<*,1,*>", "wgrad": "conv_wgrad_kernel"}[dom],
             "launches_per_step": d["launches"], "avg_launch_us": round(1000 * d["ms"] / d["launches"], 2),
             "gflop_per_launch": round(d["flops"] / d["launches"] / 1e9, 3),
             "conv_stack": {"tflops": round(allf / (allms * 1e-3) / 1e12, 2), "gflop_per_step": round(allf / 1e9, 1),

@@ -129,7 +129,7 @@ int mx_normalize_pad(const uint8_t* img, int64_t B, int64_t H, int64_t W, const 
  *   fwd:   y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,R,S,C]) (+bias[K] f32, nullable), output dtype
  *          ydtype; stats (nullable) receives per-block column partial sums for train-mode
  *          BatchNorm: stats[2][mblocks][K] f32 (sum, sum of squares) of the f32 accumulators.
- *   dgrad: dx[N,H,W,C] = conv_transpose(dy[N,Ho,Wo,K], w)   (bf16)
+ *   dgrad: dx[N,H,W,C] = conv_transpose(dy[N,Ho,Wo,K], w)   (bf16; strides 1 and 2)
  *   wgrad: dw[K,R,S,C] f32 = sum over N,Ho,Wo dy (x) x      (split-K with f32 atomics; dw zeroed
  *          by the caller)
  *   C % 8 == 0 is required (the stem input is padded to 8 channels).
@@ -145,17 +145,33 @@ int mx_conv2d_dgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* 
                     mx_stream_t stream);
 /* Hot-path forms. fwd_ex adds a fused epilogue: + residual[M][K] (bf16, nullable), then activation
  * (0 none, 1 ReLU, 2 LeakyReLU(0.2)) — the eval-mode conv+folded-BN(+add)+act of the backbone and
- * the U-Net. dgrad_t takes the weight pre-transposed to [C][R][S][K] by mx_conv_transpose_weight
- * (the plain mx_conv2d_fwd / mx_conv2d_dgrad allocate their temporaries with hipMallocAsync; the _ex / _t
+ * the U-Net. dgrad_t takes the weight in the dgrad layout written by mx_conv_pack_weight (the
+ * plain mx_conv2d_fwd / mx_conv2d_dgrad allocate their temporaries with hipMallocAsync; the _ex / _t
  * forms take caller workspaces and are the graph-capturable hot path). Small grids split K: their
- * f32 partials go to `ws` (mx_conv_workspace bytes) and a reduce kernel applies the epilogue. */
+ * f32 partials go to `ws` (mx_conv_workspace bytes) and a reduce kernel applies the epilogue.
+ * dgrad runs one dense GEMM per stride-parity class of dx (strides 1 and 2): rows with
+ * h % st == ph only receive taps r == (ph + pad) % st, so no MFMA work is spent on the zero taps
+ * of a strided conv. */
 int mx_conv2d_fwd_ex(const mx_conv_shape* s, const uint16_t* x, const uint16_t* w, const float* bias,
                      const uint16_t* residual, int act, void* y, int ydtype, float* stats, void* ws, size_t ws_bytes,
                      mx_stream_t stream);
 /* Split-K workspace for pass 0 (fwd) / 1 (dgrad): 0 when the grid fills the chip without a K split. */
 size_t mx_conv_workspace(const mx_conv_shape* s, int pass);
-/* Kernel-variant knob for A/B measurement (process-wide; 1 = direct-to-LDS staging, the default). */
+/* Kernel-variant knob for A/B measurement (process-wide): 0 register-staged, 1 direct-to-LDS 2-stage,
+ * 2 = 1 + direct-to-LDS wgrad, 3..6 multi-stage direct-to-LDS (BK32x3, BK64x2, BK32x4, BK64x3),
+ * 7 (default) per-launch choice between 3 and 4. */
 int mx_conv_set_variant(int variant);
+int mx_conv_get_variant(void);
+/* Per-step weight preparation from the f32 master parameter w[Kout][Cin][R][S] (torch layout) in
+ * one pass: wk = [Kout][R][S][s->C] bf16 (input channels zero-padded to s->C; nullable) and
+ * wt = the dgrad operand (nullable): for each tap-parity class (r0, s0) = (r % st_h, s % st_w), in
+ * order r0*st_w + s0, a contiguous block [s->C][Rc][Sc][s->K] (output channels zero-padded to s->K);
+ * for stride 1 this is the plain [C][R][S][K] transpose. Uses s->C, K, R, S, strides, pads.
+ * Replaces the per-step .to(bfloat16) weight casts of the reference's autocast-free fp32 model. */
+int mx_conv_pack_weight(const mx_conv_shape* s, const float* w, int64_t Cin, int64_t Kout, uint16_t* wk, uint16_t* wt,
+                        mx_stream_t stream);
+size_t mx_conv_dgrad_weight_elems(const mx_conv_shape* s, int64_t Cpad, int64_t Kpad);
+/* [K][RS][C] -> [C][RS][K] bf16 (the stride-1 dgrad layout). */
 int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS, int64_t C, uint16_t* wt, mx_stream_t stream);
 int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx, void* ws,
                       size_t ws_bytes, mx_stream_t stream);

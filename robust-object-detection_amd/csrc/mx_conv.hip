@@ -48,7 +48,17 @@ struct ConvP {
   float* slab;
   int splits;
   int64_t kt_per_split;
+  // dgrad parity class: GEMM row m = (n, hh, ww) of the class grid stores to dx row
+  // (n, st_h*hh + ph, st_w*ww + pw) of the full [N][H][W] grid
+  int remap, rst_h, rst_w, rph, rpw;
+  int64_t rH, rW;
 };
+
+__device__ __forceinline__ int64_t out_row(const ConvP& p, int64_t m) {
+  if (!p.remap) return m;
+  const int64_t ww = m % p.OW, t = m / p.OW, hh = t % p.OH, n = t / p.OH;
+  return (n * p.rH + hh * p.rst_h + p.rph) * p.rW + ww * p.rst_w + p.rpw;
+}
 
 __device__ __forceinline__ float act_f(float v, int act) {
   if (act == 1) return v > 0.f ? v : 0.f;
@@ -63,17 +73,17 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t id, int64_t nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
 }
 
-template <int MODE>  // 0 fwd, 1 dgrad
+// MODE 0 fwd: x[n, oh*st - pad + r, ow*st - pad + s]; MODE 1 dgrad of one stride-parity class
+// (rows = the class's (n, hh, ww) grid, taps = the class's (ri, si), pad = the class offset dh/dw):
+// dy[n, hh + dh - ri, ww + dw - si] — a dense stride-1 correlation, no wasted taps.
+template <int MODE>
 __device__ __forceinline__ bool gather_pos(const ConvP& p, int oh, int ow, int r, int s, int& ih, int& iw) {
   if (MODE == 0) {
     ih = oh * p.st_h - p.pad_h + r;
     iw = ow * p.st_w - p.pad_w + s;
   } else {
-    int th = oh + p.pad_h - r, tw = ow + p.pad_w - s;
-    if (th < 0 || tw < 0) return false;
-    if (p.st_h != 1) { if (th % p.st_h) return false; th /= p.st_h; }
-    if (p.st_w != 1) { if (tw % p.st_w) return false; tw /= p.st_w; }
-    ih = th; iw = tw;
+    ih = oh + p.pad_h - r;
+    iw = ow + p.pad_w - s;
   }
   return ih >= 0 && iw >= 0 && ih < p.IH && iw < p.IW;
 }
@@ -81,27 +91,37 @@ __device__ __forceinline__ bool gather_pos(const ConvP& p, int oh, int ow, int r
 // Epilogue shared by the fwd/dgrad kernels: BN statistics from the f32 accumulators, then the tile
 // staged through LDS (after the last K-tile's barrier) for 16-B coalesced NHWC stores with fused
 // bias / residual / activation.
-template <int BN>
+// HALVES == 2 stages the f32 tile in two 64-row passes (half the LDS: lets the multi-stage kernel
+// keep 3 blocks per CU).
+template <int BN, int HALVES = 1>
 __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[4][BN / 32], char* smem, int64_t m0, int64_t n0,
                                               int64_t mt, int wm, int wn, int lane, int tid, int split) {
   constexpr int WN = BN / 2, TJ = WN / 16;
+  constexpr int PR = BM / HALVES;  // rows staged per pass
   if (p.slab) {  // split-K partial: f32 tile to the slab, epilogue deferred to the reduce kernel
     constexpr int LD = BN + 4;
     float* Ct = (float*)smem;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Ct[(wm * 64 + i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
-    __syncthreads();
     float* dst = p.slab + (int64_t)split * p.M * p.Ncol;
     constexpr int CPR = BN / 4;
-    for (int e = tid; e < BM * CPR; e += NT) {
-      int row = e / CPR, cc = (e % CPR) * 4;
-      int64_t m = m0 + row, col0 = n0 + cc;
-      if (m < p.M && col0 < p.Ncol) *(float4*)(dst + m * p.Ncol + col0) = *(const float4*)&Ct[row * LD + cc];
+#pragma unroll
+    for (int h = 0; h < HALVES; ++h) {
+      if (HALVES == 1 || wm == h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              Ct[((HALVES == 1 ? wm * 64 : 0) + i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] =
+                  acc[i][j][r];
+      }
+      __syncthreads();
+      for (int e = tid; e < PR * CPR; e += NT) {
+        int row = e / CPR, cc = (e % CPR) * 4;
+        int64_t m = m0 + h * PR + row, col0 = n0 + cc;
+        if (m < p.M && col0 < p.Ncol) *(float4*)(dst + m * p.Ncol + col0) = *(const float4*)&Ct[row * LD + cc];
+      }
+      if (HALVES > 1) __syncthreads();
     }
     return;
   }
@@ -143,23 +163,28 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[4][BN
   // ---- stage the f32 tile through LDS, then coalesced NHWC stores ---------------------------
   constexpr int LD = BN + 4;  // padded row (floats), keeps 16-B alignment
   float* Ct = (float*)smem;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        int col = wn * WN + j * 16 + (lane & 15);
-        Ct[row * LD + col] = acc[i][j][r];
-      }
-  __syncthreads();
   constexpr int CPR = BN / 8;  // 8-column chunks per row
   const bool vec = (p.Ncol % 8) == 0;
-  for (int e = tid; e < BM * CPR; e += NT) {
+#pragma unroll
+  for (int h = 0; h < HALVES; ++h) {
+  if (HALVES == 1 || wm == h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int row = (HALVES == 1 ? wm * 64 : 0) + i * 16 + (lane >> 4) * 4 + r;
+          int col = wn * WN + j * 16 + (lane & 15);
+          Ct[row * LD + col] = acc[i][j][r];
+        }
+  }
+  __syncthreads();
+  for (int e = tid; e < PR * CPR; e += NT) {
     int row = e / CPR, cc = (e % CPR) * 8;
-    int64_t m = m0 + row, col0 = n0 + cc;
+    int64_t m = m0 + h * PR + row, col0 = n0 + cc;
     if (m >= p.M || col0 >= p.Ncol) continue;
+    m = out_row(p, m);
     float v[8];
     *(float4*)&v[0] = *(const float4*)&Ct[row * LD + cc];
     *(float4*)&v[4] = *(const float4*)&Ct[row * LD + cc + 4];
@@ -197,6 +222,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[4][BN
         else ((uint16_t*)p.out)[m * p.Ncol + col0 + t] = f2bf(x);
       }
     }
+  }
+  if (HALVES > 1) __syncthreads();
   }
 }
 
@@ -411,6 +438,134 @@ __global__ void __launch_bounds__(NT, 2) conv_igemm_glds_kernel(ConvP p) {
   conv_epilogue<BN>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Multi-stage direct-to-LDS variant: BKT-wide K-tiles (32 or 64), STAGES-deep LDS ring with
+// STAGES-1 tiles in flight. One barrier per K-tile; the wait before it is a counted vmcnt that leaves
+// the younger tiles' loads outstanding across the barrier, so HBM/L2 latency overlaps the MFMAs of
+// STAGES-2 further tiles. With BKT = 32 a tile row is 64 B: an instruction lands 16 rows and the
+// swizzle (phys chunk = logical ^ (row & 4 ? 2 : 0)) keeps the 16-lane ds_read_b128 groups
+// conflict-free. The epilogue stages the tile in two 64-row halves (LDS = max(ring, 33.8 KB)).
+template <int CPR>
+__device__ __forceinline__ int tile_swz(int row) {
+  if (CPR == 8) return row & 7;
+  return (row >> 1) & 2;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  // gfx9 s_waitcnt encoding: vmcnt[3:0], expcnt[6:4], lgkmcnt[11:8], vmcnt_hi[15:14]
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void block_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BN, int MODE, int BKT, int STAGES, int OCC>
+__global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int RB = BKT * 2;          // bytes per tile row
+  constexpr int CPR = BKT / 8;         // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;        // rows landed per wave instruction (8 or 16)
+  constexpr int AI = 32 / RPI;         // A instructions per wave (32 rows per wave)
+  constexpr int BI = (BN / 4) / RPI;   // B instructions per wave
+  constexpr int LOADS = AI + BI;       // vmem instructions per K-tile per wave
+  constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB;
+  constexpr int WN = BN / 2, TJ = WN / 16, KS = BKT / 32;
+  static_assert(BI >= 1 && KS >= 1 && STAGES >= 2, "tile shape");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t ntiles_n = (p.Ncol + BN - 1) / BN;
+  const int64_t gid = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int split = (int)(gid % p.splits);
+  const int64_t bid = gid / p.splits;
+  const int64_t mt = bid / ntiles_n, nt = bid % ntiles_n;
+  const int64_t m0 = mt * BM, n0 = nt * BN;
+  const int lrow = lane / CPR;
+  const int lch = (lane % CPR) ^ tile_swz<CPR>(lrow);  // instruction row bases are RPI-aligned
+  int a_n[AI], a_oh[AI], a_ow[AI];
+  bool a_ok[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    int64_t m = m0 + wave * 32 + i * RPI + lrow;
+    a_ok[i] = m < p.M;
+    int64_t mm = a_ok[i] ? m : 0;
+    a_ow[i] = (int)(mm % p.OW);
+    int64_t t = mm / p.OW;
+    a_oh[i] = (int)(t % p.OH);
+    a_n[i] = (int)(t / p.OH);
+  }
+  const uint16_t* zero = (const uint16_t*)g_zero_page;
+  const int64_t nk = (p.Kdim + BKT - 1) / BKT;
+  auto issue = [&](int64_t kt, int buf) {
+    char* A = smem + buf * STAGE;
+    char* B = A + A_BYTES;
+    const int64_t k = kt * BKT + lch * 8;
+    const bool kin = k < p.Kdim;
+    const int tap = (int)(k / p.IC);
+    const int c = (int)(k - (int64_t)tap * p.IC);
+    const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      int ih, iw;
+      const uint16_t* src = zero;
+      if (kin && a_ok[i] && gather_pos<MODE>(p, a_oh[i], a_ow[i], r, s, ih, iw))
+        src = p.src + (((int64_t)a_n[i] * p.IH + ih) * p.IW + iw) * p.IC + c;
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(A + (wave * 32 + i * RPI) * RB), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int row = wave * (BN / 4) + i * RPI;
+      const int64_t n = n0 + row + lrow;
+      const uint16_t* src = (kin && n < p.Ncol) ? p.wt + n * p.Kdim + k : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(B + row * RB), 16, 0, 0);
+    }
+  };
+  f32x4 acc[4][TJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t kbeg = (int64_t)split * p.kt_per_split;
+  const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
+#pragma unroll
+  for (int st = 0; st < STAGES - 1; ++st)
+    if (st < ntk) issue(kbeg + st, st);
+  for (int64_t t = 0; t < ntk; ++t) {
+    // tile t landed (this wave's part): the younger STAGES-2 tiles may stay in flight
+    if (t + STAGES - 2 < ntk) wait_vmcnt<LOADS * (STAGES - 2)>();
+    else wait_vmcnt<0>();
+    block_barrier();  // ... and every wave's part; all waves are done reading tile t-1's buffer
+    if (t + STAGES - 1 < ntk) issue(kbeg + t + STAGES - 1, (int)((t + STAGES - 1) % STAGES));
+    const char* A = smem + (int)(t % STAGES) * STAGE;
+    const char* B = A + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int ch = ks * 4 + (lane >> 4);
+      bf16x8 af[4], bfr[TJ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int row = wm * 64 + i * 16 + (lane & 15);
+        af[i] = *(const bf16x8*)(A + row * RB + ((ch ^ tile_swz<CPR>(row)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        int row = wn * WN + j * 16 + (lane & 15);
+        bfr[j] = *(const bf16x8*)(B + row * RB + ((ch ^ tile_swz<CPR>(row)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // last tile's buffer is reused by the epilogue staging
+  conv_epilogue<BN, 2>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
+}
+
 // Split-K reduce + epilogue: block = 128 rows x 64 columns; thread = 8 columns x 4 rows.
 // Sums the splits' f32 partials, then bias / residual / activation / store and the BN statistics
 // partials of the 128-row block (same [2][mblocks][Ncol] layout as the fused epilogue).
@@ -436,8 +591,9 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] += p.bias[col0 + t];
     }
+    const int64_t mo = out_row(p, m);
     if (p.residual) {
-      uint4 r4 = *(const uint4*)(p.residual + m * p.Ncol + col0);
+      uint4 r4 = *(const uint4*)(p.residual + mo * p.Ncol + col0);
       const uint16_t* rh = (const uint16_t*)&r4;
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] += bf2f(rh[t]);
@@ -445,7 +601,7 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], p.act);
     if (p.out_f32) {
-      float* o = (float*)p.out + m * p.Ncol + col0;
+      float* o = (float*)p.out + mo * p.Ncol + col0;
       *(float4*)o = *(float4*)&v[0];
       *(float4*)(o + 4) = *(float4*)&v[4];
     } else {
@@ -453,7 +609,7 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
       uint16_t* wh = (uint16_t*)&w;
 #pragma unroll
       for (int t = 0; t < 8; ++t) wh[t] = f2bf(v[t]);
-      *(uint4*)((uint16_t*)p.out + m * p.Ncol + col0) = w;
+      *(uint4*)((uint16_t*)p.out + mo * p.Ncol + col0) = w;
     }
   }
   if (!p.stats) return;
@@ -712,6 +868,65 @@ __global__ void transpose_w_kernel(const uint16_t* __restrict__ w, int64_t K, in
   wt[(c * RS + rs) * K + k] = w[i];
 }
 
+// Per-step weight preparation, one pass over the f32 master weight w[K][C][R][S] (torch layout):
+//   wk [K][R][S][Cpad] bf16      — fwd / wgrad operand (input channels zero-padded to Cpad)
+//   wt [class][Cpad][Rc][Sc][Kpad] bf16 — dgrad operand, taps grouped by stride-parity class
+// A 64(k) x 64(c) tile of one tap goes through LDS so both outputs are written along their
+// contiguous axis.
+struct PackP {
+  const float* w;
+  uint16_t* wk;
+  uint16_t* wt;
+  int64_t K, C, Cpad, Kpad;
+  int R, S, st_h, st_w;
+  int64_t off[4];
+  int Rc[4], Sc[4];
+};
+
+__global__ void __launch_bounds__(256) pack_weight_kernel(PackP p) {
+  __shared__ float T[64][65];
+  const int tid = threadIdx.x;
+  const int64_t c0 = (int64_t)blockIdx.x * 64, k0 = (int64_t)blockIdx.y * 64;
+  const int rs = blockIdx.z, r = rs / p.S, sx = rs - (rs / p.S) * p.S, RS = p.R * p.S;
+  for (int e = tid; e < 64 * 64; e += 256) {
+    const int kk = e >> 6, cc = e & 63;
+    const int64_t k = k0 + kk, c = c0 + cc;
+    T[kk][cc] = (k < p.K && c < p.C) ? p.w[(k * p.C + c) * RS + rs] : 0.f;
+  }
+  __syncthreads();
+  if (p.wk) {
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int kk = e >> 6, cc = e & 63;
+      const int64_t k = k0 + kk, c = c0 + cc;
+      if (k < p.K && c < p.Cpad) p.wk[(k * RS + rs) * p.Cpad + c] = f2bf(T[kk][cc]);
+    }
+  }
+  if (p.wt) {
+    const int ph = r % p.st_h, pw = sx % p.st_w;  // (parity of the tap) -> class with r0 = r % st
+    const int q = ph * p.st_w + pw;
+    const int ri = r / p.st_h, si = sx / p.st_w;
+    const int64_t base = p.off[q];
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int cc = e >> 6, kk = e & 63;
+      const int64_t k = k0 + kk, c = c0 + cc;
+      if (k < p.Kpad && c < p.Cpad)
+        p.wt[base + ((c * p.Rc[q] + ri) * p.Sc[q] + si) * p.Kpad + k] = f2bf(T[kk][cc]);
+    }
+  }
+}
+
+// KRSC bf16 weight -> the dgrad parity-class layout of pack_weight_kernel (element-wise; used by
+// the convenience mx_conv2d_dgrad only)
+__global__ void krsc_to_dgrad_kernel(const uint16_t* __restrict__ w, PackP p) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.K * p.R * p.S * p.C) return;
+  const int64_t c = i % p.C, t = i / p.C;
+  const int sx = (int)(t % p.S), r = (int)((t / p.S) % p.R);
+  const int64_t k = t / ((int64_t)p.S * p.R);
+  const int q = (r % p.st_h) * p.st_w + sx % p.st_w;
+  p.wt[p.off[q] + ((c * p.Rc[q] + r / p.st_h) * p.Sc[q] + sx / p.st_w) * p.Kpad + k] = w[i];
+}
+
 }  // namespace mx
 
 using namespace mx;
@@ -729,20 +944,20 @@ static int conv_check(const mx_conv_shape* s) {
 
 extern "C" int64_t mx_conv_mblocks(const mx_conv_shape* s) { return cdiv(s->N * s->Ho * s->Wo, BM); }
 
-static int g_conv_variant = 1;  // 0: register-staged loads, 1: direct-to-LDS loads (default)
+// Kernel variant (mx_conv_set_variant): 0 register staging, 1/2 direct-to-LDS 2-stage (2 also
+// direct-to-LDS wgrad), 3..6 multi-stage direct-to-LDS, 7 (default) per-launch choice of 3 / 4.
+static int g_conv_variant = 7;
 
-// GEMM geometry of a conv pass (0 fwd, 1 dgrad) and its split-K factor: grids that would leave the
-// chip under-filled (< ~1.25 blocks per CU) split the K loop, keeping >= 4 K-tiles per split.
+// GEMM geometry of one launch and its split-K factor: grids that would leave the chip under-filled
+// (< ~1.25 blocks per CU) split the K loop, keeping >= 4 K-tiles (of 64) per split.
 struct Geo {
   int64_t M, Ncol, Kdim, tiles, nk;
   int splits;
   bool narrow;
 };
-static Geo conv_geo(const mx_conv_shape* s, int pass) {
+static Geo make_geo(int64_t M, int64_t Ncol, int64_t Kdim) {
   Geo g;
-  g.M = pass == 0 ? s->N * s->Ho * s->Wo : s->N * s->H * s->W;
-  g.Ncol = pass == 0 ? s->K : s->C;
-  g.Kdim = s->R * s->S * (pass == 0 ? s->C : s->K);
+  g.M = M; g.Ncol = Ncol; g.Kdim = Kdim;
   g.narrow = g.Ncol <= 64;
   g.tiles = cdiv(g.M, BM) * (g.narrow ? cdiv(g.Ncol, 64) : cdiv(g.Ncol, 128));
   g.nk = cdiv(g.Kdim, BK);
@@ -754,38 +969,118 @@ static Geo conv_geo(const mx_conv_shape* s, int pass) {
   return g;
 }
 
+// The variant a launch runs: long K loops on big grids favour 64-wide K-tiles (fewer barriers),
+// short loops and small / split grids the 3-deep 32-wide ring at 3 blocks per CU.
+static int launch_kind(const Geo& g) {
+  if (g_conv_variant != 7) return g_conv_variant;
+  return (g.splits == 1 && g.tiles >= 512 && g.nk >= 16) ? 4 : 3;
+}
+
+// dgrad stride-parity classes. dx(h) receives dy((h + pad - r) / st) only from taps with
+// r = (h + pad) mod st, so the rows with h = st*hh + ph form an independent dense GEMM over the
+// taps r = r0 + st*ri (r0 = (ph + pad) mod st): dx[n, st*hh+ph] = sum dy[n, hh + dh - ri] w_t[ri],
+// dh = (ph + pad - r0) / st. The classes partition both dx and the taps; wt stores each tap-parity
+// class's [C][Rc][Sc][K] block contiguously (block index = tap parity r0*st_w + s0).
+struct DClass {
+  int ph, pw, r0, s0, Rc, Sc, dh, dw;
+  int64_t Hc, Wc, off;
+};
+static int tap_count(int R, int r0, int st) { return r0 < R ? (R - r0 + st - 1) / st : 0; }
+static int dgrad_classes(const mx_conv_shape* s, int64_t Cpad, int64_t Kpad, DClass* out, int64_t* blk_off,
+                         int* blk_R, int* blk_S) {
+  const int sh = s->stride_h, sw = s->stride_w;
+  // block offsets by tap parity
+  int64_t off = 0;
+  for (int a = 0; a < sh; ++a)
+    for (int b = 0; b < sw; ++b) {
+      const int q = a * sw + b;
+      blk_R[q] = tap_count((int)s->R, a, sh);
+      blk_S[q] = tap_count((int)s->S, b, sw);
+      blk_off[q] = off;
+      off += Cpad * blk_R[q] * blk_S[q] * Kpad;
+    }
+  int n = 0;
+  for (int ph = 0; ph < sh; ++ph)
+    for (int pw = 0; pw < sw; ++pw) {
+      DClass c;
+      c.ph = ph; c.pw = pw;
+      c.r0 = (ph + s->pad_h) % sh; c.s0 = (pw + s->pad_w) % sw;
+      const int q = c.r0 * sw + c.s0;
+      c.Rc = blk_R[q]; c.Sc = blk_S[q]; c.off = blk_off[q];
+      c.dh = (ph + s->pad_h - c.r0) / sh; c.dw = (pw + s->pad_w - c.s0) / sw;
+      c.Hc = ph < s->H ? (s->H - ph + sh - 1) / sh : 0;
+      c.Wc = pw < s->W ? (s->W - pw + sw - 1) / sw : 0;
+      out[n++] = c;
+    }
+  return n;
+}
+
 extern "C" size_t mx_conv_workspace(const mx_conv_shape* s, int pass) {
   if (!s || (pass != 0 && pass != 1)) return 0;
-  Geo g = conv_geo(s, pass);
-  return g.splits > 1 ? sizeof(float) * (size_t)g.splits * g.M * g.Ncol : 0;
+  if (pass == 0) {
+    Geo g = make_geo(s->N * s->Ho * s->Wo, s->K, s->R * s->S * s->C);
+    return g.splits > 1 ? sizeof(float) * (size_t)g.splits * g.M * g.Ncol : 0;
+  }
+  if (s->stride_h < 1 || s->stride_h > 2 || s->stride_w < 1 || s->stride_w > 2) return 0;
+  DClass cl[4];
+  int64_t off[4];
+  int br[4], bs[4];
+  const int n = dgrad_classes(s, s->C, s->K, cl, off, br, bs);
+  size_t mx = 0;
+  for (int i = 0; i < n; ++i) {
+    Geo g = make_geo(s->N * cl[i].Hc * cl[i].Wc, s->C, (int64_t)cl[i].Rc * cl[i].Sc * s->K);
+    if (g.splits > 1) mx = std::max(mx, sizeof(float) * (size_t)g.splits * g.M * g.Ncol);
+  }
+  return mx;
+}
+
+template <int BN, int MODE, int BKT, int STAGES, int OCC>
+static void launch_pipe(const ConvP& p, int64_t blocks, hipStream_t st) {
+  size_t ring = (size_t)STAGES * (BM + BN) * BKT * 2;
+  size_t epi = (size_t)(BM / 2) * (BN + 4) * 4;
+  conv_igemm_pipe_kernel<BN, MODE, BKT, STAGES, OCC><<<(unsigned)blocks, NT, std::max(ring, epi), st>>>(p);
+}
+
+template <int BN, int MODE>
+static void launch_variant(int v, const ConvP& p, int64_t blocks, hipStream_t st) {
+  switch (v) {
+    case 0: {
+      size_t lds = std::max<size_t>(2 * (BM + BN) * BK * 2, (size_t)BM * (BN + 4) * 4);
+      conv_igemm_kernel<BN, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
+      break;
+    }
+    case 1: case 2: {
+      size_t lds = std::max<size_t>(2 * (BM + BN) * BK * 2, (size_t)BM * (BN + 4) * 4);
+      conv_igemm_glds_kernel<BN, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
+      break;
+    }
+    case 3: launch_pipe<BN, MODE, 32, 3, 3>(p, blocks, st); break;
+    case 4: launch_pipe<BN, MODE, 64, 2, 2>(p, blocks, st); break;
+    case 5: launch_pipe<BN, MODE, 32, 4, 2>(p, blocks, st); break;
+    default: launch_pipe<BN, MODE, 64, 3, 1>(p, blocks, st); break;
+  }
 }
 
 template <int MODE>
 static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipStream_t st) {
   int64_t blocks = g.tiles;
   MX_CHECK_ARG(blocks * g.splits < (1ll << 31), "conv: grid too large");
-  const bool glds = g_conv_variant >= 1;
+  const int v = launch_kind(g);
+  const int64_t bkt = (v == 3 || v == 5) ? 32 : 64;
+  const int64_t nk = cdiv(g.Kdim, bkt);  // K-tiles in the kernel's tile width
   p.splits = 1;
-  p.kt_per_split = g.nk;
+  p.kt_per_split = nk;
   p.slab = nullptr;
   if (g.splits > 1) {
     size_t need = sizeof(float) * (size_t)g.splits * g.M * g.Ncol;
     MX_CHECK_ARG(ws && ws_bytes >= need, "conv: split-K workspace of %zu bytes required (mx_conv_workspace)", need);
-    p.splits = g.splits;
-    p.kt_per_split = cdiv(g.nk, g.splits);
-    p.splits = (int)cdiv(g.nk, p.kt_per_split);
+    p.kt_per_split = cdiv(nk, (int64_t)g.splits);
+    p.splits = (int)cdiv(nk, p.kt_per_split);
     p.slab = (float*)ws;
     blocks *= p.splits;
   }
-  if (g.narrow) {
-    size_t lds = std::max<size_t>(2 * (BM + 64) * BK * 2, (size_t)BM * (64 + 4) * 4);
-    if (glds) conv_igemm_glds_kernel<64, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
-    else conv_igemm_kernel<64, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
-  } else {
-    size_t lds = std::max<size_t>(2 * (BM + 128) * BK * 2, (size_t)BM * (128 + 4) * 4);
-    if (glds) conv_igemm_glds_kernel<128, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
-    else conv_igemm_kernel<128, MODE><<<(unsigned)blocks, NT, lds, st>>>(p);
-  }
+  if (g.narrow) launch_variant<64, MODE>(v, p, blocks, st);
+  else launch_variant<128, MODE>(v, p, blocks, st);
   MX_LAUNCH_CHECK();
   if (p.slab) {
     dim3 rg((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.Ncol, 64));
@@ -795,8 +1090,12 @@ static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipSt
   return MX_OK;
 }
 
+extern "C" int mx_conv_get_variant(void) { return g_conv_variant; }
+
 extern "C" int mx_conv_set_variant(int v) {
-  MX_CHECK_ARG(v >= 0 && v <= 2, "mx_conv_set_variant: 0 register staging, 1 direct-to-LDS fwd/dgrad, 2 also wgrad");
+  MX_CHECK_ARG(v >= 0 && v <= 7,
+               "mx_conv_set_variant: 0 register staging, 1 direct-to-LDS fwd/dgrad, 2 also wgrad, 3-6 multi-stage "
+               "direct-to-LDS (3: BK32x3, 4: BK64x2, 5: BK32x4, 6: BK64x3), 7 auto");
   g_conv_variant = v;
   return MX_OK;
 }
@@ -816,7 +1115,7 @@ extern "C" int mx_conv2d_fwd_ex(const mx_conv_shape* s, const uint16_t* x, const
   p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
   p.bias = bias; p.residual = residual; p.act = act; p.out = y; p.out_f32 = ydtype == MX_F32;
   p.stats = stats; p.mblocks = cdiv(p.M, BM);
-  return launch_igemm<0>(p, conv_geo(s, 0), ws, ws_bytes, (hipStream_t)stream);
+  return launch_igemm<0>(p, make_geo(p.M, p.Ncol, p.Kdim), ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int mx_conv2d_fwd(const mx_conv_shape* s, const uint16_t* x, const uint16_t* w, const float* bias, void* y,
@@ -837,39 +1136,97 @@ extern "C" int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS
   return MX_OK;
 }
 
-// dgrad with a pre-transposed weight wt[C][R][S][K]
+extern "C" size_t mx_conv_dgrad_weight_elems(const mx_conv_shape* s, int64_t Cpad, int64_t Kpad) {
+  if (!s) return 0;
+  return (size_t)(Cpad ? Cpad : s->C) * s->R * s->S * (Kpad ? Kpad : s->K);
+}
+
+extern "C" int mx_conv_pack_weight(const mx_conv_shape* s, const float* w, int64_t Cin, int64_t Kout, uint16_t* wk,
+                                   uint16_t* wt, mx_stream_t stream) {
+  // s->C / s->K are the padded channel counts the kernels see (Cin <= s->C real input channels,
+  // Kout <= s->K real output channels of the f32 parameter w[Kout][Cin][R][S])
+  MX_CHECK_ARG(s && w && s->R > 0 && s->S > 0 && Cin > 0 && Kout > 0 && Cin <= s->C && Kout <= s->K,
+               "conv pack: bad shape");
+  MX_CHECK_ARG(!wt || (s->stride_h >= 1 && s->stride_h <= 2 && s->stride_w >= 1 && s->stride_w <= 2),
+               "conv pack: dgrad layout supports strides 1 and 2");
+  if (!wk && !wt) return MX_OK;
+  PackP p{};
+  p.w = w; p.wk = wk; p.wt = wt;
+  p.K = Kout; p.C = Cin; p.Cpad = s->C; p.Kpad = s->K;
+  p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w;
+  if (wt) {
+    DClass cl[4];
+    dgrad_classes(s, s->C, s->K, cl, p.off, p.Rc, p.Sc);
+  } else {
+    p.st_h = p.st_w = 1;
+  }
+  // wk covers Kout rows only; wt also covers the zero-padded output channels up to s->K
+  dim3 grid((unsigned)cdiv(s->C, 64), (unsigned)cdiv(wt ? s->K : Kout, 64), (unsigned)(s->R * s->S));
+  pack_weight_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(p);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+// dgrad with the weight packed by mx_conv_pack_weight (for stride 1 that layout is the plain
+// [C][R][S][K] transpose of mx_conv_transpose_weight)
 extern "C" int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx,
                                  void* ws, size_t ws_bytes, mx_stream_t stream) {
   int rc = conv_check(s);
   if (rc) return rc;
   MX_CHECK_ARG(s->K % 8 == 0, "conv dgrad: K=%lld must be a multiple of 8", (long long)s->K);
   MX_CHECK_ARG(s->C % 8 == 0, "conv dgrad: C=%lld must be a multiple of 8", (long long)s->C);
-  ConvP p{};
-  p.src = dy; p.wt = wt;
-  p.M = s->N * s->H * s->W; p.Ncol = s->C; p.Kdim = s->R * s->S * s->K;
-  p.OH = s->H; p.OW = s->W; p.IH = s->Ho; p.IW = s->Wo; p.IC = s->K;
-  p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
-  p.out = dx; p.out_f32 = 0; p.act = 0;
-  return launch_igemm<1>(p, conv_geo(s, 1), ws, ws_bytes, (hipStream_t)stream);
+  MX_CHECK_ARG(s->stride_h <= 2 && s->stride_w <= 2, "conv dgrad: strides 1 and 2 are supported");
+  DClass cl[4];
+  int64_t off[4];
+  int br[4], bs[4];
+  const int n = dgrad_classes(s, s->C, s->K, cl, off, br, bs);
+  const bool remap = s->stride_h > 1 || s->stride_w > 1;
+  for (int i = 0; i < n; ++i) {
+    const DClass& c = cl[i];
+    if (c.Hc * c.Wc == 0) continue;
+    ConvP p{};
+    p.src = dy; p.wt = wt + c.off;
+    p.M = s->N * c.Hc * c.Wc; p.Ncol = s->C; p.Kdim = (int64_t)c.Rc * c.Sc * s->K;
+    p.OH = c.Hc; p.OW = c.Wc; p.IH = s->Ho; p.IW = s->Wo; p.IC = s->K;
+    p.R = std::max(c.Rc, 1); p.S = std::max(c.Sc, 1); p.st_h = 1; p.st_w = 1; p.pad_h = c.dh; p.pad_w = c.dw;
+    p.out = dx; p.out_f32 = 0; p.act = 0;
+    p.remap = remap; p.rst_h = s->stride_h; p.rst_w = s->stride_w; p.rph = c.ph; p.rpw = c.pw;
+    p.rH = s->H; p.rW = s->W;
+    rc = launch_igemm<1>(p, make_geo(p.M, p.Ncol, p.Kdim), ws, ws_bytes, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return MX_OK;
 }
 
 extern "C" int mx_conv2d_dgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
                                mx_stream_t stream) {
-  // Convenience form: transposes w into a stream-ordered temporary held by the caller-visible
-  // allocator is not available here, so this entry requires the caller to use mx_conv2d_dgrad_t
-  // for the hot path; it allocates once per call (not graph-capturable).
+  // Convenience form taking the KRSC bf16 weight: repacks it into a stream-ordered temporary
+  // (allocates per call; the hot path uses mx_conv_pack_weight + mx_conv2d_dgrad_t).
   int rc = conv_check(s);
   if (rc) return rc;
+  MX_CHECK_ARG(s->stride_h <= 2 && s->stride_w <= 2, "conv dgrad: strides 1 and 2 are supported");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t RS = s->R * s->S;
   uint16_t* wt = nullptr;
-  size_t bytes = sizeof(uint16_t) * s->K * s->R * s->S * s->C;
+  size_t bytes = sizeof(uint16_t) * s->K * RS * s->C;
   size_t wsb = mx_conv_workspace(s, 1);
   void* ws = nullptr;
-  MX_HIP(hipMallocAsync((void**)&wt, bytes, (hipStream_t)stream));
-  if (wsb) MX_HIP(hipMallocAsync(&ws, wsb, (hipStream_t)stream));
-  rc = mx_conv_transpose_weight(w, s->K, s->R * s->S, s->C, wt, stream);
+  MX_HIP(hipMallocAsync((void**)&wt, bytes, st));
+  if (wsb) MX_HIP(hipMallocAsync(&ws, wsb, st));
+  {
+    DClass cl[4];
+    PackP p{};
+    dgrad_classes(s, s->C, s->K, cl, p.off, p.Rc, p.Sc);
+    p.K = s->K; p.C = s->C; p.Cpad = s->C; p.Kpad = s->K;
+    p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w;
+    p.wt = wt;
+    const int64_t n = s->K * RS * s->C;
+    krsc_to_dgrad_kernel<<<(unsigned)cdiv(n, 256), 256, 0, st>>>(w, p);
+    if (hipGetLastError() != hipSuccess) rc = MX_EHIP;
+  }
   if (!rc) rc = mx_conv2d_dgrad_t(s, dy, wt, dx, ws, wsb, stream);
-  MX_HIP(hipFreeAsync(wt, (hipStream_t)stream));
-  if (ws) MX_HIP(hipFreeAsync(ws, (hipStream_t)stream));
+  MX_HIP(hipFreeAsync(wt, st));
+  if (ws) MX_HIP(hipFreeAsync(ws, st));
   return rc;
 }
 

@@ -33,20 +33,25 @@ class KernelTimer:
         e.record()
         return e
 
-    def stop(self, kind, flops, e0):
+    def stop(self, kind, flops, e0, tag=""):
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        self.rec.append((kind, float(flops), e0, e1))
+        self.rec.append((kind, float(flops), e0, e1, tag))
 
-    def summary(self):
+    def summary(self, by_tag=False):
+        """{kind: {launches, flops, ms}}; by_tag: keyed by (kind, shape tag) instead."""
         torch.cuda.synchronize()
         out = {}
-        for kind, fl, a, b in self.rec:
-            d = out.setdefault(kind, {"launches": 0, "flops": 0.0, "ms": 0.0})
+        for kind, fl, a, b, tag in self.rec:
+            d = out.setdefault((kind, tag) if by_tag else kind, {"launches": 0, "flops": 0.0, "ms": 0.0})
             d["launches"] += 1
             d["flops"] += fl
             d["ms"] += a.elapsed_time(b)
         return out
+
+
+def _tag(N, H, W, C, K, R, S, stride):
+    return f"{N}x{H}x{W}x{C}->{K} {R}x{S}/{stride[0]}"
 
 
 _timer = None
@@ -98,18 +103,36 @@ def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dty
     call("mx_conv2d_fwd_ex", ctypes.byref(sh), _p(x), _p(wk), _p(bias), _p(residual), int(act), _p(y),
          1 if out_dtype == torch.bfloat16 else 0, _p(st), _p(ws), wsb, _s())
     if _timer:
-        _timer.stop("fwd128" if K > 64 else "fwd64", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * C, t0)
+        _timer.stop("fwd128" if K > 64 else "fwd64", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * C, t0,
+                    _tag(sh.N, sh.H, sh.W, C, K, R, S, stride))
     return (y, st) if stats else y
 
 
-def conv_dgrad(dy, wk, x_shape, stride, pad):
-    """dy NHWC bf16 [N,Ho,Wo,K], wk KRSC bf16 -> dx NHWC bf16 [N,H,W,C]."""
-    K, R, S, C = wk.shape
-    N, H, W, _ = x_shape
+def pack_weight(w, cin_pad=None, stride=(1, 1), pad=(0, 0), kpad=None, krsc=True, dgrad=False):
+    """f32 [K,C,R,S] device parameter -> (wk, wt) in one kernel (mx_conv_pack_weight):
+    wk [K,R,S,Cpad] bf16 (fwd operand) and wt, the dgrad operand (taps grouped by stride-parity
+    class, output channels zero-padded to kpad); either can be skipped."""
+    w = w.detach()
+    if w.dtype != torch.float32 or not w.is_contiguous():
+        w = w.float().contiguous()
+    K, C, R, S = w.shape
+    cp = cin_pad or C
+    kp = kpad or K
+    sh = _lib.ConvShape(1, 1, 1, cp, kp, R, S, 1, 1, stride[0], stride[1], pad[0], pad[1])
+    wk = torch.empty((K, R, S, cp), dtype=torch.bfloat16, device=w.device) if krsc else None
+    wt = torch.empty(cp * R * S * kp, dtype=torch.bfloat16, device=w.device) if dgrad else None
+    call("mx_conv_pack_weight", ctypes.byref(sh), _p(w), C, K, _p(wk), _p(wt), _s())
+    return wk, wt
+
+
+def conv_dgrad(dy, wt, x_shape, R, S, stride, pad):
+    """dy NHWC bf16 [N,Ho,Wo,K] (K = the wt's padded output channels), wt from
+    pack_weight(dgrad=True) -> dx NHWC bf16 [N,H,W,C]."""
+    N, H, W, C = x_shape
+    K = dy.shape[3]
+    assert wt.numel() == C * R * S * K, (wt.numel(), C, R, S, K)
     Ho, Wo = out_hw(H, W, R, S, stride, pad)
     sh = _lib.ConvShape(N, H, W, C, K, R, S, Ho, Wo, stride[0], stride[1], pad[0], pad[1])
-    wt = torch.empty((C, R, S, K), dtype=torch.bfloat16, device=dy.device)
-    call("mx_conv_transpose_weight", _p(wk), K, R * S, C, _p(wt), _s())
     dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=dy.device)
     dyc = dy.contiguous()
     wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 1)
@@ -117,7 +140,7 @@ def conv_dgrad(dy, wk, x_shape, stride, pad):
     t0 = _timer.start() if _timer else None
     call("mx_conv2d_dgrad_t", ctypes.byref(sh), _p(dyc), _p(wt), _p(dx), _p(ws), wsb, _s())
     if _timer:
-        _timer.stop("dgrad", 2.0 * N * Ho * Wo * K * R * S * C, t0)
+        _timer.stop("dgrad", 2.0 * N * Ho * Wo * K * R * S * C, t0, _tag(N, H, W, C, K, R, S, stride))
     return dx
 
 
@@ -129,7 +152,8 @@ def conv_wgrad(dy, x, K, R, S, stride, pad):
     t0 = _timer.start() if _timer else None
     call("mx_conv2d_wgrad", ctypes.byref(sh), _p(dyc), _p(x), _p(dw), _s())
     if _timer:
-        _timer.stop("wgrad", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * x.shape[3], t0)
+        _timer.stop("wgrad", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * x.shape[3], t0,
+                    _tag(sh.N, sh.H, sh.W, x.shape[3], K, R, S, stride))
     return dw
 
 
@@ -146,26 +170,28 @@ class ConvAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, act, out_dtype):
-        wk = weight_krsc(w, x.shape[3])
+        K = w.shape[0]
+        need_dx = ctx.needs_input_grad[0]
+        # narrow heads (RPN cls+box 15, predictor 35): the dgrad operand is zero-padded to K8
+        wk, wt = pack_weight(w, x.shape[3], stride, pad, kpad=(K + 7) // 8 * 8, dgrad=need_dx)
         y = conv_fwd(x, wk, stride, pad, bias=b.detach() if b is not None else None, act=act, out_dtype=out_dtype)
-        ctx.save_for_backward(x, wk, y)
+        ctx.save_for_backward(x, y, wt if need_dx else None)
         ctx.cfg = (stride, pad, act, w.shape, b is not None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, wk, y = ctx.saved_tensors
+        x, y, wt = ctx.saved_tensors
         stride, pad, act, wshape, has_b = ctx.cfg
         g = _act_grad(gy, y, act).to(torch.bfloat16).contiguous()
-        K, R, S, C = wk.shape
+        K, _, R, S = wshape
         dx = dw = db = None
         K8 = (K + 7) // 8 * 8
-        gk, wkk = g, wk
-        if K8 != K:  # narrow heads (RPN cls+box 15, predictor 35): zero-pad the output channels
+        gk = g
+        if K8 != K:
             gk = torch.nn.functional.pad(g, (0, K8 - K)).contiguous()
-            wkk = torch.cat([wk, wk.new_zeros((K8 - K, R, S, C))])
         if ctx.needs_input_grad[0]:
-            dx = conv_dgrad(gk, wkk, x.shape, stride, pad)
+            dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad)
         if ctx.needs_input_grad[1]:
             dwk = conv_wgrad(gk, x, K8, R, S, stride, pad)[:K]
             dw = dwk[..., : wshape[1]].permute(0, 3, 1, 2)
@@ -179,7 +205,8 @@ class ConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, residual, rmean, rvar, stride, pad, act, eps, momentum):
-        wk = weight_krsc(w, x.shape[3])
+        need_dx = ctx.needs_input_grad[0]
+        wk, wt = pack_weight(w, x.shape[3], stride, pad, dgrad=need_dx)
         z, st = conv_fwd(x, wk, stride, pad, stats=True)
         K = wk.shape[0]
         M = z.numel() // K
@@ -190,15 +217,15 @@ class ConvBNAct(torch.autograd.Function):
         y = torch.empty_like(z)
         res = residual.contiguous() if residual is not None else None
         call("mx_bn_apply", _p(z), 1, M, K, _p(scale), _p(shift), _p(res), int(act), _p(y), _s())
-        ctx.save_for_backward(x, wk, z, y, mean, invstd, gamma)
+        ctx.save_for_backward(x, wt if need_dx else None, z, y, mean, invstd, gamma)
         ctx.cfg = (stride, pad, act, w.shape, residual is not None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, wk, z, y, mean, invstd, gamma = ctx.saved_tensors
+        x, wt, z, y, mean, invstd, gamma = ctx.saved_tensors
         stride, pad, act, wshape, has_res = ctx.cfg
-        K, R, S, C = wk.shape
+        K, _, R, S = wshape
         M = z.numel() // K
         gy = gy.to(torch.bfloat16).contiguous()
         sums = torch.zeros((2, K), dtype=torch.float32, device=z.device)
@@ -209,7 +236,7 @@ class ConvBNAct(torch.autograd.Function):
              _p(sums), _p(dz), _p(dres), _s())
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = conv_dgrad(dz, wk, x.shape, stride, pad)
+            dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad)
         if ctx.needs_input_grad[1]:
             dwk = conv_wgrad(dz, x, K, R, S, stride, pad)
             dw = dwk[..., : wshape[1]].permute(0, 3, 1, 2)
@@ -294,5 +321,5 @@ def fold_bn(conv, bn):
 
 def eval_conv_bn(x, conv, bn, act, residual=None):
     w, b = fold_bn(conv, bn)
-    wk = weight_krsc(w, x.shape[3])
+    wk, _ = pack_weight(w, x.shape[3], conv.stride, conv.padding)
     return conv_fwd(x.contiguous(), wk, conv.stride, conv.padding, bias=b, residual=residual, act=act)

@@ -21,7 +21,19 @@ CASES = [
     (2, 7, 7, 256, 256, 3, 1, 1),      # box head conv on RoI tiles
     (2, 25, 42, 1024, 256, 1, 1, 0),   # small grid -> split-K (slab + reduce epilogue)
     (2, 13, 21, 512, 512, 3, 1, 1),    # split-K, 3x3
+    (1, 15, 19, 64, 64, 3, 2, 1),      # stride 2, odd sizes: 4 parity classes of unequal shape
+    (2, 16, 22, 64, 256, 1, 2, 0),     # 1x1 stride 2: three classes receive no taps (dx = 0)
 ]
+
+
+@pytest.fixture(params=[0, 1, 3, 4, 5, 6])
+def variant(request):
+    """Every fwd/dgrad staging variant of the implicit-GEMM kernel (mx_conv_set_variant)."""
+    from mx_det import _lib
+    old = _lib.load().mx_conv_get_variant()
+    _lib.call("mx_conv_set_variant", request.param)
+    yield request.param
+    _lib.call("mx_conv_set_variant", old)
 
 
 def _scale(x, w, k):
@@ -29,14 +41,15 @@ def _scale(x, w, k):
 
 
 @pytest.mark.parametrize("N,H,W,C,K,k,st,pd", CASES)
-def test_conv_fwd(dev, N, H, W, C, K, k, st, pd):
+def test_conv_fwd(dev, variant, N, H, W, C, K, k, st, pd):
     from mx_det import conv as mc
     g = torch.Generator().manual_seed(N * 1000 + C + K)
     x = torch.randn(N, H, W, C, generator=g).bfloat16()
     w = (torch.randn(K, C, k, k, generator=g) * 0.05).bfloat16()
     b = torch.randn(K, generator=g)
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float(), b, st, pd).permute(0, 2, 3, 1)
-    wk = mc.weight_krsc(w.float()).to(dev)
+    wk, _ = mc.pack_weight(w.float().to(dev), C, (st, st), (pd, pd))
+    assert torch.equal(wk.cpu(), mc.weight_krsc(w.float()))  # fused cast+permute == torch's
     y, stats = mc.conv_fwd(x.to(dev), wk, (st, st), (pd, pd), bias=b.to(dev), out_dtype=torch.float32, stats=True)
     tol = 2e-5 * _scale(x.float(), w.float(), k)
     torch.testing.assert_close(y.cpu(), ref, rtol=0, atol=tol)
@@ -62,8 +75,8 @@ def test_conv_fwd_residual_leaky(dev):
     torch.testing.assert_close(y.cpu(), ref, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("N,H,W,C,K,k,st,pd", [c for c in CASES if c[3] != 8 and c[4] % 8 == 0])
-def test_conv_dgrad_wgrad(dev, N, H, W, C, K, k, st, pd):
+@pytest.mark.parametrize("N,H,W,C,K,k,st,pd", [c for c in CASES if c[4] % 8 == 0])
+def test_conv_dgrad_wgrad(dev, variant, N, H, W, C, K, k, st, pd):
     from mx_det import conv as mc
     g = torch.Generator().manual_seed(7 + C + K)
     x = torch.randn(N, H, W, C, generator=g).bfloat16()
@@ -73,9 +86,9 @@ def test_conv_dgrad_wgrad(dev, N, H, W, C, K, k, st, pd):
     yr = F.conv2d(xr, wr, None, st, pd)
     dy = torch.randn(yr.shape, generator=g).bfloat16()
     yr.backward(dy.float())
-    wk = mc.weight_krsc(w.float()).to(dev)
+    _, wt = mc.pack_weight(w.float().to(dev), C, (st, st), (pd, pd), krsc=False, dgrad=True)
     dyn = dy.permute(0, 2, 3, 1).contiguous().to(dev)
-    dx = mc.conv_dgrad(dyn, wk, x.shape, (st, st), (pd, pd))
+    dx = mc.conv_dgrad(dyn, wt, x.shape, k, k, (st, st), (pd, pd))
     ref_dx = xr.grad.permute(0, 2, 3, 1)
     tol = 2e-5 * (dy.abs().amax() * w.abs().amax() * K * k * k).item()
     torch.testing.assert_close(dx.float().cpu(), ref_dx, rtol=1e-2, atol=tol + 1e-2 * ref_dx.abs().amax().item())
@@ -125,3 +138,22 @@ def test_conv_bn_train_matches_torch(dev, act):
     rel = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
     assert rel(xd.grad.float().cpu(), xr.grad.permute(0, 2, 3, 1)) < 2e-2
     assert rel(wd.grad.cpu(), wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("st,k,pd", [(2, 3, 1), (1, 3, 1), (2, 1, 0)])
+def test_dgrad_convenience_entry_matches_packed(dev, st, k, pd):
+    """mx_conv2d_dgrad (KRSC weight, repacked inside) == the packed hot path, bit for bit."""
+    import ctypes
+    from mx_det import _lib, conv as mc
+    g = torch.Generator().manual_seed(11)
+    N, H, W, C, K = 2, 13, 17, 64, 128
+    w = (torch.randn(K, C, k, k, generator=g) * 0.05).to(dev)
+    Ho, Wo = mc.out_hw(H, W, k, k, (st, st), (pd, pd))
+    dy = torch.randn(N, Ho, Wo, K, generator=g).bfloat16().to(dev)
+    wk, wt = mc.pack_weight(w, C, (st, st), (pd, pd), dgrad=True)
+    ref = mc.conv_dgrad(dy, wt, (N, H, W, C), k, k, (st, st), (pd, pd))
+    dx = torch.empty_like(ref)
+    sh = _lib.ConvShape(N, H, W, C, K, k, k, Ho, Wo, st, st, pd, pd)
+    _lib.call("mx_conv2d_dgrad", ctypes.byref(sh), mc._p(dy), mc._p(wk), mc._p(dx), mc._s())
+    torch.cuda.synchronize()
+    assert torch.equal(dx, ref)

@@ -45,7 +45,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="")
-    ap.add_argument("--variants", default="1")
+    ap.add_argument("--variants", default="7")
     args = ap.parse_args()
     from mx_det import _lib
     for v in [int(x) for x in args.variants.split(",")]:
@@ -62,13 +62,13 @@ def run(args):
             continue
         x = torch.randn(N, H, W, C, device=dev).bfloat16()
         w = (torch.randn(K, C, k, k, device=dev) * 0.05)
-        wk = mc.weight_krsc(w)
+        wk, wt = mc.pack_weight(w, C, (st, st), (pd, pd), dgrad=True)
         Ho, Wo = mc.out_hw(H, W, k, k, (st, st), (pd, pd))
         dy = torch.randn(N, Ho, Wo, K, device=dev).bfloat16()
         fl = 2.0 * N * Ho * Wo * K * k * k * C
         res = []
         for kind, fn in (("fwd", lambda: mc.conv_fwd(x, wk, (st, st), (pd, pd), stats=True)),
-                         ("dgrad", lambda: mc.conv_dgrad(dy, wk, x.shape, (st, st), (pd, pd))),
+                         ("dgrad", lambda: mc.conv_dgrad(dy, wt, x.shape, k, k, (st, st), (pd, pd))),
                          ("wgrad", lambda: mc.conv_wgrad(dy, x, K, k, k, (st, st), (pd, pd)))):
             ms = timeit(fn, args.reps)
             tot[kind][0] += fl

@@ -1,0 +1,55 @@
+"""Per-conv-shape time breakdown of one bench.py train step (HIP events around every conv launch).
+
+    python tools/step_breakdown.py [--variant 7] [--top 40]
+Prints, per (pass, shape), launches / ms / TFLOP/s, sorted by time, plus the per-pass totals.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "robust-object-detection_amd")]
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from mx_det import _lib, conv as mc  # noqa: E402
+from mx_det.data import synth_batch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", type=int, default=-1)
+    ap.add_argument("--top", type=int, default=40)
+    args = ap.parse_args()
+    if args.variant >= 0:
+        _lib.call("mx_conv_set_variant", args.variant)
+    dev = torch.device("cuda")
+    torch.manual_seed(42)
+    model = bench.build_model(dev).train()
+    opt = bench.make_optimizer(model)
+    imgs, tg = synth_batch(0, 2, device=dev)
+    for _ in range(3):
+        bench.train_step(model, opt, imgs, tg)
+    t = mc.KernelTimer()
+    mc.set_timer(t)
+    bench.train_step(model, opt, imgs, tg)
+    mc.set_timer(None)
+    rows = sorted(t.summary(by_tag=True).items(), key=lambda kv: -kv[1]["ms"])
+    tot = {}
+    for (kind, tag), d in rows:
+        a = tot.setdefault(kind, [0, 0.0, 0.0])
+        a[0] += d["launches"]
+        a[1] += d["ms"]
+        a[2] += d["flops"]
+    allms = sum(v[1] for v in tot.values())
+    print(f"conv stack {allms:.2f} ms, {sum(v[2] for v in tot.values()) / allms / 1e9:.1f} TF/s")
+    for k, (n, ms, fl) in sorted(tot.items()):
+        print(f"  {k:7s} {n:4d} launches {ms:7.3f} ms {fl / ms / 1e9:7.1f} TF/s")
+    for (kind, tag), d in rows[: args.top]:
+        print(f"{kind:7s} {tag:32s} x{d['launches']:<3d} {d['ms']:7.3f} ms {d['flops'] / d['ms'] / 1e9:7.1f} TF/s "
+              f"{100 * d['ms'] / allms:5.1f}%")
+
+
+if __name__ == "__main__":
+    main()
