@@ -130,8 +130,8 @@ int mx_normalize_pad(const uint8_t* img, int64_t B, int64_t H, int64_t W, const 
  *          ydtype; stats (nullable) receives per-block column partial sums for train-mode
  *          BatchNorm: stats[2][mblocks][K] f32 (sum, sum of squares) of the f32 accumulators.
  *   dgrad: dx[N,H,W,C] = conv_transpose(dy[N,Ho,Wo,K], w)   (bf16; strides 1 and 2)
- *   wgrad: dw[K,R,S,C] f32 = sum over N,Ho,Wo dy (x) x      (split-K with f32 atomics; dw zeroed
- *          by the caller)
+ *   wgrad: dw[K,R,S,C] f32 = sum over N,Ho,Wo dy (x) x      (overwritten; the pixel axis is split
+ *          into per-split partials in a workspace and summed by a reduce kernel — no atomics)
  *   C % 8 == 0 is required (the stem input is padded to 8 channels).
  * ------------------------------------------------------------------------------------------- */
 typedef struct {
@@ -155,13 +155,16 @@ int mx_conv2d_dgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* 
 int mx_conv2d_fwd_ex(const mx_conv_shape* s, const uint16_t* x, const uint16_t* w, const float* bias,
                      const uint16_t* residual, int act, void* y, int ydtype, float* stats, void* ws, size_t ws_bytes,
                      mx_stream_t stream);
-/* Split-K workspace for pass 0 (fwd) / 1 (dgrad): 0 when the grid fills the chip without a K split. */
+/* Split workspace for pass 0 (fwd) / 1 (dgrad) / 2 (wgrad): 0 when the grid fills the chip unsplit. */
 size_t mx_conv_workspace(const mx_conv_shape* s, int pass);
-/* Kernel-variant knob for A/B measurement (process-wide): 0 register-staged, 1 direct-to-LDS 2-stage,
- * 2 = 1 + direct-to-LDS wgrad, 3..6 multi-stage direct-to-LDS (BK32x3, BK64x2, BK32x4, BK64x3),
- * 7 (default) per-launch choice between 3 and 4. */
+/* Kernel-variant knobs for A/B measurement (process-wide). fwd/dgrad: 0 register-staged,
+ * 1/2 direct-to-LDS 2-stage, 3..6 multi-stage direct-to-LDS (BK32x3, BK64x2, BK32x4, BK64x3),
+ * 7 (default) per-launch choice between 3 and 4. wgrad: 0 32-pixel K-tiles, 1 (default) 64-pixel,
+ * 2 direct-to-LDS. */
 int mx_conv_set_variant(int variant);
 int mx_conv_get_variant(void);
+int mx_conv_set_wgrad_variant(int variant);
+int mx_conv_get_wgrad_variant(void);
 /* Per-step weight preparation from the f32 master parameter w[Kout][Cin][R][S] (torch layout) in
  * one pass: wk = [Kout][R][S][s->C] bf16 (input channels zero-padded to s->C; nullable) and
  * wt = the dgrad operand (nullable): for each tap-parity class (r0, s0) = (r % st_h, s % st_w), in
@@ -176,6 +179,13 @@ int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS, int64_t C
 int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx, void* ws,
                       size_t ws_bytes, mx_stream_t stream);
 int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw, mx_stream_t stream);
+/* Hot-path wgrad: dw written directly in layout 0 ([Kout][R][S][Cin]) or 1 ([Kout][Cin][R][S], the
+ * torch parameter layout, so the result is the weight's .grad as is), dropping the zero-padded
+ * channels (Kout <= s->K, Cin <= s->C); ws = mx_conv_workspace(s, 2) bytes. */
+int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw, int64_t Kout,
+                       int64_t Cin, int layout, void* ws, size_t ws_bytes, mx_stream_t stream);
+/* wgrad grid sizing knob: split the pixel axis until ~blocks workgroups (default 512). */
+int mx_conv_set_wgrad_target(int64_t blocks);
 
 /* NHWC pooling / resampling (bf16, C % 8 == 0).
  * maxpool: F.max_pool2d (ResNet stem k3 s2 p1 — torchvision resnet50 reached at

@@ -486,34 +486,59 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
   const int64_t m0 = mt * BM, n0 = nt * BN;
   const int lrow = lane / CPR;
   const int lch = (lane % CPR) ^ tile_swz<CPR>(lrow);  // instruction row bases are RPI-aligned
-  int a_n[AI], a_oh[AI], a_ow[AI];
-  bool a_ok[AI];
+  // per A row: gather origin (h0, w0) and its pixel index; tap (r, s) moves it by +-(r, s)
+  // (MODE 0: ih = oh*st - pad + r; MODE 1: ih = hh + dh - r)
+  const int IH = (int)p.IH, IW = (int)p.IW;
+  int a_h0[AI], a_w0[AI];
+  int64_t a_pix[AI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     int64_t m = m0 + wave * 32 + i * RPI + lrow;
-    a_ok[i] = m < p.M;
-    int64_t mm = a_ok[i] ? m : 0;
-    a_ow[i] = (int)(mm % p.OW);
+    const bool ok = m < p.M;
+    int64_t mm = ok ? m : 0;
+    const int ow = (int)(mm % p.OW);
     int64_t t = mm / p.OW;
-    a_oh[i] = (int)(t % p.OH);
-    a_n[i] = (int)(t / p.OH);
+    const int oh = (int)(t % p.OH);
+    const int n = (int)(t / p.OH);
+    a_h0[i] = MODE == 0 ? oh * p.st_h - p.pad_h : oh + p.pad_h;
+    a_w0[i] = MODE == 0 ? ow * p.st_w - p.pad_w : ow + p.pad_w;
+    if (!ok) a_h0[i] = -(1 << 28);  // never in range
+    a_pix[i] = ((int64_t)n * IH + a_h0[i]) * IW + a_w0[i];
   }
   const uint16_t* zero = (const uint16_t*)g_zero_page;
   const int64_t nk = (p.Kdim + BKT - 1) / BKT;
-  auto issue = [&](int64_t kt, int buf) {
+  const int64_t kbeg = (int64_t)split * p.kt_per_split;
+  const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
+  // this lane's K position (k = kt*BKT + lch*8 -> tap (r, s), channel c), advanced incrementally:
+  // tiles are issued strictly in order, so no per-tile division
+  const int IC = (int)p.IC, Kd = (int)p.Kdim;
+  int ik = (int)(kbeg * BKT) + lch * 8;
+  int ic_c, ic_r, ic_s;
+  {
+    const int tap = ik / IC;
+    ic_c = ik - tap * IC;
+    ic_r = tap / p.S;
+    ic_s = tap - ic_r * p.S;
+  }
+  auto issue = [&](int buf) {
     char* A = smem + buf * STAGE;
     char* B = A + A_BYTES;
-    const int64_t k = kt * BKT + lch * 8;
-    const bool kin = k < p.Kdim;
-    const int tap = (int)(k / p.IC);
-    const int c = (int)(k - (int64_t)tap * p.IC);
-    const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
+    const int k = ik;
+    const bool kin = k < Kd;
+    const int c = ic_c, r = ic_r, s = ic_s;
+    ik += BKT;
+    ic_c += BKT;
+    while (ic_c >= IC) {
+      ic_c -= IC;
+      if (++ic_s == p.S) { ic_s = 0; ++ic_r; }
+    }
+    const int dr = MODE == 0 ? r : -r, ds = MODE == 0 ? s : -s;
+    const int64_t toff = (int64_t)dr * IW + ds;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      int ih, iw;
+      const int ih = a_h0[i] + dr, iw = a_w0[i] + ds;
       const uint16_t* src = zero;
-      if (kin && a_ok[i] && gather_pos<MODE>(p, a_oh[i], a_ow[i], r, s, ih, iw))
-        src = p.src + (((int64_t)a_n[i] * p.IH + ih) * p.IW + iw) * p.IC + c;
+      if (kin && (unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW) src = p.src + (a_pix[i] + toff) * IC + c;
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(A + (wave * 32 + i * RPI) * RB), 16, 0, 0);
     }
 #pragma unroll
@@ -529,17 +554,15 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int64_t kbeg = (int64_t)split * p.kt_per_split;
-  const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
 #pragma unroll
   for (int st = 0; st < STAGES - 1; ++st)
-    if (st < ntk) issue(kbeg + st, st);
+    if (st < ntk) issue(st);
   for (int64_t t = 0; t < ntk; ++t) {
     // tile t landed (this wave's part): the younger STAGES-2 tiles may stay in flight
     if (t + STAGES - 2 < ntk) wait_vmcnt<LOADS * (STAGES - 2)>();
     else wait_vmcnt<0>();
     block_barrier();  // ... and every wave's part; all waves are done reading tile t-1's buffer
-    if (t + STAGES - 1 < ntk) issue(kbeg + t + STAGES - 1, (int)((t + STAGES - 1) % STAGES));
+    if (t + STAGES - 1 < ntk) issue((int)((t + STAGES - 1) % STAGES));
     const char* A = smem + (int)(t % STAGES) * STAGE;
     const char* B = A + A_BYTES;
 #pragma unroll
@@ -630,22 +653,90 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
 struct WgP {
   const uint16_t* dy;  // [P][K]
   const uint16_t* x;   // [N][H][W][C]
-  float* dw;           // [K][R*S*C]
+  float* dw;           // layout 0: [Kout][R][S][Cin]; 1: [Kout][Cin][R][S] (torch's weight layout)
   int64_t P, K, Ncol;  // Ncol = R*S*C
   int64_t OH, OW, H, W, C;
   int R, S, st_h, st_w, pad_h, pad_w;
   int64_t kchunk;      // pixels per split
+  float* slab;         // splits > 1: per-split partials [splits][K][Ncol], summed by wgrad_reduce_kernel
+  int64_t Kout, Cin;   // real (unpadded) output / input channels written to dw
+  int layout;
 };
 
-static constexpr int BKW = 32;  // pixels per K-tile (one MFMA k-step)
+// dw element (k, col = tap*C + c) -> its offset in the requested layout, or -1 for padding
+__device__ __forceinline__ int64_t wgrad_dst(const WgP& p, int64_t k, int col) {
+  const int C = (int)p.C;
+  const int tap = col / C, c = col - tap * C;
+  if (k >= p.Kout || c >= p.Cin) return -1;
+  const int64_t RS = (int64_t)p.R * p.S;
+  return p.layout == 0 ? (k * RS + tap) * p.Cin + c : (k * p.Cin + c) * RS + tap;
+}
+
+// Block epilogue: the split's partial tile to the slab (plain stores), or, unsplit, the final dw.
+__device__ __forceinline__ void wgrad_store(const WgP& p, f32x4 (&acc)[4][4], int64_t k0, int64_t c0, int wm, int wn,
+                                            int lane) {
+  float* slab = p.slab ? p.slab + (int64_t)blockIdx.y * p.K * p.Ncol : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int64_t k = k0 + wm * 64 + i * 16 + (lane >> 4) * 4 + rr;
+        const int64_t cl = c0 + wn * 64 + j * 16 + (lane & 15);
+        if (k >= p.K || cl >= p.Ncol) continue;
+        if (slab) {
+          slab[k * p.Ncol + cl] = acc[i][j][rr];
+        } else {
+          const int64_t o = wgrad_dst(p, k, (int)cl);
+          if (o >= 0) p.dw[o] = acc[i][j][rr];
+        }
+      }
+}
+
+// Sum of the split partials, written in dw's layout: thread = (k, 4 consecutive columns), reads
+// coalesced along the column axis of every split plane.
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(WgP p, int splits) {
+  const int64_t nc4 = p.Ncol >> 2;  // Ncol = R*S*C, C % 8 == 0
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.Kout * nc4) return;
+  const int64_t k = i / nc4, col = (i - k * nc4) * 4;
+  const int64_t plane = p.K * p.Ncol;
+  const float* src = p.slab + k * p.Ncol + col;
+  float4 v = *(const float4*)src;
+  int sp = 1;
+  for (; sp + 3 < splits; sp += 4) {
+    const float4 a = *(const float4*)(src + sp * plane), b = *(const float4*)(src + (sp + 1) * plane);
+    const float4 c = *(const float4*)(src + (sp + 2) * plane), d = *(const float4*)(src + (sp + 3) * plane);
+    v.x += (a.x + b.x) + (c.x + d.x);
+    v.y += (a.y + b.y) + (c.y + d.y);
+    v.z += (a.z + b.z) + (c.z + d.z);
+    v.w += (a.w + b.w) + (c.w + d.w);
+  }
+  for (; sp < splits; ++sp) {
+    const float4 a = *(const float4*)(src + sp * plane);
+    v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+  }
+  const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int64_t o = wgrad_dst(p, k, (int)(col + t));
+    if (o >= 0) p.dw[o] = vv[t];
+  }
+}
+
+static constexpr int BKW = 32;  // pixels per MFMA k-step
 
 __device__ __forceinline__ int swz_w(int row, int chunk) {
   return chunk ^ (((row & 3) << 1) | (((row >> 3) & 1) << 3));
 }
 
+// PXT pixels per K-tile (32 or 64: one or two MFMA k-steps per barrier)
+template <int PXT>
 __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(WgP p) {
-  // LDS per stage: A [32 px][128 k] + B [32 px][128 col], 256-B rows, swizzled 16-B chunks
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKW * 256];
+  // LDS per stage: A [PXT px][128 k] + B [PXT px][128 col], 256-B rows, swizzled 16-B chunks
+  constexpr int NR = PXT / 16;  // pixel rows per thread per operand
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * PXT * 256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int64_t ntn = (p.Ncol + 127) / 128;
@@ -666,30 +757,54 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(WgP p) {
   const int r = tap / p.S, s = tap % p.S;
   const bool kk_ok = (k0 + ch * 8) < p.K;
 
-  uint4 ra[2], rb[2];
-  auto load = [&](int64_t pb) {
+  uint4 ra[NR], rb[NR];
+  // this thread's pixel rows px = pb + (tid>>4) + 16*i as (n, oh, ow), advanced by PXT per
+  // K-tile without divisions
+  const int OW = (int)p.OW, OH = (int)p.OH, H = (int)p.H, W = (int)p.W;
+  int px_n[NR], px_oh[NR], px_ow[NR];
+  int64_t px_i[NR];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int64_t px = pb + (tid >> 4) + 16 * i;
+  for (int i = 0; i < NR; ++i) {
+    px_i[i] = pbeg + (tid >> 4) + 16 * i;
+    const int64_t t = px_i[i] / OW;
+    px_ow[i] = (int)(px_i[i] - t * OW);
+    px_oh[i] = (int)(t % OH);
+    px_n[i] = (int)(t / OH);
+  }
+  auto load = [&]() {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int64_t px = px_i[i];
       uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
       if (px < pend) {
         if (kk_ok) va = *(const uint4*)(p.dy + px * p.K + k0 + ch * 8);
         if (col_ok) {
-          int64_t ow = px % p.OW, t = px / p.OW;
-          int64_t oh = t % p.OH, n = t / p.OH;
-          int64_t ih = oh * p.st_h - p.pad_h + r, iw = ow * p.st_w - p.pad_w + s;
-          if (ih >= 0 && iw >= 0 && ih < p.H && iw < p.W) vb = *(const uint4*)(p.x + ((n * p.H + ih) * p.W + iw) * p.C + cc);
+          const int ih = px_oh[i] * p.st_h - p.pad_h + r, iw = px_ow[i] * p.st_w - p.pad_w + s;
+          if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+            vb = *(const uint4*)(p.x + (((int64_t)px_n[i] * H + ih) * W + iw) * p.C + cc);
         }
       }
       ra[i] = va;
       rb[i] = vb;
+      px_i[i] += PXT;
+      px_ow[i] += PXT;
+      if (px_ow[i] >= OW) {  // small maps (RoI 7x7, 1x1 FC) wrap several rows per tile
+        const int q = px_ow[i] / OW;
+        px_ow[i] -= q * OW;
+        px_oh[i] += q;
+        if (px_oh[i] >= OH) {
+          const int q2 = px_oh[i] / OH;
+          px_oh[i] -= q2 * OH;
+          px_n[i] += q2;
+        }
+      }
     }
   };
   auto store = [&](int buf) {
-    char* A = smem + buf * (2 * BKW * 256);
-    char* B = A + BKW * 256;
+    char* A = smem + buf * (2 * PXT * 256);
+    char* B = A + PXT * 256;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NR; ++i) {
       int row = (tid >> 4) + 16 * i;
       *(uint4*)(A + row * 256 + (swz_w(row, ch) << 4)) = ra[i];
       *(uint4*)(B + row * 256 + (swz_w(row, ch) << 4)) = rb[i];
@@ -711,47 +826,41 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(WgP p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int64_t nk = (pend - pbeg + BKW - 1) / BKW;
-  load(pbeg);
+  const int64_t nk = (pend - pbeg + PXT - 1) / PXT;
+  load();
   store(0);
   __syncthreads();
   for (int64_t it = 0; it < nk; ++it) {
     const int buf = (int)(it & 1);
-    if (it + 1 < nk) load(pbeg + (it + 1) * BKW);
-    const char* A = smem + buf * (2 * BKW * 256);
-    const char* B = A + BKW * 256;
-    bf16x8 af[4], bfr[4];
+    if (it + 1 < nk) load();
+    const char* A = smem + buf * (2 * PXT * 256);
+    const char* B = A + PXT * 256;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      s16x4 lo = tr_read(A, 0, wm * 64 + i * 16);
-      s16x4 hi = tr_read(A, 4, wm * 64 + i * 16);
-      short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      af[i] = *(bf16x8*)tmp;
+    for (int ks = 0; ks < PXT / BKW; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s16x4 lo = tr_read(A, ks * BKW + 0, wm * 64 + i * 16);
+        s16x4 hi = tr_read(A, ks * BKW + 4, wm * 64 + i * 16);
+        short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = *(bf16x8*)tmp;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s16x4 lo = tr_read(B, ks * BKW + 0, wn * 64 + j * 16);
+        s16x4 hi = tr_read(B, ks * BKW + 4, wn * 64 + j * 16);
+        short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = *(bf16x8*)tmp;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s16x4 lo = tr_read(B, 0, wn * 64 + j * 16);
-      s16x4 hi = tr_read(B, 4, wn * 64 + j * 16);
-      short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      bfr[j] = *(bf16x8*)tmp;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     if (it + 1 < nk) store(buf ^ 1);
     __syncthreads();
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        int64_t k = k0 + wm * 64 + i * 16 + (lane >> 4) * 4 + rr;
-        int64_t cl = c0 + wn * 64 + j * 16 + (lane & 15);
-        if (k < p.K && cl < p.Ncol) atomicAdd(p.dw + k * p.Ncol + cl, acc[i][j][rr]);
-      }
+  wgrad_store(p, acc, k0, c0, wm, wn, lane);
 }
 
 // wgrad, direct-to-LDS: 64-pixel K-tiles (two MFMA k-steps per barrier), both operands staged by
@@ -848,16 +957,7 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_glds_kernel(WgP p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        int64_t k = k0 + wm * 64 + i * 16 + (lane >> 4) * 4 + rr;
-        int64_t cl = c0 + wn * 64 + j * 16 + (lane & 15);
-        if (k < p.K && cl < p.Ncol) atomicAdd(p.dw + k * p.Ncol + cl, acc[i][j][rr]);
-      }
+  wgrad_store(p, acc, k0, c0, wm, wn, lane);
 }
 
 __global__ void transpose_w_kernel(const uint16_t* __restrict__ w, int64_t K, int64_t RS, int64_t C, uint16_t* __restrict__ wt) {
@@ -1015,8 +1115,11 @@ static int dgrad_classes(const mx_conv_shape* s, int64_t Cpad, int64_t Kpad, DCl
   return n;
 }
 
+static size_t wgrad_ws(const mx_conv_shape* s);
+
 extern "C" size_t mx_conv_workspace(const mx_conv_shape* s, int pass) {
-  if (!s || (pass != 0 && pass != 1)) return 0;
+  if (!s || pass < 0 || pass > 2) return 0;
+  if (pass == 2) return wgrad_ws(s);
   if (pass == 0) {
     Geo g = make_geo(s->N * s->Ho * s->Wo, s->K, s->R * s->S * s->C);
     return g.splits > 1 ? sizeof(float) * (size_t)g.splits * g.M * g.Ncol : 0;
@@ -1064,6 +1167,7 @@ static void launch_variant(int v, const ConvP& p, int64_t blocks, hipStream_t st
 template <int MODE>
 static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipStream_t st) {
   int64_t blocks = g.tiles;
+  MX_CHECK_ARG(g.Kdim < (1ll << 30) && p.IH < (1ll << 26) && p.IW < (1ll << 26), "conv: GEMM K or spatial size too large");
   MX_CHECK_ARG(blocks * g.splits < (1ll << 31), "conv: grid too large");
   const int v = launch_kind(g);
   const int64_t bkt = (v == 3 || v == 5) ? 32 : 64;
@@ -1092,9 +1196,18 @@ static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipSt
 
 extern "C" int mx_conv_get_variant(void) { return g_conv_variant; }
 
+// wgrad kernel variant: 0 register-staged 32-pixel K-tiles, 1 64-pixel K-tiles, 2 direct-to-LDS
+static int g_wgrad_variant = 0;
+extern "C" int mx_conv_set_wgrad_variant(int v) {
+  MX_CHECK_ARG(v >= 0 && v <= 2, "mx_conv_set_wgrad_variant: 0 px32, 1 px64, 2 direct-to-LDS");
+  g_wgrad_variant = v;
+  return MX_OK;
+}
+extern "C" int mx_conv_get_wgrad_variant(void) { return g_wgrad_variant; }
+
 extern "C" int mx_conv_set_variant(int v) {
   MX_CHECK_ARG(v >= 0 && v <= 7,
-               "mx_conv_set_variant: 0 register staging, 1 direct-to-LDS fwd/dgrad, 2 also wgrad, 3-6 multi-stage "
+               "mx_conv_set_variant: 0 register staging, 1/2 direct-to-LDS fwd/dgrad, 3-6 multi-stage "
                "direct-to-LDS (3: BK32x3, 4: BK64x2, 5: BK32x4, 6: BK64x3), 7 auto");
   g_conv_variant = v;
   return MX_OK;
@@ -1230,28 +1343,97 @@ extern "C" int mx_conv2d_dgrad(const mx_conv_shape* s, const uint16_t* dy, const
   return rc;
 }
 
-extern "C" int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw, mx_stream_t stream) {
+// wgrad launch geometry: 128x128 (k, col) tiles; the pixel axis is split until the grid covers
+// ~g_wgrad_target blocks (each split's partial goes to a slab, summed by wgrad_reduce_kernel).
+static int64_t g_wgrad_target = 0;  // 0: one full wave of resident blocks (occupancy x CUs)
+struct WGeo {
+  int64_t tiles, splits, kchunk;
+  int pxt;
+};
+static int g_num_cus = 0;
+static int num_cus() {
+  if (!g_num_cus) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_num_cus = n;
+    else
+      g_num_cus = 256;
+  }
+  return g_num_cus;
+}
+static WGeo wgrad_geo(const mx_conv_shape* s) {
+  WGeo g;
+  const int64_t P = s->N * s->Ho * s->Wo, Ncol = s->R * s->S * s->C;
+  g.tiles = cdiv(s->K, 128) * cdiv(Ncol, 128);
+  const int v = g_wgrad_variant;
+  g.pxt = v == 2 ? BKG : (v == 1 ? 64 : BKW);
+  // resident blocks per CU: px32 3 (142 VGPRs), px64 / direct-to-LDS 2
+  const int64_t slots = g_wgrad_target ? g_wgrad_target : (int64_t)num_cus() * (v == 0 ? 3 : 2);
+  int64_t splits = std::max<int64_t>(1, slots / g.tiles);  // never past one wave of blocks
+  const int64_t max_splits = std::max<int64_t>(1, P / (g.pxt * 4));
+  splits = std::min(splits, max_splits);
+  g.kchunk = cdiv(cdiv(P, splits), g.pxt) * g.pxt;
+  g.splits = cdiv(P, g.kchunk);
+  return g;
+}
+
+extern "C" int mx_conv_set_wgrad_target(int64_t blocks) {
+  MX_CHECK_ARG(blocks >= 0 && blocks <= (1 << 20), "mx_conv_set_wgrad_target: bad block count (0 = auto)");
+  g_wgrad_target = blocks;
+  return MX_OK;
+}
+
+static size_t wgrad_ws(const mx_conv_shape* s) {
+  WGeo g = wgrad_geo(s);
+  return g.splits > 1 ? sizeof(float) * (size_t)g.splits * s->K * s->R * s->S * s->C : 0;
+}
+
+extern "C" int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw,
+                                  int64_t Kout, int64_t Cin, int layout, void* ws, size_t ws_bytes,
+                                  mx_stream_t stream) {
   int rc = conv_check(s);
   if (rc) return rc;
   MX_CHECK_ARG(s->K % 8 == 0 && s->C % 8 == 0, "conv wgrad: K and C must be multiples of 8");
+  MX_CHECK_ARG(Kout >= 1 && Kout <= s->K && Cin >= 1 && Cin <= s->C, "conv wgrad: Kout/Cin out of range");
+  MX_CHECK_ARG(layout == 0 || layout == 1, "conv wgrad: layout 0 (KRSC) or 1 (KCRS)");
+  MX_CHECK_ARG(s->K * s->R * s->S * s->C < (1ll << 31), "conv wgrad: weight too large");
+  hipStream_t st = (hipStream_t)stream;
   WgP p{};
   p.dy = dy; p.x = x; p.dw = dw;
   p.P = s->N * s->Ho * s->Wo; p.K = s->K; p.Ncol = s->R * s->S * s->C;
   p.OH = s->Ho; p.OW = s->Wo; p.H = s->H; p.W = s->W; p.C = s->C;
   p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
-  int64_t tiles = cdiv(p.K, 128) * cdiv(p.Ncol, 128);
-  const bool glds = g_conv_variant == 2;  // direct-to-LDS wgrad: correct but slower so far (see DESIGN)
-  const int bk = glds ? BKG : BKW;
-  // split the pixel axis so that the grid covers the chip ~4x, at >= 4-8 K-tiles per split
-  int64_t splits = cdiv(1024, tiles);
-  int64_t max_splits = std::max<int64_t>(1, p.P / (bk * (glds ? 4 : 8)));
-  splits = std::max<int64_t>(1, std::min(splits, max_splits));
-  p.kchunk = cdiv(cdiv(p.P, splits), bk) * bk;
-  splits = cdiv(p.P, p.kchunk);
-  MX_CHECK_ARG(tiles < (1ll << 31) && splits < 65536, "conv wgrad: grid too large");
-  dim3 grid((unsigned)tiles, (unsigned)splits);
-  if (glds) conv_wgrad_glds_kernel<<<grid, NT, 2 * 2 * BKG * 256, (hipStream_t)stream>>>(p);
-  else conv_wgrad_kernel<<<grid, NT, 0, (hipStream_t)stream>>>(p);
+  p.Kout = Kout; p.Cin = Cin; p.layout = layout;
+  WGeo g = wgrad_geo(s);
+  p.kchunk = g.kchunk;
+  if (g.splits > 1) {
+    const size_t need = sizeof(float) * (size_t)g.splits * p.K * p.Ncol;
+    MX_CHECK_ARG(ws && ws_bytes >= need, "conv wgrad: split workspace of %zu bytes required (mx_conv_workspace pass 2)",
+                 need);
+    p.slab = (float*)ws;
+  }
+  MX_CHECK_ARG(g.tiles < (1ll << 31) && g.splits < 65536, "conv wgrad: grid too large");
+  dim3 grid((unsigned)g.tiles, (unsigned)g.splits);
+  const int v = g_wgrad_variant;
+  if (v == 2) conv_wgrad_glds_kernel<<<grid, NT, 2 * 2 * BKG * 256, st>>>(p);
+  else if (v == 1) conv_wgrad_kernel<64><<<grid, NT, 0, st>>>(p);
+  else conv_wgrad_kernel<32><<<grid, NT, 0, st>>>(p);
   MX_LAUNCH_CHECK();
+  if (g.splits > 1) {
+    wgrad_reduce_kernel<<<(unsigned)cdiv(Kout * (p.Ncol / 4), 256), 256, 0, st>>>(p, (int)g.splits);
+    MX_LAUNCH_CHECK();
+  }
   return MX_OK;
+}
+
+extern "C" int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw, mx_stream_t stream) {
+  // convenience form: dw [K][R][S][C] f32 (overwritten), temporaries allocated per call
+  int rc = conv_check(s);
+  if (rc) return rc;
+  size_t wsb = wgrad_ws(s);
+  void* ws = nullptr;
+  if (wsb) MX_HIP(hipMallocAsync(&ws, wsb, (hipStream_t)stream));
+  rc = mx_conv2d_wgrad_ex(s, dy, x, dw, s->K, s->C, 0, ws, wsb, stream);
+  if (ws) MX_HIP(hipFreeAsync(ws, (hipStream_t)stream));
+  return rc;
 }

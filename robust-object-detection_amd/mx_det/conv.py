@@ -144,13 +144,18 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad):
     return dx
 
 
-def conv_wgrad(dy, x, K, R, S, stride, pad):
-    """-> dW f32 [K,R,S,C]."""
+def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None):
+    """dy NHWC bf16 [N,Ho,Wo,K], x NHWC bf16 -> dW f32 [kout, cin, R, S] (torch weight layout; the
+    zero-padded channels K > kout, C > cin are dropped)."""
     sh = shape(x, K, R, S, stride, pad)
-    dw = torch.zeros((K, R, S, x.shape[3]), dtype=torch.float32, device=x.device)
+    kout = kout or K
+    cin = cin or x.shape[3]
+    dw = torch.empty((kout, cin, R, S), dtype=torch.float32, device=x.device)
     dyc = dy.contiguous()
+    wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 2)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=x.device) if wsb else None
     t0 = _timer.start() if _timer else None
-    call("mx_conv2d_wgrad", ctypes.byref(sh), _p(dyc), _p(x), _p(dw), _s())
+    call("mx_conv2d_wgrad_ex", ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws), wsb, _s())
     if _timer:
         _timer.stop("wgrad", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * x.shape[3], t0,
                     _tag(sh.N, sh.H, sh.W, x.shape[3], K, R, S, stride))
@@ -193,8 +198,7 @@ class ConvAct(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad)
         if ctx.needs_input_grad[1]:
-            dwk = conv_wgrad(gk, x, K8, R, S, stride, pad)[:K]
-            dw = dwk[..., : wshape[1]].permute(0, 3, 1, 2)
+            dw = conv_wgrad(gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1])
         if has_b and ctx.needs_input_grad[2]:
             db = g.float().sum(dim=(0, 1, 2))
         return dx, dw, db, None, None, None, None
@@ -238,8 +242,7 @@ class ConvBNAct(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad)
         if ctx.needs_input_grad[1]:
-            dwk = conv_wgrad(dz, x, K, R, S, stride, pad)
-            dw = dwk[..., : wshape[1]].permute(0, 3, 1, 2)
+            dw = conv_wgrad(dz, x, K, R, S, stride, pad, cin=wshape[1])
         dgamma = sums[1] if ctx.needs_input_grad[2] else None
         dbeta = sums[0] if ctx.needs_input_grad[3] else None
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None

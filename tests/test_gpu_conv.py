@@ -32,8 +32,11 @@ def variant(request):
     from mx_det import _lib
     old = _lib.load().mx_conv_get_variant()
     _lib.call("mx_conv_set_variant", request.param)
+    oldw = _lib.load().mx_conv_get_wgrad_variant()
+    _lib.call("mx_conv_set_wgrad_variant", {0: 0, 1: 2, 3: 1}.get(request.param, 1))
     yield request.param
     _lib.call("mx_conv_set_variant", old)
+    _lib.call("mx_conv_set_wgrad_variant", oldw)
 
 
 def _scale(x, w, k):
@@ -93,7 +96,7 @@ def test_conv_dgrad_wgrad(dev, variant, N, H, W, C, K, k, st, pd):
     tol = 2e-5 * (dy.abs().amax() * w.abs().amax() * K * k * k).item()
     torch.testing.assert_close(dx.float().cpu(), ref_dx, rtol=1e-2, atol=tol + 1e-2 * ref_dx.abs().amax().item())
     dw = mc.conv_wgrad(dyn, x.to(dev), K, k, k, (st, st), (pd, pd))
-    ref_dw = wr.grad.permute(0, 2, 3, 1)
+    ref_dw = wr.grad
     tolw = 2e-5 * (dy.abs().amax() * x.abs().amax()).item() * dy.numel() / K
     torch.testing.assert_close(dw.cpu(), ref_dw, rtol=0, atol=tolw)
 
@@ -157,3 +160,48 @@ def test_dgrad_convenience_entry_matches_packed(dev, st, k, pd):
     _lib.call("mx_conv2d_dgrad", ctypes.byref(sh), mc._p(dy), mc._p(wk), mc._p(dx), mc._s())
     torch.cuda.synchronize()
     assert torch.equal(dx, ref)
+
+
+def test_wgrad_layouts_and_channel_padding(dev):
+    """mx_conv2d_wgrad_ex writes KCRS (torch) and KRSC layouts and drops zero-padded channels; the
+    convenience mx_conv2d_wgrad (KRSC, all channels) agrees with both."""
+    import ctypes
+    from mx_det import _lib, conv as mc
+    g = torch.Generator().manual_seed(5)
+    N, H, W, C, K, k = 2, 21, 19, 16, 40, 3
+    x = torch.randn(N, H, W, C, generator=g).bfloat16()
+    x[..., 11:] = 0          # channels 11.. are padding
+    dy = torch.randn(N, H, W, K, generator=g).bfloat16()
+    dy[..., 35:] = 0         # output channels 35.. are padding
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, k, k),
+                                      dy.float().permute(0, 3, 1, 2), 1, 1)
+    xd, dyd = x.to(dev), dy.to(dev)
+    dw = mc.conv_wgrad(dyd, xd, K, k, k, (1, 1), (1, 1), kout=35, cin=11)
+    tol = 2e-5 * (dy.abs().amax() * x.abs().amax()).item() * N * H * W
+    torch.testing.assert_close(dw.cpu(), ref[:35, :11], rtol=0, atol=tol)
+    sh = _lib.ConvShape(N, H, W, C, K, k, k, H, W, 1, 1, 1, 1)
+    wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 2)
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    krsc = torch.empty(35, k, k, 11, device=dev)
+    _lib.call("mx_conv2d_wgrad_ex", ctypes.byref(sh), mc._p(dyd), mc._p(xd), mc._p(krsc), 35, 11, 0, mc._p(ws),
+              wsb, mc._s())
+    full = torch.full((K, k, k, C), float("nan"), device=dev)
+    _lib.call("mx_conv2d_wgrad", ctypes.byref(sh), mc._p(dyd), mc._p(xd), mc._p(full), mc._s())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(krsc.permute(0, 3, 1, 2).cpu(), dw.cpu(), rtol=0, atol=0)
+    torch.testing.assert_close(full.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=tol)
+
+
+@pytest.mark.parametrize("target", [64, 512, 4096])
+def test_wgrad_split_counts_agree(dev, target):
+    """Unsplit (direct store) and split (slab + reduce) wgrad give the same weights."""
+    from mx_det import _lib, conv as mc
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 30, 40, 64, generator=g).bfloat16().to(dev)
+    dy = torch.randn(2, 30, 40, 128, generator=g).bfloat16().to(dev)
+    _lib.call("mx_conv_set_wgrad_target", 1)
+    ref = mc.conv_wgrad(dy, x, 128, 3, 3, (1, 1), (1, 1))
+    _lib.call("mx_conv_set_wgrad_target", target)
+    dw = mc.conv_wgrad(dy, x, 128, 3, 3, (1, 1), (1, 1))
+    _lib.call("mx_conv_set_wgrad_target", 0)
+    torch.testing.assert_close(dw, ref, rtol=1e-5, atol=1e-3)

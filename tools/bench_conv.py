@@ -46,12 +46,18 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--variants", default="7")
+    ap.add_argument("--wgrad", default="0")
+    ap.add_argument("--wtarget", default="0")
     args = ap.parse_args()
     from mx_det import _lib
     for v in [int(x) for x in args.variants.split(",")]:
-        _lib.call("mx_conv_set_variant", v)
-        print(f"== conv variant {v}", flush=True)
-        run(args)
+        for wv in [int(x) for x in args.wgrad.split(",")]:
+            for wt in [int(x) for x in args.wtarget.split(",")]:
+                _lib.call("mx_conv_set_variant", v)
+                _lib.call("mx_conv_set_wgrad_variant", wv)
+                _lib.call("mx_conv_set_wgrad_target", wt)
+                print(f"== conv variant {v} wgrad variant {wv} wgrad target {wt}", flush=True)
+                run(args)
 
 
 def run(args):
