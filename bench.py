@@ -97,7 +97,7 @@ def conv_roofline(model, opt, imgs, tg):
         train_step(model, opt, imgs, tg)
     finally:
         mc.set_timer(None)
-    s = t.summary()
+    s = {k: v for k, v in t.summary().items() if not k.startswith("bn_")}  # conv kinds only
     dom = max(s, key=lambda k: s[k]["ms"])
     d = s[dom]
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12

@@ -211,8 +211,19 @@ int mx_bn_finalize(const float* stats, int64_t mblocks, int64_t K, int64_t count
                    float* mean_out, float* invstd_out, float* scale_out, float* shift_out, mx_stream_t stream);
 int mx_bn_apply(const void* x, int xdtype, int64_t M, int64_t K, const float* scale, const float* shift,
                 const uint16_t* residual, int act, uint16_t* y, mx_stream_t stream);
+/* Hot-path backward: reduce_ex = per-row-block partials (workspace mx_bn_bwd_workspace bytes, no
+ * atomics) + an f64 column reduce writing sums[2][K] = (sum g, sum g*xhat) = (dbeta, dgamma) and
+ * coef[3][K], the per-channel affine form dx = coef0*g + coef1*x + coef2; apply_ex streams
+ * dx (and dres = g, nullable). g = dy * act'(y); y may be null when act == 0. */
+size_t mx_bn_bwd_workspace(int64_t M, int64_t K);
+int mx_bn_bwd_reduce_ex(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
+                        const float* mean, const float* invstd, const float* gamma, void* ws, size_t ws_bytes,
+                        float* sums, float* coef, mx_stream_t stream);
+int mx_bn_bwd_apply_ex(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
+                       const float* coef, uint16_t* dx, uint16_t* dres, mx_stream_t stream);
+/* Convenience forms (allocate per call): sums[2][K] is overwritten. */
 int mx_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
-                     const float* mean, const float* invstd, float* sums /*[2][K] zeroed*/, mx_stream_t stream);
+                     const float* mean, const float* invstd, float* sums, mx_stream_t stream);
 int mx_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
                     const float* mean, const float* invstd, const float* gamma, const float* sums,
                     uint16_t* dx, uint16_t* dres /*nullable: grad of residual = masked dy*/,

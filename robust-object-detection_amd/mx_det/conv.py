@@ -220,7 +220,10 @@ class ConvBNAct(torch.autograd.Function):
              float(momentum), _p(rmean), _p(rvar), _p(mean), _p(invstd), _p(scale), _p(shift), _s())
         y = torch.empty_like(z)
         res = residual.contiguous() if residual is not None else None
+        t0 = _timer.start() if _timer else None
         call("mx_bn_apply", _p(z), 1, M, K, _p(scale), _p(shift), _p(res), int(act), _p(y), _s())
+        if _timer:  # bn kinds record algorithmic HBM bytes instead of FLOPs
+            _timer.stop("bn_apply", M * K * (4 + (2 if res is not None else 0)), t0, f"{M}x{K}")
         ctx.save_for_backward(x, wt if need_dx else None, z, y, mean, invstd, gamma)
         ctx.cfg = (stride, pad, act, w.shape, residual is not None)
         return y
@@ -232,12 +235,21 @@ class ConvBNAct(torch.autograd.Function):
         K, _, R, S = wshape
         M = z.numel() // K
         gy = gy.to(torch.bfloat16).contiguous()
-        sums = torch.zeros((2, K), dtype=torch.float32, device=z.device)
-        call("mx_bn_bwd_reduce", _p(gy), _p(y), _p(z), M, K, int(act), _p(mean), _p(invstd), _p(sums), _s())
+        sums = torch.empty((2, K), dtype=torch.float32, device=z.device)
+        coef = torch.empty((3, K), dtype=torch.float32, device=z.device)
+        wsb = _lib.load().mx_bn_bwd_workspace(M, K)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
+        t0 = _timer.start() if _timer else None
+        call("mx_bn_bwd_reduce_ex", _p(gy), _p(y), _p(z), M, K, int(act), _p(mean), _p(invstd), _p(gamma.detach()),
+             _p(ws), wsb, _p(sums), _p(coef), _s())
+        if _timer:
+            _timer.stop("bn_bwd_reduce", M * K * (6 if act else 4), t0, f"{M}x{K}")
         dz = torch.empty_like(z)
         dres = torch.empty_like(z) if has_res else None
-        call("mx_bn_bwd_apply", _p(gy), _p(y), _p(z), M, K, int(act), _p(mean), _p(invstd), _p(gamma.detach()),
-             _p(sums), _p(dz), _p(dres), _s())
+        t0 = _timer.start() if _timer else None
+        call("mx_bn_bwd_apply_ex", _p(gy), _p(y), _p(z), M, K, int(act), _p(coef), _p(dz), _p(dres), _s())
+        if _timer:
+            _timer.stop("bn_bwd_apply", M * K * (8 + (2 if has_res else 0)), t0, f"{M}x{K}")
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad)

@@ -35,7 +35,19 @@ def main():
     mc.set_timer(t)
     bench.train_step(model, opt, imgs, tg)
     mc.set_timer(None)
-    rows = sorted(t.summary(by_tag=True).items(), key=lambda kv: -kv[1]["ms"])
+    allrows = t.summary(by_tag=True).items()
+    bn = sorted([kv for kv in allrows if kv[0][0].startswith("bn_")], key=lambda kv: -kv[1]["ms"])
+    rows = sorted([kv for kv in allrows if not kv[0][0].startswith("bn_")], key=lambda kv: -kv[1]["ms"])
+    btot = {}
+    for (kind, tag), d in bn:
+        a = btot.setdefault(kind, [0, 0.0, 0.0])
+        a[0] += d["launches"]
+        a[1] += d["ms"]
+        a[2] += d["flops"]
+    for k, (n, ms, by) in sorted(btot.items()):
+        print(f"  {k:14s} {n:4d} launches {ms:7.3f} ms {by / ms / 1e6:7.1f} GB/s")
+    for (kind, tag), d in bn[:20]:
+        print(f"{kind:14s} {tag:16s} x{d['launches']:<3d} {d['ms']:7.3f} ms {d['flops'] / d['ms'] / 1e6:7.1f} GB/s")
     tot = {}
     for (kind, tag), d in rows:
         a = tot.setdefault(kind, [0, 0.0, 0.0])
