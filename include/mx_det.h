@@ -174,6 +174,23 @@ int mx_conv_get_wgrad_variant(void);
 int mx_conv_pack_weight(const mx_conv_shape* s, const float* w, int64_t Cin, int64_t Kout, uint16_t* wk, uint16_t* wt,
                         mx_stream_t stream);
 size_t mx_conv_dgrad_weight_elems(const mx_conv_shape* s, int64_t Cpad, int64_t Kpad);
+/* The same packing for a list of weights in ONE launch (per-step operand preparation of a whole
+ * model). A job: f32 w[Kout][Cin][R][S] -> wk [Kout][R][S][Cpad] (nullable) and wt, the dgrad layout
+ * with Cpad / Kpad (nullable). `plan` is a caller-owned device buffer of mx_conv_pack_plan_bytes(njobs)
+ * holding the job table; upload=1 (re)writes it from `jobs` (synchronizes the stream; do it when the
+ * job list changes), upload=0 reuses it. */
+typedef struct {
+  const float* w;
+  uint16_t* wk;
+  uint16_t* wt;
+  int64_t Cin, Kout, Cpad, Kpad;
+  int32_t R, S, stride_h, stride_w, pad_h, pad_w;
+  int32_t flags; /* bit 0: "dense" dgrad layout [R][S][Cpad][Kpad] for a conv whose output is 1x1 (FC6 as a
+                    valid 7x7 conv): its dgrad runs as the 1x1 GEMM dX[N, R*S*C] = dY[N, K] * W */
+} mx_pack_desc;
+size_t mx_conv_pack_plan_bytes(int64_t njobs);
+int mx_conv_pack_batched(const mx_pack_desc* jobs, int64_t njobs, void* plan, size_t plan_bytes, int upload,
+                         mx_stream_t stream);
 /* [K][RS][C] -> [C][RS][K] bf16 (the stride-1 dgrad layout). */
 int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS, int64_t C, uint16_t* wt, mx_stream_t stream);
 int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx, void* ws,

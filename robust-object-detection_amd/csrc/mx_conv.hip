@@ -19,6 +19,8 @@
 // over pixels with f32 atomic accumulation.
 #include "mx_common.h"
 
+#include <vector>
+
 namespace mx {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -981,13 +983,12 @@ struct PackP {
   int R, S, st_h, st_w;
   int64_t off[4];
   int Rc[4], Sc[4];
+  int dense;  // wt as [R][S][Cpad][Kpad]: the 1x1-GEMM dgrad operand of a conv whose output is 1x1
 };
 
-__global__ void __launch_bounds__(256) pack_weight_kernel(PackP p) {
-  __shared__ float T[64][65];
+__device__ __forceinline__ void pack_tile(const PackP& p, int64_t c0, int64_t k0, int rs, float (*T)[65]) {
   const int tid = threadIdx.x;
-  const int64_t c0 = (int64_t)blockIdx.x * 64, k0 = (int64_t)blockIdx.y * 64;
-  const int rs = blockIdx.z, r = rs / p.S, sx = rs - (rs / p.S) * p.S, RS = p.R * p.S;
+  const int r = rs / p.S, sx = rs - (rs / p.S) * p.S, RS = p.R * p.S;
   for (int e = tid; e < 64 * 64; e += 256) {
     const int kk = e >> 6, cc = e & 63;
     const int64_t k = k0 + kk, c = c0 + cc;
@@ -1001,7 +1002,13 @@ __global__ void __launch_bounds__(256) pack_weight_kernel(PackP p) {
       if (k < p.K && c < p.Cpad) p.wk[(k * RS + rs) * p.Cpad + c] = f2bf(T[kk][cc]);
     }
   }
-  if (p.wt) {
+  if (p.wt && p.dense) {
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int cc = e >> 6, kk = e & 63;
+      const int64_t k = k0 + kk, c = c0 + cc;
+      if (k < p.Kpad && c < p.Cpad) p.wt[((int64_t)rs * p.Cpad + c) * p.Kpad + k] = f2bf(T[kk][cc]);
+    }
+  } else if (p.wt) {
     const int ph = r % p.st_h, pw = sx % p.st_w;  // (parity of the tap) -> class with r0 = r % st
     const int q = ph * p.st_w + pw;
     const int ri = r / p.st_h, si = sx / p.st_w;
@@ -1013,6 +1020,32 @@ __global__ void __launch_bounds__(256) pack_weight_kernel(PackP p) {
         p.wt[base + ((c * p.Rc[q] + ri) * p.Sc[q] + si) * p.Kpad + k] = f2bf(T[kk][cc]);
     }
   }
+}
+
+__global__ void __launch_bounds__(256) pack_weight_kernel(PackP p) {
+  __shared__ float T[64][65];
+  pack_tile(p, (int64_t)blockIdx.x * 64, (int64_t)blockIdx.y * 64, blockIdx.z, T);
+}
+
+// Every conv weight of a step in one launch: block -> (job, tile) through the tile prefix sums.
+__device__ __forceinline__ int64_t pack_tiles_c(const PackP& p) { return (p.Cpad + 63) / 64; }
+__device__ __forceinline__ int64_t pack_tiles_k(const PackP& p) { return ((p.wt ? p.Kpad : p.K) + 63) / 64; }
+
+__global__ void __launch_bounds__(256) pack_batched_kernel(const PackP* __restrict__ jobs, const int64_t* __restrict__ prefix,
+                                                           int njobs) {
+  __shared__ float T[64][65];
+  const int64_t b = blockIdx.x;
+  int lo = 0, hi = njobs - 1;  // last job with prefix[j] <= b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (prefix[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const PackP p = jobs[lo];
+  const int64_t t = b - prefix[lo];
+  const int64_t nc = pack_tiles_c(p), nk = pack_tiles_k(p);
+  const int64_t cx = t % nc, ky = (t / nc) % nk;
+  const int rs = (int)(t / (nc * nk));
+  pack_tile(p, cx * 64, ky * 64, rs, T);
 }
 
 // KRSC bf16 weight -> the dgrad parity-class layout of pack_weight_kernel (element-wise; used by
@@ -1276,6 +1309,63 @@ extern "C" int mx_conv_pack_weight(const mx_conv_shape* s, const float* w, int64
   // wk covers Kout rows only; wt also covers the zero-padded output channels up to s->K
   dim3 grid((unsigned)cdiv(s->C, 64), (unsigned)cdiv(wt ? s->K : Kout, 64), (unsigned)(s->R * s->S));
   pack_weight_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(p);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+static int make_pack(const mx_pack_desc& d, PackP& p, int64_t& tiles) {
+  MX_CHECK_ARG(d.w && d.R > 0 && d.S > 0 && d.Cin > 0 && d.Kout > 0 && d.Cin <= d.Cpad && d.Kout <= d.Kpad,
+               "conv pack: bad job");
+  MX_CHECK_ARG(!d.wt || (d.stride_h >= 1 && d.stride_h <= 2 && d.stride_w >= 1 && d.stride_w <= 2),
+               "conv pack: dgrad layout supports strides 1 and 2");
+  p = PackP{};
+  p.w = d.w; p.wk = d.wk; p.wt = d.wt;
+  p.K = d.Kout; p.C = d.Cin; p.Cpad = d.Cpad; p.Kpad = d.Kpad;
+  p.R = d.R; p.S = d.S; p.st_h = d.stride_h; p.st_w = d.stride_w;
+  p.dense = d.flags & 1;
+  if (d.wt && !p.dense) {
+    mx_conv_shape s{};
+    s.C = d.Cpad; s.K = d.Kpad; s.R = d.R; s.S = d.S; s.H = 1; s.W = 1;
+    s.stride_h = d.stride_h; s.stride_w = d.stride_w; s.pad_h = d.pad_h; s.pad_w = d.pad_w;
+    DClass cl[4];
+    dgrad_classes(&s, d.Cpad, d.Kpad, cl, p.off, p.Rc, p.Sc);
+  } else {
+    p.st_h = p.st_w = 1;
+  }
+  tiles = cdiv(d.Cpad, 64) * cdiv(d.wt ? d.Kpad : d.Kout, 64) * (int64_t)d.R * d.S;
+  return MX_OK;
+}
+
+extern "C" size_t mx_conv_pack_plan_bytes(int64_t njobs) {
+  return njobs > 0 ? sizeof(PackP) * (size_t)njobs + sizeof(int64_t) * (size_t)(njobs + 1) : 0;
+}
+
+extern "C" int mx_conv_pack_batched(const mx_pack_desc* jobs, int64_t njobs, void* plan, size_t plan_bytes, int upload,
+                                    mx_stream_t stream) {
+  MX_CHECK_ARG(jobs && njobs > 0 && njobs < (1 << 20), "conv pack batched: bad job list");
+  MX_CHECK_ARG(plan && plan_bytes >= mx_conv_pack_plan_bytes(njobs), "conv pack batched: plan buffer too small");
+  std::vector<PackP> host((size_t)njobs);
+  std::vector<int64_t> prefix((size_t)njobs + 1, 0);
+  for (int64_t j = 0; j < njobs; ++j) {
+    int64_t t = 0;
+    int rc = make_pack(jobs[j], host[(size_t)j], t);
+    if (rc) return rc;
+    if (!jobs[j].wk && !jobs[j].wt) t = 0;
+    prefix[(size_t)j + 1] = prefix[(size_t)j] + t;
+  }
+  const int64_t total = prefix[(size_t)njobs];
+  MX_CHECK_ARG(total < (1ll << 31), "conv pack batched: too many tiles");
+  hipStream_t st = (hipStream_t)stream;
+  PackP* dj = (PackP*)plan;
+  int64_t* dp = (int64_t*)((char*)plan + sizeof(PackP) * (size_t)njobs);
+  if (upload) {
+    // the host vectors die with this call: synchronous copies (the plan changes rarely)
+    MX_HIP(hipStreamSynchronize(st));
+    MX_HIP(hipMemcpy(dj, host.data(), sizeof(PackP) * (size_t)njobs, hipMemcpyHostToDevice));
+    MX_HIP(hipMemcpy(dp, prefix.data(), sizeof(int64_t) * (size_t)(njobs + 1), hipMemcpyHostToDevice));
+  }
+  if (total == 0) return MX_OK;
+  pack_batched_kernel<<<(unsigned)total, 256, 0, st>>>(dj, dp, (int)njobs);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

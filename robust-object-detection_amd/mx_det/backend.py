@@ -71,6 +71,23 @@ class HipBackend:
     act_dtype = torch.bfloat16
     stem_channels = 8  # RGB padded to 8 channels for the 16-B gather of the stem conv
 
+    def prepare(self, model):
+        """Register every conv weight of the model with one WeightPacker (first call) and repack the
+        changed ones in a single launch; the conv autograd functions then read the packed operands."""
+        pk = model.__dict__.get("_mx_packer")
+        if pk is None:
+            from .frcnn import FastRCNNConvFCHead
+            pk = mc.WeightPacker()
+            for m in model.modules():
+                if isinstance(m, mc.Conv2d):
+                    pk.register(m.weight, m.stride, m.padding, m.weight.requires_grad)
+                elif isinstance(m, FastRCNNConvFCHead):
+                    for i, (lin, w) in enumerate(m.fc_weight_views()):
+                        pk.register(w, (1, 1), (0, 0), lin.weight.requires_grad, dense=i == 0)
+            model.__dict__["_mx_packer"] = pk
+        mc.set_packer(pk)
+        pk.refresh()
+
     # ---- dense ---------------------------------------------------------------------------
     def conv_bn(self, x, conv, bn, act, residual=None):
         return mc.conv_bn(x, conv, bn, act, residual)

@@ -125,6 +125,116 @@ def pack_weight(w, cin_pad=None, stride=(1, 1), pad=(0, 0), kpad=None, krsc=True
     return wk, wt
 
 
+def _ceil8(n):
+    return (n + 7) // 8 * 8
+
+
+class PackDesc(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p), ("wk", ctypes.c_void_p), ("wt", ctypes.c_void_p), ("Cin", ctypes.c_int64),
+                ("Kout", ctypes.c_int64), ("Cpad", ctypes.c_int64), ("Kpad", ctypes.c_int64), ("R", ctypes.c_int32),
+                ("S", ctypes.c_int32), ("stride_h", ctypes.c_int32), ("stride_w", ctypes.c_int32),
+                ("pad_h", ctypes.c_int32), ("pad_w", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+class _Entry:
+    __slots__ = ("w", "cp", "kp", "stride", "pad", "wk", "wt", "version", "dense")
+
+
+class WeightPacker:
+    """Per-step bf16 conv operands of a whole model, packed in ONE launch (mx_conv_pack_batched).
+
+    Weights are registered once (f32 parameter or a view of one, its padded channel counts, stride,
+    pad, whether the dgrad layout is needed); `refresh()` repacks exactly the entries whose version
+    counter moved since they were packed (optimizer step, load_state_dict) -- frozen layers are
+    packed once. ConvAct / ConvBNAct take their operands from here when registered and fall back
+    to a per-call pack_weight otherwise. Buffers are rewritten in place on the stream, so a
+    backward must run before the next refresh that changes its weights (the train loop's order)."""
+
+    def __init__(self):
+        self.entries = {}
+        self.order = []
+        self._plan = None
+        self._plan_key = None
+        self._descs = None
+
+    @staticmethod
+    def key(w, cp, kp, stride, pad):
+        return (w.data_ptr(), tuple(w.shape), cp, kp, tuple(stride), tuple(pad))
+
+    def register(self, w, stride, pad, dgrad, dense=False):
+        """dense: the conv covers its whole input (output 1x1, e.g. FC6 as a 7x7 conv on the RoI tile);
+        its dgrad operand is laid out for the 1x1-GEMM form."""
+        K, C, R, S = w.shape
+        cp, kp = _ceil8(C), _ceil8(K)
+        k = self.key(w, cp, kp, stride, pad)
+        if k in self.entries:
+            return
+        e = _Entry()
+        e.w, e.cp, e.kp, e.stride, e.pad, e.dense = w, cp, kp, tuple(stride), tuple(pad), bool(dense)
+        e.wk = torch.empty((K, R, S, cp), dtype=torch.bfloat16, device=w.device)
+        e.wt = torch.empty(cp * R * S * kp, dtype=torch.bfloat16, device=w.device) if dgrad else None
+        e.version = None
+        self.entries[k] = e
+        self.order.append(k)
+
+    def refresh(self):
+        dirty = [k for k in self.order if self.entries[k].version != self.entries[k].w._version]
+        if not dirty:
+            return
+        upload = tuple(dirty) != self._plan_key
+        if upload:
+            descs = (PackDesc * len(dirty))()
+            for i, k in enumerate(dirty):
+                e = self.entries[k]
+                K, C, R, S = e.w.shape
+                descs[i] = PackDesc(e.w.data_ptr(), e.wk.data_ptr(), e.wt.data_ptr() if e.wt is not None else None,
+                                    C, K, e.cp, e.kp, R, S, e.stride[0], e.stride[1], e.pad[0], e.pad[1],
+                                    1 if e.dense else 0)
+            nb = _lib.load().mx_conv_pack_plan_bytes(len(dirty))
+            self._plan = torch.empty(nb, dtype=torch.uint8, device=self.entries[dirty[0]].w.device)
+            self._descs = descs
+            self._plan_key = tuple(dirty)
+        call("mx_conv_pack_batched", ctypes.cast(self._descs, ctypes.c_void_p), len(dirty), _p(self._plan),
+             self._plan.numel(), int(upload), _s())
+        for k in dirty:
+            e = self.entries[k]
+            e.version = e.w._version
+
+    def lookup(self, w, cp, kp, stride, pad, dgrad, dense=False):
+        e = self.entries.get(self.key(w, cp, kp, stride, pad))
+        if e is None or e.version != w._version or (dgrad and (e.wt is None or e.dense != dense)):
+            return None
+        return e.wk, e.wt
+
+
+_packer = None
+
+
+def set_packer(p):
+    global _packer
+    _packer = p
+
+
+def operands(w, cin_pad, stride, pad, kpad, dgrad, dense=False):
+    """(wk, wt) for a conv weight: from the model's WeightPacker when registered and current, else
+    packed now (one launch; the dense dgrad layout by a transpose of wk)."""
+    if _packer is not None:
+        r = _packer.lookup(w, cin_pad, kpad, stride, pad, dgrad, dense)
+        if r is not None:
+            return r
+    if dense and dgrad:
+        wk, _ = pack_weight(w, cin_pad, stride, pad)
+        K = wk.shape[0]
+        wt = torch.nn.functional.pad(wk.reshape(K, -1).t(), (0, kpad - K)).contiguous().view(-1)
+        return wk, wt
+    return pack_weight(w, cin_pad, stride, pad, kpad=kpad, dgrad=dgrad)
+
+
+def _is_dense(x_shape, R, S, stride, pad):
+    """A conv whose single output pixel sees the whole input (valid RxS conv on an RxS map)."""
+    return (x_shape[1], x_shape[2]) == (R, S) and tuple(pad) == (0, 0) and R * S > 1
+
+
 def conv_dgrad(dy, wt, x_shape, R, S, stride, pad):
     """dy NHWC bf16 [N,Ho,Wo,K] (K = the wt's padded output channels), wt from
     pack_weight(dgrad=True) -> dx NHWC bf16 [N,H,W,C]."""
@@ -177,8 +287,9 @@ class ConvAct(torch.autograd.Function):
     def forward(ctx, x, w, b, stride, pad, act, out_dtype):
         K = w.shape[0]
         need_dx = ctx.needs_input_grad[0]
+        dense = _is_dense(x.shape, w.shape[2], w.shape[3], stride, pad)
         # narrow heads (RPN cls+box 15, predictor 35): the dgrad operand is zero-padded to K8
-        wk, wt = pack_weight(w, x.shape[3], stride, pad, kpad=(K + 7) // 8 * 8, dgrad=need_dx)
+        wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(K), need_dx, dense)
         y = conv_fwd(x, wk, stride, pad, bias=b.detach() if b is not None else None, act=act, out_dtype=out_dtype)
         ctx.save_for_backward(x, y, wt if need_dx else None)
         ctx.cfg = (stride, pad, act, w.shape, b is not None)
@@ -196,7 +307,11 @@ class ConvAct(torch.autograd.Function):
         if K8 != K:
             gk = torch.nn.functional.pad(g, (0, K8 - K)).contiguous()
         if ctx.needs_input_grad[0]:
-            dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad)
+            if _is_dense(x.shape, R, S, stride, pad):  # 1x1-GEMM form: dX[N, R*S*C] = dY[N, K8] wt
+                N, H, W, C = x.shape
+                dx = conv_dgrad(gk.view(N, 1, 1, K8), wt, (N, 1, 1, H * W * C), 1, 1, (1, 1), (0, 0)).view(N, H, W, C)
+            else:
+                dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad)
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad(gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1])
         if has_b and ctx.needs_input_grad[2]:
@@ -210,7 +325,7 @@ class ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, gamma, beta, residual, rmean, rvar, stride, pad, act, eps, momentum):
         need_dx = ctx.needs_input_grad[0]
-        wk, wt = pack_weight(w, x.shape[3], stride, pad, dgrad=need_dx)
+        wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(w.shape[0]), need_dx)
         z, st = conv_fwd(x, wk, stride, pad, stats=True)
         K = wk.shape[0]
         M = z.numel() // K

@@ -351,8 +351,9 @@ class FastRCNNPredictor(nn.Module):
 
 
 class FastRCNNConvFCHead(nn.Sequential):
-    """FastRCNNConvFCHead((256,7,7), [256]*4, [1024], norm_layer=BatchNorm2d). FC6/FC7 run as 1x1 MFMA
-    GEMMs; FC6's weight columns are permuted from torch's NCHW flatten order to the NHWC tile order."""
+    """FastRCNNConvFCHead((256,7,7), [256]*4, [1024], norm_layer=BatchNorm2d). FC6 runs as a valid 7x7
+    conv over the NHWC RoI tile: torch's NCHW flatten + Linear is exactly a conv whose KCRS weight is
+    the Linear weight viewed [1024, 256, 7, 7] (no permute copy, forward or backward); FC7 as 1x1."""
 
     def __init__(self, in_channels=256, conv_layers=(256, 256, 256, 256), fc_layers=(1024,), hw=7):
         blocks, prev = [], in_channels
@@ -373,21 +374,28 @@ class FastRCNNConvFCHead(nn.Sequential):
                 if m.bias is not None:
                     nn.init.zeros_(m.bias)
 
+    def fc_weight_views(self):
+        """(Linear, its conv-shaped weight view) for FC6 (valid hw x hw conv) and the following FCs (1x1)."""
+        out, first = [], True
+        for m in self:
+            if isinstance(m, Linear):
+                w = m.weight
+                if first:
+                    c = m.in_features // (self.hw * self.hw)
+                    out.append((m, w.view(m.out_features, c, self.hw, self.hw)))
+                    first = False
+                else:
+                    out.append((m, w[:, :, None, None]))
+        return out
+
     def forward(self, x, be):
-        first = True
+        fcs = iter(self.fc_weight_views())
         for m in self:
             if isinstance(m, ConvNormAct):
                 x = m(x, be)
             elif isinstance(m, Linear):
-                w = m.weight
-                if first:
-                    # torch flattens the RoI tile in (C, H, W) order; the NHWC tile flattens (H, W, C):
-                    # permute FC6's input dimension once and run it as a 1x1 GEMM over [R,1,1,H*W*C]
-                    R, H, W, C = x.shape
-                    w = w.view(m.out_features, C, H, W).permute(0, 2, 3, 1).reshape(m.out_features, H * W * C)
-                    x = x.reshape(R, 1, 1, H * W * C)
-                    first = False
-                x = be.conv(x, w[:, :, None, None], m.bias, (1, 1), (0, 0), ACT_RELU)  # Linear + ReLU
+                _, w = next(fcs)
+                x = be.conv(x, w, m.bias, (1, 1), (0, 0), ACT_RELU)  # Linear + ReLU; [R,7,7,C] -> [R,1,1,1024]
         return x  # [R, 1, 1, 1024]
 
 
@@ -568,6 +576,8 @@ class FasterRCNN(nn.Module):
 
     def forward(self, images, targets=None):
         be = self.be
+        if hasattr(be, "prepare"):
+            be.prepare(self)  # per-step operand preparation (HIP: every conv weight packed in one launch)
         if self.training:
             if targets is None:
                 raise ValueError("In training mode, targets should be passed")

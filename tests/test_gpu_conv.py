@@ -205,3 +205,65 @@ def test_wgrad_split_counts_agree(dev, target):
     dw = mc.conv_wgrad(dy, x, 128, 3, 3, (1, 1), (1, 1))
     _lib.call("mx_conv_set_wgrad_target", 0)
     torch.testing.assert_close(dw, ref, rtol=1e-5, atol=1e-3)
+
+
+def test_weight_packer_batched_matches_single_and_tracks_versions(dev):
+    """WeightPacker: one batched launch == per-weight pack_weight for every registered conv (strides 1/2,
+    padded stem channels, FC6 as a 7x7 view, narrow K); frozen weights are not repacked; an in-place
+    update (optimizer step) is picked up by the next refresh."""
+    from mx_det import conv as mc
+    g = torch.Generator().manual_seed(2)
+    specs = [((64, 3, 7, 7), (2, 2), (3, 3), True), ((256, 64, 1, 1), (1, 1), (0, 0), True),
+             ((128, 128, 3, 3), (2, 2), (1, 1), True), ((512, 256, 1, 1), (2, 2), (0, 0), False),
+             ((15, 256, 1, 1), (1, 1), (0, 0), True)]
+    ws = [(torch.randn(*shp, generator=g) * 0.1).to(dev) for shp, _, _, _ in specs]
+    fc = (torch.randn(1024, 256 * 49, generator=g) * 0.01).to(dev)
+    pk = mc.WeightPacker()
+    for w, (_, st, pd, dg) in zip(ws, specs):
+        pk.register(w, st, pd, dg)
+    fcv = fc.view(1024, 256, 7, 7)
+    pk.register(fcv, (1, 1), (0, 0), True, dense=True)
+    pk.refresh()
+    wk, wt = pk.lookup(fcv, 256, 1024, (1, 1), (0, 0), True, dense=True)
+    assert torch.equal(wk, mc.weight_krsc(fcv))
+    assert torch.equal(wt.view(-1, 1024), wk.reshape(1024, -1).t())  # [R*S*C][K]: the 1x1-GEMM dgrad operand
+    for w, (_, st, pd, dg) in zip(ws, specs):
+        K, C = w.shape[:2]
+        got = pk.lookup(w, mc._ceil8(C), mc._ceil8(K), st, pd, dg)
+        assert got is not None
+        ref = mc.pack_weight(w, mc._ceil8(C), st, pd, kpad=mc._ceil8(K), dgrad=dg)
+        assert torch.equal(got[0], ref[0])
+        if dg:
+            assert torch.equal(got[1], ref[1])
+    # in-place update of one weight -> stale until refresh, then repacked
+    ws[1].add_(1.0)
+    assert pk.lookup(ws[1], 64, 256, (1, 1), (0, 0), True) is None
+    pk.refresh()
+    got = pk.lookup(ws[1], 64, 256, (1, 1), (0, 0), True)
+    ref = mc.pack_weight(ws[1], 64, (1, 1), (0, 0), dgrad=True)
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+
+
+def test_fc6_dense_conv_matches_linear(dev):
+    """FC6 as a valid 7x7 conv over the NHWC RoI tile == torch flatten(NCHW) + Linear + ReLU, forward
+    and backward (the dense dgrad runs as a 1x1 GEMM)."""
+    from mx_det import conv as mc
+    g = torch.Generator().manual_seed(4)
+    R, C, K = 96, 256, 1024
+    x = torch.randn(R, 7, 7, C, generator=g).bfloat16()
+    w = (torch.randn(K, C * 49, generator=g) * 0.01).bfloat16().float()
+    b = torch.randn(K, generator=g) * 0.1
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = torch.relu(torch.nn.functional.linear(xr.flatten(1), wr, br))
+    dy = torch.randn(yr.shape, generator=g).bfloat16().float()
+    yr.backward(dy)
+    xd = x.to(dev).requires_grad_(True)
+    wd, bd = w.to(dev).requires_grad_(True), b.to(dev).requires_grad_(True)
+    y = mc.ConvAct.apply(xd, wd.view(K, C, 7, 7), bd, (1, 1), (0, 0), mc.ACT_RELU, torch.float32)
+    y.backward(dy.view(R, 1, 1, K).to(dev))
+    torch.testing.assert_close(y.view(R, K).cpu(), yr.detach(), rtol=1e-2, atol=2e-2)
+    rel = lambda a, c: ((a - c).norm() / c.norm()).item()  # noqa: E731
+    assert rel(xd.grad.float().cpu().permute(0, 3, 1, 2), xr.grad) < 1e-2
+    assert rel(wd.grad.cpu(), wr.grad) < 1e-2
+    assert rel(bd.grad.cpu(), br.grad) < 1e-3

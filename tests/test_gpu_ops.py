@@ -195,6 +195,8 @@ def test_roi_align_backward(dev):
     N, C, H, W, scale = 2, 64, 30, 41, 0.125
     feat = rng.standard_normal((N, C, H, W)).astype(np.float32)
     rois = _rois(rng, 120, N, H, W, scale)
+    rois[2, 1:] = [0, 0, W / scale, H / scale]  # footprint > the LDS tile: direct-atomic fallback
+    rois[3, 1:] = [8, 8, 8 + 20 / scale, 8 + 17 / scale]  # 21x18 cells: just over the tile
     gout = rng.standard_normal((120, C, 7, 7)).astype(np.float32)
     ref = orc.roi_align_backward(gout, rois, scale, (N, C, H, W), 2, False)
     f = torch.from_numpy(feat).to(dev).permute(0, 2, 3, 1).contiguous().requires_grad_(True)
