@@ -93,13 +93,18 @@ __device__ __forceinline__ bool gather_pos(const ConvP& p, int oh, int ow, int r
 // Epilogue shared by the fwd/dgrad kernels: BN statistics from the f32 accumulators, then the tile
 // staged through LDS (after the last K-tile's barrier) for 16-B coalesced NHWC stores with fused
 // bias / residual / activation.
-// HALVES == 2 stages the f32 tile in two 64-row passes (half the LDS: lets the multi-stage kernel
-// keep 3 blocks per CU).
-template <int BN, int HALVES = 1>
-__device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[4][BN / 32], char* smem, int64_t m0, int64_t n0,
-                                              int64_t mt, int wm, int wn, int lane, int tid, int split) {
-  constexpr int WN = BN / 2, TJ = WN / 16;
-  constexpr int PR = BM / HALVES;  // rows staged per pass
+// BMT = block tile rows (128 or 64; each wave-row wm covers BMT/2 rows, TI = BMT/32 MFMA row
+// tiles). HALVES == 2 stages the f32 tile in two passes of BMT/2 rows (half the LDS: lets the
+// multi-stage kernel keep 3 blocks per CU). BatchNorm statistics partials have 64-row
+// granularity: stats[2][ceil(M/64)][Ncol] (row = m / 64).
+static constexpr int SROWS = 64;
+
+template <int BN, int HALVES = 1, int BMT = BM>
+__device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT / 32][BN / 32], char* smem, int64_t m0,
+                                              int64_t n0, int64_t mt, int wm, int wn, int lane, int tid, int split) {
+  constexpr int WN = BN / 2, TJ = WN / 16, WM = BMT / 2, TI = BMT / 32;
+  constexpr int PR = BMT / HALVES;  // rows staged per pass
+  (void)mt;
   if (p.slab) {  // split-K partial: f32 tile to the slab, epilogue deferred to the reduce kernel
     constexpr int LD = BN + 4;
     float* Ct = (float*)smem;
@@ -109,12 +114,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[4][BN
     for (int h = 0; h < HALVES; ++h) {
       if (HALVES == 1 || wm == h) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              Ct[((HALVES == 1 ? wm * 64 : 0) + i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] =
+              Ct[((HALVES == 1 ? wm * WM : 0) + i * 16 + (lane >> 4) * 4 + r) * LD + wn * WN + j * 16 + (lane & 15)] =
                   acc[i][j][r];
       }
       __syncthreads();
@@ -135,10 +140,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[4][BN
     for (int j = 0; j < TJ; ++j) {
       float s = 0.f, q = 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          int64_t m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+          int64_t m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
           float v = m < p.M ? acc[i][j][r] : 0.f;
           s += v;
           q += v * v;
@@ -152,11 +157,19 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[4][BN
       }
     }
     __syncthreads();
+    const int64_t srow = m0 / SROWS;
     for (int c = tid; c < BN; c += NT) {
       int64_t col = n0 + c;
-      if (col < p.Ncol) {
-        p.stats[mt * p.Ncol + col] = red[c] + red[2 * BN + c];
-        p.stats[(p.mblocks + mt) * p.Ncol + col] = red[BN + c] + red[3 * BN + c];
+      if (col >= p.Ncol) continue;
+      if (WM == SROWS) {  // each wave-row is one statistics row
+        for (int w = 0; w < 2; ++w)
+          if (m0 + w * WM < p.M) {
+            p.stats[(srow + w) * p.Ncol + col] = red[(w * 2) * BN + c];
+            p.stats[(p.mblocks + srow + w) * p.Ncol + col] = red[(w * 2 + 1) * BN + c];
+          }
+      } else {  // BMT == 64: both wave-rows form one statistics row
+        p.stats[srow * p.Ncol + col] = red[c] + red[2 * BN + c];
+        p.stats[(p.mblocks + srow) * p.Ncol + col] = red[BN + c] + red[3 * BN + c];
       }
     }
     __syncthreads();
@@ -171,12 +184,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[4][BN
   for (int h = 0; h < HALVES; ++h) {
   if (HALVES == 1 || wm == h) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          int row = (HALVES == 1 ? wm * 64 : 0) + i * 16 + (lane >> 4) * 4 + r;
+          int row = (HALVES == 1 ? wm * WM : 0) + i * 16 + (lane >> 4) * 4 + r;
           int col = wn * WN + j * 16 + (lane & 15);
           Ct[row * LD + col] = acc[i][j][r];
         }
@@ -466,18 +479,19 @@ __device__ __forceinline__ void block_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BN, int MODE, int BKT, int STAGES, int OCC>
+template <int BN, int MODE, int BKT, int STAGES, int OCC, int BMT = BM>
 __global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int RB = BKT * 2;          // bytes per tile row
   constexpr int CPR = BKT / 8;         // 16-B chunks per row
   constexpr int RPI = 64 / CPR;        // rows landed per wave instruction (8 or 16)
-  constexpr int AI = 32 / RPI;         // A instructions per wave (32 rows per wave)
+  constexpr int AR = BMT / 4;          // A rows landed per wave
+  constexpr int AI = AR / RPI;         // A instructions per wave
   constexpr int BI = (BN / 4) / RPI;   // B instructions per wave
   constexpr int LOADS = AI + BI;       // vmem instructions per K-tile per wave
-  constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB;
-  constexpr int WN = BN / 2, TJ = WN / 16, KS = BKT / 32;
-  static_assert(BI >= 1 && KS >= 1 && STAGES >= 2, "tile shape");
+  constexpr int A_BYTES = BMT * RB, STAGE = (BMT + BN) * RB;
+  constexpr int WN = BN / 2, TJ = WN / 16, KS = BKT / 32, WM = BMT / 2, TI = WM / 16;
+  static_assert(AI >= 1 && BI >= 1 && KS >= 1 && STAGES >= 2, "tile shape");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int64_t ntiles_n = (p.Ncol + BN - 1) / BN;
@@ -485,7 +499,7 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
   const int split = (int)(gid % p.splits);
   const int64_t bid = gid / p.splits;
   const int64_t mt = bid / ntiles_n, nt = bid % ntiles_n;
-  const int64_t m0 = mt * BM, n0 = nt * BN;
+  const int64_t m0 = mt * BMT, n0 = nt * BN;
   const int lrow = lane / CPR;
   const int lch = (lane % CPR) ^ tile_swz<CPR>(lrow);  // instruction row bases are RPI-aligned
   // per A row: gather origin (h0, w0) and its pixel index; tap (r, s) moves it by +-(r, s)
@@ -495,7 +509,7 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
   int64_t a_pix[AI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
-    int64_t m = m0 + wave * 32 + i * RPI + lrow;
+    int64_t m = m0 + wave * AR + i * RPI + lrow;
     const bool ok = m < p.M;
     int64_t mm = ok ? m : 0;
     const int ow = (int)(mm % p.OW);
@@ -541,7 +555,7 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
       const int ih = a_h0[i] + dr, iw = a_w0[i] + ds;
       const uint16_t* src = zero;
       if (kin && (unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW) src = p.src + (a_pix[i] + toff) * IC + c;
-      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(A + (wave * 32 + i * RPI) * RB), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(A + (wave * AR + i * RPI) * RB), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
@@ -551,9 +565,9 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(B + row * RB), 16, 0, 0);
     }
   };
-  f32x4 acc[4][TJ];
+  f32x4 acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -570,10 +584,10 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int ch = ks * 4 + (lane >> 4);
-      bf16x8 af[4], bfr[TJ];
+      bf16x8 af[TI], bfr[TJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int row = wm * 64 + i * 16 + (lane & 15);
+      for (int i = 0; i < TI; ++i) {
+        int row = wm * WM + i * 16 + (lane & 15);
         af[i] = *(const bf16x8*)(A + row * RB + ((ch ^ tile_swz<CPR>(row)) << 4));
       }
 #pragma unroll
@@ -582,13 +596,13 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
         bfr[j] = *(const bf16x8*)(B + row * RB + ((ch ^ tile_swz<CPR>(row)) << 4));
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
   __syncthreads();  // last tile's buffer is reused by the epilogue staging
-  conv_epilogue<BN, 2>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
+  conv_epilogue<BN, 2, BMT>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
 }
 
 // Split-K reduce + epilogue: block = 128 rows x 64 columns; thread = 8 columns x 4 rows.
@@ -599,7 +613,7 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
   const int tid = threadIdx.x, cl = tid & 7, rl = tid >> 3;
   const int64_t mt = blockIdx.x, col0 = (int64_t)blockIdx.y * 64 + cl * 8;
   const bool cok = col0 < p.Ncol;
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float s2[2][8] = {}, q2[2][8] = {};
   const int64_t stride = p.M * p.Ncol;
   for (int rr = 0; rr < 4; ++rr) {
     const int64_t m = mt * BM + rl + 32 * rr;
@@ -611,7 +625,7 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
       v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
     }
 #pragma unroll
-    for (int t = 0; t < 8; ++t) { s[t] += v[t]; q[t] += v[t] * v[t]; }
+    for (int t = 0; t < 8; ++t) { s2[rr >> 1][t] += v[t]; q2[rr >> 1][t] += v[t] * v[t]; }
     if (p.bias) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] += p.bias[col0 + t];
@@ -638,15 +652,21 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
     }
   }
   if (!p.stats) return;
+  // 64-row statistics rows: half h = rows [64h, 64h+64) of this 128-row block = rr in {2h, 2h+1}
 #pragma unroll
-  for (int t = 0; t < 8; ++t) { red[0][rl][cl * 8 + t] = s[t]; red[1][rl][cl * 8 + t] = q[t]; }
-  __syncthreads();
-  if (tid < 128) {
-    const int w = tid >> 6, c = tid & 63;
-    float a = 0.f;
-    for (int r = 0; r < 32; ++r) a += red[w][r][c];
-    const int64_t col = (int64_t)blockIdx.y * 64 + c;
-    if (col < p.Ncol) p.stats[(w * p.mblocks + mt) * p.Ncol + col] = a;
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) { red[0][rl][cl * 8 + t] = s2[h][t]; red[1][rl][cl * 8 + t] = q2[h][t]; }
+    __syncthreads();
+    if (tid < 128) {
+      const int w = tid >> 6, c = tid & 63;
+      float a = 0.f;
+      for (int r = 0; r < 32; ++r) a += red[w][r][c];
+      const int64_t col = (int64_t)blockIdx.y * 64 + c;
+      const int64_t srow = 2 * mt + h;
+      if (col < p.Ncol && srow * SROWS < p.M) p.stats[(w * p.mblocks + srow) * p.Ncol + col] = a;
+    }
+    __syncthreads();
   }
 }
 
@@ -1075,7 +1095,8 @@ static int conv_check(const mx_conv_shape* s) {
   return MX_OK;
 }
 
-extern "C" int64_t mx_conv_mblocks(const mx_conv_shape* s) { return cdiv(s->N * s->Ho * s->Wo, BM); }
+// rows of the BatchNorm statistics partials (64 output pixels each)
+extern "C" int64_t mx_conv_mblocks(const mx_conv_shape* s) { return cdiv(s->N * s->Ho * s->Wo, SROWS); }
 
 // Kernel variant (mx_conv_set_variant): 0 register staging, 1/2 direct-to-LDS 2-stage (2 also
 // direct-to-LDS wgrad), 3..6 multi-stage direct-to-LDS, 7 (default) per-launch choice of 3 / 4.
@@ -1085,17 +1106,25 @@ static int g_conv_variant = 7;
 // (< ~1.25 blocks per CU) split the K loop, keeping >= 4 K-tiles (of 64) per split.
 struct Geo {
   int64_t M, Ncol, Kdim, tiles, nk;
-  int splits;
+  int splits, bmt;
   bool narrow;
 };
 static Geo make_geo(int64_t M, int64_t Ncol, int64_t Kdim) {
   Geo g;
   g.M = M; g.Ncol = Ncol; g.Kdim = Kdim;
   g.narrow = g.Ncol <= 64;
-  g.tiles = cdiv(g.M, BM) * (g.narrow ? cdiv(g.Ncol, 64) : cdiv(g.Ncol, 128));
+  const int64_t ntn = g.narrow ? cdiv(g.Ncol, 64) : cdiv(g.Ncol, 128);
+  g.bmt = BM;
+  g.tiles = cdiv(g.M, BM) * ntn;
+  // small grids: 64-row tiles first (twice the blocks, no partial-sum traffic), split-K only below that
+  if (g_conv_variant == 8 || (g_conv_variant == 7 && g.tiles < 320)) {
+    g.bmt = 64;
+    g.tiles = cdiv(g.M, 64) * ntn;
+  }
   g.nk = cdiv(g.Kdim, BK);
   g.splits = 1;
-  if (g_conv_variant >= 1 && g.Ncol % 8 == 0 && g.tiles < 320 && g.nk >= 8) {
+  const int64_t split_below = 320;
+  if (g_conv_variant >= 1 && g.Ncol % 8 == 0 && g.tiles < split_below && g.nk >= 8) {
     int64_t sp = std::min<int64_t>(std::min<int64_t>(cdiv(640, g.tiles), g.nk / 4), 16);
     g.splits = (int)std::max<int64_t>(1, sp);
   }
@@ -1103,10 +1132,17 @@ static Geo make_geo(int64_t M, int64_t Ncol, int64_t Kdim) {
 }
 
 // The variant a launch runs: long K loops on big grids favour 64-wide K-tiles (fewer barriers),
-// short loops and small / split grids the 3-deep 32-wide ring at 3 blocks per CU.
+// short loops and small / split grids the 3-deep 32-wide ring at 3 blocks per CU; 64-row tiles
+// for grids under ~1.25 blocks per CU.
+static int num_cus();
 static int launch_kind(const Geo& g) {
+  if (g.bmt == 64) return 8;
   if (g_conv_variant != 7) return g_conv_variant;
-  return (g.splits == 1 && g.tiles >= 512 && g.nk >= 16) ? 4 : 3;
+  if (g.splits > 1 || g.nk < 16) return 3;
+  // wave quantisation: BK32x3 holds 3 blocks per CU, BK64x2 holds 2 (each then ~1.5x faster)
+  const int64_t cus = num_cus();
+  const double c3 = (double)cdiv(g.tiles, 3 * cus), c4 = (double)cdiv(g.tiles, 2 * cus) * (2.0 / 3.0);
+  return c4 < c3 ? 4 : 3;
 }
 
 // dgrad stride-parity classes. dx(h) receives dy((h + pad - r) / st) only from taps with
@@ -1170,11 +1206,11 @@ extern "C" size_t mx_conv_workspace(const mx_conv_shape* s, int pass) {
   return mx;
 }
 
-template <int BN, int MODE, int BKT, int STAGES, int OCC>
+template <int BN, int MODE, int BKT, int STAGES, int OCC, int BMT = BM>
 static void launch_pipe(const ConvP& p, int64_t blocks, hipStream_t st) {
-  size_t ring = (size_t)STAGES * (BM + BN) * BKT * 2;
-  size_t epi = (size_t)(BM / 2) * (BN + 4) * 4;
-  conv_igemm_pipe_kernel<BN, MODE, BKT, STAGES, OCC><<<(unsigned)blocks, NT, std::max(ring, epi), st>>>(p);
+  size_t ring = (size_t)STAGES * (BMT + BN) * BKT * 2;
+  size_t epi = (size_t)(BMT / 2) * (BN + 4) * 4;
+  conv_igemm_pipe_kernel<BN, MODE, BKT, STAGES, OCC, BMT><<<(unsigned)blocks, NT, std::max(ring, epi), st>>>(p);
 }
 
 template <int BN, int MODE>
@@ -1193,6 +1229,7 @@ static void launch_variant(int v, const ConvP& p, int64_t blocks, hipStream_t st
     case 3: launch_pipe<BN, MODE, 32, 3, 3>(p, blocks, st); break;
     case 4: launch_pipe<BN, MODE, 64, 2, 2>(p, blocks, st); break;
     case 5: launch_pipe<BN, MODE, 32, 4, 2>(p, blocks, st); break;
+    case 8: launch_pipe<BN, MODE, 32, 3, 3, 64>(p, blocks, st); break;
     default: launch_pipe<BN, MODE, 64, 3, 1>(p, blocks, st); break;
   }
 }
@@ -1203,7 +1240,7 @@ static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipSt
   MX_CHECK_ARG(g.Kdim < (1ll << 30) && p.IH < (1ll << 26) && p.IW < (1ll << 26), "conv: GEMM K or spatial size too large");
   MX_CHECK_ARG(blocks * g.splits < (1ll << 31), "conv: grid too large");
   const int v = launch_kind(g);
-  const int64_t bkt = (v == 3 || v == 5) ? 32 : 64;
+  const int64_t bkt = (v == 3 || v == 5 || v == 8) ? 32 : 64;
   const int64_t nk = cdiv(g.Kdim, bkt);  // K-tiles in the kernel's tile width
   p.splits = 1;
   p.kt_per_split = nk;
@@ -1220,7 +1257,7 @@ static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipSt
   else launch_variant<128, MODE>(v, p, blocks, st);
   MX_LAUNCH_CHECK();
   if (p.slab) {
-    dim3 rg((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.Ncol, 64));
+    dim3 rg((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.Ncol, 64));  // the reduce works in 128-row blocks
     conv_splitk_reduce_kernel<<<rg, 256, 0, st>>>(p);
     MX_LAUNCH_CHECK();
   }
@@ -1239,9 +1276,9 @@ extern "C" int mx_conv_set_wgrad_variant(int v) {
 extern "C" int mx_conv_get_wgrad_variant(void) { return g_wgrad_variant; }
 
 extern "C" int mx_conv_set_variant(int v) {
-  MX_CHECK_ARG(v >= 0 && v <= 7,
+  MX_CHECK_ARG(v >= 0 && v <= 8,
                "mx_conv_set_variant: 0 register staging, 1/2 direct-to-LDS fwd/dgrad, 3-6 multi-stage "
-               "direct-to-LDS (3: BK32x3, 4: BK64x2, 5: BK32x4, 6: BK64x3), 7 auto");
+               "direct-to-LDS (3: BK32x3, 4: BK64x2, 5: BK32x4, 6: BK64x3), 7 auto, 8 64-row tiles BK32x3");
   g_conv_variant = v;
   return MX_OK;
 }
@@ -1260,7 +1297,7 @@ extern "C" int mx_conv2d_fwd_ex(const mx_conv_shape* s, const uint16_t* x, const
   p.OH = s->Ho; p.OW = s->Wo; p.IH = s->H; p.IW = s->W; p.IC = s->C;
   p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
   p.bias = bias; p.residual = residual; p.act = act; p.out = y; p.out_f32 = ydtype == MX_F32;
-  p.stats = stats; p.mblocks = cdiv(p.M, BM);
+  p.stats = stats; p.mblocks = cdiv(p.M, SROWS);
   return launch_igemm<0>(p, make_geo(p.M, p.Ncol, p.Kdim), ws, ws_bytes, (hipStream_t)stream);
 }
 

@@ -26,7 +26,7 @@ CASES = [
 ]
 
 
-@pytest.fixture(params=[0, 1, 3, 4, 5, 6])
+@pytest.fixture(params=[0, 1, 3, 4, 5, 6, 7, 8])
 def variant(request):
     """Every fwd/dgrad staging variant of the implicit-GEMM kernel (mx_conv_set_variant)."""
     from mx_det import _lib

@@ -23,7 +23,9 @@ SHAPES = [  # name, N, H, W, C, K, k, stride, pad
     ("L3 1x1 1024->256", 2, 50, 84, 1024, 256, 1, 1, 0),
     ("L4 1x1 2048->512", 2, 25, 42, 2048, 512, 1, 1, 0),
     ("box head 3x3 on 1024 RoIs", 1024, 7, 7, 256, 256, 3, 1, 1),
-    ("FC6 as 1x1 GEMM (12544->1024)", 1024, 1, 1, 12544, 1024, 1, 1, 0),
+    ("FC6 as 7x7 valid conv (12544->1024)", 1024, 7, 7, 256, 1024, 7, 1, 0),
+    ("L4 3x3 512->512", 2, 25, 42, 512, 512, 3, 1, 1),
+    ("L3 1x1 256->1024", 2, 50, 84, 256, 1024, 1, 1, 0),
     ("stem 7x7 s2 (8->64)", 2, 800, 1344, 8, 64, 7, 2, 3),
     ("L3.0 3x3 s2 128->256 (dgrad s2)", 2, 100, 168, 256, 256, 3, 2, 1),
 ]
