@@ -115,12 +115,31 @@ def declared_symbols():
     return list(_SIGS)
 
 
+_fns = {}
+
+
 def call(name, *args):
-    lib = load()
-    if not hasattr(lib, name):
-        raise MxError(f"libmx_det.so does not export {name}")
-    rc = getattr(lib, name)(*args)
+    """Call an entry point; a non-zero return raises MxError with mx_last_error(). Pointer arguments
+    may be plain ints (argtypes are bound), so the hot path passes data_ptr() values directly."""
+    fn = _fns.get(name)
+    if fn is None:
+        lib = load()
+        if not hasattr(lib, name):
+            raise MxError(f"libmx_det.so does not export {name}")
+        fn = _fns[name] = getattr(lib, name)
+    rc = fn(*args)
     if rc != 0:
         msg = load().mx_last_error().decode(errors="replace")
         raise MxError(f"{name} failed ({rc}): {msg}")
     return rc
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return t.data_ptr() if t is not None else None
+
+
+def stream():
+    """The current HIP stream of the current device as a raw pointer (the C entry points enqueue on it)."""
+    import torch
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())

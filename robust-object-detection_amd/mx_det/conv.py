@@ -18,7 +18,7 @@ ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
 
 
 def _s():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    return _lib.stream()
 
 
 class KernelTimer:
@@ -63,7 +63,7 @@ def set_timer(t):
 
 
 def _p(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    return t.data_ptr() if t is not None else None
 
 
 def out_hw(H, W, R, S, stride, pad):

@@ -23,11 +23,11 @@ BBOX_CLIP = math.log(1000.0 / 16)
 
 
 def _stream():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    return _lib.stream()
 
 
 def _p(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    return t.data_ptr() if t is not None else None
 
 
 def _check(cond, msg):

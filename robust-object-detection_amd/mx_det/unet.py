@@ -17,15 +17,16 @@ from torch import nn
 
 from . import conv as mc
 from . import ops
+from . import _lib
 from ._lib import call
 
 
 def _s():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    return _lib.stream()
 
 
 def _p(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    return t.data_ptr() if t is not None else None
 
 
 class ConvBlock(nn.Module):
