@@ -1,0 +1,39 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, smoke, bench line, rocprofv3 kernel stats of a short bench.
+# Usage (from this container): gpurun --timeout 1100 -- bash tools/gpu_check.sh <tag> [tests|bench|prof ...]
+set -o pipefail
+TAG=${1:-run}; shift
+STEPS=${*:-tests bench prof}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > "$OUT/tests.log" 2>&1 || { echo "tests failed rc=$?"; tail -40 "$OUT/tests.log"; exit 1; }
+      tail -3 "$OUT/tests.log" ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+        || { echo "smoke failed rc=$?"; tail -30 "$OUT/smoke.log"; exit 1; }
+      tail -2 "$OUT/smoke.log" ;;
+    bench)
+      timeout -k 10 400 python -u bench.py > "$OUT/bench.log" 2>&1 \
+        || { echo "bench failed rc=$?"; tail -30 "$OUT/bench.log"; exit 1; }
+      tail -1 "$OUT/bench.log" ;;
+    benchfast)
+      timeout -k 10 300 python -u bench.py --no-cpu-baseline > "$OUT/bench.log" 2>&1 \
+        || { echo "bench failed rc=$?"; tail -30 "$OUT/bench.log"; exit 1; }
+      tail -1 "$OUT/bench.log" ;;
+    prof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o prof -- \
+        python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/prof.log" 2>&1 \
+        || { echo "prof failed rc=$?"; tail -30 "$OUT/prof.log"; exit 1; }
+      for f in $(find "$OUT/prof" -name '*_stats.csv'); do cp "$f" "$OUT/"; done
+      rm -rf "$OUT/prof"
+      tail -1 "$OUT/prof.log" ;;
+    *)
+      echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "gpu_check $TAG done"
