@@ -226,18 +226,37 @@ int mx_upsample_nearest_bwd(const uint16_t* gy, int64_t N, int64_t H, int64_t W,
 int mx_bn_finalize(const float* stats, int64_t mblocks, int64_t K, int64_t count, const float* gamma,
                    const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                    float* mean_out, float* invstd_out, float* scale_out, float* shift_out, mx_stream_t stream);
+/* Hot-path finalize: one launch (row-slice partials + the last block per 64-channel chunk finishes).
+ * ws = mx_bn_finalize_workspace(mblocks, K) bytes; its first 256 bytes are arrival counters that
+ * must be zero before the first use and are left zero by every launch, so one zero-filled scratch
+ * serves all launches on a stream (use one scratch per concurrent stream). */
+size_t mx_bn_finalize_workspace(int64_t mblocks, int64_t K);
+int mx_bn_finalize_ex(const float* stats, int64_t mblocks, int64_t K, int64_t count, const float* gamma,
+                      const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                      float* mean_out, float* invstd_out, float* scale_out, float* shift_out, void* ws,
+                      size_t ws_bytes, mx_stream_t stream);
 int mx_bn_apply(const void* x, int xdtype, int64_t M, int64_t K, const float* scale, const float* shift,
                 const uint16_t* residual, int act, uint16_t* y, mx_stream_t stream);
-/* Hot-path backward: reduce_ex = per-row-block partials (workspace mx_bn_bwd_workspace bytes, no
- * atomics) + an f64 column reduce writing sums[2][K] = (sum g, sum g*xhat) = (dbeta, dgamma) and
- * coef[3][K], the per-channel affine form dx = coef0*g + coef1*x + coef2; apply_ex streams
- * dx (and dres = g, nullable). g = dy * act'(y); y may be null when act == 0. */
+/* Hot-path backward: reduce_ex = one launch of per-row-block partials (no float atomics) whose last
+ * block per 64-channel chunk does the f64 column reduce, writing sums[2][K] = (sum g, sum g*xhat) =
+ * (dbeta, dgamma) and coef[3][K], the per-channel affine form dx = coef0*g + coef1*x + coef2;
+ * workspace mx_bn_bwd_workspace bytes whose first 256 bytes are arrival counters (zero before first
+ * use, left zero: see mx_bn_finalize_ex). apply_ex streams dx (and dres = g, nullable).
+ * g = dy * act'(y); y may be null when act == 0. */
 size_t mx_bn_bwd_workspace(int64_t M, int64_t K);
 int mx_bn_bwd_reduce_ex(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
                         const float* mean, const float* invstd, const float* gamma, void* ws, size_t ws_bytes,
                         float* sums, float* coef, mx_stream_t stream);
 int mx_bn_bwd_apply_ex(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
                        const float* coef, uint16_t* dx, uint16_t* dres, mx_stream_t stream);
+/* Backward head of conv (+bias) (+act) (the ConvAct layers: RPN head convs, cls/bbox heads, FC6/FC7,
+ * predictor): g[M][K8] bf16 = gy * act'(y) (columns K..K8-1 zero), db[K] f32 = column sums of the
+ * unrounded g (nullable). gy, y: [M][K] of dtype MX_BF16 / MX_F32 (y nullable when act == 0).
+ * ws = mx_act_bias_bwd_workspace(M, K) bytes with the zero-kept counters of mx_bn_finalize_ex
+ * (needed only when db is given). */
+size_t mx_act_bias_bwd_workspace(int64_t M, int64_t K);
+int mx_act_bias_bwd(const void* gy, const void* y, int dtype, int64_t M, int64_t K, int64_t K8, int act,
+                    uint16_t* g, float* db, void* ws, size_t ws_bytes, mx_stream_t stream);
 /* Convenience forms (allocate per call): sums[2][K] is overwritten. */
 int mx_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
                      const float* mean, const float* invstd, float* sums, mx_stream_t stream);

@@ -162,6 +162,76 @@ __global__ void __launch_bounds__(64) nms_scan_kernel(const uint64_t* __restrict
   }
 }
 
+// LDS-staged scan (segments of up to 64*SCAN_LDS_W boxes): one 256-thread block per segment. Per
+// 64-row block, all threads stage the block's mask rows (words blk..W-1, coalesced) in LDS in one
+// round trip; wave 0 resolves the in-tile chain on the diagonal word; then all threads OR the kept
+// rows into the removed bitmap from LDS. Same result as nms_scan_kernel (kept = the greedy set).
+static constexpr int SCAN_LDS_W = 112;  // (Wm + 64 Wm) * 8 B <= 64 KB of dynamic LDS
+__global__ void __launch_bounds__(256) nms_scan_lds_kernel(const uint64_t* __restrict__ mask,
+                                                           const int32_t* __restrict__ seg_start,
+                                                           const int32_t* __restrict__ nseg_p,
+                                                           const int32_t* __restrict__ svals, int Wm,
+                                                           int32_t* __restrict__ flags, int32_t* __restrict__ nkeep) {
+  extern __shared__ uint64_t sm[];
+  uint64_t* removed = sm;             // [Wm]
+  uint64_t* rows = sm + Wm;           // [64][Wm]: row t, word w at rows[t * Wm + w]
+  __shared__ uint64_t kept_s;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int nseg = *nseg_p;
+  for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    const int64_t s0 = seg_start[seg], len = seg_start[seg + 1] - s0;
+    const int W = (int)((len + 63) / 64);
+    if (W > Wm) {
+      if (tid == 0) atomicExch(nkeep, (int32_t)0x80000000);
+      continue;
+    }
+    for (int w = tid; w < W; w += 256) removed[w] = 0;
+    int kept_total = 0;
+    for (int blk = 0; blk < W; ++blk) {
+      const int64_t rbase = s0 + (int64_t)blk * 64;
+      const int cnt = (int)min<int64_t>(64, len - (int64_t)blk * 64);
+      const int nw = W - blk;  // words blk..W-1
+      for (int e = tid; e < cnt * nw; e += 256) {
+        const int t = e / nw, w = blk + (e - t * nw);
+        rows[t * Wm + w] = mask[(rbase + t) * Wm + w];
+      }
+      __syncthreads();
+      if (tid < 64) {
+        const uint64_t diag = lane < cnt ? rows[lane * Wm + blk] : 0ull;
+        uint64_t cur = removed[blk];
+        uint64_t kept = 0;
+        const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
+        for (int t = 0; t < cnt; ++t) {
+          if (!((cur >> t) & 1ull)) {
+            kept |= 1ull << t;
+            const uint64_t row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, t) << 32) |
+                                 (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, t);
+            cur |= row;
+          }
+        }
+        if (lane < cnt && ((kept >> lane) & 1ull)) flags[svals[rbase + lane]] = 1;
+        if (lane == 0) kept_s = kept;
+      }
+      __syncthreads();
+      const uint64_t kept = kept_s;
+      if (tid == 0) kept_total += __popcll(kept);
+      for (int w = blk + 1 + tid; w < W; w += 256) {
+        uint64_t acc = removed[w];
+        uint64_t k = kept;
+        while (k) {
+          const int t = __ffsll((unsigned long long)k) - 1;
+          k &= k - 1;
+          acc |= rows[t * Wm + w];
+        }
+        removed[w] = acc;
+      }
+      __syncthreads();
+    }
+    if (tid == 0 && kept_total) atomicAdd(nkeep, kept_total);
+    __syncthreads();
+  }
+}
+
 // final order: kept first by (group, score desc, index); the rest after
 __global__ void nms_final_keys_kernel(const float* __restrict__ scores, const int32_t* __restrict__ group,
                                       const int32_t* __restrict__ flags, int64_t n, uint64_t* __restrict__ keys,
@@ -276,7 +346,11 @@ extern "C" int mx_batched_nms(const float* boxes, const float* scores, const int
   nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask);
   MX_LAUNCH_CHECK();
   int sgrid = (int)std::min<int64_t>(n, 1024);
-  nms_scan_kernel<<<sgrid, 64, sizeof(uint64_t) * Wm, s>>>(w.mask, w.seg_start, w.nseg, w.v1, Wm, w.flags, w.nk);
+  if (Wm <= SCAN_LDS_W)
+    nms_scan_lds_kernel<<<sgrid, 256, sizeof(uint64_t) * (Wm + 64 * (size_t)Wm), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
+                                                                                       Wm, w.flags, w.nk);
+  else
+    nms_scan_kernel<<<sgrid, 64, sizeof(uint64_t) * Wm, s>>>(w.mask, w.seg_start, w.nseg, w.v1, Wm, w.flags, w.nk);
   MX_LAUNCH_CHECK();
   nms_final_keys_kernel<<<nb, T, 0, s>>>(scores, group, w.flags, n, w.k0, w.v0);
   MX_LAUNCH_CHECK();

@@ -75,6 +75,12 @@ _SIGS = {
     "mx_restore_finish": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mx_bn_finalize": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_vp]),
+    "mx_bn_finalize_workspace": (ctypes.c_size_t, [c_i64, c_i64]),
+    "mx_bn_finalize_ex": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp, ctypes.c_size_t, c_vp]),
+    "mx_act_bias_bwd_workspace": (ctypes.c_size_t, [c_i64, c_i64]),
+    "mx_act_bias_bwd": (c_int, [c_vp, c_vp, c_int, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, ctypes.c_size_t,
+                                c_vp]),
     "mx_bn_apply": (c_int, [c_vp, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "mx_bn_bwd_reduce": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
     "mx_bn_bwd_apply": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -88,6 +88,10 @@ class HipBackend:
             model.__dict__["_mx_packer"] = pk
         mc.set_packer(pk)
         pk.refresh()
+        bns = model.__dict__.get("_mx_bns")
+        if bns is None:
+            bns = model.__dict__["_mx_bns"] = [m for m in model.modules() if isinstance(m, mc.BatchNorm2d)]
+        mc.count_batches([b for b in bns if b.training] if model.training else [])
 
     # ---- dense ---------------------------------------------------------------------------
     def conv_bn(self, x, conv, bn, act, residual=None):

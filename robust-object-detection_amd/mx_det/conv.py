@@ -272,12 +272,21 @@ def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None):
     return dw
 
 
-def _act_grad(g, y, act):
-    if act == ACT_RELU:
-        return g * (y > 0).to(g.dtype)
-    if act == ACT_LEAKY:
-        return g * torch.where(y > 0, 1.0, 0.2).to(g.dtype)
-    return g
+def act_bias_bwd(gy, y, act, K8, need_db):
+    """(g, db): g = gy * act'(y) as bf16 [..., K8] (zero-padded columns), db = sum of g over all but
+    the last dim (f32, or None) -- one launch (mx_act_bias_bwd)."""
+    K = gy.shape[-1]
+    gy = gy.contiguous()
+    M = gy.numel() // K
+    assert gy.dtype in (torch.bfloat16, torch.float32) and y.dtype == gy.dtype and y.shape == gy.shape
+    g = torch.empty(gy.shape[:-1] + (K8,), dtype=torch.bfloat16, device=gy.device)
+    db = torch.empty(K, dtype=torch.float32, device=gy.device) if need_db else None
+    ws = None
+    if need_db:
+        ws = bn_scratch(_lib.load().mx_act_bias_bwd_workspace(M, K), gy.device)
+    call("mx_act_bias_bwd", _p(gy), _p(y.contiguous()) if act else None, 1 if gy.dtype == torch.bfloat16 else 0,
+         M, K, K8, int(act), _p(g), _p(db), _p(ws), ws.numel() if ws is not None else 0, _s())
+    return g, db
 
 
 class ConvAct(torch.autograd.Function):
@@ -299,13 +308,10 @@ class ConvAct(torch.autograd.Function):
     def backward(ctx, gy):
         x, y, wt = ctx.saved_tensors
         stride, pad, act, wshape, has_b = ctx.cfg
-        g = _act_grad(gy, y, act).to(torch.bfloat16).contiguous()
         K, _, R, S = wshape
         dx = dw = db = None
         K8 = (K + 7) // 8 * 8
-        gk = g
-        if K8 != K:
-            gk = torch.nn.functional.pad(g, (0, K8 - K)).contiguous()
+        gk, db = act_bias_bwd(gy, y, act, K8, has_b and ctx.needs_input_grad[2])
         if ctx.needs_input_grad[0]:
             if _is_dense(x.shape, R, S, stride, pad):  # 1x1-GEMM form: dX[N, R*S*C] = dY[N, K8] wt
                 N, H, W, C = x.shape
@@ -314,9 +320,21 @@ class ConvAct(torch.autograd.Function):
                 dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad)
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad(gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1])
-        if has_b and ctx.needs_input_grad[2]:
-            db = g.float().sum(dim=(0, 1, 2))
         return dx, dw, db, None, None, None, None
+
+
+_scratch = {}
+
+
+def bn_scratch(nbytes, device):
+    """Persistent per-device workspace of the one-launch BN reductions: zero-filled when allocated;
+    its leading arrival counters are left zero by every launch, so it is reused across calls (all of
+    them are stream-ordered on the current stream)."""
+    t = _scratch.get(device)
+    if t is None or t.numel() < nbytes:
+        t = torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _scratch[device] = t
+    return t
 
 
 class ConvBNAct(torch.autograd.Function):
@@ -331,8 +349,11 @@ class ConvBNAct(torch.autograd.Function):
         M = z.numel() // K
         mean = torch.empty(K, dtype=torch.float32, device=x.device)
         invstd, scale, shift = torch.empty_like(mean), torch.empty_like(mean), torch.empty_like(mean)
-        call("mx_bn_finalize", _p(st), st.shape[1], K, M, _p(gamma.detach()), _p(beta.detach()), float(eps),
-             float(momentum), _p(rmean), _p(rvar), _p(mean), _p(invstd), _p(scale), _p(shift), _s())
+        fwb = _lib.load().mx_bn_finalize_workspace(st.shape[1], K)
+        fws = bn_scratch(fwb, x.device)
+        call("mx_bn_finalize_ex", _p(st), st.shape[1], K, M, _p(gamma.detach()), _p(beta.detach()), float(eps),
+             float(momentum), _p(rmean), _p(rvar), _p(mean), _p(invstd), _p(scale), _p(shift), _p(fws), fws.numel(),
+             _s())
         y = torch.empty_like(z)
         res = residual.contiguous() if residual is not None else None
         t0 = _timer.start() if _timer else None
@@ -353,10 +374,10 @@ class ConvBNAct(torch.autograd.Function):
         sums = torch.empty((2, K), dtype=torch.float32, device=z.device)
         coef = torch.empty((3, K), dtype=torch.float32, device=z.device)
         wsb = _lib.load().mx_bn_bwd_workspace(M, K)
-        ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
+        ws = bn_scratch(wsb, z.device)
         t0 = _timer.start() if _timer else None
         call("mx_bn_bwd_reduce_ex", _p(gy), _p(y), _p(z), M, K, int(act), _p(mean), _p(invstd), _p(gamma.detach()),
-             _p(ws), wsb, _p(sums), _p(coef), _s())
+             _p(ws), ws.numel(), _p(sums), _p(coef), _s())
         if _timer:
             _timer.stop("bn_bwd_reduce", M * K * (6 if act else 4), t0, f"{M}x{K}")
         dz = torch.empty_like(z)
@@ -407,11 +428,24 @@ class BatchNorm2d(torch.nn.Module):
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
 
 
+_nbt_batched = set()
+
+
+def count_batches(bns):
+    """num_batches_tracked += 1 for every module in `bns` in one foreach launch (called once per
+    training forward by the model); conv_bn then skips its own per-layer increment for them."""
+    global _nbt_batched
+    t = [b.num_batches_tracked for b in bns if b.num_batches_tracked is not None]
+    if t:
+        torch._foreach_add_(t, 1)
+    _nbt_batched = {id(b) for b in bns}
+
+
 def conv_bn(x, conv, bn, act, residual=None):
     """Conv2d(bias=False) + BatchNorm2d (+ residual) + activation as one fused unit. Train mode:
     batch statistics + running-stat update (nn.BatchNorm2d semantics); eval: BN folded into the conv."""
     if bn.training:
-        if bn.num_batches_tracked is not None:
+        if bn.num_batches_tracked is not None and id(bn) not in _nbt_batched:
             bn.num_batches_tracked.add_(1)
         return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
                                conv.stride, conv.padding, act, bn.eps, bn.momentum)

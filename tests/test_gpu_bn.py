@@ -31,11 +31,18 @@ def test_bn_backward_matches_torch(dev, M, K, act):
     zd, yd, dyd = z.to(dev), y.to(dev), dy.to(dev)
     meand, invd, gd = mean.to(dev), invstd.to(dev), gamma.to(dev)
     wsb = _lib.load().mx_bn_bwd_workspace(M, K)
-    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)  # arrival counters start (and stay) zero
     sums = torch.empty(2, K, device=dev)
     coef = torch.empty(3, K, device=dev)
     _lib.call("mx_bn_bwd_reduce_ex", _p(dyd), _p(yd), _p(zd), M, K, act, _p(meand), _p(invd), _p(gd), _p(ws), wsb,
               _p(sums), _p(coef), _s())
+    # second launch on the same workspace: the counters were left zero, results identical
+    sums_b, coef_b = torch.empty_like(sums), torch.empty_like(coef)
+    _lib.call("mx_bn_bwd_reduce_ex", _p(dyd), _p(yd), _p(zd), M, K, act, _p(meand), _p(invd), _p(gd), _p(ws), wsb,
+              _p(sums_b), _p(coef_b), _s())
+    torch.cuda.synchronize()
+    assert torch.equal(sums, sums_b) and torch.equal(coef, coef_b)
+    assert int(ws[:256].sum()) == 0
     dx = torch.empty_like(zd)
     dres = torch.empty_like(zd)
     _lib.call("mx_bn_bwd_apply_ex", _p(dyd), _p(yd), _p(zd), M, K, act, _p(coef), _p(dx), _p(dres), _s())
@@ -81,3 +88,36 @@ def test_bn_finalize_matches_torch(dev, M, K):
     torch.testing.assert_close(outs[1].cpu().double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(rm.cpu().double(), 0.1 * mean, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(rv.cpu().double(), 0.9 + 0.1 * zd.var(0, unbiased=True), rtol=1e-5, atol=1e-6)
+    # hot-path form (one launch, persistent zero-filled workspace), twice on the same workspace
+    wsb = _lib.load().mx_bn_finalize_workspace(mb, K)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+    for _ in range(2):
+        o2 = [torch.empty(K, device=dev) for _ in range(4)]
+        _lib.call("mx_bn_finalize_ex", _p(stats), mb, K, M, _p(gamma.to(dev)), _p(beta.to(dev)), 1e-5, 0.1, None,
+                  None, *[_p(o) for o in o2], _p(ws), wsb, _s())
+        torch.cuda.synchronize()
+        for a, b in zip(outs, o2):
+            assert torch.equal(a, b)
+        assert int(ws[:256].sum()) == 0
+
+
+@pytest.mark.parametrize("M,K,act,dt", [(134400, 15, 0, torch.float32), (8400, 256, 1, torch.bfloat16),
+                                        (1024, 1024, 1, torch.bfloat16), (1024, 35, 0, torch.float32),
+                                        (77, 24, 2, torch.bfloat16), (5, 3, 1, torch.float32)])
+def test_act_bias_bwd_matches_torch(dev, M, K, act, dt):
+    """ConvAct backward head: g = gy*act'(y) (bf16, zero-padded to K8) and db = sum of g."""
+    from mx_det import conv as mc
+    g = torch.Generator().manual_seed(M + K)
+    gy = torch.randn(M, K, generator=g).to(dt)
+    y = torch.randn(M, K, generator=g).to(dt)
+    K8 = (K + 7) // 8 * 8
+    for _ in range(2):  # second call reuses the persistent scratch (counters left zero)
+        out, db = mc.act_bias_bwd(gy.to(dev), y.to(dev), act, K8, True)
+        torch.cuda.synchronize()
+    yf = y.float()
+    mask = (yf > 0).float() if act == 1 else torch.where(yf > 0, 1.0, 0.2) if act == 2 else torch.ones_like(yf)
+    ref = gy.float() * mask
+    assert out.shape == (M, K8)
+    assert torch.equal(out[:, :K].cpu(), ref.bfloat16())
+    assert int((out[:, K:] != 0).sum()) == 0
+    torch.testing.assert_close(db.cpu().double(), ref.double().sum(0), rtol=1e-5, atol=1e-3)

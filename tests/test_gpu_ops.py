@@ -101,7 +101,7 @@ def test_roi_matcher_labels(dev):
     np.testing.assert_allclose(tgt.cpu().numpy(), reft, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("n,thr", [(1, 0.7), (50, 0.7), (999, 0.5), (2000, 0.7), (6000, 0.5)])
+@pytest.mark.parametrize("n,thr", [(1, 0.7), (50, 0.7), (999, 0.5), (2000, 0.7), (6000, 0.5), (7200, 0.7)])
 def test_nms_bitexact(dev, n, thr):
     from mx_det import ops
     rng = np.random.default_rng(n)

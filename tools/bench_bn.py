@@ -48,7 +48,7 @@ def main():
         t = timeit(lambda: call("mx_bn_apply", _p(z), 1, M, K, _p(invstd), _p(mean), None, 1, _p(out), _s()))
         res.append(("apply", t, M * K * 4))
         wsb = _lib.load().mx_bn_bwd_workspace(M, K)
-        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
         coef = torch.empty(3, K, device=dev)
         t = timeit(lambda: call("mx_bn_bwd_reduce_ex", _p(dy), _p(y), _p(z), M, K, 1, _p(mean), _p(invstd),
                                 _p(gamma), _p(ws), wsb, _p(sums), _p(coef), _s()))
@@ -56,6 +56,17 @@ def main():
         t = timeit(lambda: call("mx_bn_bwd_apply_ex", _p(dy), _p(y), _p(z), M, K, 1, _p(coef), _p(out), _p(out2),
                                 _s()))
         res.append(("bwd_apply", t, M * K * 10))
+        mb = (M + 63) // 64
+        st = torch.randn(2, mb, K, device=dev).abs()
+        fwb = _lib.load().mx_bn_finalize_workspace(mb, K)
+        fws = torch.zeros(fwb, dtype=torch.uint8, device=dev)
+        outs = [torch.empty(K, device=dev) for _ in range(4)]
+        t = timeit(lambda: call("mx_bn_finalize_ex", _p(st), mb, K, M, _p(gamma), _p(mean), 1e-5, 0.1, None, None,
+                                *[_p(o) for o in outs], _p(fws), fwb, _s()))
+        res.append(("finalize", t, mb * K * 8))
+        from mx_det import conv as mc
+        t = timeit(lambda: mc.act_bias_bwd(dy, y, 1, K, True))
+        res.append(("act_bias", t, M * K * 6))
         print(f"{M:7d}x{K:<5d} " + " | ".join(f"{n} {ms * 1000:6.1f}us {by / ms / 1e6:6.0f}GB/s" for n, ms, by in res),
               flush=True)
 
