@@ -175,6 +175,59 @@ __global__ void __launch_bounds__(256) roi_align_bwd_kernel(Levels L, int64_t C,
   }
 }
 
+// ---- bf16 forward, 8 channels per lane ----------------------------------------------------------
+// Same per-channel arithmetic (and order) as roi_align_fwd_kernel, 16-B loads: a group of C/8 lanes
+// covers one bin's channel row, 256 / (C/8) groups stride the bins.
+__global__ void __launch_bounds__(256) roi_align_fwd_v8_kernel(Levels L, int64_t C, const float* __restrict__ rois, int PH,
+                                                               int PW, int sampling, int aligned, int multiscale,
+                                                               uint16_t* __restrict__ out, int32_t* __restrict__ lv_out) {
+  __shared__ Samp tab[kMaxSamp];
+  __shared__ RoiGeo sg;
+  __shared__ int slv;
+  const int64_t k = blockIdx.x;
+  const float* r = rois + 5 * k;
+  if (threadIdx.x == 0) {
+    int lv = multiscale ? level_of(r, L.k_min, L.n) : 0;
+    slv = lv;
+    sg = roi_geo(r, L.scale[lv], PH, PW, sampling, aligned);
+    if (lv_out) lv_out[k] = lv;
+  }
+  __syncthreads();
+  const int lv = slv;
+  const RoiGeo g = sg;
+  const int64_t H = L.H[lv], W = L.W[lv];
+  const int per_bin = g.gh * g.gw;
+  const int nbins = PH * PW;
+  const int ns = nbins * per_bin;
+  for (int i = threadIdx.x; i < ns; i += blockDim.x) {
+    int bin = i / per_bin, sidx = i % per_bin;
+    tab[i] = make_samp(g, H, W, bin / PW, bin % PW, sidx / g.gw, sidx % g.gw);
+  }
+  __syncthreads();
+  const int C8 = (int)(C / 8);
+  const uint16_t* f = (const uint16_t*)L.f[lv] + g.b * H * W * C;
+  for (int e = threadIdx.x; e < nbins * C8; e += blockDim.x) {
+    const int bin = e / C8, c0 = (e - bin * C8) * 8;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < per_bin; ++s) {
+      const Samp p = tab[bin * per_bin + s];
+      if (p.p1 < 0) continue;
+      const uint4 u1 = *(const uint4*)(f + (int64_t)p.p1 * C + c0), u2 = *(const uint4*)(f + (int64_t)p.p2 * C + c0);
+      const uint4 u3 = *(const uint4*)(f + (int64_t)p.p3 * C + c0), u4 = *(const uint4*)(f + (int64_t)p.p4 * C + c0);
+      const uint16_t *h1 = (const uint16_t*)&u1, *h2 = (const uint16_t*)&u2, *h3 = (const uint16_t*)&u3,
+                     *h4 = (const uint16_t*)&u4;
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        v[t] += ((p.w1 * bf2f(h1[t]) + p.w2 * bf2f(h2[t])) + p.w3 * bf2f(h3[t])) + p.w4 * bf2f(h4[t]);
+    }
+    uint4 o;
+    uint16_t* oh = (uint16_t*)&o;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) oh[t] = f2bf(v[t] / g.count);
+    *(uint4*)(out + (k * nbins + bin) * C + c0) = o;
+  }
+}
+
 static int check_grid(int PH, int PW, int sampling) {
   if (PH <= 0 || PW <= 0) return 0;
   if (sampling > 0 && PH * PW * sampling * sampling > kMaxSamp) return 0;
@@ -194,6 +247,8 @@ static int launch_fwd(const Levels& L, int dtype, int64_t C, const float* rois, 
   int threads = C >= 256 ? 256 : (int)(cdiv(C, 64) * 64);
   if (dtype == MX_F32)
     roi_align_fwd_kernel<float><<<(unsigned)K, threads, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms, (float*)out, lv);
+  else if (C % 8 == 0)
+    roi_align_fwd_v8_kernel<<<(unsigned)K, 256, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms, (uint16_t*)out, lv);
   else
     roi_align_fwd_kernel<uint16_t><<<(unsigned)K, threads, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms,
                                                                     (uint16_t*)out, lv);
