@@ -45,7 +45,8 @@ def build_model(device, trainable=3, backend=None):
 
 def make_optimizer(model):
     params = [p for p in model.parameters() if p.requires_grad]
-    return torch.optim.SGD(params, lr=0.005, momentum=0.9, weight_decay=0.0005)
+    from mx_det.optim import SGD
+    return SGD(params, lr=0.005, momentum=0.9, weight_decay=0.0005)
 
 
 def train_step(model, opt, images, targets, augment=False, gen=None):

@@ -202,6 +202,11 @@ int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* 
 int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw, int64_t Kout,
                        int64_t Cin, int layout, void* ws, size_t ws_bytes, mx_stream_t stream);
 /* wgrad grid sizing knob: split the pixel axis until ~blocks workgroups (default 512). */
+/* fwd/dgrad operand loader knob: 1 (default) buffer descriptors with wave-uniform tap offsets where
+ * the shape allows (input channels % 32 == 0, R*S <= 64, operands < 2 GiB), 0 per-lane global loads. */
+int mx_conv_set_loader(int loader);
+/* fwd/dgrad block-tile override for tuning: (0, 0) automatic, else rows 64/128 x columns 64/128/256. */
+int mx_conv_set_tile(int block_rows, int block_cols);
 int mx_conv_set_wgrad_target(int64_t blocks);
 
 /* NHWC pooling / resampling (bf16, C % 8 == 0).
@@ -264,6 +269,15 @@ int mx_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, in
                     const float* mean, const float* invstd, const float* gamma, const float* sums,
                     uint16_t* dx, uint16_t* dres /*nullable: grad of residual = masked dy*/,
                     mx_stream_t stream);
+
+/* Multi-tensor SGD step (torch.optim.SGD semantics; the reference's SGD(lr 0.005, momentum 0.9,
+ * weight_decay 5e-4), scripts/train_frcnn_baseline.py:149-153, step at :176): for each of `count`
+ * f32 tensors (host arrays of device pointers / element counts), d = g + wd*p; buf = first[i] ? d :
+ * momentum*buf + (1-dampening)*d; p -= lr * (nesterov ? d + momentum*buf : buf). One launch per 64
+ * tensors. */
+int mx_sgd_step(float* const* params, const float* const* grads, float* const* momentum_bufs,
+                const int64_t* numels, const uint8_t* first, int64_t count, float lr, float momentum,
+                float dampening, float weight_decay, int nesterov, mx_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Restoration pre-pass on device (scripts/restore_testsets.py:53-79, restoration_net.py:44-106).

@@ -54,6 +54,8 @@ struct ConvP {
   // (n, st_h*hh + ph, st_w*ww + pw) of the full [N][H][W] grid
   int remap, rst_h, rst_w, rph, rpw;
   int64_t rH, rW;
+  // element counts of the A source and of the B operand (buffer-descriptor ranges)
+  int64_t src_elems, wt_elems;
 };
 
 __device__ __forceinline__ int64_t out_row(const ConvP& p, int64_t m) {
@@ -605,6 +607,142 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
   conv_epilogue<BN, 2, BMT>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Buffer-descriptor variant of conv_igemm_pipe_kernel (BKT = 32, IC % 32 == 0, R*S <= 64): a 32-wide
+// K-tile lies inside one tap, so the tap (r, s) and channel offset are wave-uniform and ride in the
+// SGPR soffset of buffer_load_dwordx4 ... lds; every lane keeps a loop-invariant 32-bit voffset per
+// A row / B row. Padding taps come from a per-row 64-bit validity mask (one bit per tap): an
+// invalid row points its voffset past the descriptor's range, so the hardware range check returns
+// zeros (no zero page, no per-tile 64-bit address arithmetic). Same LDS ring, MFMA loop and
+// epilogue as the pipe kernel.
+static constexpr uint32_t kOOB = 0x80000000u;
+
+template <int BN, int MODE, int STAGES, int OCC, int BMT = BM>
+__global__ void __launch_bounds__(NT, OCC) conv_igemm_buf_kernel(ConvP p) {
+#if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BKT = 32, RB = BKT * 2, CPR = BKT / 8, RPI = 64 / CPR;
+  constexpr int AR = BMT / 4, AI = AR / RPI, BI = (BN / 4) / RPI, LOADS = AI + BI;
+  constexpr int A_BYTES = BMT * RB, STAGE = (BMT + BN) * RB;
+  constexpr int WN = BN / 2, TJ = WN / 16, WM = BMT / 2, TI = WM / 16;
+  static_assert(AI >= 1 && BI >= 1 && STAGES >= 2, "tile shape");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t ntiles_n = (p.Ncol + BN - 1) / BN;
+  const int64_t gid = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int split = (int)(gid % p.splits);
+  const int64_t bid = gid / p.splits;
+  const int64_t mt = bid / ntiles_n, nt = bid % ntiles_n;
+  const int64_t m0 = mt * BMT, n0 = nt * BN;
+  const int lrow = lane / CPR;
+  const int lch = (lane % CPR) ^ tile_swz<CPR>(lrow);
+  const int IH = (int)p.IH, IW = (int)p.IW, IC = (int)p.IC, R = p.R, S = p.S;
+  // A rows: origin pixel offset (elements) and tap validity mask
+  uint32_t a_voff[AI];
+  uint64_t a_mask[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int64_t m = m0 + wave * AR + i * RPI + lrow;
+    uint64_t mask = 0;
+    int32_t off = 0;
+    if (m < p.M) {
+      const int ow = (int)(m % p.OW);
+      const int64_t t = m / p.OW;
+      const int oh = (int)(t % p.OH);
+      const int n = (int)(t / p.OH);
+      // MODE 0: ih = oh*st - pad + r; MODE 1: ih = hh + dh - ri = (hh + dh - (R-1)) + (R-1-ri)
+      const int h0 = MODE == 0 ? oh * p.st_h - p.pad_h : oh + p.pad_h - (R - 1);
+      const int w0 = MODE == 0 ? ow * p.st_w - p.pad_w : ow + p.pad_w - (S - 1);
+      off = ((n * IH + h0) * IW + w0) * IC + lch * 8;
+      for (int r = 0; r < R; ++r)
+        for (int q = 0; q < S; ++q) {
+          // tap index in the B column order; its source row/col offset (rr, qq) from the origin
+          const int rr = MODE == 0 ? r : R - 1 - r, qq = MODE == 0 ? q : S - 1 - q;
+          if ((unsigned)(h0 + rr) < (unsigned)IH && (unsigned)(w0 + qq) < (unsigned)IW) mask |= 1ull << (r * S + q);
+        }
+    }
+    a_voff[i] = (uint32_t)off * 2u;
+    a_mask[i] = mask;
+  }
+  uint32_t b_voff[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int64_t n = n0 + wave * (BN / 4) + i * RPI + lrow;
+    b_voff[i] = n < p.Ncol ? (uint32_t)((n * p.Kdim + lch * 8) * 2) : kOOB;
+  }
+  const __amdgpu_buffer_rsrc_t arsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.src, (short)0, (int)(p.src_elems * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t brsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.wt, (short)0, (int)(p.wt_elems * 2), 0x00020000);
+  const int64_t nk = p.Kdim / BKT;
+  const int64_t kbeg = (int64_t)split * p.kt_per_split;
+  const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
+  // wave-uniform K position of the next tile to issue: tap (r, q), channel c
+  int ck = (int)(kbeg * BKT);
+  int ctap = ck / IC;
+  int cc = ck - ctap * IC;
+  int cr = ctap / S, cq = ctap - (ctap / S) * S;
+  auto issue = [&](int buf) {
+    char* A = smem + buf * STAGE;
+    char* B = A + A_BYTES;
+    const int rr = MODE == 0 ? cr : R - 1 - cr, qq = MODE == 0 ? cq : S - 1 - cq;
+    const uint32_t a_soff = (uint32_t)(((rr * IW + qq) * IC + cc) * 2);
+    const uint32_t b_soff = (uint32_t)(ck * 2);
+    const int tap = cr * S + cq;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      // the whole offset in voffset (the origin may be negative; the tap offset brings it in range)
+      const uint32_t v = ((a_mask[i] >> tap) & 1ull) ? a_voff[i] + a_soff : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (LDS_AS void*)(A + (wave * AR + i * RPI) * RB), 16, v, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (LDS_AS void*)(B + (wave * (BN / 4) + i * RPI) * RB), 16, b_voff[i],
+                                               b_soff, 0, 0);
+    ck += BKT;
+    cc += BKT;
+    if (cc == IC) {
+      cc = 0;
+      if (++cq == S) { cq = 0; ++cr; }
+    }
+  };
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < STAGES - 1; ++st)
+    if (st < ntk) issue(st);
+  for (int64_t t = 0; t < ntk; ++t) {
+    if (t + STAGES - 2 < ntk) wait_vmcnt<LOADS * (STAGES - 2)>();
+    else wait_vmcnt<0>();
+    block_barrier();
+    if (t + STAGES - 1 < ntk) issue((int)((t + STAGES - 1) % STAGES));
+    const char* A = smem + (int)(t % STAGES) * STAGE;
+    const char* B = A + A_BYTES;
+    const int ch = lane >> 4;
+    bf16x8 af[TI], bfr[TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      int row = wm * WM + i * 16 + (lane & 15);
+      af[i] = *(const bf16x8*)(A + row * RB + ((ch ^ tile_swz<CPR>(row)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      int row = wn * WN + j * 16 + (lane & 15);
+      bfr[j] = *(const bf16x8*)(B + row * RB + ((ch ^ tile_swz<CPR>(row)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();
+  conv_epilogue<BN, 2, BMT>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
+#endif
+}
+
 // Split-K reduce + epilogue: block = 128 rows x 64 columns; thread = 8 columns x 4 rows.
 // Sums the splits' f32 partials, then bias / residual / activation / store and the BN statistics
 // partials of the 128-row block (same [2][mblocks][Ncol] layout as the fused epilogue).
@@ -1106,20 +1244,60 @@ static int g_conv_variant = 7;
 // (< ~1.25 blocks per CU) split the K loop, keeping >= 4 K-tiles (of 64) per split.
 struct Geo {
   int64_t M, Ncol, Kdim, tiles, nk;
-  int splits, bmt;
+  int splits, bmt, bn;
   bool narrow;
 };
+static int num_cus();
+static int g_force_bmt = 0, g_force_bn = 0;  // mx_conv_set_tile (0 = automatic)
+extern "C" int mx_conv_set_tile(int bmt, int bn) {
+  MX_CHECK_ARG((bmt == 0 && bn == 0) || ((bmt == 64 || bmt == 128) && (bn == 64 || bn == 128 || bn == 256)),
+               "mx_conv_set_tile: (0,0) auto, or bmt 64/128 x bn 64/128/256");
+  g_force_bmt = bmt;
+  g_force_bn = bn;
+  return MX_OK;
+}
+
 static Geo make_geo(int64_t M, int64_t Ncol, int64_t Kdim) {
   Geo g;
   g.M = M; g.Ncol = Ncol; g.Kdim = Kdim;
   g.narrow = g.Ncol <= 64;
-  const int64_t ntn = g.narrow ? cdiv(g.Ncol, 64) : cdiv(g.Ncol, 128);
+  g.bn = g.narrow ? 64 : 128;
   g.bmt = BM;
-  g.tiles = cdiv(g.M, BM) * ntn;
+  g.tiles = cdiv(g.M, BM) * cdiv(g.Ncol, g.bn);
+  if (g_conv_variant == 9 && g.Ncol >= 256) {
+    g.bn = 256;
+    g.tiles = cdiv(g.M, BM) * cdiv(g.Ncol, 256);
+  } else if (g_conv_variant == 7 && !g.narrow && g.tiles >= 320) {
+    // big grids: pick the block tile by (relative per-round throughput) x (wave fill), where a
+    // round is one resident block per slot (occupancy x CUs): 128x256 reads the gathered A operand
+    // once per 256 output channels and issues 12 LDS reads per 32 MFMAs (fastest per full round),
+    // but few, large tiles leave the last round mostly empty (measured, MI355X: P2 3x3 picks
+    // 128x128, the box-head 3x3 on 1024 RoIs 128x256, layer2 3x3 64x128)
+    struct Cand { int bmt, bn, occ; double thr; };
+    const Cand cand[3] = {{128, 256, 2, 1.0}, {128, 128, 3, 0.78}, {64, 128, 4, 0.62}};
+    const int64_t cus = num_cus();
+    double best = -1.0;
+    for (const Cand& c : cand) {
+      if (c.bn > g.Ncol) continue;
+      const int64_t tiles = cdiv(g.M, c.bmt) * cdiv(g.Ncol, c.bn), slots = c.occ * cus;
+      const double fill = (double)tiles / (double)(cdiv(tiles, slots) * slots);
+      if (c.thr * fill > best) {
+        best = c.thr * fill;
+        g.bmt = c.bmt; g.bn = c.bn; g.tiles = tiles;
+      }
+    }
+  }
+  const int64_t ntn = cdiv(g.Ncol, g.bn);
   // small grids: 64-row tiles first (twice the blocks, no partial-sum traffic), split-K only below that
-  if (g_conv_variant == 8 || (g_conv_variant == 7 && g.tiles < 320)) {
+  if (g.bn != 256 && g.bmt == BM && (g_conv_variant == 8 || (g_conv_variant == 7 && g.tiles < 320))) {
     g.bmt = 64;
     g.tiles = cdiv(g.M, 64) * ntn;
+  }
+  if (g_force_bmt) {
+    g.bmt = g_force_bmt;
+    g.bn = g_force_bn;
+    g.narrow = g.bn == 64;
+    g.tiles = cdiv(g.M, g.bmt) * cdiv(g.Ncol, g.bn);
   }
   g.nk = cdiv(g.Kdim, BK);
   g.splits = 1;
@@ -1134,8 +1312,8 @@ static Geo make_geo(int64_t M, int64_t Ncol, int64_t Kdim) {
 // The variant a launch runs: long K loops on big grids favour 64-wide K-tiles (fewer barriers),
 // short loops and small / split grids the 3-deep 32-wide ring at 3 blocks per CU; 64-row tiles
 // for grids under ~1.25 blocks per CU.
-static int num_cus();
 static int launch_kind(const Geo& g) {
+  if (g.bn == 256 && g.bmt == 128) return 9;
   if (g.bmt == 64) return 8;
   if (g_conv_variant != 7) return g_conv_variant;
   if (g.splits > 1 || g.nk < 16) return 3;
@@ -1213,6 +1391,24 @@ static void launch_pipe(const ConvP& p, int64_t blocks, hipStream_t st) {
   conv_igemm_pipe_kernel<BN, MODE, BKT, STAGES, OCC, BMT><<<(unsigned)blocks, NT, std::max(ring, epi), st>>>(p);
 }
 
+template <int BN, int MODE, int STAGES, int OCC, int BMT>
+static void launch_buf(const ConvP& p, int64_t blocks, hipStream_t st) {
+  size_t ring = (size_t)STAGES * (BMT + BN) * 32 * 2;
+  size_t epi = (size_t)(BMT / 2) * (BN + 4) * 4;
+  conv_igemm_buf_kernel<BN, MODE, STAGES, OCC, BMT><<<(unsigned)blocks, NT, std::max(ring, epi), st>>>(p);
+}
+
+// A/B loader: 1 (default) buffer descriptors with wave-uniform tap offsets where the shape allows
+// (conv_igemm_buf_kernel), 0 the per-lane 64-bit global_load_lds kernels only
+static int g_conv_loader = 1;
+extern "C" int mx_conv_set_loader(int v) {
+  // 2 / 3: timing-only diagnostics (wrong results): the A / B descriptor gets zero records, so the
+  // range check drops that operand's loads (prices its memory traffic)
+  MX_CHECK_ARG(v >= 0 && v <= 3, "mx_conv_set_loader: 0 global_load_lds, 1 buffer descriptors, 2/3 timing-only");
+  g_conv_loader = v;
+  return MX_OK;
+}
+
 template <int BN, int MODE>
 static void launch_variant(int v, const ConvP& p, int64_t blocks, hipStream_t st) {
   switch (v) {
@@ -1239,8 +1435,11 @@ static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipSt
   int64_t blocks = g.tiles;
   MX_CHECK_ARG(g.Kdim < (1ll << 30) && p.IH < (1ll << 26) && p.IW < (1ll << 26), "conv: GEMM K or spatial size too large");
   MX_CHECK_ARG(blocks * g.splits < (1ll << 31), "conv: grid too large");
-  const int v = launch_kind(g);
-  const int64_t bkt = (v == 3 || v == 5 || v == 8) ? 32 : 64;
+  const bool buf = g_conv_loader >= 1 && p.IC % 32 == 0 && p.R * p.S <= 64 && p.Kdim % 32 == 0 && p.src_elems > 0 &&
+                   p.src_elems * 2 < (1ll << 31) && p.wt_elems > 0 && p.wt_elems * 2 < (1ll << 31);
+  MX_CHECK_ARG(buf || g.bn != 256 || g.bmt == BM, "conv: 64x256 tiles need the buffer loader");
+  const int v = buf ? 3 : launch_kind(g);
+  const int64_t bkt = (buf || v == 3 || v == 5 || v == 8 || v == 9) ? 32 : 64;
   const int64_t nk = cdiv(g.Kdim, bkt);  // K-tiles in the kernel's tile width
   p.splits = 1;
   p.kt_per_split = nk;
@@ -1253,7 +1452,18 @@ static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipSt
     p.slab = (float*)ws;
     blocks *= p.splits;
   }
-  if (g.narrow) launch_variant<64, MODE>(v, p, blocks, st);
+  if (buf) {
+    if (g_conv_loader == 2) p.src_elems = 0;
+    if (g_conv_loader == 3) p.wt_elems = 0;
+    if (g.bmt == 64) {
+      if (g.bn == 256) launch_buf<256, MODE, 3, 2, 64>(p, blocks, st);
+      else if (g.narrow) launch_buf<64, MODE, 3, 4, 64>(p, blocks, st);
+      else launch_buf<128, MODE, 3, 4, 64>(p, blocks, st);
+    } else if (g.bn == 256) launch_buf<256, MODE, 3, 2, 128>(p, blocks, st);
+    else if (g.narrow) launch_buf<64, MODE, 3, 3, 128>(p, blocks, st);
+    else launch_buf<128, MODE, 3, 3, 128>(p, blocks, st);
+  } else if (g.bn == 256) launch_pipe<256, MODE, 32, 3, 2>(p, blocks, st);
+  else if (g.narrow) launch_variant<64, MODE>(v, p, blocks, st);
   else launch_variant<128, MODE>(v, p, blocks, st);
   MX_LAUNCH_CHECK();
   if (p.slab) {
@@ -1276,9 +1486,10 @@ extern "C" int mx_conv_set_wgrad_variant(int v) {
 extern "C" int mx_conv_get_wgrad_variant(void) { return g_wgrad_variant; }
 
 extern "C" int mx_conv_set_variant(int v) {
-  MX_CHECK_ARG(v >= 0 && v <= 8,
+  MX_CHECK_ARG(v >= 0 && v <= 9,
                "mx_conv_set_variant: 0 register staging, 1/2 direct-to-LDS fwd/dgrad, 3-6 multi-stage "
-               "direct-to-LDS (3: BK32x3, 4: BK64x2, 5: BK32x4, 6: BK64x3), 7 auto, 8 64-row tiles BK32x3");
+               "direct-to-LDS (3: BK32x3, 4: BK64x2, 5: BK32x4, 6: BK64x3), 7 auto, 8 64-row tiles BK32x3, "
+               "9 as 7 with 128x256 tiles wherever Ncol >= 256");
   g_conv_variant = v;
   return MX_OK;
 }
@@ -1298,6 +1509,7 @@ extern "C" int mx_conv2d_fwd_ex(const mx_conv_shape* s, const uint16_t* x, const
   p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
   p.bias = bias; p.residual = residual; p.act = act; p.out = y; p.out_f32 = ydtype == MX_F32;
   p.stats = stats; p.mblocks = cdiv(p.M, SROWS);
+  p.src_elems = s->N * s->H * s->W * s->C; p.wt_elems = p.Ncol * p.Kdim;
   return launch_igemm<0>(p, make_geo(p.M, p.Ncol, p.Kdim), ws, ws_bytes, (hipStream_t)stream);
 }
 
@@ -1432,6 +1644,7 @@ extern "C" int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, con
     p.out = dx; p.out_f32 = 0; p.act = 0;
     p.remap = remap; p.rst_h = s->stride_h; p.rst_w = s->stride_w; p.rph = c.ph; p.rpw = c.pw;
     p.rH = s->H; p.rW = s->W;
+    p.src_elems = s->N * s->Ho * s->Wo * s->K; p.wt_elems = p.Ncol * p.Kdim;
     rc = launch_igemm<1>(p, make_geo(p.M, p.Ncol, p.Kdim), ws, ws_bytes, (hipStream_t)stream);
     if (rc) return rc;
   }

@@ -42,9 +42,12 @@ __device__ __forceinline__ float unord_f32(uint32_t u) {
 // keys for the segment sort; offset boxes for the coordinate trick
 __global__ void nms_keys_kernel(const float4* __restrict__ boxes, const float* __restrict__ scores,
                                 const int64_t* __restrict__ idxs, int64_t n, int trick, const uint32_t* __restrict__ maxbits,
-                                uint64_t* __restrict__ keys, int32_t* __restrict__ vals, float4* __restrict__ obox) {
+                                uint64_t* __restrict__ keys, int32_t* __restrict__ vals, float4* __restrict__ obox,
+                                int32_t* __restrict__ flags, int32_t* __restrict__ nk) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  flags[i] = 0;  // keep flags / keep count for the scan (no separate memsets)
+  if (i == 0) *nk = 0;
   float4 b = boxes[i];
   uint32_t hi = 0;
   if (trick) {
@@ -324,14 +327,13 @@ extern "C" int mx_batched_nms(const float* boxes, const float* scores, const int
   MX_CHECK_ARG(Wm * 8 <= 64 * 1024, "mx_batched_nms: segment bound %lld too large", (long long)max_seg);
   const int T = 256;
   const int nb = (int)cdiv(n, T);
-  MX_HIP(hipMemsetAsync(w.flags, 0, sizeof(int32_t) * n, s));
-  MX_HIP(hipMemsetAsync(w.nk, 0, sizeof(int32_t), s));
   if (trick) {
     MX_HIP(hipMemsetAsync(w.maxbits, 0, sizeof(uint32_t), s));
     nms_max_kernel<<<(int)std::min<int64_t>(cdiv(4 * n, T), 1024), T, 0, s>>>(boxes, 4 * n, w.maxbits);
     MX_LAUNCH_CHECK();
   }
-  nms_keys_kernel<<<nb, T, 0, s>>>((const float4*)boxes, scores, idxs, n, trick, w.maxbits, w.k0, w.v0, w.obox);
+  nms_keys_kernel<<<nb, T, 0, s>>>((const float4*)boxes, scores, idxs, n, trick, w.maxbits, w.k0, w.v0, w.obox, w.flags,
+                                   w.nk);
   MX_LAUNCH_CHECK();
   size_t cb = w.cub_bytes;
   int end_bit = (idxs && !trick) ? 64 : 32;

@@ -55,6 +55,8 @@ _SIGS = {
     "mx_conv_workspace": (c_sz, [ctypes.POINTER(ConvShape), c_int]),
     "mx_conv_set_variant": (c_int, [c_int]),
     "mx_conv_get_variant": (c_int, []),
+    "mx_conv_set_loader": (c_int, [c_int]),
+    "mx_conv_set_tile": (c_int, [c_int, c_int]),
     "mx_conv_set_wgrad_variant": (c_int, [c_int]),
     "mx_conv_get_wgrad_variant": (c_int, []),
     "mx_conv_set_wgrad_target": (c_int, [c_i64]),
@@ -81,6 +83,7 @@ _SIGS = {
     "mx_act_bias_bwd_workspace": (ctypes.c_size_t, [c_i64, c_i64]),
     "mx_act_bias_bwd": (c_int, [c_vp, c_vp, c_int, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, ctypes.c_size_t,
                                 c_vp]),
+    "mx_sgd_step": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_f, c_f, c_int, c_vp]),
     "mx_bn_apply": (c_int, [c_vp, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "mx_bn_bwd_reduce": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
     "mx_bn_bwd_apply": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -173,7 +173,8 @@ def train_frcnn(cfg):
         ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index], broadcast_buffers=False,
                                                         gradient_as_bucket_view=True)
     params = [p for p in model.parameters() if p.requires_grad]
-    optimizer = torch.optim.SGD(params, lr=cfg["LR"], momentum=cfg["MOMENTUM"], weight_decay=cfg["WEIGHT_DECAY"])
+    from .optim import SGD
+    optimizer = SGD(params, lr=cfg["LR"], momentum=cfg["MOMENTUM"], weight_decay=cfg["WEIGHT_DECAY"])
     sched = torch.optim.lr_scheduler.StepLR(optimizer, step_size=8, gamma=0.1)
     corrupt = RandomCorruptionGPU(p=0.5) if cfg.get("AUGMENT") else None
     history, best_ckpt, last_ckpt = out_dir / "history.jsonl", out_dir / "best.pth", out_dir / "last.pth"

@@ -50,16 +50,23 @@ def main():
     ap.add_argument("--variants", default="7")
     ap.add_argument("--wgrad", default="0")
     ap.add_argument("--wtarget", default="0")
+    ap.add_argument("--loaders", default="1")
+    ap.add_argument("--tiles", default="0x0", help="comma list of BMTxBN overrides, 0x0 = auto")
     args = ap.parse_args()
     from mx_det import _lib
-    for v in [int(x) for x in args.variants.split(",")]:
-        for wv in [int(x) for x in args.wgrad.split(",")]:
-            for wt in [int(x) for x in args.wtarget.split(",")]:
-                _lib.call("mx_conv_set_variant", v)
-                _lib.call("mx_conv_set_wgrad_variant", wv)
-                _lib.call("mx_conv_set_wgrad_target", wt)
-                print(f"== conv variant {v} wgrad variant {wv} wgrad target {wt}", flush=True)
-                run(args)
+    for ld in [int(x) for x in args.loaders.split(",")]:
+        for v in [int(x) for x in args.variants.split(",")]:
+            for wv in [int(x) for x in args.wgrad.split(",")]:
+                for wt in [int(x) for x in args.wtarget.split(",")]:
+                  for tl in args.tiles.split(","):
+                    bm, bn = [int(x) for x in tl.split("x")]
+                    _lib.call("mx_conv_set_tile", bm, bn)
+                    _lib.call("mx_conv_set_loader", ld)
+                    _lib.call("mx_conv_set_variant", v)
+                    _lib.call("mx_conv_set_wgrad_variant", wv)
+                    _lib.call("mx_conv_set_wgrad_target", wt)
+                    print(f"== loader {ld} tile {tl} conv variant {v} wgrad variant {wv} wgrad target {wt}", flush=True)
+                    run(args)
 
 
 def run(args):
