@@ -94,10 +94,16 @@ def conv_roofline(model, opt, imgs, tg):
     from mx_det import conv as mc
     t = mc.KernelTimer()
     mc.set_timer(t)
+    graphs = os.environ.get("MX_GRAPHS")
+    os.environ["MX_GRAPHS"] = "0"  # an eager step: every conv launch passes through the timer
     try:
         train_step(model, opt, imgs, tg)
     finally:
         mc.set_timer(None)
+        if graphs is None:
+            del os.environ["MX_GRAPHS"]
+        else:
+            os.environ["MX_GRAPHS"] = graphs
     s = {k: v for k, v in t.summary().items() if not k.startswith("bn_")}  # conv kinds only
     dom = max(s, key=lambda k: s[k]["ms"])
     d = s[dom]
@@ -106,8 +112,10 @@ def conv_roofline(model, opt, imgs, tg):
     allms = sum(v["ms"] for v in s.values())
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
-            "kernel": {"fwd128": "conv_igemm_pipe_kernel<128,0,*>", "fwd64": "conv_igemm_pipe_kernel<64,0,*>",
-                       "dgrad": "conv_igemm_pipe_kernel<*,1,*>", "wgrad": "conv_wgrad_kernel"}[dom],
+            "kernel": {"fwd128": "conv_igemm_buf_kernel<128|256,0,*> (+ conv_splitk_reduce_kernel)",
+                       "fwd64": "conv_igemm_buf_kernel<64,0,*> (+ conv_splitk_reduce_kernel)",
+                       "dgrad": "conv_igemm_buf_kernel<*,1,*> (+ conv_splitk_reduce_kernel)",
+                       "wgrad": "conv_wgrad_buf_kernel (+ wgrad_reduce_kernel)"}[dom],
             "launches_per_step": d["launches"], "avg_launch_us": round(1000 * d["ms"] / d["launches"], 2),
             "gflop_per_launch": round(d["flops"] / d["launches"] / 1e9, 3),
             "conv_stack": {"tflops": round(allf / (allms * 1e-3) / 1e12, 2), "gflop_per_step": round(allf / 1e9, 1),

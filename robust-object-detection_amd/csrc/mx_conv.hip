@@ -815,7 +815,7 @@ struct WgP {
   const uint16_t* x;   // [N][H][W][C]
   float* dw;           // layout 0: [Kout][R][S][Cin]; 1: [Kout][Cin][R][S] (torch's weight layout)
   int64_t P, K, Ncol;  // Ncol = R*S*C
-  int64_t OH, OW, H, W, C;
+  int64_t OH, OW, H, W, C, N;
   int R, S, st_h, st_w, pad_h, pad_w;
   int64_t kchunk;      // pixels per split
   float* slab;         // splits > 1: per-split partials [splits][K][Ncol], summed by wgrad_reduce_kernel
@@ -1118,6 +1118,123 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_glds_kernel(WgP p) {
     __syncthreads();
   }
   wgrad_store(p, acc, k0, c0, wm, wn, lane);
+}
+
+// wgrad on buffer descriptors (the buf analogue of conv_wgrad_glds_kernel): 32-pixel K-tiles in a
+// 3-deep LDS ring (48 KiB, 3 blocks per CU), both operands staged by buffer_load_dwordx4 ... lds (one
+// wave instruction = 4 pixel rows x 256 B; the swz_w XOR applied on the source chunk). Every lane
+// owns fixed rows of every tile and one fixed column chunk, so its gather position advances by a
+// division-free (n, oh, ow) walk and its offsets stay 32-bit: dy rows through a descriptor whose
+// range ends at this split's last pixel (later rows read zero), x rows through a validity select.
+__global__ void __launch_bounds__(NT, 3) conv_wgrad_buf_kernel(WgP p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int PXT = 32, STAGES = 3, OPB = PXT * 256, STAGE = 2 * OPB, LOADS = 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t ntn = (p.Ncol + 127) / 128;
+  const int64_t tile = blockIdx.x;
+  const int64_t mt = tile / ntn, nt = tile % ntn;
+  const int64_t k0 = mt * 128, c0 = nt * 128;
+  const int64_t pbeg = (int64_t)blockIdx.y * p.kchunk;
+  const int64_t pend = min<int64_t>(p.P, pbeg + p.kchunk);
+  if (pbeg >= pend) return;
+  const int lr = lane >> 4;
+  const int K = (int)p.K, C = (int)p.C, H = (int)p.H, W = (int)p.W, OW = (int)p.OW, OH = (int)p.OH;
+  // per instruction i (0, 1): tile row = wave * 8 + i * 4 + lr
+  uint32_t a_off[2];
+  int bn_[2], boh[2], bow[2], bpx[2];
+  int lcs[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 8 + i * 4 + lr;
+    lcs[i] = swz_w(row, lane & 15);
+    const int64_t px = pbeg + row;
+    a_off[i] = (k0 + lcs[i] * 8 < p.K) ? (uint32_t)((px * p.K + k0 + lcs[i] * 8) * 2) : kOOB;
+    bpx[i] = (int)px;
+    const int64_t t = px / OW;
+    bow[i] = (int)(px - t * OW);
+    boh[i] = (int)(t % OH);
+    bn_[i] = (int)(t / OH);
+  }
+  // B column chunk of each instruction's lane (fixed over the pixel loop): tap (r, s), channel c
+  int b_r[2], b_s[2], b_c[2];
+  bool b_col[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int64_t col = c0 + lcs[i] * 8;
+    b_col[i] = col < p.Ncol;
+    const int tap = b_col[i] ? (int)(col / C) : 0;
+    b_c[i] = b_col[i] ? (int)(col - (int64_t)tap * C) : 0;
+    b_r[i] = tap / p.S;
+    b_s[i] = tap - b_r[i] * p.S;
+  }
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, (short)0, (int)(pend * p.K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t brsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)(p.N * p.H * p.W * p.C * 2), 0x00020000);
+  const uint32_t a_step = (uint32_t)(PXT * K * 2);
+  auto issue = [&](int buf) {
+    char* A = smem + buf * STAGE;
+    char* B = A + OPB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = wave * 8 + i * 4;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (LDS_AS void*)(A + row * 256), 16, a_off[i], 0, 0, 0);
+      const int ih = boh[i] * p.st_h - p.pad_h + b_r[i], iw = bow[i] * p.st_w - p.pad_w + b_s[i];
+      const bool ok = b_col[i] && bpx[i] < pend && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const uint32_t bo = ok ? (uint32_t)((((bn_[i] * H + ih) * W + iw) * C + b_c[i]) * 2) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (LDS_AS void*)(B + row * 256), 16, bo, 0, 0, 0);
+      // advance this lane's rows by one tile
+      a_off[i] = a_off[i] == kOOB ? kOOB : a_off[i] + a_step;
+      bpx[i] += PXT;
+      bow[i] += PXT;
+      while (bow[i] >= OW) {
+        bow[i] -= OW;
+        if (++boh[i] == OH) { boh[i] = 0; ++bn_[i]; }
+      }
+    }
+  };
+  auto tr_read = [&](const char* T, int prow0, int colbase) -> s16x4 {
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    int row = prow0 + 8 * g + q;
+    int colx = colbase + 4 * pp;
+    int chunk = colx >> 3, within = (colx & 7) * 2;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(T + row * 256 + (swz_w(row, chunk) << 4) + within));
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nk = (pend - pbeg + PXT - 1) / PXT;
+#pragma unroll
+  for (int st = 0; st < STAGES - 1; ++st)
+    if (st < nk) issue(st);
+  for (int64_t it = 0; it < nk; ++it) {
+    if (it + STAGES - 2 < nk) wait_vmcnt<LOADS * (STAGES - 2)>();
+    else wait_vmcnt<0>();
+    block_barrier();
+    if (it + STAGES - 1 < nk) issue((int)((it + STAGES - 1) % STAGES));
+    const char* A = smem + (int)(it % STAGES) * STAGE;
+    const char* B = A + OPB;
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const s16x4 lo = tr_read(A, 0, wm * 64 + i * 16), hi = tr_read(A, 4, wm * 64 + i * 16);
+      af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const s16x4 lo = tr_read(B, 0, wn * 64 + j * 16), hi = tr_read(B, 4, wn * 64 + j * 16);
+      bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  wgrad_store(p, acc, k0, c0, wm, wn, lane);
+#endif
 }
 
 __global__ void transpose_w_kernel(const uint16_t* __restrict__ w, int64_t K, int64_t RS, int64_t C, uint16_t* __restrict__ wt) {
@@ -1476,10 +1593,11 @@ static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipSt
 
 extern "C" int mx_conv_get_variant(void) { return g_conv_variant; }
 
-// wgrad kernel variant: 0 register-staged 32-pixel K-tiles, 1 64-pixel K-tiles, 2 direct-to-LDS
-static int g_wgrad_variant = 0;
+// wgrad kernel variant: 0 register-staged 32-pixel K-tiles, 1 64-pixel K-tiles, 2 direct-to-LDS,
+// 3 (default) buffer descriptors (conv_wgrad_buf_kernel; maps under 32 output pixels take 0)
+static int g_wgrad_variant = 3;
 extern "C" int mx_conv_set_wgrad_variant(int v) {
-  MX_CHECK_ARG(v >= 0 && v <= 2, "mx_conv_set_wgrad_variant: 0 px32, 1 px64, 2 direct-to-LDS");
+  MX_CHECK_ARG(v >= 0 && v <= 3, "mx_conv_set_wgrad_variant: 0 px32, 1 px64, 2 direct-to-LDS, 3 buffer descriptors");
   g_wgrad_variant = v;
   return MX_OK;
 }
@@ -1707,8 +1825,8 @@ static WGeo wgrad_geo(const mx_conv_shape* s) {
   g.tiles = cdiv(s->K, 128) * cdiv(Ncol, 128);
   const int v = g_wgrad_variant;
   g.pxt = v == 2 ? BKG : (v == 1 ? 64 : BKW);
-  // resident blocks per CU: px32 3 (142 VGPRs), px64 / direct-to-LDS 2
-  const int64_t slots = g_wgrad_target ? g_wgrad_target : (int64_t)num_cus() * (v == 0 ? 3 : 2);
+  // resident blocks per CU: px32 / buffer 3 (142 VGPRs), px64 / direct-to-LDS 2
+  const int64_t slots = g_wgrad_target ? g_wgrad_target : (int64_t)num_cus() * ((v == 0 || v == 3) ? 3 : 2);
   int64_t splits = std::max<int64_t>(1, slots / g.tiles);  // never past one wave of blocks
   const int64_t max_splits = std::max<int64_t>(1, P / (g.pxt * 4));
   splits = std::min(splits, max_splits);
@@ -1741,7 +1859,7 @@ extern "C" int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, co
   WgP p{};
   p.dy = dy; p.x = x; p.dw = dw;
   p.P = s->N * s->Ho * s->Wo; p.K = s->K; p.Ncol = s->R * s->S * s->C;
-  p.OH = s->Ho; p.OW = s->Wo; p.H = s->H; p.W = s->W; p.C = s->C;
+  p.OH = s->Ho; p.OW = s->Wo; p.H = s->H; p.W = s->W; p.C = s->C; p.N = s->N;
   p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
   p.Kout = Kout; p.Cin = Cin; p.layout = layout;
   WGeo g = wgrad_geo(s);
@@ -1754,8 +1872,13 @@ extern "C" int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, co
   }
   MX_CHECK_ARG(g.tiles < (1ll << 31) && g.splits < 65536, "conv wgrad: grid too large");
   dim3 grid((unsigned)g.tiles, (unsigned)g.splits);
-  const int v = g_wgrad_variant;
-  if (v == 2) conv_wgrad_glds_kernel<<<grid, NT, 2 * 2 * BKG * 256, st>>>(p);
+  int v = g_wgrad_variant;
+  // the buffer kernel walks each lane's pixels by (n, oh, ow) increments: maps of fewer than 32
+  // output pixels (FC6 as a 7x7 conv on the RoI tile) would wrap many times per tile -> register kernel
+  if (v == 3 && !(p.P * p.K * 2 < (1ll << 31) && s->N * s->H * s->W * s->C * 2 < (1ll << 31) && p.OH * p.OW >= 32))
+    v = 0;
+  if (v == 3) conv_wgrad_buf_kernel<<<grid, NT, 3 * 2 * 32 * 256, st>>>(p);
+  else if (v == 2) conv_wgrad_glds_kernel<<<grid, NT, 2 * 2 * BKG * 256, st>>>(p);
   else if (v == 1) conv_wgrad_kernel<64><<<grid, NT, 0, st>>>(p);
   else conv_wgrad_kernel<32><<<grid, NT, 0, st>>>(p);
   MX_LAUNCH_CHECK();

@@ -283,9 +283,9 @@ class RegionProposalNetwork(nn.Module):
             final_scores.append(ks[k])
         return final_boxes, final_scores
 
-    def forward(self, images, features, targets=None, be=None):
+    def forward(self, images, features, targets=None, be=None, head=None):
         feats = list(features.values())
-        logits, deltas = self.head(feats, be)
+        logits, deltas = head if head is not None else self.head(feats, be)
         grid = [(f.shape[1], f.shape[2]) for f in feats]
         anchors = self.anchor_generator(images.tensors.shape[1:3], grid, feats[0].device, be)
         N = feats[0].shape[0]
@@ -574,6 +574,24 @@ class FasterRCNN(nn.Module):
         self._be = be
         return self
 
+    def _trunk(self, x, be):
+        """Backbone + FPN + RPN-head convs as one captured HIP graph per input shape (training, HIP
+        backend): their ~400 kernels per step replay from one forward and one backward graph launch
+        instead of being issued op by op from Python (torch.cuda.make_graphed_callables; the op
+        kernels are the same libmx_det launches, recorded on the capture stream). Off with
+        MX_GRAPHS=0, in eval, or for non-HIP backends."""
+        if not (self.training and x.is_cuda and getattr(be, "name", "") == "hip" and _graphs_enabled()):
+            return None
+        key = (tuple(x.shape), x.dtype)
+        cache = self.__dict__.setdefault("_mx_graphs", {})
+        g = cache.get(key)
+        if g is None:
+            g = cache[key] = _capture_trunk(self, be, x)
+        outs = g(x)
+        nf = len(self.backbone.fpn.inner_blocks) + 1
+        feats = OrderedDict(zip([str(i) for i in range(nf - 1)] + ["pool"], outs[:nf]))
+        return feats, (list(outs[nf:2 * nf]), list(outs[2 * nf:]))
+
     def forward(self, images, targets=None):
         be = self.be
         if hasattr(be, "prepare"):
@@ -593,8 +611,12 @@ class FasterRCNN(nn.Module):
             original = [(int(im.shape[0]), int(im.shape[1])) if im.dtype == torch.uint8 else
                         (int(im.shape[-2]), int(im.shape[-1])) for im in images]
         il, targets = self.transform(images, targets, be)
-        features = self.backbone(il.tensors, be)
-        proposals, rpn_losses = self.rpn(il, features, targets, be)
+        trunk = self._trunk(il.tensors, be)
+        if trunk is not None:  # HIP-graph replay of backbone + FPN + RPN head (static shapes)
+            features, head = trunk
+        else:
+            features, head = self.backbone(il.tensors, be), None
+        proposals, rpn_losses = self.rpn(il, features, targets, be, head=head)
         detections, det_losses = self.roi_heads(features, proposals, il.image_sizes, targets, be)
         if self.training:
             losses = {}
@@ -602,6 +624,107 @@ class FasterRCNN(nn.Module):
             losses.update(rpn_losses)
             return losses
         return self.transform.postprocess(detections, il.image_sizes, original)
+
+
+def _graphs_enabled():
+    import os
+    if os.environ.get("MX_GRAPHS", "1") == "0":
+        return False
+    import torch.distributed as dist
+    # under DDP the gradient all-reduce hooks live on the parameters' AccumulateGrad nodes, which the
+    # replayed backward graph bypasses: multi-rank training runs the trunk eagerly
+    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+
+class _Trunk(nn.Module):
+    """backbone + FPN + RPN head as one tensor -> tuple(tensors) callable (the graphed unit)."""
+
+    def __init__(self, model, be):
+        super().__init__()
+        self.backbone, self.head = model.backbone, model.rpn.head
+        self.be = be
+
+    def forward(self, x):
+        feats = self.backbone(x, self.be)
+        logits, deltas = self.head(list(feats.values()), self.be)
+        return tuple(feats.values()) + tuple(logits) + tuple(deltas)
+
+
+class _TrunkGraphs:
+    """Forward and backward HIP graphs of the trunk for one input shape. The backward graph writes
+    the trunk parameters' gradients into graph-owned buffers that become their .grad after each
+    replay (added when a .grad already exists), so no per-parameter autograd work runs in the step.
+    Capture follows torch.cuda.graph: eager warmup on a side stream, then one forward and one
+    backward capture in a shared private pool; BatchNorm running stats are restored afterwards."""
+
+    def __init__(self, model, be, x):
+        trunk = _Trunk(model, be)
+        self.params = [p for p in trunk.parameters() if p.requires_grad]
+        saved = {k: v.clone() for k, v in model.state_dict().items()
+                 if k.endswith(("running_mean", "running_var", "num_batches_tracked"))}
+        grads = [p.grad for p in self.params]
+        self.static_x = x.detach().clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                outs = trunk(self.static_x)
+                torch.autograd.backward(outs, [torch.ones_like(o) for o in outs])
+                for p in self.params:
+                    p.grad = None
+        torch.cuda.current_stream().wait_stream(side)
+        pool = torch.cuda.graph_pool_handle()
+        self.fwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.fwd, pool=pool):
+            self.static_out = trunk(self.static_x)
+        self.static_gout = [torch.zeros_like(o) for o in self.static_out]
+        self.bwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.bwd, pool=pool):
+            torch.autograd.backward(self.static_out, self.static_gout)
+        self.static_grads = [p.grad for p in self.params]
+        self.static_out = tuple(o.detach() for o in self.static_out)
+        for p, g in zip(self.params, grads):
+            p.grad = g
+        with torch.no_grad():
+            sd = model.state_dict()
+            for k, v in saved.items():
+                sd[k].copy_(v)
+        self.anchor = torch.zeros((), device=x.device, requires_grad=True)
+
+    def __call__(self, x):
+        return _TrunkFn.apply(x, self.anchor, self)
+
+
+class _TrunkFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, tg):
+        tg.static_x.copy_(x)
+        tg.fwd.replay()
+        ctx.tg = tg
+        # fresh tensor objects over the graph's static outputs (overwritten by the next replay)
+        return tuple(o.detach() for o in tg.static_out)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        tg = ctx.tg
+        for s, g in zip(tg.static_gout, gouts):
+            if g is None:
+                s.zero_()
+            else:
+                s.copy_(g)
+        tg.bwd.replay()
+        for p, g in zip(tg.params, tg.static_grads):
+            if g is None:
+                continue
+            if p.grad is None:
+                p.grad = g
+            else:
+                p.grad.add_(g)
+        return None, None, None
+
+
+def _capture_trunk(model, be, x):
+    return _TrunkGraphs(model, be, x)
 
 
 def fasterrcnn_resnet50_fpn_v2(weights=None, progress=True, num_classes=None, weights_backbone=None,

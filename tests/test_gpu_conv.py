@@ -26,16 +26,22 @@ CASES = [
 ]
 
 
-@pytest.fixture(params=[0, 1, 3, 4, 5, 6, 7, 8])
+@pytest.fixture(params=[(0, 0, 0), (1, 0, 2), (3, 0, 1), (4, 0, 1), (5, 0, 1), (6, 0, 1), (7, 0, 0), (8, 0, 1),
+                        (7, 1, 3), (8, 1, 3), (9, 1, 3), (7, 1, 0)])
 def variant(request):
-    """Every fwd/dgrad staging variant of the implicit-GEMM kernel (mx_conv_set_variant)."""
+    """Every fwd/dgrad staging variant of the implicit-GEMM kernel (mx_conv_set_variant), with the
+    per-lane global loader (0) or the buffer-descriptor loader (1, the default), and the wgrad
+    variants (mx_conv_set_wgrad_variant)."""
     from mx_det import _lib
+    v, loader, wv = request.param
     old = _lib.load().mx_conv_get_variant()
-    _lib.call("mx_conv_set_variant", request.param)
     oldw = _lib.load().mx_conv_get_wgrad_variant()
-    _lib.call("mx_conv_set_wgrad_variant", {0: 0, 1: 2, 3: 1}.get(request.param, 1))
-    yield request.param
+    _lib.call("mx_conv_set_variant", v)
+    _lib.call("mx_conv_set_loader", loader)
+    _lib.call("mx_conv_set_wgrad_variant", wv)
+    yield v
     _lib.call("mx_conv_set_variant", old)
+    _lib.call("mx_conv_set_loader", 1)
     _lib.call("mx_conv_set_wgrad_variant", oldw)
 
 
