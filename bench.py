@@ -88,6 +88,35 @@ def cpu_baseline(gpu_model, seconds_hint=30.0):
             "sample": f"{n} train step(s) x 2 images 1333x800 on {cores} CPU threads ({dt:.1f} s)"}
 
 
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_traffic.json")
+# kernels of one op: outer list = the op's sequential kernels (summed), inner = alternative template
+# instances of one kernel (launch-weighted mean)
+KIND_KERNELS = {"wgrad": [["mx::conv_wgrad_buf_kernel"], ["mx::wgrad_reduce_kernel"]],
+                "fwd128": [["mx::conv_igemm_buf_kernel<128, 0", "mx::conv_igemm_buf_kernel<256, 0"]],
+                "dgrad": [["mx::conv_igemm_buf_kernel<128, 1", "mx::conv_igemm_buf_kernel<256, 1",
+                           "mx::conv_igemm_buf_kernel<64, 1"]],
+                "fwd64": [["mx::conv_igemm_buf_kernel<64, 0"]]}
+
+
+def pmc_traffic(kind):
+    """HBM bytes per launch of the dominant op's kernels, from the committed rocprofv3 PMC pass
+    (tools/pmc_traffic.sh -> profiles/r01_traffic.json: 2*FETCH_SIZE + WRITE_SIZE, gfx950-corrected);
+    bench.py cannot run the profiler itself. None when the file or the kernels are absent."""
+    try:
+        import json as _j
+        d = _j.load(open(TRAFFIC_FILE))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    tot, hit = 0.0, False
+    for alts in KIND_KERNELS.get(kind, []):
+        ks = [v for k, v in d.items() if any(k.startswith(a) for a in alts)]
+        if ks:
+            n = sum(v["launches"] for v in ks)
+            tot += sum(v["bytes_per_launch"] * v["launches"] for v in ks) / n
+            hit = True
+    return round(tot / 1e6, 2) if hit else None
+
+
 def conv_roofline(model, opt, imgs, tg):
     """Live HIP-event timing of every conv kernel launch in one train step; the dominant kernel kind
     (largest total time) is reported against the bf16 MFMA peak with its algorithmic FLOPs."""
@@ -111,7 +140,8 @@ def conv_roofline(model, opt, imgs, tg):
     allf = sum(v["flops"] for v in s.values())
     allms = sum(v["ms"] for v in s.values())
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None,
+            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(dom),
+            "traffic_unit": "MB per launch (HBM, rocprofv3 PMC, profiles/r01_traffic.json)",
             "kernel": {"fwd128": "conv_igemm_buf_kernel<128|256,0,*> (+ conv_splitk_reduce_kernel)",
                        "fwd64": "conv_igemm_buf_kernel<64,0,*> (+ conv_splitk_reduce_kernel)",
                        "dgrad": "conv_igemm_buf_kernel<*,1,*> (+ conv_splitk_reduce_kernel)",
