@@ -753,15 +753,33 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
   const bool cok = col0 < p.Ncol;
   float s2[2][8] = {}, q2[2][8] = {};
   const int64_t stride = p.M * p.Ncol;
+  // the 4 rows' loads of one split plane are issued together (8 x 16 B in flight per thread); the
+  // per-element summation order over the splits is sequential
+  float va[4][8] = {};
+  for (int k = 0; k < p.splits; ++k) {
+    float4 a[4], b[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int64_t m = mt * BM + rl + 32 * rr;
+      if (cok && m < p.M) {
+        const float* src = p.slab + k * stride + m * p.Ncol + col0;
+        a[rr] = *(const float4*)src;
+        b[rr] = *(const float4*)(src + 4);
+      } else {
+        a[rr] = b[rr] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      va[rr][0] += a[rr].x; va[rr][1] += a[rr].y; va[rr][2] += a[rr].z; va[rr][3] += a[rr].w;
+      va[rr][4] += b[rr].x; va[rr][5] += b[rr].y; va[rr][6] += b[rr].z; va[rr][7] += b[rr].w;
+    }
+  }
+#pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     const int64_t m = mt * BM + rl + 32 * rr;
     if (!cok || m >= p.M) continue;
-    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const float* src = p.slab + m * p.Ncol + col0;
-    for (int k = 0; k < p.splits; ++k) {
-      float4 a = *(const float4*)(src + k * stride), b = *(const float4*)(src + k * stride + 4);
-      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
-    }
+    float* v = va[rr];
 #pragma unroll
     for (int t = 0; t < 8; ++t) { s2[rr >> 1][t] += v[t]; q2[rr >> 1][t] += v[t] * v[t]; }
     if (p.bias) {
@@ -854,33 +872,46 @@ __device__ __forceinline__ void wgrad_store(const WgP& p, f32x4 (&acc)[4][4], in
       }
 }
 
-// Sum of the split partials, written in dw's layout: thread = (k, 4 consecutive columns), reads
-// coalesced along the column axis of every split plane.
+// Sum of the split partials, written in dw's layout. Block = one output channel k x 256 columns:
+// wave w sums the split planes w, w+4, w+8, ... for its 64 float4 column groups (4 independent
+// 1-KiB loads in flight per wave per step), then wave 0 adds the other three waves' sums from LDS
+// in a fixed order (deterministic).
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(WgP p, int splits) {
+  __shared__ float4 part[3][64];
+  const int cg = threadIdx.x & 63, sg = threadIdx.x >> 6;
   const int64_t nc4 = p.Ncol >> 2;  // Ncol = R*S*C, C % 8 == 0
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= p.Kout * nc4) return;
-  const int64_t k = i / nc4, col = (i - k * nc4) * 4;
-  const int64_t plane = p.K * p.Ncol;
-  const float* src = p.slab + k * p.Ncol + col;
-  float4 v = *(const float4*)src;
-  int sp = 1;
-  for (; sp + 3 < splits; sp += 4) {
-    const float4 a = *(const float4*)(src + sp * plane), b = *(const float4*)(src + (sp + 1) * plane);
-    const float4 c = *(const float4*)(src + (sp + 2) * plane), d = *(const float4*)(src + (sp + 3) * plane);
-    v.x += (a.x + b.x) + (c.x + d.x);
-    v.y += (a.y + b.y) + (c.y + d.y);
-    v.z += (a.z + b.z) + (c.z + d.z);
-    v.w += (a.w + b.w) + (c.w + d.w);
+  const int64_t k = blockIdx.y, c4 = (int64_t)blockIdx.x * 64 + cg;
+  const bool ok = c4 < nc4;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    const int64_t plane = p.K * p.Ncol;
+    const float* src = p.slab + k * p.Ncol + c4 * 4;
+    int sp = sg;
+    for (; sp + 12 < splits; sp += 16) {
+      const float4 a = *(const float4*)(src + sp * plane), b = *(const float4*)(src + (sp + 4) * plane);
+      const float4 c = *(const float4*)(src + (sp + 8) * plane), d = *(const float4*)(src + (sp + 12) * plane);
+      v.x += (a.x + b.x) + (c.x + d.x);
+      v.y += (a.y + b.y) + (c.y + d.y);
+      v.z += (a.z + b.z) + (c.z + d.z);
+      v.w += (a.w + b.w) + (c.w + d.w);
+    }
+    for (; sp < splits; sp += 4) {
+      const float4 a = *(const float4*)(src + sp * plane);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
   }
-  for (; sp < splits; ++sp) {
-    const float4 a = *(const float4*)(src + sp * plane);
-    v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+  if (sg) part[sg - 1][cg] = v;
+  __syncthreads();
+  if (sg || !ok) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    const float4 o = part[w][cg];
+    v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
   }
   const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const int64_t o = wgrad_dst(p, k, (int)(col + t));
+    const int64_t o = wgrad_dst(p, k, (int)(c4 * 4 + t));
     if (o >= 0) p.dw[o] = vv[t];
   }
 }
@@ -1248,8 +1279,8 @@ __global__ void transpose_w_kernel(const uint16_t* __restrict__ w, int64_t K, in
 // Per-step weight preparation, one pass over the f32 master weight w[K][C][R][S] (torch layout):
 //   wk [K][R][S][Cpad] bf16      — fwd / wgrad operand (input channels zero-padded to Cpad)
 //   wt [class][Cpad][Rc][Sc][Kpad] bf16 — dgrad operand, taps grouped by stride-parity class
-// A 64(k) x 64(c) tile of one tap goes through LDS so both outputs are written along their
-// contiguous axis.
+// Tiles go through LDS so the f32 reads and both bf16 writes run along their contiguous axes
+// (pack_plan; R*S <= 196).
 struct PackP {
   const float* w;
   uint16_t* wk;
@@ -1259,56 +1290,150 @@ struct PackP {
   int64_t off[4];
   int Rc[4], Sc[4];
   int dense;  // wt as [R][S][Cpad][Kpad]: the 1x1-GEMM dgrad operand of a conv whose output is 1x1
+  // tiling (pack_plan): wk tiles = kr output rows x cw input channels x all taps (nwk of them, first),
+  // then wt tiles = 64 output channels x tct input channels x all taps
+  int kr, cw, tct;
+  int64_t nwk, nwt;
 };
 
-__device__ __forceinline__ void pack_tile(const PackP& p, int64_t c0, int64_t k0, int rs, float (*T)[65]) {
-  const int tid = threadIdx.x;
-  const int r = rs / p.S, sx = rs - (rs / p.S) * p.S, RS = p.R * p.S;
-  for (int e = tid; e < 64 * 64; e += 256) {
-    const int kk = e >> 6, cc = e & 63;
-    const int64_t k = k0 + kk, c = c0 + cc;
-    T[kk][cc] = (k < p.K && c < p.C) ? p.w[(k * p.C + c) * RS + rs] : 0.f;
+// Two tile kinds, each with contiguous f32 reads and 128-B bf16 write runs (values staged in LDS as
+// bf16, so the rounding is the one f2bf of the f32 master value):
+//  * wk tile: kr whole output rows (cw input channels x all taps each; cw = Cpad unless one row
+//    exceeds the LDS tile) -- a per-row [C][RS] -> [RS][Cpad] transpose, both sides contiguous;
+//  * wt tile: 64 output channels x tct input channels x all taps -- read as 64 contiguous runs of
+//    tct*RS floats, written along the innermost Kpad axis as output-channel pairs.
+static constexpr int PACK_LDS = 25600;  // bf16 elements (50 KiB)
+static constexpr int PK = 64;
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t a, uint32_t d, float inv) {  // a / d for a < 2^22
+  uint32_t q = (uint32_t)((float)a * inv);
+  if (q * d > a) --q;
+  else if ((q + 1) * d <= a) ++q;
+  return q;
+}
+
+__device__ __forceinline__ void st_bf2(uint16_t* d, uint16_t a, uint16_t b, bool two) {
+  if (two && ((uintptr_t)d & 3) == 0) {
+    *(uint32_t*)d = (uint32_t)a | ((uint32_t)b << 16);
+  } else {
+    d[0] = a;
+    if (two) d[1] = b;
+  }
+}
+
+// T[row * ldt + j] = bf16(w[(k0 + row) * C * RS + c0 * RS + j]) for j < n_valid (zero past the real
+// input channels / output rows); ldt % 4 == 0
+__device__ __forceinline__ void pack_stage(const PackP& p, int64_t k0, int64_t c0, int rows, int width, int ldt,
+                                           uint16_t* T) {
+  const int RS = p.R * p.S;
+  const int64_t cend = p.C < c0 + width / RS ? p.C : c0 + width / RS;
+  const int nvalid = cend > c0 ? (int)((cend - c0) * RS) : 0;
+  // U independent loads in flight per thread before the first LDS write (a load -> ds_write loop
+  // would wait out the full memory latency once per element)
+  constexpr int U = 8;
+  if ((p.C & 3) == 0 && (c0 & 3) == 0 && (width & 3) == 0 && ((uintptr_t)p.w & 15) == 0) {
+    // float4 path: every row run starts 16-B aligned and holds whole groups of 4
+    const int w4 = width >> 2, total4 = rows * w4, nv4 = nvalid >> 2;
+    const float inv4 = 1.f / (float)w4;
+    for (int base = 0; base < total4; base += 256 * U) {
+      float4 v[U];
+      int dst[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = base + u * 256 + threadIdx.x;
+        const int row = (int)fdiv((uint32_t)e, (uint32_t)w4, inv4), j4 = e - row * w4;
+        const int64_t k = k0 + row;
+        dst[u] = e < total4 ? row * ldt + 4 * j4 : -1;
+        v[u] = (e < total4 && k < p.K && j4 < nv4) ? *(const float4*)(p.w + (k * p.C + c0) * RS + 4 * j4)
+                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (dst[u] >= 0)
+          *(uint2*)(T + dst[u]) = make_uint2((uint32_t)f2bf(v[u].x) | ((uint32_t)f2bf(v[u].y) << 16),
+                                             (uint32_t)f2bf(v[u].z) | ((uint32_t)f2bf(v[u].w) << 16));
+    }
+    __syncthreads();
+    return;
+  }
+  const float inv = 1.f / (float)width;
+  const int total = rows * width;
+  for (int base = 0; base < total; base += 256 * U) {
+    float v[U];
+    int dst[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * 256 + threadIdx.x;
+      const int row = (int)fdiv((uint32_t)e, (uint32_t)width, inv), j = e - row * width;
+      const int64_t k = k0 + row;
+      dst[u] = e < total ? row * ldt + j : -1;
+      v[u] = (e < total && k < p.K && j < nvalid) ? p.w[(k * p.C + c0) * RS + j] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (dst[u] >= 0) T[dst[u]] = f2bf(v[u]);
   }
   __syncthreads();
-  if (p.wk) {
-    for (int e = tid; e < 64 * 64; e += 256) {
-      const int kk = e >> 6, cc = e & 63;
-      const int64_t k = k0 + kk, c = c0 + cc;
-      if (k < p.K && c < p.Cpad) p.wk[(k * RS + rs) * p.Cpad + c] = f2bf(T[kk][cc]);
-    }
-  }
-  if (p.wt && p.dense) {
-    for (int e = tid; e < 64 * 64; e += 256) {
-      const int cc = e >> 6, kk = e & 63;
-      const int64_t k = k0 + kk, c = c0 + cc;
-      if (k < p.Kpad && c < p.Cpad) p.wt[((int64_t)rs * p.Cpad + c) * p.Kpad + k] = f2bf(T[kk][cc]);
-    }
-  } else if (p.wt) {
-    const int ph = r % p.st_h, pw = sx % p.st_w;  // (parity of the tap) -> class with r0 = r % st
-    const int q = ph * p.st_w + pw;
-    const int ri = r / p.st_h, si = sx / p.st_w;
-    const int64_t base = p.off[q];
-    for (int e = tid; e < 64 * 64; e += 256) {
-      const int cc = e >> 6, kk = e & 63;
-      const int64_t k = k0 + kk, c = c0 + cc;
-      if (k < p.Kpad && c < p.Cpad)
-        p.wt[base + ((c * p.Rc[q] + ri) * p.Sc[q] + si) * p.Kpad + k] = f2bf(T[kk][cc]);
-    }
+}
+
+__device__ __forceinline__ void pack_wk_tile(const PackP& p, int64_t t, uint16_t* T) {
+  const int RS = p.R * p.S;
+  const int64_t nc = (p.Cpad + p.cw - 1) / p.cw;
+  const int64_t k0 = (t / nc) * p.kr, c0 = (t % nc) * p.cw;
+  const int cwv = (int)(p.Cpad - c0 < p.cw ? p.Cpad - c0 : p.cw);
+  const int width = cwv * RS, ldt = width + 4;
+  pack_stage(p, k0, c0, p.kr, width, ldt, T);
+  const int h = (cwv + 1) >> 1, per = RS * h;  // channel pairs per (row, tap)
+  const float inv_per = 1.f / (float)per, inv_h = 1.f / (float)h;
+  for (int e = threadIdx.x; e < p.kr * per; e += 256) {
+    const int row = (int)fdiv((uint32_t)e, (uint32_t)per, inv_per), rem = e - row * per;
+    const int rs = (int)fdiv((uint32_t)rem, (uint32_t)h, inv_h), c2 = rem - rs * h;
+    const int64_t k = k0 + row;
+    if (k >= p.K) continue;
+    const int cc = 2 * c2;
+    const uint16_t* tt = T + row * ldt + cc * RS + rs;
+    st_bf2(p.wk + (k * RS + rs) * p.Cpad + c0 + cc, tt[0], cc + 1 < cwv ? tt[RS] : (uint16_t)0, cc + 1 < cwv);
   }
 }
 
-__global__ void __launch_bounds__(256) pack_weight_kernel(PackP p) {
-  __shared__ float T[64][65];
-  pack_tile(p, (int64_t)blockIdx.x * 64, (int64_t)blockIdx.y * 64, blockIdx.z, T);
+__device__ __forceinline__ void pack_wt_tile(const PackP& p, int64_t t, uint16_t* T) {
+  const int RS = p.R * p.S;
+  const int64_t nc = (p.Cpad + p.tct - 1) / p.tct;
+  const int64_t k0 = (t / nc) * PK, c0 = (t % nc) * p.tct;
+  const int width = p.tct * RS, ldt = width + 4;
+  pack_stage(p, k0, c0, PK, width, ldt, T);
+  constexpr int PK2 = PK / 2;
+  const int per = RS * PK2;
+  const float inv_per = 1.f / (float)per;
+  for (int e = threadIdx.x; e < p.tct * per; e += 256) {
+    const int cc = (int)fdiv((uint32_t)e, (uint32_t)per, inv_per), rem = e - cc * per;
+    const int rs = rem / PK2, k2 = rem % PK2;  // PK2 is a power of two
+    const int64_t k = k0 + 2 * k2, c = c0 + cc;
+    if (k >= p.Kpad || c >= p.Cpad) continue;
+    const uint16_t* tt = T + 2 * k2 * ldt + cc * RS + rs;
+    int64_t dst;
+    if (p.dense) {  // [R][S][Cpad][Kpad]: the 1x1-GEMM dgrad operand of a conv whose output is 1x1
+      dst = ((int64_t)rs * p.Cpad + c) * p.Kpad + k;
+    } else {  // tap-parity class q (r % st_h, s % st_w): [c][r / st_h][s / st_w][Kpad]
+      const int r = rs / p.S, sx = rs - r * p.S;
+      const int q = (r % p.st_h) * p.st_w + (sx % p.st_w);
+      dst = p.off[q] + ((c * p.Rc[q] + r / p.st_h) * p.Sc[q] + sx / p.st_w) * p.Kpad + k;
+    }
+    st_bf2(p.wt + dst, tt[0], tt[ldt], k + 1 < p.Kpad);
+  }
 }
+
+__device__ __forceinline__ void pack_tile(const PackP& p, int64_t t) {
+  __shared__ uint16_t T[PACK_LDS];
+  if (t < p.nwk) pack_wk_tile(p, t, T);
+  else pack_wt_tile(p, t - p.nwk, T);
+}
+
+__global__ void __launch_bounds__(256) pack_weight_kernel(PackP p) { pack_tile(p, blockIdx.x); }
 
 // Every conv weight of a step in one launch: block -> (job, tile) through the tile prefix sums.
-__device__ __forceinline__ int64_t pack_tiles_c(const PackP& p) { return (p.Cpad + 63) / 64; }
-__device__ __forceinline__ int64_t pack_tiles_k(const PackP& p) { return ((p.wt ? p.Kpad : p.K) + 63) / 64; }
-
 __global__ void __launch_bounds__(256) pack_batched_kernel(const PackP* __restrict__ jobs, const int64_t* __restrict__ prefix,
                                                            int njobs) {
-  __shared__ float T[64][65];
   const int64_t b = blockIdx.x;
   int lo = 0, hi = njobs - 1;  // last job with prefix[j] <= b
   while (lo < hi) {
@@ -1316,11 +1441,26 @@ __global__ void __launch_bounds__(256) pack_batched_kernel(const PackP* __restri
     if (prefix[mid] <= b) lo = mid; else hi = mid - 1;
   }
   const PackP p = jobs[lo];
-  const int64_t t = b - prefix[lo];
-  const int64_t nc = pack_tiles_c(p), nk = pack_tiles_k(p);
-  const int64_t cx = t % nc, ky = (t / nc) % nk;
-  const int rs = (int)(t / (nc * nk));
-  pack_tile(p, cx * 64, ky * 64, rs, T);
+  pack_tile(p, b - prefix[lo]);
+}
+
+// Host: tile sizes of one pack job (both tile kinds fit PACK_LDS, rows padded by 4 elements)
+static int pack_plan(PackP& p) {
+  const int RS = p.R * p.S;
+  if (RS > 196) return MX_EINVAL;
+  p.tct = RS == 1 ? 64 : (RS <= 9 ? 32 : ((392 / RS) & ~3));  // multiples of 4: float4 staging
+  if (p.tct < 2) p.tct = 2;
+  int64_t cw = p.Cpad;
+  if (cw * RS + 4 > PACK_LDS) cw = ((PACK_LDS - 4) / RS) & ~3ll;
+  p.cw = (int)cw;
+  int64_t kr = 12288 / (cw * RS);
+  if (kr > 64) kr = 64;
+  while (kr > 1 && kr * (cw * RS + 4) > PACK_LDS) --kr;
+  if (kr < 1) kr = 1;
+  p.kr = (int)kr;
+  p.nwk = p.wk ? cdiv(p.K, p.kr) * cdiv(p.Cpad, p.cw) : 0;
+  p.nwt = p.wt ? cdiv(p.Kpad, (int64_t)PK) * cdiv(p.Cpad, (int64_t)p.tct) : 0;
+  return MX_OK;
 }
 
 // KRSC bf16 weight -> the dgrad parity-class layout of pack_weight_kernel (element-wise; used by
@@ -1674,8 +1814,10 @@ extern "C" int mx_conv_pack_weight(const mx_conv_shape* s, const float* w, int64
     p.st_h = p.st_w = 1;
   }
   // wk covers Kout rows only; wt also covers the zero-padded output channels up to s->K
-  dim3 grid((unsigned)cdiv(s->C, 64), (unsigned)cdiv(wt ? s->K : Kout, 64), (unsigned)(s->R * s->S));
-  pack_weight_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(p);
+  MX_CHECK_ARG(pack_plan(p) == MX_OK, "conv pack: at most 196 taps");
+  const int64_t tiles = p.nwk + p.nwt;
+  MX_CHECK_ARG(tiles < (1ll << 31), "conv pack: too many tiles");
+  pack_weight_kernel<<<(unsigned)tiles, 256, 0, (hipStream_t)stream>>>(p);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }
@@ -1699,7 +1841,8 @@ static int make_pack(const mx_pack_desc& d, PackP& p, int64_t& tiles) {
   } else {
     p.st_h = p.st_w = 1;
   }
-  tiles = cdiv(d.Cpad, 64) * cdiv(d.wt ? d.Kpad : d.Kout, 64) * (int64_t)d.R * d.S;
+  MX_CHECK_ARG(pack_plan(p) == MX_OK, "conv pack: at most 196 taps");
+  tiles = p.nwk + p.nwt;
   return MX_OK;
 }
 
@@ -1883,7 +2026,8 @@ extern "C" int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, co
   else conv_wgrad_kernel<32><<<grid, NT, 0, st>>>(p);
   MX_LAUNCH_CHECK();
   if (g.splits > 1) {
-    wgrad_reduce_kernel<<<(unsigned)cdiv(Kout * (p.Ncol / 4), 256), 256, 0, st>>>(p, (int)g.splits);
+    MX_CHECK_ARG(Kout < 65536, "conv wgrad: too many output channels for the split reduce");
+    wgrad_reduce_kernel<<<dim3((unsigned)cdiv(p.Ncol / 4, 64), (unsigned)Kout), 256, 0, st>>>(p, (int)g.splits);
     MX_LAUNCH_CHECK();
   }
   return MX_OK;

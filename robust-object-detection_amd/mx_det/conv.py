@@ -8,6 +8,7 @@ running buffers), so state_dicts load both ways; the kernels ta
 made once per step.
 """
 import ctypes
+import weakref
 
 import torch
 
@@ -254,9 +255,64 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad):
     return dx
 
 
-def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None):
+# ---- weight gradients on a side stream ----------------------------------------------------------
+# In the backward pass every conv's wgrad is independent of the dgrad chain that the next layers
+# wait for, so it runs on a second HIP stream: small-grid layers (layer3/4, small FPN levels) then
+# share the chip with the next layers' BN-backward and dgrad instead of running back to back. The
+# main stream joins the side stream at the end of the backward pass (an autograd engine callback);
+# the operands stay referenced until then. Single-process only: DDP's reducer reads each gradient
+# from its AccumulateGrad hook on the main stream, so multi-rank runs keep wgrad in order.
+_side = {}
+_pending = []
+
+
+class _Uses:
+    """Forward uses of one weight by the autograd graphs still waiting for their backward."""
+    __slots__ = ("n", "__weakref__")
+
+    def __init__(self):
+        self.n = 0
+
+
+_uses = weakref.WeakValueDictionary()
+
+
+def _count_use(w):
+    c = _uses.get(id(w))
+    if c is None:
+        c = _uses[id(w)] = _Uses()
+    c.n += 1
+    return c
+
+
+def side_wgrad_enabled(ctx):
+    """Only the gradient of a leaf weight used ONCE in the graph, whose .grad is None, qualifies:
+    AccumulateGrad then adopts the tensor without a kernel, so nothing on the main stream reads it
+    before the join. A weight shared by several calls (the RPN head over the FPN levels) has its
+    gradients summed in autograd's input buffer on the main stream, and an existing .grad is added
+    to: both would read dw too early. The use count is dropped by the backward that reads it."""
+    import os
+    uses, ctx.uses = ctx.uses, None
+    if os.environ.get("MX_SIDE_WGRAD", "1") == "0" or _timer is not None:
+        return False
+    w = ctx.wref()
+    if w is None or not w.is_leaf or w.grad is not None or uses is None or uses.n != 1:
+        return False
+    import torch.distributed as dist
+    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+
+def _join_side():
+    cur = torch.cuda.current_stream()
+    for ev, _keep in _pending:
+        cur.wait_event(ev)
+    _pending.clear()
+
+
+def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False):
     """dy NHWC bf16 [N,Ho,Wo,K], x NHWC bf16 -> dW f32 [kout, cin, R, S] (torch weight layout; the
-    zero-padded channels K > kout, C > cin are dropped)."""
+    zero-padded channels K > kout, C > cin are dropped). side=True (inside a backward pass only):
+    launched on the side stream, joined at the end of the backward."""
     sh = shape(x, K, R, S, stride, pad)
     kout = kout or K
     cin = cin or x.shape[3]
@@ -265,7 +321,22 @@ def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None):
     wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 2)
     ws = torch.empty(wsb, dtype=torch.uint8, device=x.device) if wsb else None
     t0 = _timer.start() if _timer else None
-    call("mx_conv2d_wgrad_ex", ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws), wsb, _s())
+    stream = _s()
+    if side:
+        st = _side.get(x.device)
+        if st is None:
+            st = _side[x.device] = torch.cuda.Stream(device=x.device)
+        st.wait_stream(torch.cuda.current_stream())
+        stream = st.cuda_stream
+    call("mx_conv2d_wgrad_ex", ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws), wsb, stream)
+    if side:
+        ev = torch.cuda.Event()
+        ev.record(st)
+        if not _pending:
+            torch.autograd.Variable._execution_engine.queue_callback(_join_side)
+        # dw itself is NOT held: AccumulateGrad adopts the tensor only while autograd holds the sole
+        # reference (an extra one makes it clone dw on the main stream, before the side kernel ran)
+        _pending.append((ev, (dyc, x, ws)))
     if _timer:
         _timer.stop("wgrad", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * x.shape[3], t0,
                     _tag(sh.N, sh.H, sh.W, x.shape[3], K, R, S, stride))
@@ -302,6 +373,7 @@ class ConvAct(torch.autograd.Function):
         y = conv_fwd(x, wk, stride, pad, bias=b.detach() if b is not None else None, act=act, out_dtype=out_dtype)
         ctx.save_for_backward(x, y, wt if need_dx else None)
         ctx.cfg = (stride, pad, act, w.shape, b is not None)
+        ctx.wref, ctx.uses = weakref.ref(w), _count_use(w)
         return y
 
     @staticmethod
@@ -319,7 +391,7 @@ class ConvAct(torch.autograd.Function):
             else:
                 dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad)
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1])
+            dw = conv_wgrad(gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1], side=side_wgrad_enabled(ctx))
         return dx, dw, db, None, None, None, None
 
 
@@ -362,6 +434,7 @@ class ConvBNAct(torch.autograd.Function):
             _timer.stop("bn_apply", M * K * (4 + (2 if res is not None else 0)), t0, f"{M}x{K}")
         ctx.save_for_backward(x, wt if need_dx else None, z, y, mean, invstd, gamma)
         ctx.cfg = (stride, pad, act, w.shape, residual is not None)
+        ctx.wref, ctx.uses = weakref.ref(w), _count_use(w)
         return y
 
     @staticmethod
@@ -390,7 +463,7 @@ class ConvBNAct(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad)
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(dz, x, K, R, S, stride, pad, cin=wshape[1])
+            dw = conv_wgrad(dz, x, K, R, S, stride, pad, cin=wshape[1], side=side_wgrad_enabled(ctx))
         dgamma = sums[1] if ctx.needs_input_grad[2] else None
         dbeta = sums[0] if ctx.needs_input_grad[3] else None
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None

@@ -192,30 +192,41 @@ class AnchorGenerator(nn.Module):
         return self._cache[key]
 
 
-def _smooth_l1_sum(x, y, beta):
-    return F.smooth_l1_loss(x, y, beta=beta, reduction="sum")
+def _compact(mask, total):
+    """Indices of the True entries of a flat bool mask, ascending, when their number is already
+    known on the host (torch.nonzero without its device->host sync)."""
+    slot = torch.where(mask, torch.cumsum(mask, 0) - 1, total)
+    idx = torch.empty(total + 1, dtype=torch.int64, device=mask.device)
+    idx.scatter_(0, slot, torch.arange(mask.numel(), device=mask.device))  # unselected -> spare slot
+    return idx[:total]
 
 
 class BalancedPositiveNegativeSampler:
+    """torchvision det_utils.BalancedPositiveNegativeSampler(batch_size_per_image, positive_fraction):
+    per image min(#pos, B*frac) positives (label >= 1) and min(#neg, B - num_pos) negatives (label 0),
+    each drawn uniformly without replacement. The draw takes the k smallest of i.i.d. uniform keys (a
+    uniform random subset, as randperm(n)[:k] is) and keeps the counts on the device, so sampling
+    never waits for the GPU. labels: [N, L] (padding -1) -> boolean masks (pos, neg) of that shape."""
+
     def __init__(self, batch_size_per_image, positive_fraction):
         self.batch, self.frac = batch_size_per_image, positive_fraction
 
-    def __call__(self, labels_list):
-        pos_idx, neg_idx = [], []
-        for lab in labels_list:
-            positive = torch.where(lab >= 1)[0]
-            negative = torch.where(lab == 0)[0]
-            num_pos = min(positive.numel(), int(self.batch * self.frac))
-            num_neg = min(negative.numel(), self.batch - num_pos)
-            perm1 = torch.randperm(positive.numel(), device=lab.device)[:num_pos]
-            perm2 = torch.randperm(negative.numel(), device=lab.device)[:num_neg]
-            pm = torch.zeros_like(lab, dtype=torch.bool)
-            nm = torch.zeros_like(lab, dtype=torch.bool)
-            pm[positive[perm1]] = True
-            nm[negative[perm2]] = True
-            pos_idx.append(pm)
-            neg_idx.append(nm)
-        return pos_idx, neg_idx
+    def __call__(self, lab):
+        L = lab.shape[1]
+        pos, neg = lab >= 1, lab == 0
+        P = int(self.batch * self.frac)
+        num_pos = pos.sum(1).clamp(max=P)
+        num_neg = torch.minimum(neg.sum(1), self.batch - num_pos)
+        r = torch.rand(lab.shape, device=lab.device)
+        return self._pick(pos, r, min(P, L), num_pos), self._pick(neg, r, min(self.batch, L), num_neg)
+
+    @staticmethod
+    def _pick(cand, r, k, num):
+        m = torch.zeros_like(cand)
+        if k > 0:
+            _, idx = torch.where(cand, r, 2.0).topk(k, dim=1, largest=False)  # ascending keys
+            m.scatter_(1, idx, torch.arange(k, device=cand.device)[None, :] < num[:, None])
+        return m
 
 
 class RegionProposalNetwork(nn.Module):
@@ -230,6 +241,7 @@ class RegionProposalNetwork(nn.Module):
         self._pre = pre_nms_top_n or dict(training=2000, testing=1000)
         self._post = post_nms_top_n or dict(training=2000, testing=1000)
         self.nms_thresh, self.score_thresh, self.min_size = nms_thresh, score_thresh, min_size
+        self._hw = {}
 
     def pre_nms_top_n(self):
         return self._pre["training" if self.training else "testing"]
@@ -254,15 +266,19 @@ class RegionProposalNetwork(nn.Module):
         bi = torch.arange(N, device=dev)[:, None]
         prob = torch.sigmoid(ob[bi, top])
         boxes = proposals[bi, top]
-        hw = torch.tensor(image_sizes, dtype=torch.float32, device=dev)  # (h, w) per image
+        key = (tuple(map(tuple, image_sizes)), dev)
+        hw = self._hw.get(key)
+        if hw is None:  # (h, w) per image; built once per size set (a host->device copy waits for the GPU)
+            hw = self._hw[key] = torch.tensor(image_sizes, dtype=torch.float32, device=dev)
         x = torch.minimum(boxes[..., 0::2].clamp(min=0), hw[:, 1, None, None])
         y = torch.minimum(boxes[..., 1::2].clamp(min=0), hw[:, 0, None, None])
         boxes = torch.stack((x[..., 0], y[..., 0], x[..., 1], y[..., 1]), dim=-1)
         ws, hs = boxes[..., 2] - boxes[..., 0], boxes[..., 3] - boxes[..., 1]
         keep = (ws >= self.min_size) & (hs >= self.min_size) & (prob >= self.score_thresh)
-        img = bi.expand_as(lvl)
-        kb, ks, kl, ki = boxes[keep], prob[keep], lvl[keep], img[keep]
-        counts = keep.sum(1).tolist()
+        counts = keep.sum(1).tolist()  # host sync: the NMS dispatch rule and the per-image split need them
+        T = keep.shape[1]
+        sel = _compact(keep.flatten(), sum(counts))
+        kb, ks, kl, ki = boxes.reshape(-1, 4)[sel], prob.flatten()[sel], lvl.reshape(-1)[sel], sel // T
         nl = len(num_per_level)
         post = self.post_nms_top_n()
         if min(counts) * 4 > 4000:  # CPU batched_nms rule per image -> per-level ("vanilla") path
@@ -293,28 +309,29 @@ class RegionProposalNetwork(nn.Module):
         objectness = torch.cat(logits, 1)                 # [N, A]
         pred_deltas = torch.cat(deltas, 1)                # [N, A, 4]
         A = anchors.shape[0]
-        proposals = be.box_decode(pred_deltas.detach().reshape(-1, 4), anchors.repeat(N, 1), RPN_WEIGHTS)
-        proposals = proposals.view(N, A, 4)
-        boxes, scores = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
         losses = {}
         if self.training:
+            # targets, sampling and losses never wait for the GPU: issued while the trunk still runs
             labels, reg_targets = [], []
             for t in targets:
                 _, lab, tg = be.match_assign(t["boxes"], anchors, self.fg, self.bg, True, mode=1,
                                              weights=RPN_WEIGHTS)
                 labels.append(lab)
                 reg_targets.append(tg)
-            pos_m, neg_m = self.fg_bg_sampler(labels)
-            pos = torch.where(torch.cat(pos_m))[0]
-            neg = torch.where(torch.cat(neg_m))[0]
-            sampled = torch.cat([pos, neg])
-            ob = objectness.flatten()
-            lab = torch.cat(labels)
-            rt = torch.cat(reg_targets)
-            pd = pred_deltas.reshape(-1, 4)
-            box_loss = _smooth_l1_sum(pd[pos], rt[pos], 1.0 / 9) / sampled.numel()
-            obj_loss = F.binary_cross_entropy_with_logits(ob[sampled], lab[sampled])
-            losses = {"loss_objectness": obj_loss, "loss_rpn_box_reg": box_loss}
+            lab = torch.stack(labels)                     # [N, A] 1 / 0 / -1
+            rt = torch.stack(reg_targets)                 # [N, A, 4]
+            pm, nm = self.fg_bg_sampler(lab)
+            sm = pm | nm
+            cnt = sm.sum()
+            # torchvision: BCE mean over the sampled anchors; smooth-L1 (beta 1/9) sum over the sampled
+            # positives / number sampled
+            obj = F.binary_cross_entropy_with_logits(objectness, lab.clamp(min=0), reduction="none")
+            bl = F.smooth_l1_loss(pred_deltas, rt, beta=1.0 / 9, reduction="none").sum(-1)
+            losses = {"loss_objectness": torch.where(sm, obj, 0.0).sum() / cnt,
+                      "loss_rpn_box_reg": torch.where(pm, bl, 0.0).sum() / cnt}
+        proposals = be.box_decode(pred_deltas.detach().reshape(-1, 4), anchors.repeat(N, 1), RPN_WEIGHTS)
+        proposals = proposals.view(N, A, 4)
+        boxes, scores = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
         return boxes, losses
 
 
@@ -429,13 +446,21 @@ class RoIHeads(nn.Module):
                 props.append(pg)
                 labels.append(lab)
                 tgts.append(tg)
-            pos_m, neg_m = self.fg_bg_sampler(labels)
-            for i in range(len(props)):
-                s = torch.where(pos_m[i] | neg_m[i])[0]
-                props[i], labels[i], tgts[i] = props[i][s], labels[i][s], tgts[i][s]
-            proposals = props
-        rois = torch.cat([torch.cat([torch.full((p.shape[0], 1), float(i), device=dev), p], 1)
-                          for i, p in enumerate(proposals)])
+            # candidates of all images padded to [N, Cmax] (label -1 = padding) and sampled on the device;
+            # the one host sync of this stage reads the number of sampled RoIs
+            pad = nn.utils.rnn.pad_sequence
+            lab_p = pad(labels, batch_first=True, padding_value=-1)
+            box_p = pad(props, batch_first=True)
+            tg_p = pad(tgts, batch_first=True)
+            pos_m, neg_m = self.fg_bg_sampler(lab_p)
+            sm = (pos_m | neg_m).flatten()
+            idx = _compact(sm, int(sm.sum()))             # per image ascending, as torch.where per image
+            cm = lab_p.shape[1]
+            rois = torch.cat([(idx // cm).to(torch.float32)[:, None], box_p.reshape(-1, 4)[idx]], 1)
+            labels, tgts = [lab_p.reshape(-1)[idx]], [tg_p.reshape(-1, 4)[idx]]
+        else:
+            rois = torch.cat([torch.cat([torch.full((p.shape[0], 1), float(i), device=dev), p], 1)
+                              for i, p in enumerate(proposals)])
         scales, k_min = self._scales(feats, image_sizes)
         x = be.multiscale_roi_align(feats, rois, scales, k_min)
         x = self.box_head(x, be)
@@ -444,10 +469,11 @@ class RoIHeads(nn.Module):
             lab = torch.cat(labels)
             rt = torch.cat(tgts)
             loss_cls = F.cross_entropy(class_logits, lab)
-            pos = torch.where(lab > 0)[0]
             R = class_logits.shape[0]
-            reg = box_regression.reshape(R, -1, 4)
-            loss_box = _smooth_l1_sum(reg[pos, lab[pos]], rt[pos], 1.0 / 9) / lab.numel()
+            reg = box_regression.reshape(R, -1, 4)[torch.arange(R, device=dev), lab]
+            # torchvision: smooth-L1 (beta 1/9) summed over the positive RoIs / number of sampled RoIs
+            bl = F.smooth_l1_loss(reg, rt, beta=1.0 / 9, reduction="none").sum(-1)
+            loss_box = torch.where(lab > 0, bl, 0.0).sum() / lab.numel()
             return [], {"loss_classifier": loss_cls, "loss_box_reg": loss_box}
         return self.postprocess_detections(class_logits, box_regression, proposals, image_sizes, be), {}
 
@@ -577,15 +603,17 @@ class FasterRCNN(nn.Module):
     def _trunk(self, x, be):
         """Backbone + FPN + RPN-head convs as one captured HIP graph per input shape (training, HIP
         backend): their ~400 kernels per step replay from one forward and one backward graph launch
-        instead of being issued op by op from Python (torch.cuda.make_graphed_callables; the op
-        kernels are the same libmx_det launches, recorded on the capture stream). Off with
-        MX_GRAPHS=0, in eval, or for non-HIP backends."""
+        instead of being issued op by op from Python (_TrunkGraphs; the op kernels are the same
+        libmx_det launches, recorded on the capture stream). At most 8 input shapes are captured;
+        further shapes, eval, MX_GRAPHS=0 and non-HIP backends run eagerly."""
         if not (self.training and x.is_cuda and getattr(be, "name", "") == "hip" and _graphs_enabled()):
             return None
         key = (tuple(x.shape), x.dtype)
         cache = self.__dict__.setdefault("_mx_graphs", {})
         g = cache.get(key)
         if g is None:
+            if len(cache) >= 8:  # many distinct padded sizes (real datasets): the rest run eagerly
+                return None
             g = cache[key] = _capture_trunk(self, be, x)
         outs = g(x)
         nf = len(self.backbone.fpn.inner_blocks) + 1
@@ -670,6 +698,7 @@ class _TrunkGraphs:
             for _ in range(2):
                 outs = trunk(self.static_x)
                 torch.autograd.backward(outs, [torch.ones_like(o) for o in outs])
+                del outs
                 for p in self.params:
                     p.grad = None
         torch.cuda.current_stream().wait_stream(side)

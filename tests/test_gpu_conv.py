@@ -273,3 +273,63 @@ def test_fc6_dense_conv_matches_linear(dev):
     assert rel(xd.grad.float().cpu().permute(0, 3, 1, 2), xr.grad) < 1e-2
     assert rel(wd.grad.cpu(), wr.grad) < 1e-2
     assert rel(bd.grad.cpu(), br.grad) < 1e-3
+
+
+def test_side_stream_wgrad_matches_in_order(dev, monkeypatch):
+    """Weight gradients on the side stream (conv.side_wgrad_enabled) equal the in-order ones bit for
+    bit: a chain of single-use convs, a weight shared by two calls (its gradients are summed by
+    autograd on the main stream, so it must stay in order), and a second backward that accumulates
+    into existing .grad (also in order)."""
+    from mx_det import conv as mc
+    g = torch.Generator().manual_seed(11)
+    N, H, W, C = 2, 40, 48, 64
+    x0 = torch.randn(N, H, W, C, generator=g).bfloat16().to(dev)
+    ws = [(torch.randn(C, C, 3, 3, generator=g) * 0.05).to(dev) for _ in range(3)]
+    shared = (torch.randn(C, C, 3, 3, generator=g) * 0.05).to(dev)
+    gam = torch.ones(C, device=dev)
+    bet = torch.zeros(C, device=dev)
+
+    def run():
+        ps = [w.clone().requires_grad_(True) for w in ws] + [shared.clone().requires_grad_(True)]
+        out = []
+        for rep in range(2):  # the second pass accumulates into .grad
+            y = x0
+            for w in ps[:3]:
+                y = mc.ConvBNAct.apply(y, w, gam, bet, None, torch.zeros(C, device=dev), torch.ones(C, device=dev),
+                                       (1, 1), (1, 1), mc.ACT_RELU, 1e-5, 0.1)
+            a = mc.ConvAct.apply(y, ps[3], None, (1, 1), (1, 1), mc.ACT_RELU, torch.bfloat16)
+            b = mc.ConvAct.apply(y[:, ::2, ::2].contiguous(), ps[3], None, (1, 1), (1, 1), mc.ACT_RELU, torch.bfloat16)
+            (a.float().square().mean() + b.float().mean()).backward()
+            out.append([p.grad.clone() for p in ps])
+        return out
+
+    monkeypatch.setenv("MX_SIDE_WGRAD", "0")
+    ref = run()
+    monkeypatch.setenv("MX_SIDE_WGRAD", "1")
+    got = run()
+    torch.cuda.synchronize()
+    for r, o in zip(ref, got):
+        for a, b in zip(r, o):
+            assert torch.isfinite(b).all()
+            assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("K,C,k,cp,kp", [(64, 3, 7, 8, 64), (1024, 256, 7, 256, 1024), (35, 256, 1, 256, 40),
+                                         (96, 4096, 3, 4096, 96), (16, 24, 5, 24, 16), (130, 66, 3, 72, 136)])
+def test_pack_weight_layouts(dev, K, C, k, cp, kp):
+    """mx_conv_pack_weight: wk = bf16(w) as [K][R][S][Cpad] (zero channels past C) bit-exact, for
+    every tile kind (single-row transposes, channel-split rows when C*R*S exceeds the LDS tile, 7x7
+    and 5x5 taps, odd K), and the dense dgrad layout [R][S][Cpad][Kpad] (zero rows past K)."""
+    from mx_det import conv as mc
+    g = torch.Generator().manual_seed(K + C)
+    w = torch.randn(K, C, k, k, generator=g).to(dev)
+    wk, _ = mc.pack_weight(w, cin_pad=cp, kpad=kp)
+    ref = torch.zeros(K, k, k, cp, dtype=torch.bfloat16, device=dev)
+    ref[..., :C] = w.permute(0, 2, 3, 1).bfloat16()
+    assert torch.equal(wk, ref)
+    if k > 1:
+        return
+    _, wt = mc.pack_weight(w, cin_pad=cp, kpad=kp, krsc=False, dgrad=True)
+    reft = torch.zeros(k, k, cp, kp, dtype=torch.bfloat16, device=dev)
+    reft[:, :, :C, :K] = w.permute(2, 3, 1, 0).bfloat16()
+    assert torch.equal(wt.view(k, k, cp, kp), reft)

@@ -179,8 +179,15 @@ def test_graphed_trunk_matches_eager(dev, monkeypatch):
         assert rel(gg[k], ge[k]) <= max(5e-2, 3 * rel(g2[k], ge[k])), (k, rel(gg[k], ge[k]), rel(g2[k], ge[k]))
     for a, b, c in zip(le, l2, lg):
         assert abs(c - a) <= max(3e-2 * abs(a), 3 * abs(b - a)), (le, l2, lg)
+    # after 3 steps the atomic-order noise has been amplified chaotically (eager vs eager reaches
+    # ~0.6 on some BN biases and its per-parameter size is itself random): each parameter is held to
+    # max(0.1, 3x its own eager noise), and the mean drift over all parameters to 1.5x the eager one
+    dg, de = [], []
     for k in se:
         if k.endswith("num_batches_tracked"):
             assert int(se[k]) == int(sg[k]) == 3, k
         else:
-            assert rel(sg[k], se[k]) <= max(5e-2, 3 * rel(s2[k], se[k])), (k, rel(sg[k], se[k]), rel(s2[k], se[k]))
+            dg.append(rel(sg[k], se[k]))
+            de.append(rel(s2[k], se[k]))
+            assert dg[-1] <= max(0.1, 3 * de[-1]), (k, dg[-1], de[-1])
+    assert sum(dg) <= 1.5 * sum(de) + 0.01 * len(de), (sum(dg) / len(dg), sum(de) / len(de))

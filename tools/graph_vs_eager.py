@@ -1,0 +1,47 @@
+"""Graph-vs-eager drift report (the quantities test_graphed_trunk_matches_eager bounds): per parameter,
+rel-L2 of graph vs eager and eager vs eager after 3 steps; prints the worst ratios."""
+import copy
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "robust-object-detection_amd"))
+from mx_det import frcnn  # noqa: E402
+from mx_det.data import synth_batch  # noqa: E402
+from mx_det.optim import SGD  # noqa: E402
+
+
+def main():
+    dev = "cuda:0"
+    torch.manual_seed(0)
+    base = frcnn.fasterrcnn_resnet50_fpn_v2(weights=None)
+    base.roi_heads.box_predictor = frcnn.FastRCNNPredictor(base.roi_heads.box_predictor.cls_score.in_features, 7)
+    frcnn.set_trainable_layers(base.backbone.body, 3)
+    base = base.to(dev).train()
+    imgs, tg = synth_batch(0, 2, H=320, W=480, device=dev)
+    res = {}
+    for run, mode in (("eager", "0"), ("eager2", "0"), ("graph", "1")):
+        os.environ["MX_GRAPHS"] = mode
+        m = copy.deepcopy(base)
+        opt = SGD([p for p in m.parameters() if p.requires_grad], lr=0.005, momentum=0.9, weight_decay=5e-4)
+        torch.manual_seed(5)
+        losses = []
+        for it in range(3):
+            loss = sum(m(imgs, tg).values())
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+            losses.append(float(loss.detach()))
+        res[run] = (losses, {k: v.detach().clone() for k, v in m.state_dict().items()})
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()  # noqa: E731
+    (le, se), (l2, s2), (lg, sg) = res["eager"], res["eager2"], res["graph"]
+    print("losses", le, l2, lg)
+    rows = sorted(((rel(sg[k], se[k]), rel(s2[k], se[k]), k) for k in se if not k.endswith("num_batches_tracked")),
+                  reverse=True)
+    for g, e, k in rows[:12]:
+        print(f"{k:60s} graph {g:.4f} eager2 {e:.4f}")
+
+
+if __name__ == "__main__":
+    main()
