@@ -207,6 +207,10 @@ int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, const uint16_
 int mx_conv_set_loader(int loader);
 /* fwd/dgrad block-tile override for tuning: (0, 0) automatic, else rows 64/128 x columns 64/128/256. */
 int mx_conv_set_tile(int block_rows, int block_cols);
+/* Upper bound on the split-K factor of fwd / dgrad launches (0 = automatic; tuning only). */
+int mx_conv_set_max_splits(int max_splits);
+/* LDS ring depth of the 64x128 / 128x128 buffer-descriptor kernels (0 = automatic; tuning only). */
+int mx_conv_set_stages(int stages);
 int mx_conv_set_wgrad_target(int64_t blocks);
 
 /* NHWC pooling / resampling (bf16, C % 8 == 0).

@@ -743,24 +743,28 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_buf_kernel(ConvP p) {
 #endif
 }
 
-// Split-K reduce + epilogue: block = 128 rows x 64 columns; thread = 8 columns x 4 rows.
-// Sums the splits' f32 partials, then bias / residual / activation / store and the BN statistics
-// partials of the 128-row block (same [2][mblocks][Ncol] layout as the fused epilogue).
+// Split-K reduce + epilogue: block = 128 rows x (8*CG) columns; thread = 8 columns x 128/(256/CG)
+// rows (CG 8: 64 columns, 4 rows per thread; CG 2: 16 columns, one row -- 4x the blocks for small
+// maps, where 64-column blocks would leave most CUs idle). Sums the splits' f32 partials, then
+// bias / residual / activation / store and the BN statistics partials of the 128-row block (same
+// [2][mblocks][Ncol] layout as the fused epilogue).
+template <int CG>
 __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
-  __shared__ float red[2][32][65];
-  const int tid = threadIdx.x, cl = tid & 7, rl = tid >> 3;
-  const int64_t mt = blockIdx.x, col0 = (int64_t)blockIdx.y * 64 + cl * 8;
+  constexpr int RL = 256 / CG, RPT = BM / RL, CW = 8 * CG;
+  __shared__ float red[2][RL][CW + 1];
+  const int tid = threadIdx.x, cl = tid % CG, rl = tid / CG;
+  const int64_t mt = blockIdx.x, col0 = (int64_t)blockIdx.y * CW + cl * 8;
   const bool cok = col0 < p.Ncol;
   float s2[2][8] = {}, q2[2][8] = {};
   const int64_t stride = p.M * p.Ncol;
-  // the 4 rows' loads of one split plane are issued together (8 x 16 B in flight per thread); the
+  // the rows' loads of one split plane are issued together (2*RPT x 16 B in flight per thread); the
   // per-element summation order over the splits is sequential
-  float va[4][8] = {};
+  float va[RPT][8] = {};
   for (int k = 0; k < p.splits; ++k) {
-    float4 a[4], b[4];
+    float4 a[RPT], b[RPT];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int64_t m = mt * BM + rl + 32 * rr;
+    for (int rr = 0; rr < RPT; ++rr) {
+      const int64_t m = mt * BM + rl + RL * rr;
       if (cok && m < p.M) {
         const float* src = p.slab + k * stride + m * p.Ncol + col0;
         a[rr] = *(const float4*)src;
@@ -770,18 +774,19 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
       }
     }
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
+    for (int rr = 0; rr < RPT; ++rr) {
       va[rr][0] += a[rr].x; va[rr][1] += a[rr].y; va[rr][2] += a[rr].z; va[rr][3] += a[rr].w;
       va[rr][4] += b[rr].x; va[rr][5] += b[rr].y; va[rr][6] += b[rr].z; va[rr][7] += b[rr].w;
     }
   }
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int64_t m = mt * BM + rl + 32 * rr;
+  for (int rr = 0; rr < RPT; ++rr) {
+    const int64_t m = mt * BM + rl + RL * rr;
     if (!cok || m >= p.M) continue;
     float* v = va[rr];
+    const int h = (rl + RL * rr) >= 64;  // 64-row statistics half of this row
 #pragma unroll
-    for (int t = 0; t < 8; ++t) { s2[rr >> 1][t] += v[t]; q2[rr >> 1][t] += v[t] * v[t]; }
+    for (int t = 0; t < 8; ++t) { s2[h][t] += v[t]; q2[h][t] += v[t] * v[t]; }
     if (p.bias) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] += p.bias[col0 + t];
@@ -808,17 +813,17 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
     }
   }
   if (!p.stats) return;
-  // 64-row statistics rows: half h = rows [64h, 64h+64) of this 128-row block = rr in {2h, 2h+1}
+  // 64-row statistics rows: half h = rows [64h, 64h+64) of this 128-row block
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) { red[0][rl][cl * 8 + t] = s2[h][t]; red[1][rl][cl * 8 + t] = q2[h][t]; }
     __syncthreads();
-    if (tid < 128) {
-      const int w = tid >> 6, c = tid & 63;
+    if (tid < 2 * CW) {
+      const int w = tid / CW, c = tid % CW;
       float a = 0.f;
-      for (int r = 0; r < 32; ++r) a += red[w][r][c];
-      const int64_t col = (int64_t)blockIdx.y * 64 + c;
+      for (int r = 0; r < RL; ++r) a += red[w][r][c];
+      const int64_t col = (int64_t)blockIdx.y * CW + c;
       const int64_t srow = 2 * mt + h;
       if (col < p.Ncol && srow * SROWS < p.M) p.stats[(w * p.mblocks + srow) * p.Ncol + col] = a;
     }
@@ -1514,6 +1519,19 @@ extern "C" int mx_conv_set_tile(int bmt, int bn) {
   return MX_OK;
 }
 
+static int g_buf_stages = 0;  // mx_conv_set_stages: LDS ring depth of the 64x128 / 128x128 buffer kernels
+extern "C" int mx_conv_set_stages(int n) {
+  MX_CHECK_ARG(n == 0 || n == 3 || n == 4 || n == 6, "mx_conv_set_stages: 0 (auto), 3, 4 or 6");
+  g_buf_stages = n;
+  return MX_OK;
+}
+static int g_max_splits = 0;  // mx_conv_set_max_splits (0 = automatic, 1 = never split K)
+extern "C" int mx_conv_set_max_splits(int n) {
+  MX_CHECK_ARG(n >= 0 && n <= 16, "mx_conv_set_max_splits: 0 (auto) .. 16");
+  g_max_splits = n;
+  return MX_OK;
+}
+
 static Geo make_geo(int64_t M, int64_t Ncol, int64_t Kdim) {
   Geo g;
   g.M = M; g.Ncol = Ncol; g.Kdim = Kdim;
@@ -1563,6 +1581,7 @@ static Geo make_geo(int64_t M, int64_t Ncol, int64_t Kdim) {
     int64_t sp = std::min<int64_t>(std::min<int64_t>(cdiv(640, g.tiles), g.nk / 4), 16);
     g.splits = (int)std::max<int64_t>(1, sp);
   }
+  if (g_max_splits && g.splits > g_max_splits) g.splits = g_max_splits;
   return g;
 }
 
@@ -1715,17 +1734,27 @@ static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipSt
     if (g.bmt == 64) {
       if (g.bn == 256) launch_buf<256, MODE, 3, 2, 64>(p, blocks, st);
       else if (g.narrow) launch_buf<64, MODE, 3, 4, 64>(p, blocks, st);
+      else if (g_buf_stages == 4) launch_buf<128, MODE, 4, 3, 64>(p, blocks, st);
+      else if (g_buf_stages == 6) launch_buf<128, MODE, 6, 2, 64>(p, blocks, st);
       else launch_buf<128, MODE, 3, 4, 64>(p, blocks, st);
     } else if (g.bn == 256) launch_buf<256, MODE, 3, 2, 128>(p, blocks, st);
     else if (g.narrow) launch_buf<64, MODE, 3, 3, 128>(p, blocks, st);
+    else if (g_buf_stages == 4) launch_buf<128, MODE, 4, 2, 128>(p, blocks, st);
+    else if (g_buf_stages == 6) launch_buf<128, MODE, 6, 1, 128>(p, blocks, st);
     else launch_buf<128, MODE, 3, 3, 128>(p, blocks, st);
   } else if (g.bn == 256) launch_pipe<256, MODE, 32, 3, 2>(p, blocks, st);
   else if (g.narrow) launch_variant<64, MODE>(v, p, blocks, st);
   else launch_variant<128, MODE>(v, p, blocks, st);
   MX_LAUNCH_CHECK();
   if (p.slab) {
-    dim3 rg((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.Ncol, 64));  // the reduce works in 128-row blocks
-    conv_splitk_reduce_kernel<<<rg, 256, 0, st>>>(p);
+    // the reduce works in 128-row blocks; 16-column blocks when 64-column ones would not fill the chip
+    if (cdiv(g.M, BM) * cdiv(g.Ncol, 64) >= 2 * (int64_t)num_cus()) {
+      dim3 rg((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.Ncol, 64));
+      conv_splitk_reduce_kernel<8><<<rg, 256, 0, st>>>(p);
+    } else {
+      dim3 rg((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.Ncol, 16));
+      conv_splitk_reduce_kernel<2><<<rg, 256, 0, st>>>(p);
+    }
     MX_LAUNCH_CHECK();
   }
   return MX_OK;

@@ -15,6 +15,9 @@ import torch  # noqa: E402
 from mx_det import conv as mc  # noqa: E402
 
 SHAPES = [  # name, N, H, W, C, K, k, stride, pad
+    ("L3 1x1 256->1024 (M 8400)", 2, 50, 84, 256, 1024, 1, 1, 0),
+    ("L4 3x3 256->256 (FPN P5, M 2100)", 2, 25, 42, 256, 256, 3, 1, 1),
+    ("P6-ish 3x3 256->256 (M 546)", 2, 13, 21, 256, 256, 3, 1, 1),
     ("P2 3x3 256->256 (RPN/FPN)", 2, 200, 336, 256, 256, 3, 1, 1),
     ("P2 1x1 256->256 (FPN inner)", 2, 200, 336, 256, 256, 1, 1, 0),
     ("L2 1x1 128->512", 2, 100, 168, 128, 512, 1, 1, 0),
@@ -31,9 +34,26 @@ SHAPES = [  # name, N, H, W, C, K, k, stride, pad
 ]
 
 
+GRAPH = False
+
+
 def timeit(fn, reps):
     for _ in range(3):
         fn()
+    if GRAPH:  # replay reps launches from one HIP graph: kernel time without host launch cost
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(reps):
@@ -52,21 +72,29 @@ def main():
     ap.add_argument("--wtarget", default="0")
     ap.add_argument("--loaders", default="1")
     ap.add_argument("--tiles", default="0x0", help="comma list of BMTxBN overrides, 0x0 = auto")
+    ap.add_argument("--splits", default="0", help="comma list of fwd/dgrad split-K caps, 0 = auto")
+    ap.add_argument("--stages", default="0", help="comma list of buffer-kernel ring depths, 0 = auto")
+    ap.add_argument("--graph", action="store_true", help="time launches replayed from a HIP graph")
     args = ap.parse_args()
+    global GRAPH
+    GRAPH = args.graph
+    import itertools
     from mx_det import _lib
-    for ld in [int(x) for x in args.loaders.split(",")]:
-        for v in [int(x) for x in args.variants.split(",")]:
-            for wv in [int(x) for x in args.wgrad.split(",")]:
-                for wt in [int(x) for x in args.wtarget.split(",")]:
-                  for tl in args.tiles.split(","):
-                    bm, bn = [int(x) for x in tl.split("x")]
-                    _lib.call("mx_conv_set_tile", bm, bn)
-                    _lib.call("mx_conv_set_loader", ld)
-                    _lib.call("mx_conv_set_variant", v)
-                    _lib.call("mx_conv_set_wgrad_variant", wv)
-                    _lib.call("mx_conv_set_wgrad_target", wt)
-                    print(f"== loader {ld} tile {tl} conv variant {v} wgrad variant {wv} wgrad target {wt}", flush=True)
-                    run(args)
+    ints = lambda v: [int(x) for x in v.split(",")]  # noqa: E731
+    for ld, v, wv, wt, stg, sp, tl in itertools.product(ints(args.loaders), ints(args.variants), ints(args.wgrad),
+                                                         ints(args.wtarget), ints(args.stages), ints(args.splits),
+                                                         args.tiles.split(",")):
+        bm, bn = [int(x) for x in tl.split("x")]
+        _lib.call("mx_conv_set_tile", bm, bn)
+        _lib.call("mx_conv_set_max_splits", sp)
+        _lib.call("mx_conv_set_stages", stg)
+        _lib.call("mx_conv_set_loader", ld)
+        _lib.call("mx_conv_set_variant", v)
+        _lib.call("mx_conv_set_wgrad_variant", wv)
+        _lib.call("mx_conv_set_wgrad_target", wt)
+        print(f"== loader {ld} tile {tl} conv variant {v} wgrad variant {wv} wgrad target {wt} "
+              f"max splits {sp} stages {stg}", flush=True)
+        run(args)
 
 
 def run(args):
