@@ -215,18 +215,32 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const uint16_t* __re
     for (int t = 0; t < 8; ++t) { mu[t] = mean[c0 + t]; is[t] = invstd[c0 + t]; }
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = min<int64_t>(M, r0 + rows_per_block);
-    for (int64_t r = r0 + rl; r < r1; r += 32) {
-      const uint4 ud = *(const uint4*)(dy + r * K + c0);
-      const uint4 ux = *(const uint4*)(x + r * K + c0);
-      uint4 uy = make_uint4(0, 0, 0, 0);
-      if (ACT) uy = *(const uint4*)(y + r * K + c0);
-      const uint16_t *hd = (const uint16_t*)&ud, *hy = (const uint16_t*)&uy, *hx = (const uint16_t*)&ux;
+    // U rows per thread per step: all 3*U 16-B loads issued before the arithmetic (one row per
+    // step would leave a single load set in flight per thread); per-row summation order unchanged
+    constexpr int U = 4;
+    for (int64_t rb = r0 + rl; rb < r1; rb += 32 * U) {
+      uint4 ud[U], ux[U], uy[U];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const float g = bf2f(hd[t]) * act_grad<ACT>(bf2f(hy[t]));
-        const float xh = (bf2f(hx[t]) - mu[t]) * is[t];
-        s[t] += g;
-        q[t] += g * xh;
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = rb + 32 * u;
+        ud[u] = ux[u] = uy[u] = make_uint4(0, 0, 0, 0);
+        if (r < r1) {
+          ud[u] = *(const uint4*)(dy + r * K + c0);
+          ux[u] = *(const uint4*)(x + r * K + c0);
+          if (ACT) uy[u] = *(const uint4*)(y + r * K + c0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (rb + 32 * u >= r1) break;
+        const uint16_t *hd = (const uint16_t*)&ud[u], *hy = (const uint16_t*)&uy[u], *hx = (const uint16_t*)&ux[u];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const float g = bf2f(hd[t]) * act_grad<ACT>(bf2f(hy[t]));
+          const float xh = (bf2f(hx[t]) - mu[t]) * is[t];
+          s[t] += g;
+          q[t] += g * xh;
+        }
       }
     }
   }

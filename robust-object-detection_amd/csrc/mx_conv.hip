@@ -844,14 +844,15 @@ struct WgP {
   float* slab;         // splits > 1: per-split partials [splits][K][Ncol], summed by wgrad_reduce_kernel
   int64_t Kout, Cin;   // real (unpadded) output / input channels written to dw
   int layout;
+  int dC, dRS;         // dw's (channels per tap, taps): = (C, R*S) unless a dense conv runs as a 1x1 GEMM
 };
 
 // dw element (k, col = tap*C + c) -> its offset in the requested layout, or -1 for padding
 __device__ __forceinline__ int64_t wgrad_dst(const WgP& p, int64_t k, int col) {
-  const int C = (int)p.C;
+  const int C = p.dC;
   const int tap = col / C, c = col - tap * C;
   if (k >= p.Kout || c >= p.Cin) return -1;
-  const int64_t RS = (int64_t)p.R * p.S;
+  const int64_t RS = p.dRS;
   return p.layout == 0 ? (k * RS + tap) * p.Cin + c : (k * p.Cin + c) * RS + tap;
 }
 
@@ -1223,10 +1224,14 @@ __global__ void __launch_bounds__(NT, 3) conv_wgrad_buf_kernel(WgP p) {
       // advance this lane's rows by one tile
       a_off[i] = a_off[i] == kOOB ? kOOB : a_off[i] + a_step;
       bpx[i] += PXT;
-      bow[i] += PXT;
-      while (bow[i] >= OW) {
-        bow[i] -= OW;
-        if (++boh[i] == OH) { boh[i] = 0; ++bn_[i]; }
+      if (OW == 1 && OH == 1) {  // 1x1 maps (a dense conv as a GEMM over images): pixel = image
+        bn_[i] += PXT;
+      } else {
+        bow[i] += PXT;
+        while (bow[i] >= OW) {
+          bow[i] -= OW;
+          if (++boh[i] == OH) { boh[i] = 0; ++bn_[i]; }
+        }
       }
     }
   };
@@ -2013,7 +2018,25 @@ extern "C" int mx_conv_set_wgrad_target(int64_t blocks) {
   return MX_OK;
 }
 
-static size_t wgrad_ws(const mx_conv_shape* s) {
+// A dense conv (valid RxS on an RxS map: one output pixel per image, FC6 as a 7x7 conv) has the
+// same weight gradient as a 1x1 conv over R*S*C channels (NHWC order = (r, s, c) column order):
+// that form gives the pixel-tiled wgrad kernel one image per pixel row instead of wrapping 7x7 maps.
+static mx_conv_shape wgrad_shape(const mx_conv_shape* s, bool* dense) {
+  mx_conv_shape d = *s;
+  *dense = s->Ho == 1 && s->Wo == 1 && s->H == s->R && s->W == s->S && s->pad_h == 0 && s->pad_w == 0 &&
+           s->R * s->S > 1;
+  if (*dense) {
+    d.C = s->R * s->S * s->C;
+    d.H = d.W = d.R = d.S = 1;
+    d.stride_h = d.stride_w = 1;
+  }
+  return d;
+}
+
+static size_t wgrad_ws(const mx_conv_shape* s0) {
+  bool dense;
+  const mx_conv_shape sd = wgrad_shape(s0, &dense);
+  const mx_conv_shape* s = &sd;
   WGeo g = wgrad_geo(s);
   return g.splits > 1 ? sizeof(float) * (size_t)g.splits * s->K * s->R * s->S * s->C : 0;
 }
@@ -2028,12 +2051,17 @@ extern "C" int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, co
   MX_CHECK_ARG(layout == 0 || layout == 1, "conv wgrad: layout 0 (KRSC) or 1 (KCRS)");
   MX_CHECK_ARG(s->K * s->R * s->S * s->C < (1ll << 31), "conv wgrad: weight too large");
   hipStream_t st = (hipStream_t)stream;
+  const int dC = (int)s->C, dRS = (int)(s->R * s->S);
+  bool dense;
+  const mx_conv_shape sd = wgrad_shape(s, &dense);
+  s = &sd;
   WgP p{};
   p.dy = dy; p.x = x; p.dw = dw;
   p.P = s->N * s->Ho * s->Wo; p.K = s->K; p.Ncol = s->R * s->S * s->C;
   p.OH = s->Ho; p.OW = s->Wo; p.H = s->H; p.W = s->W; p.C = s->C; p.N = s->N;
   p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
   p.Kout = Kout; p.Cin = Cin; p.layout = layout;
+  p.dC = dC; p.dRS = dRS;
   WGeo g = wgrad_geo(s);
   p.kchunk = g.kchunk;
   if (g.splits > 1) {
@@ -2047,7 +2075,8 @@ extern "C" int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, co
   int v = g_wgrad_variant;
   // the buffer kernel walks each lane's pixels by (n, oh, ow) increments: maps of fewer than 32
   // output pixels (FC6 as a 7x7 conv on the RoI tile) would wrap many times per tile -> register kernel
-  if (v == 3 && !(p.P * p.K * 2 < (1ll << 31) && s->N * s->H * s->W * s->C * 2 < (1ll << 31) && p.OH * p.OW >= 32))
+  if (v == 3 && !(p.P * p.K * 2 < (1ll << 31) && s->N * s->H * s->W * s->C * 2 < (1ll << 31) &&
+                 (p.OH * p.OW >= 32 || (p.OH == 1 && p.OW == 1))))
     v = 0;
   if (v == 3) conv_wgrad_buf_kernel<<<grid, NT, 3 * 2 * 32 * 256, st>>>(p);
   else if (v == 2) conv_wgrad_glds_kernel<<<grid, NT, 2 * 2 * BKG * 256, st>>>(p);
