@@ -171,7 +171,10 @@ class WeightPacker:
         if k in self.entries:
             return
         e = _Entry()
-        e.w, e.cp, e.kp, e.stride, e.pad, e.dense = w, cp, kp, tuple(stride), tuple(pad), bool(dense)
+        # detached alias (same storage and version counter): a registered VIEW of a parameter (FC6 /
+        # FC7) must not keep its autograd node -- and the parameter's AccumulateGrad node, bound to
+        # the stream it was created on -- alive across steps and graph captures
+        e.w, e.cp, e.kp, e.stride, e.pad, e.dense = w.detach(), cp, kp, tuple(stride), tuple(pad), bool(dense)
         e.wk = torch.empty((K, R, S, cp), dtype=torch.bfloat16, device=w.device)
         e.wt = torch.empty(cp * R * S * kp, dtype=torch.bfloat16, device=w.device) if dgrad else None
         e.version = None

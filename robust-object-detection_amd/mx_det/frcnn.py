@@ -427,6 +427,27 @@ class RoIHeads(nn.Module):
         self.score_thresh, self.nms_thresh, self.detections_per_img = score_thresh, nms_thresh, detections_per_img
         self.featmap_names = ["0", "1", "2", "3"]
 
+    def _head_graph(self, x, be):
+        """Box head + predictor forward/backward as two HIP graphs per RoI count (training, HIP
+        backend): the ~90 launches of 4 conv+BN+ReLU, FC6, FC7 and the predictor (and their
+        backward, including the RoI-feature gradient for RoIAlign's backward) replay from two graph
+        launches. Training samples a fixed 512 RoIs per image whenever enough candidates exist, so
+        one shape recurs; at most 4 shapes are captured, others run eagerly (as do MX_GRAPHS=0,
+        eval and non-HIP backends)."""
+        import os
+        if not (x.is_cuda and getattr(be, "name", "") == "hip" and _graphs_enabled()
+                and os.environ.get("MX_HEAD_GRAPHS", "1") != "0"):
+            return None
+        key = (tuple(x.shape), x.dtype)
+        cache = self.__dict__.setdefault("_mx_graphs", {})
+        g = cache.get(key)
+        if g is None:
+            if len(cache) >= 4:
+                return None
+            head = _Head(self, be)
+            g = cache[key] = _Graphs(head, head.parameters(), self, x, input_grad=True)
+        return g
+
     def _scales(self, feats, image_sizes):
         # MultiScaleRoIAlign._setup_scales / _infer_scale (height-based), LevelMapper k_min/k_max
         max_h = max(s[0] for s in image_sizes)
@@ -463,8 +484,11 @@ class RoIHeads(nn.Module):
                               for i, p in enumerate(proposals)])
         scales, k_min = self._scales(feats, image_sizes)
         x = be.multiscale_roi_align(feats, rois, scales, k_min)
-        x = self.box_head(x, be)
-        class_logits, box_regression = self.box_predictor(x, be)
+        head = self._head_graph(x, be) if self.training else None
+        if head is not None:  # HIP-graph replay of box head + predictor (static RoI count)
+            class_logits, box_regression = head(x)
+        else:
+            class_logits, box_regression = self.box_predictor(self.box_head(x, be), be)
         if self.training:
             lab = torch.cat(labels)
             rt = torch.cat(tgts)
@@ -603,7 +627,7 @@ class FasterRCNN(nn.Module):
     def _trunk(self, x, be):
         """Backbone + FPN + RPN-head convs as one captured HIP graph per input shape (training, HIP
         backend): their ~400 kernels per step replay from one forward and one backward graph launch
-        instead of being issued op by op from Python (_TrunkGraphs; the op kernels are the same
+        instead of being issued op by op from Python (_Graphs; the op kernels are the same
         libmx_det launches, recorded on the capture stream). At most 8 input shapes are captured;
         further shapes, eval, MX_GRAPHS=0 and non-HIP backends run eagerly."""
         if not (self.training and x.is_cuda and getattr(be, "name", "") == "hip" and _graphs_enabled()):
@@ -678,53 +702,56 @@ class _Trunk(nn.Module):
         return tuple(feats.values()) + tuple(logits) + tuple(deltas)
 
 
-class _TrunkGraphs:
-    """Forward and backward HIP graphs of the trunk for one input shape. The backward graph writes
-    the trunk parameters' gradients into graph-owned buffers that become their .grad after each
-    replay (added when a .grad already exists), so no per-parameter autograd work runs in the step.
-    Capture follows torch.cuda.graph: eager warmup on a side stream, then one forward and one
-    backward capture in a shared private pool; BatchNorm running stats are restored afterwards."""
+class _Graphs:
+    """Forward and backward HIP graphs of a static-shape sub-network fn(x) -> tuple(tensors). The
+    backward graph writes the parameters' gradients (and, with input_grad, x's) into graph-owned
+    buffers that become their .grad after each replay (added when a .grad already exists), so no
+    per-parameter autograd work runs in the step. Capture follows torch.cuda.graph: eager warmup on
+    a side stream, then one forward and one backward capture in a shared private pool; the BatchNorm
+    running statistics of `stats_module` are restored afterwards."""
 
-    def __init__(self, model, be, x):
-        trunk = _Trunk(model, be)
-        self.params = [p for p in trunk.parameters() if p.requires_grad]
-        saved = {k: v.clone() for k, v in model.state_dict().items()
+    def __init__(self, fn, params, stats_module, x, input_grad=False):
+        self.params = [p for p in params if p.requires_grad]
+        saved = {k: v.clone() for k, v in stats_module.state_dict().items()
                  if k.endswith(("running_mean", "running_var", "num_batches_tracked"))}
         grads = [p.grad for p in self.params]
-        self.static_x = x.detach().clone()
+        self.input_grad = input_grad
+        self.static_x = x.detach().clone().requires_grad_(input_grad)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(2):
-                outs = trunk(self.static_x)
+                outs = fn(self.static_x)
                 torch.autograd.backward(outs, [torch.ones_like(o) for o in outs])
                 del outs
                 for p in self.params:
                     p.grad = None
+                self.static_x.grad = None
         torch.cuda.current_stream().wait_stream(side)
         pool = torch.cuda.graph_pool_handle()
         self.fwd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.fwd, pool=pool):
-            self.static_out = trunk(self.static_x)
+            self.static_out = fn(self.static_x)
         self.static_gout = [torch.zeros_like(o) for o in self.static_out]
         self.bwd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.bwd, pool=pool):
             torch.autograd.backward(self.static_out, self.static_gout)
         self.static_grads = [p.grad for p in self.params]
+        self.static_xgrad = self.static_x.grad
         self.static_out = tuple(o.detach() for o in self.static_out)
         for p, g in zip(self.params, grads):
             p.grad = g
         with torch.no_grad():
-            sd = model.state_dict()
+            sd = stats_module.state_dict()
             for k, v in saved.items():
                 sd[k].copy_(v)
         self.anchor = torch.zeros((), device=x.device, requires_grad=True)
 
     def __call__(self, x):
-        return _TrunkFn.apply(x, self.anchor, self)
+        return _GraphFn.apply(x, self.anchor, self)
 
 
-class _TrunkFn(torch.autograd.Function):
+class _GraphFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, tg):
         tg.static_x.copy_(x)
@@ -749,11 +776,26 @@ class _TrunkFn(torch.autograd.Function):
                 p.grad = g
             else:
                 p.grad.add_(g)
-        return None, None, None
+        # the input gradient is the graph's static buffer: consumed by the producer's backward in
+        # this same backward pass, before the next replay overwrites it
+        return (tg.static_xgrad if tg.input_grad else None), None, None
 
 
 def _capture_trunk(model, be, x):
-    return _TrunkGraphs(model, be, x)
+    trunk = _Trunk(model, be)
+    return _Graphs(trunk, trunk.parameters(), model, x)
+
+
+class _Head(nn.Module):
+    """box head + predictor as one tensor -> (class_logits, box_regression) callable."""
+
+    def __init__(self, roi_heads, be):
+        super().__init__()
+        self.box_head, self.box_predictor = roi_heads.box_head, roi_heads.box_predictor
+        self.be = be
+
+    def forward(self, x):
+        return self.box_predictor(self.box_head(x, self.be), self.be)
 
 
 def fasterrcnn_resnet50_fpn_v2(weights=None, progress=True, num_classes=None, weights_backbone=None,
