@@ -26,7 +26,10 @@ class SGD(torch.optim.SGD):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        fast = self.__dict__.setdefault("_fast", {})
         for group in self.param_groups:
+            if self._fast_step(group, fast):
+                continue
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
                 continue
@@ -55,7 +58,38 @@ class SGD(torch.optim.SGD):
             # would (autograd checks, and the conv WeightPacker repacks by version)
             increment_version(ps)
             increment_version(bufs)
+            if len(ps) == len(group["params"]):  # all present: cache the static arrays for _fast_step
+                self.__dict__.setdefault("_fast", {})[id(group)] = (
+                    group["params"], n, P, B, N, (ctypes.c_uint8 * n)(), bufs, [p.data_ptr() for p in ps],
+                    [b.data_ptr() for b in bufs])
         return loss
+
+    def _fast_step(self, group, fast):
+        """Steady state: every parameter of the group has a grad and a momentum buffer, and the
+        parameter list is unchanged -> reuse the cached pointer arrays; only the grads' pointers
+        (new tensors each step) are gathered. Returns False to take the general path."""
+        ps = group["params"]
+        c = fast.get(id(group))
+        if c is None or c[0] is not ps or c[1] != len(ps):
+            fast.pop(id(group), None)
+            return False
+        # parameters and momentum buffers still the cached storage (p.data =, load_state_dict, ...)
+        st = self.state
+        bufs = [st[p].get("momentum_buffer") if p in st else None for p in ps]
+        if (any(b is None for b in bufs) or [p.data_ptr() for p in ps] != c[7]
+                or [b.data_ptr() for b in bufs] != c[8]):
+            fast.pop(id(group), None)
+            return False
+        grads = [p.grad for p in ps]
+        if any(g is None or not g.is_contiguous() for g in grads):
+            return False
+        n = len(ps)
+        G = (ctypes.c_void_p * n)(*[g.data_ptr() for g in grads])
+        _lib.call("mx_sgd_step", c[2], G, c[3], c[4], c[5], n, float(group["lr"]), float(group["momentum"]),
+                  float(group["dampening"]), float(group["weight_decay"]), int(group["nesterov"]), _lib.stream())
+        increment_version(ps)
+        increment_version(c[6])
+        return True
 
     def _torch_step(self, group, ps):
         for p in ps:

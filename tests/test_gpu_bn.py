@@ -124,8 +124,9 @@ def test_act_bias_bwd_matches_torch(dev, M, K, act, dt):
 
 
 def test_sgd_matches_torch(dev):
-    """mx_det.optim.SGD (one multi-tensor launch) == torch.optim.SGD over 3 steps (momentum, wd),
-    including a parameter without grad and odd sizes (scalar tail path)."""
+    """mx_det.optim.SGD (one multi-tensor launch) == torch.optim.SGD over 6 steps (momentum, wd),
+    including a parameter without grad, odd sizes (scalar tail path), the cached steady-state path
+    and a load_state_dict in between."""
     from mx_det.optim import SGD
     g = torch.Generator().manual_seed(3)
     shapes = [(256, 256, 3, 3), (1000,), (7,), (12, 5), (3, 3)]
@@ -134,7 +135,10 @@ def test_sgd_matches_torch(dev):
     b = [r.clone().to(dev).requires_grad_(True) for r in ref]
     oa = SGD(a, lr=0.005, momentum=0.9, weight_decay=5e-4)
     ob = torch.optim.SGD(b, lr=0.005, momentum=0.9, weight_decay=5e-4)
-    for it in range(3):
+    for it in range(6):
+        if it == 4:  # new momentum-buffer storage: the cached pointer arrays must be dropped
+            oa.load_state_dict(oa.state_dict())
+            ob.load_state_dict(ob.state_dict())
         for i, (x, y) in enumerate(zip(a, b)):
             if i == 4 and it == 1:  # no grad this step
                 x.grad = y.grad = None
