@@ -65,6 +65,17 @@ int mx_box_iou(const float* b1, int64_t n, const float* b2, int64_t m, float* ou
  *   keep[n] int64 receives kept indices; *num_keep (device int64) the count.
  *   max_seg: upper bound on the number of boxes that share one idx value (n is always safe).
  * ------------------------------------------------------------------------------------------- */
+/* One call for all images of RegionProposalNetwork.filter_proposals (torchvision calls batched_nms
+ * once per image, rpn.py filter_proposals): box i belongs to image group[i] (entries with
+ * group >= G are dead and never kept) and level lvl[i] in [0, L). Per image, the CPU dispatch rule
+ * of torchvision.ops.batched_nms is applied on the device: more than 1000 live boxes -> NMS per
+ * level, else the coordinate trick with that image's max coordinate. keep[0:num_keep] = survivors
+ * ordered by (image, score desc, index); num_keep is written on the device (-1: a segment exceeded
+ * max_seg). Workspace from mx_nms_grouped_workspace(n, G, max_seg). */
+size_t mx_nms_grouped_workspace(int64_t n, int64_t G, int64_t max_seg);
+int mx_batched_nms_grouped(const float* boxes, const float* scores, const int64_t* lvl, const int32_t* group,
+                           int64_t n, int64_t G, int64_t L, int64_t max_seg, double iou_threshold, int64_t* keep,
+                           int64_t* num_keep, void* ws, size_t ws_bytes, mx_stream_t stream);
 size_t mx_nms_workspace(int64_t n, int64_t max_seg);
 int mx_batched_nms(const float* boxes, const float* scores, const int64_t* idxs, const int32_t* group, int64_t n,
                    int64_t max_seg, double iou_threshold, int mode, int64_t* keep, int64_t* num_keep, void* ws,

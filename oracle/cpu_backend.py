@@ -132,6 +132,26 @@ class CpuBackend:
             out.append(sel[k])
         return torch.from_numpy(np.concatenate(out) if out else np.zeros(0, np.int64))
 
+    def proposal_nms(self, boxes, scores, lvl, group, G, L, thr, max_seg):
+        """Per image (group g < G), torchvision's batched_nms with its CPU dispatch rule; output padded
+        to n with num_keep as a 1-element tensor (the HIP entry's contract)."""
+        b = boxes.detach().float().numpy()
+        s = scores.detach().float().numpy()
+        lv = lvl.numpy()
+        gr = group.numpy()
+        out = []
+        for g in range(G):
+            sel = np.where(gr == g)[0]
+            if sel.size == 0:
+                continue
+            k = orc.batched_nms(b[sel], s[sel], lv[sel], thr)
+            out.append(sel[k])
+        keep = np.concatenate(out) if out else np.zeros(0, np.int64)
+        n = b.shape[0]
+        full = np.zeros(n, np.int64)
+        full[:keep.size] = keep
+        return torch.from_numpy(full), torch.tensor([keep.size], dtype=torch.int64)
+
     def box_decode(self, rel, boxes, weights):
         return torch.from_numpy(orc.box_decode(rel.detach().numpy(), boxes.detach().numpy(), weights))
 

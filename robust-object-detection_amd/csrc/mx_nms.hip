@@ -258,10 +258,86 @@ __global__ void nms_out_kernel(const int32_t* __restrict__ vals, int64_t n, cons
   if (i == 0) *num_keep = *nk32;
 }
 
+// ---- grouped dispatch (mx_batched_nms_grouped) -------------------------------------------------
+// torchvision's filter_proposals calls batched_nms once per image; the CPU dispatch rule then picks
+// per image: 4n > 4000 -> per-level ("vanilla") NMS, else the coordinate trick with that image's
+// own max coordinate. Here all images go in one call and the rule is evaluated per group on the
+// device (no host round trip for the counts): pass 1 counts each group's live boxes and takes its
+// max coordinate; the keys then put a trick group in one segment with offset boxes and a vanilla
+// group in one segment per level. Dead entries (group >= G) get singleton segments and are dropped
+// from the output.
+__global__ void nms_group_stats_kernel(const float4* __restrict__ boxes, const int32_t* __restrict__ group, int64_t n,
+                                       int G, int32_t* __restrict__ gcnt, uint32_t* __restrict__ gmax) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int g = group[i];
+  if (g < 0 || g >= G) return;
+  const float4 b = boxes[i];
+  atomicAdd(gcnt + g, 1);
+  atomicMax(gmax + g, max(max(ord_f32(b.x), ord_f32(b.y)), max(ord_f32(b.z), ord_f32(b.w))));
+}
+
+__global__ void nms_group_keys_kernel(const float4* __restrict__ boxes, const float* __restrict__ scores,
+                                      const int64_t* __restrict__ lvl, const int32_t* __restrict__ group, int64_t n, int G,
+                                      int L, const int32_t* __restrict__ gcnt, const uint32_t* __restrict__ gmax,
+                                      uint64_t* __restrict__ keys, int32_t* __restrict__ vals, float4* __restrict__ obox,
+                                      int32_t* __restrict__ flags, int32_t* __restrict__ nk) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  flags[i] = 0;
+  if (i == 0) *nk = 0;
+  float4 b = boxes[i];
+  const int g = group[i];
+  uint32_t hi;
+  if (g < 0 || g >= G) {
+    hi = (uint32_t)G * (uint32_t)(L + 1) + (uint32_t)i;  // dead: a segment of its own
+  } else if ((int64_t)gcnt[g] * 4 <= 4000) {               // coordinate trick over the whole image
+    const float step = unord_f32(gmax[g]) + 1.0f;
+    const float off = (float)lvl[i] * step;
+    b.x = b.x + off; b.y = b.y + off; b.z = b.z + off; b.w = b.w + off;
+    hi = (uint32_t)g * (uint32_t)(L + 1) + (uint32_t)L;
+  } else {                                                 // per level
+    hi = (uint32_t)g * (uint32_t)(L + 1) + (uint32_t)lvl[i];
+  }
+  obox[i] = b;
+  keys[i] = ((uint64_t)hi << 32) | (uint64_t)(~ord_f32(scores[i]));
+  vals[i] = (int32_t)i;
+}
+
+__global__ void nms_group_final_keys_kernel(const float* __restrict__ scores, const int32_t* __restrict__ group,
+                                            const int32_t* __restrict__ flags, int64_t n, int G,
+                                            uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t k = ~0ull;
+  const int g = group[i];
+  if (flags[i] && g >= 0 && g < G) {
+    k = ((uint64_t)ord_i32(g) << 32) | (uint64_t)(~ord_f32(scores[i]));
+    if (k == ~0ull) k = ~0ull - 1;
+  }
+  keys[i] = k;
+  vals[i] = (int32_t)i;
+}
+
+// keep = survivors by (group, score desc, index); num_keep = number of non-sentinel keys
+__global__ void nms_group_out_kernel(const uint64_t* __restrict__ skeys, const int32_t* __restrict__ vals, int64_t n,
+                                     const int32_t* __restrict__ nk32, int64_t* __restrict__ keep,
+                                     int64_t* __restrict__ num_keep) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keep[i] = vals[i];
+  const bool live = skeys[i] != ~0ull;
+  // -1: a segment exceeded max_seg (the scan's overflow flag)
+  if (live && (i == n - 1 || skeys[i + 1] == ~0ull)) *num_keep = *nk32 < 0 ? -1 : i + 1;
+  if (i == 0 && !live) *num_keep = *nk32 < 0 ? -1 : 0;
+}
+
 struct NmsWs {
   uint64_t *k0, *k1, *mask;
   int32_t *v0, *v1, *head, *incl, *seg_start, *nseg, *flags, *nk;
   uint32_t* maxbits;
+  int32_t* gcnt;
+  uint32_t* gmax;
   float4 *obox, *sbox;
   float* sarea;
   void* cub;
@@ -276,8 +352,10 @@ static size_t cub_bytes_needed(int64_t n) {
   return a > b ? a : b;
 }
 
-static size_t carve(Carver& c, int64_t n, int Wm, NmsWs* w) {
+static size_t carve(Carver& c, int64_t n, int Wm, NmsWs* w, int G = 0) {
   int64_t m = n > 0 ? n : 1;
+  w->gcnt = G > 0 ? c.take<int32_t>(2 * (size_t)G) : nullptr;  // [G] counts then [G] max bits
+  w->gmax = G > 0 ? (uint32_t*)(w->gcnt + G) : nullptr;
   w->k0 = c.take<uint64_t>(m); w->k1 = c.take<uint64_t>(m);
   w->v0 = c.take<int32_t>(m); w->v1 = c.take<int32_t>(m);
   w->head = c.take<int32_t>(m); w->incl = c.take<int32_t>(m);
@@ -359,6 +437,67 @@ extern "C" int mx_batched_nms(const float* boxes, const float* scores, const int
   cb = w.cub_bytes;
   MX_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.k0, w.k1, w.v0, w.v1, (int)n, 0, 64, s));
   nms_out_kernel<<<nb, T, 0, s>>>(w.v1, n, w.nk, keep, num_keep);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" size_t mx_nms_grouped_workspace(int64_t n, int64_t G, int64_t max_seg) {
+  if (n <= 0 || G <= 0) return 0;
+  if (max_seg <= 0 || max_seg > n) max_seg = n;
+  Carver c(nullptr, 0);
+  NmsWs w;
+  return carve(c, n, (int)cdiv(max_seg, 64), &w, (int)G);
+}
+
+extern "C" int mx_batched_nms_grouped(const float* boxes, const float* scores, const int64_t* lvl, const int32_t* group,
+                                      int64_t n, int64_t G, int64_t L, int64_t max_seg, double thr, int64_t* keep,
+                                      int64_t* num_keep, void* ws, size_t ws_bytes, mx_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  MX_CHECK_ARG(n >= 0 && n < (1ll << 30) && G > 0 && L > 0 && G * (L + 1) + n < (1ll << 31),
+               "mx_batched_nms_grouped: bad sizes n=%lld G=%lld L=%lld", (long long)n, (long long)G, (long long)L);
+  MX_CHECK_ARG(boxes && scores && lvl && group && keep && num_keep, "mx_batched_nms_grouped: null pointer");
+  if (n == 0) {
+    MX_HIP(hipMemsetAsync(num_keep, 0, sizeof(int64_t), s));
+    return MX_OK;
+  }
+  if (max_seg <= 0 || max_seg > n) max_seg = n;
+  const int Wm = (int)cdiv(max_seg, 64);
+  Carver c(ws, ws_bytes);
+  NmsWs w;
+  carve(c, n, Wm, &w, (int)G);
+  MX_CHECK_ARG(c.ok(), "mx_batched_nms_grouped: workspace too small (%zu < %zu)", ws_bytes, c.off);
+  MX_CHECK_ARG(Wm * 8 <= 64 * 1024, "mx_batched_nms_grouped: segment bound %lld too large", (long long)max_seg);
+  const int T = 256;
+  const int nb = (int)cdiv(n, T);
+  MX_HIP(hipMemsetAsync(w.gcnt, 0, sizeof(int32_t) * 2 * (size_t)G, s));
+  nms_group_stats_kernel<<<nb, T, 0, s>>>((const float4*)boxes, group, n, (int)G, w.gcnt, w.gmax);
+  MX_LAUNCH_CHECK();
+  nms_group_keys_kernel<<<nb, T, 0, s>>>((const float4*)boxes, scores, lvl, group, n, (int)G, (int)L, w.gcnt, w.gmax,
+                                         w.k0, w.v0, w.obox, w.flags, w.nk);
+  MX_LAUNCH_CHECK();
+  size_t cb = w.cub_bytes;
+  MX_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.k0, w.k1, w.v0, w.v1, (int)n, 0, 64, s));
+  nms_gather_kernel<<<nb, T, 0, s>>>(w.k1, w.v1, w.obox, n, w.sbox, w.sarea, w.head);
+  MX_LAUNCH_CHECK();
+  cb = w.cub_bytes;
+  MX_HIP(hipcub::DeviceScan::InclusiveSum(w.cub, cb, w.head, w.incl, (int)n, s));
+  nms_seg_kernel<<<nb, T, 0, s>>>(w.head, w.incl, n, w.seg_start, w.nseg);
+  MX_LAUNCH_CHECK();
+  dim3 mg((unsigned)cdiv(n, 64), (unsigned)Wm);
+  nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask);
+  MX_LAUNCH_CHECK();
+  const int sgrid = (int)std::min<int64_t>(n, 1024);
+  if (Wm <= SCAN_LDS_W)
+    nms_scan_lds_kernel<<<sgrid, 256, sizeof(uint64_t) * (Wm + 64 * (size_t)Wm), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
+                                                                                       Wm, w.flags, w.nk);
+  else
+    nms_scan_kernel<<<sgrid, 64, sizeof(uint64_t) * Wm, s>>>(w.mask, w.seg_start, w.nseg, w.v1, Wm, w.flags, w.nk);
+  MX_LAUNCH_CHECK();
+  nms_group_final_keys_kernel<<<nb, T, 0, s>>>(scores, group, w.flags, n, (int)G, w.k0, w.v0);
+  MX_LAUNCH_CHECK();
+  cb = w.cub_bytes;
+  MX_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.k0, w.k1, w.v0, w.v1, (int)n, 0, 64, s));
+  nms_group_out_kernel<<<nb, T, 0, s>>>(w.k1, w.v1, n, w.nk, keep, num_keep);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

@@ -116,6 +116,9 @@ class HipBackend:
     def batched_nms(self, boxes, scores, idxs, thr, group=None, max_seg=None, mode=0):
         return ops.batched_nms(boxes, scores, idxs, thr, group=group, max_seg=max_seg, mode=mode)
 
+    def proposal_nms(self, boxes, scores, lvl, group, G, L, thr, max_seg):
+        return ops.batched_nms_grouped(boxes, scores, lvl, group, G, L, thr, max_seg)
+
     def box_decode(self, rel, boxes, weights):
         return ops.box_decode(rel, boxes, weights)
 

@@ -249,7 +249,9 @@ class RegionProposalNetwork(nn.Module):
     def post_nms_top_n(self):
         return self._post["training" if self.training else "testing"]
 
-    def filter_proposals(self, proposals, objectness, image_sizes, num_per_level, be):
+    def filter_proposals_padded(self, proposals, objectness, image_sizes, num_per_level, be):
+        """torchvision's filter_proposals with padded outputs: boxes [N, post, 4], scores [N, post] and
+        a validity mask (each image's survivors in score order form a prefix of its row)."""
         N = proposals.shape[0]
         dev = proposals.device
         ob = objectness.detach()
@@ -275,29 +277,30 @@ class RegionProposalNetwork(nn.Module):
         boxes = torch.stack((x[..., 0], y[..., 0], x[..., 1], y[..., 1]), dim=-1)
         ws, hs = boxes[..., 2] - boxes[..., 0], boxes[..., 3] - boxes[..., 1]
         keep = (ws >= self.min_size) & (hs >= self.min_size) & (prob >= self.score_thresh)
-        counts = keep.sum(1).tolist()  # host sync: the NMS dispatch rule and the per-image split need them
+        # one NMS for all images, torchvision's per-image CPU dispatch rule evaluated on the device;
+        # filtered-out candidates are dead entries (group N): nothing here waits for the GPU
         T = keep.shape[1]
-        sel = _compact(keep.flatten(), sum(counts))
-        kb, ks, kl, ki = boxes.reshape(-1, 4)[sel], prob.flatten()[sel], lvl.reshape(-1)[sel], sel // T
-        nl = len(num_per_level)
+        n = N * T
+        grp = torch.where(keep, bi, N).reshape(-1)
+        kk, nk = be.proposal_nms(boxes.reshape(-1, 4), prob.reshape(-1), lvl.reshape(-1), grp, N,
+                                 len(num_per_level), self.nms_thresh, max(pre, 1000))
+        kk, nk = kk.to(dev), nk.to(dev)
+        live = torch.arange(n, device=dev) < nk
+        cnt = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+        cnt.scatter_add_(0, torch.where(live, grp[kk], N), live.to(torch.int64))
+        cnt = cnt[:N]
         post = self.post_nms_top_n()
-        if min(counts) * 4 > 4000:  # CPU batched_nms rule per image -> per-level ("vanilla") path
-            kk = be.batched_nms(kb, ks, ki * nl + kl, self.nms_thresh, group=ki, max_seg=pre, mode=1)
-            per = torch.bincount(ki[kk], minlength=N).tolist()
-            outs = torch.split(kk, per)
-        else:
-            outs, start = [], 0
-            for c in counts:
-                sl = slice(start, start + c)
-                k = be.batched_nms(kb[sl], ks[sl], kl[sl], self.nms_thresh, max_seg=pre)
-                outs.append(k + start)
-                start += c
-        final_boxes, final_scores = [], []
-        for k in outs:
-            k = k[:post]
-            final_boxes.append(kb[k])
-            final_scores.append(ks[k])
-        return final_boxes, final_scores
+        r = torch.arange(post, device=dev)
+        sel = kk[((torch.cumsum(cnt, 0) - cnt)[:, None] + r[None, :]).clamp(max=n - 1)]  # [N, post]
+        valid = r[None, :] < cnt[:, None]                 # survivors are a prefix of each row
+        return boxes.reshape(-1, 4)[sel], prob.reshape(-1)[sel], valid
+
+    def filter_proposals(self, proposals, objectness, image_sizes, num_per_level, be):
+        """torchvision's filter_proposals: per image, the kept proposal boxes and scores (lists; one
+        host sync for the per-image counts)."""
+        pb, ps, valid = self.filter_proposals_padded(proposals, objectness, image_sizes, num_per_level, be)
+        counts = valid.sum(1).tolist()
+        return [pb[i, :c] for i, c in enumerate(counts)], [ps[i, :c] for i, c in enumerate(counts)]
 
     def forward(self, images, features, targets=None, be=None, head=None):
         feats = list(features.values())
@@ -331,7 +334,10 @@ class RegionProposalNetwork(nn.Module):
                       "loss_rpn_box_reg": torch.where(pm, bl, 0.0).sum() / cnt}
         proposals = be.box_decode(pred_deltas.detach().reshape(-1, 4), anchors.repeat(N, 1), RPN_WEIGHTS)
         proposals = proposals.view(N, A, 4)
-        boxes, scores = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
+        if self.training:  # padded (boxes, scores, valid): the RoI sampler works on the device
+            boxes = self.filter_proposals_padded(proposals, objectness, images.image_sizes, num_per_level, be)
+        else:
+            boxes, _ = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
         return boxes, losses
 
 
@@ -458,21 +464,27 @@ class RoIHeads(nn.Module):
         feats = [features[k] for k in self.featmap_names]
         dev = feats[0].device
         if self.training:
-            props, labels, tgts = [], [], []
-            for p, t in zip(proposals, targets):
-                gt = t["boxes"].float()
-                pg = torch.cat([p, gt])
-                _, lab, tg = be.match_assign(gt, pg, self.fg, self.bg, False, mode=2, gt_labels=t["labels"],
-                                             weights=ROI_WEIGHTS)
-                props.append(pg)
-                labels.append(lab)
-                tgts.append(tg)
-            # candidates of all images padded to [N, Cmax] (label -1 = padding) and sampled on the device;
-            # the one host sync of this stage reads the number of sampled RoIs
-            pad = nn.utils.rnn.pad_sequence
-            lab_p = pad(labels, batch_first=True, padding_value=-1)
-            box_p = pad(props, batch_first=True)
-            tg_p = pad(tgts, batch_first=True)
+            # candidates per image = its kept proposals (a valid prefix of `post` slots, score order)
+            # then its GT boxes (torchvision: cat([proposals, gt])), padded to [N, post + Gmax] with
+            # label -1 on padding, matched and sampled on the device; the one host sync of this stage
+            # reads the number of sampled RoIs
+            pb, _, pvalid = proposals
+            N, post = pvalid.shape
+            gts = [t["boxes"].float().to(dev) for t in targets]
+            gm = max(1, max(g.shape[0] for g in gts))
+            gslot = torch.arange(gm, device=dev)
+            box_p = torch.zeros((N, post + gm, 4), dtype=torch.float32, device=dev)
+            box_p[:, :post] = pb
+            lab_l, tg_l, val_l = [], [], []
+            for i, (gt, t) in enumerate(zip(gts, targets)):
+                box_p[i, post:post + gt.shape[0]] = gt
+                _, lab, tg = be.match_assign(gt, box_p[i], self.fg, self.bg, False, mode=2,
+                                             gt_labels=t["labels"], weights=ROI_WEIGHTS)
+                lab_l.append(lab.to(dev))
+                tg_l.append(tg.to(dev))
+                val_l.append(torch.cat([pvalid[i], gslot < gt.shape[0]]))
+            lab_p = torch.where(torch.stack(val_l), torch.stack(lab_l), -1)
+            tg_p = torch.stack(tg_l)
             pos_m, neg_m = self.fg_bg_sampler(lab_p)
             sm = (pos_m | neg_m).flatten()
             idx = _compact(sm, int(sm.sum()))             # per image ascending, as torch.where per image

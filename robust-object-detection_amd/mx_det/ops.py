@@ -122,6 +122,29 @@ def batched_nms(boxes, scores, idxs, iou_threshold, group=None, max_seg=None, mo
     return keep[:k]
 
 
+def batched_nms_grouped(boxes, scores, lvl, group, G, L, iou_threshold, max_seg):
+    """All images of RegionProposalNetwork.filter_proposals in one NMS (mx_batched_nms_grouped):
+    box i is in image group[i] (>= G: dead) and level lvl[i]; torchvision's per-image CPU dispatch
+    rule (4n > 4000 -> per level, else coordinate trick) is applied per image on the device.
+    Returns (keep [n] int64, num_keep [1] int64) on the device: keep[:num_keep] ordered by
+    (image, score desc, index). No host synchronisation."""
+    _dev(boxes, scores)
+    n = boxes.shape[0]
+    dev = boxes.device
+    keep = torch.empty(n, dtype=torch.int64, device=dev)
+    nk = torch.zeros(1, dtype=torch.int64, device=dev)
+    if n == 0:
+        return keep, nk
+    b = boxes.float().contiguous()
+    s = scores.float().contiguous()
+    lv = lvl.to(torch.int64).contiguous()
+    g = group.to(torch.int32).contiguous()
+    ws = _ws(_lib.load().mx_nms_grouped_workspace(n, G, max_seg), dev)
+    call("mx_batched_nms_grouped", _p(b), _p(s), _p(lv), _p(g), n, G, L, int(max_seg), float(iou_threshold),
+         _p(keep), _p(nk), _p(ws), ws.numel(), _stream())
+    return keep, nk
+
+
 def nms(boxes, scores, iou_threshold):
     """torchvision.ops.nms: kept indices sorted by decreasing score."""
     return batched_nms(boxes, scores, None, iou_threshold)

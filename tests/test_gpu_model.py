@@ -115,17 +115,24 @@ def test_postprocess_matches_cpu_backend(dev):
     torch.testing.assert_close(got["boxes"].cpu(), ref["boxes"], rtol=1e-5, atol=1e-3)
 
 
-def test_filter_proposals_matches_cpu_backend(dev):
-    """RPN filter_proposals (per-level top-k, sigmoid, clip, remove_small, per-level NMS, top-2000)
-    on identical decoded proposals and logits: identical proposal sets as the CPU restatement."""
+@pytest.mark.parametrize("levels,tiny", [
+    ([200 * 336 * 3, 100 * 168 * 3, 50 * 84 * 3, 25 * 42 * 3, 13 * 21 * 3], 0.0),  # per-level NMS
+    ([200, 100, 60, 30, 9], 0.0),        # <= 1000 boxes per image: coordinate-trick dispatch
+    ([900, 500, 200, 60, 20], 0.8),      # image 0 per level, image 1 (80% removed as small) trick
+])
+def test_filter_proposals_matches_cpu_backend(dev, levels, tiny):
+    """RPN filter_proposals (per-level top-k, sigmoid, clip, remove_small, one grouped NMS with
+    torchvision's per-image dispatch rule evaluated on the device, top-2000) on identical decoded
+    proposals and logits: identical proposal sets as the CPU restatement (per-image batched_nms)."""
     from oracle.cpu_backend import CpuBackend
     from mx_det.backend import default_backend
     g = torch.Generator().manual_seed(4)
     m = _model("cpu").train()
-    levels = [200 * 336 * 3, 100 * 168 * 3, 50 * 84 * 3, 25 * 42 * 3, 13 * 21 * 3]
     A = sum(levels)
     ctr = torch.rand(2, A, 2, generator=g) * torch.tensor([1400., 860.]) - 30
     wh = torch.rand(2, A, 2, generator=g) * 200 + 0.0005
+    if tiny:
+        wh[1, torch.rand(A, generator=g) < tiny] = 1e-4  # below min_size: filtered before NMS
     props = torch.cat([ctr - wh / 2, ctr + wh / 2], -1)
     # well-separated logits (spacing >> one ulp of sigmoid), so host/device sigmoid ulp differences
     # cannot reorder scores
