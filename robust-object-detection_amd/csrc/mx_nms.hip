@@ -266,15 +266,39 @@ __global__ void nms_out_kernel(const int32_t* __restrict__ vals, int64_t n, cons
 // max coordinate; the keys then put a trick group in one segment with offset boxes and a vanilla
 // group in one segment per level. Dead entries (group >= G) get singleton segments and are dropped
 // from the output.
+// Per wave: one global atomic pair per distinct group present (groups are contiguous runs of the
+// image-major candidate list, so usually one or two per wave) instead of one per box -- thousands of
+// same-address atomics serialise at L2.
 __global__ void nms_group_stats_kernel(const float4* __restrict__ boxes, const int32_t* __restrict__ group, int64_t n,
                                        int G, int32_t* __restrict__ gcnt, uint32_t* __restrict__ gmax) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int g = group[i];
-  if (g < 0 || g >= G) return;
-  const float4 b = boxes[i];
-  atomicAdd(gcnt + g, 1);
-  atomicMax(gmax + g, max(max(ord_f32(b.x), ord_f32(b.y)), max(ord_f32(b.z), ord_f32(b.w))));
+  const int lane = threadIdx.x & 63;
+  int g = -1;
+  uint32_t m = 0;
+  if (i < n) {
+    g = group[i];
+    if (g >= 0 && g < G) {
+      const float4 b = boxes[i];
+      m = max(max(ord_f32(b.x), ord_f32(b.y)), max(ord_f32(b.z), ord_f32(b.w)));
+    } else {
+      g = -1;
+    }
+  }
+  bool todo = g >= 0;
+  while (__ballot(todo)) {
+    const uint64_t act = __ballot(todo);
+    const int leader = __ffsll((unsigned long long)act) - 1;
+    const int gg = __shfl(g, leader);
+    const bool mine = todo && g == gg;
+    const uint64_t sel = __ballot(mine);
+    uint32_t v = mine ? m : 0u;
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    if (lane == leader) {
+      atomicAdd(gcnt + gg, (int)__popcll(sel));
+      atomicMax(gmax + gg, v);
+    }
+    todo = todo && !mine;
+  }
 }
 
 __global__ void nms_group_keys_kernel(const float4* __restrict__ boxes, const float* __restrict__ scores,
