@@ -206,6 +206,11 @@ int mx_conv_pack_batched(const mx_pack_desc* jobs, int64_t njobs, void* plan, si
 int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS, int64_t C, uint16_t* wt, mx_stream_t stream);
 int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx, void* ws,
                       size_t ws_bytes, mx_stream_t stream);
+/* mx_conv2d_dgrad_t plus a bf16 [N][H][W][C] tensor added to dx in the epilogue before the single
+ * bf16 rounding (stride 1): the gradient of an input that also feeds a residual branch (ResNet
+ * bottleneck x -> conv1 and x -> + identity) without a separate add pass. */
+int mx_conv2d_dgrad_ex(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, const uint16_t* residual,
+                       uint16_t* dx, void* ws, size_t ws_bytes, mx_stream_t stream);
 int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw, mx_stream_t stream);
 /* Hot-path wgrad: dw written directly in layout 0 ([Kout][R][S][Cin]) or 1 ([Kout][Cin][R][S], the
  * torch parameter layout, so the result is the weight's .grad as is), dropping the zero-padded

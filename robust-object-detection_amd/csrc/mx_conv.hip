@@ -1918,6 +1918,14 @@ extern "C" int mx_conv_pack_batched(const mx_pack_desc* jobs, int64_t njobs, voi
 // [C][R][S][K] transpose of mx_conv_transpose_weight)
 extern "C" int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx,
                                  void* ws, size_t ws_bytes, mx_stream_t stream) {
+  return mx_conv2d_dgrad_ex(s, dy, wt, nullptr, dx, ws, ws_bytes, stream);
+}
+
+extern "C" int mx_conv2d_dgrad_ex(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt,
+                                  const uint16_t* residual, uint16_t* dx, void* ws, size_t ws_bytes,
+                                  mx_stream_t stream) {
+  MX_CHECK_ARG(!residual || (s && s->stride_h == 1 && s->stride_w == 1),
+               "conv dgrad: a residual (gradient accumulated in the epilogue) needs stride 1");
   int rc = conv_check(s);
   if (rc) return rc;
   MX_CHECK_ARG(s->K % 8 == 0, "conv dgrad: K=%lld must be a multiple of 8", (long long)s->K);
@@ -1936,7 +1944,7 @@ extern "C" int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, con
     p.M = s->N * c.Hc * c.Wc; p.Ncol = s->C; p.Kdim = (int64_t)c.Rc * c.Sc * s->K;
     p.OH = c.Hc; p.OW = c.Wc; p.IH = s->Ho; p.IW = s->Wo; p.IC = s->K;
     p.R = std::max(c.Rc, 1); p.S = std::max(c.Sc, 1); p.st_h = 1; p.st_w = 1; p.pad_h = c.dh; p.pad_w = c.dw;
-    p.out = dx; p.out_f32 = 0; p.act = 0;
+    p.out = dx; p.out_f32 = 0; p.act = 0; p.residual = residual;
     p.remap = remap; p.rst_h = s->stride_h; p.rst_w = s->stride_w; p.rph = c.ph; p.rpw = c.pw;
     p.rH = s->H; p.rW = s->W;
     p.src_elems = s->N * s->Ho * s->Wo * s->K; p.wt_elems = p.Ncol * p.Kdim;

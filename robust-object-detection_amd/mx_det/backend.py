@@ -94,8 +94,12 @@ class HipBackend:
         mc.count_batches([b for b in bns if b.training] if model.training else [])
 
     # ---- dense ---------------------------------------------------------------------------
-    def conv_bn(self, x, conv, bn, act, residual=None):
-        return mc.conv_bn(x, conv, bn, act, residual)
+    def conv_bn(self, x, conv, bn, act, residual=None, link=None):
+        return mc.conv_bn(x, conv, bn, act, residual, link)
+
+    @staticmethod
+    def res_link():
+        return mc.ResLink()
 
     def conv(self, x, weight, bias, stride, pad, act, out_dtype=torch.bfloat16):
         return mc.ConvAct.apply(x, weight, bias, stride, pad, act, out_dtype)

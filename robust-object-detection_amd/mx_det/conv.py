@@ -239,9 +239,10 @@ def _is_dense(x_shape, R, S, stride, pad):
     return (x_shape[1], x_shape[2]) == (R, S) and tuple(pad) == (0, 0) and R * S > 1
 
 
-def conv_dgrad(dy, wt, x_shape, R, S, stride, pad):
+def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None):
     """dy NHWC bf16 [N,Ho,Wo,K] (K = the wt's padded output channels), wt from
-    pack_weight(dgrad=True) -> dx NHWC bf16 [N,H,W,C]."""
+    pack_weight(dgrad=True) -> dx NHWC bf16 [N,H,W,C] (+ residual, a bf16 tensor of dx's shape added
+    in the epilogue; stride 1)."""
     N, H, W, C = x_shape
     K = dy.shape[3]
     assert wt.numel() == C * R * S * K, (wt.numel(), C, R, S, K)
@@ -252,7 +253,9 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad):
     wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 1)
     ws = torch.empty(wsb, dtype=torch.uint8, device=dy.device) if wsb else None
     t0 = _timer.start() if _timer else None
-    call("mx_conv2d_dgrad_t", ctypes.byref(sh), _p(dyc), _p(wt), _p(dx), _p(ws), wsb, _s())
+    if residual is not None:
+        assert residual.dtype == torch.bfloat16 and residual.shape == dx.shape and residual.is_contiguous()
+    call("mx_conv2d_dgrad_ex", ctypes.byref(sh), _p(dyc), _p(wt), _p(residual), _p(dx), _p(ws), wsb, _s())
     if _timer:
         _timer.stop("dgrad", 2.0 * N * Ho * Wo * K * R * S * C, t0, _tag(N, H, W, C, K, R, S, stride))
     return dx
@@ -416,8 +419,9 @@ class ConvBNAct(torch.autograd.Function):
     """y = act(BN_train(conv(x, w)) (+ residual)). Updates running stats in place."""
 
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, residual, rmean, rvar, stride, pad, act, eps, momentum):
+    def forward(ctx, x, w, gamma, beta, residual, rmean, rvar, stride, pad, act, eps, momentum, link=None):
         need_dx = ctx.needs_input_grad[0]
+        ctx.link, ctx.role = link if link is not None else (None, None)
         wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(w.shape[0]), need_dx)
         z, st = conv_fwd(x, wk, stride, pad, stats=True)
         K = wk.shape[0]
@@ -463,13 +467,19 @@ class ConvBNAct(torch.autograd.Function):
         if _timer:
             _timer.stop("bn_bwd_apply", M * K * (8 + (2 if has_res else 0)), t0, f"{M}x{K}")
         dx = dw = None
+        link = ctx.link
+        if ctx.role == "sink" and dres is not None:
+            link.dres, dres = dres, None  # handed to the block's first conv: added in its dgrad epilogue
         if ctx.needs_input_grad[0]:
-            dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad)
+            res = None
+            if ctx.role == "src":
+                res, link.dres = link.dres, None
+            dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad, residual=res)
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad(dz, x, K, R, S, stride, pad, cin=wshape[1], side=side_wgrad_enabled(ctx))
         dgamma = sums[1] if ctx.needs_input_grad[2] else None
         dbeta = sums[0] if ctx.needs_input_grad[3] else None
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 
 
 class Conv2d(torch.nn.Module):
@@ -517,14 +527,28 @@ def count_batches(bns):
     _nbt_batched = {id(b) for b in bns}
 
 
-def conv_bn(x, conv, bn, act, residual=None):
+class ResLink:
+    """Residual-gradient hand-off inside a ResNet bottleneck without downsample: the block input x
+    feeds conv1 and is the identity added after bn3, so autograd would add conv1's dgrad and the
+    identity gradient in a separate pass. The last conv ("sink") keeps its residual gradient here
+    instead of returning it, and the first conv ("src", whose backward always runs later: it is
+    upstream of the sink) adds it in its dgrad epilogue."""
+
+    def __init__(self):
+        self.dres = None
+
+    def bind(self, role):
+        return (self, role)
+
+
+def conv_bn(x, conv, bn, act, residual=None, link=None):
     """Conv2d(bias=False) + BatchNorm2d (+ residual) + activation as one fused unit. Train mode:
     batch statistics + running-stat update (nn.BatchNorm2d semantics); eval: BN folded into the conv."""
     if bn.training:
         if bn.num_batches_tracked is not None and id(bn) not in _nbt_batched:
             bn.num_batches_tracked.add_(1)
         return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
-                               conv.stride, conv.padding, act, bn.eps, bn.momentum)
+                               conv.stride, conv.padding, act, bn.eps, bn.momentum, link)
     return eval_conv_bn(x, conv, bn, act, residual)
 
 

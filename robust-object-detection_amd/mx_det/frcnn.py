@@ -46,12 +46,15 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x, be):
-        out = be.conv_bn(x, self.conv1, self.bn1, ACT_RELU)
+        # no downsample: the identity gradient is added inside conv1's dgrad (HIP backend, training)
+        link = be.res_link() if (self.downsample is None and self.training and x.requires_grad
+                                 and hasattr(be, "res_link")) else None
+        out = be.conv_bn(x, self.conv1, self.bn1, ACT_RELU, link=link and link.bind("src"))
         out = be.conv_bn(out, self.conv2, self.bn2, ACT_RELU)
         identity = x
         if self.downsample is not None:
             identity = be.conv_bn(x, self.downsample[0], self.downsample[1], ACT_NONE)
-        return be.conv_bn(out, self.conv3, self.bn3, ACT_RELU, residual=identity)
+        return be.conv_bn(out, self.conv3, self.bn3, ACT_RELU, residual=identity, link=link and link.bind("sink"))
 
 
 class ResNet50Body(nn.Module):
