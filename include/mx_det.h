@@ -211,6 +211,14 @@ int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t
  * bottleneck x -> conv1 and x -> + identity) without a separate add pass. */
 int mx_conv2d_dgrad_ex(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, const uint16_t* residual,
                        uint16_t* dx, void* ws, size_t ws_bytes, mx_stream_t stream);
+/* mx_conv2d_dgrad_ex whose output dx is the incoming gradient of a train-mode BatchNorm (+act)
+ * that produced z -> y with batch mean / invstd: the epilogue also writes, per 64-row block, the
+ * column sums of g = bf16(dx) * act'(y) and g * (z - mean) * invstd into part [2][part_mb][C]
+ * (part_mb = cdiv(N*H*W, 64)); mx_bn_bwd_finalize then replaces mx_bn_bwd_reduce_ex (no second
+ * pass over dx, y, z). Stride 1. */
+int mx_conv2d_dgrad_bnb(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, const uint16_t* residual,
+                        uint16_t* dx, const uint16_t* y, const uint16_t* z, const float* mean, const float* invstd,
+                        int act, float* part, int64_t part_mb, void* ws, size_t ws_bytes, mx_stream_t stream);
 int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* x, float* dw, mx_stream_t stream);
 /* Hot-path wgrad: dw written directly in layout 0 ([Kout][R][S][Cin]) or 1 ([Kout][Cin][R][S], the
  * torch parameter layout, so the result is the weight's .grad as is), dropping the zero-padded
@@ -255,6 +263,11 @@ int mx_bn_finalize(const float* stats, int64_t mblocks, int64_t K, int64_t count
  * ws = mx_bn_finalize_workspace(mblocks, K) bytes; its first 256 bytes are arrival counters that
  * must be zero before the first use and are left zero by every launch, so one zero-filled scratch
  * serves all launches on a stream (use one scratch per concurrent stream). */
+/* BN backward from column partials [2][mb][K] (mx_conv2d_dgrad_bnb): sums (dbeta, dgamma) and coef
+ * as mx_bn_bwd_reduce_ex produces them. Workspace: mx_bn_finalize_workspace(mb, K), counters
+ * zero-kept. */
+int mx_bn_bwd_finalize(const float* part, int64_t mb, int64_t K, int64_t M, const float* mean, const float* invstd,
+                       const float* gamma, float* sums, float* coef, void* ws, size_t ws_bytes, mx_stream_t stream);
 size_t mx_bn_finalize_workspace(int64_t mblocks, int64_t K);
 int mx_bn_finalize_ex(const float* stats, int64_t mblocks, int64_t K, int64_t count, const float* gamma,
                       const float* beta, float eps, float momentum, float* running_mean, float* running_var,

@@ -71,7 +71,7 @@ class CpuBackend:
     act_dtype = torch.float32
     stem_channels = 3
 
-    def conv_bn(self, x, conv, bn, act, residual=None, link=None):
+    def conv_bn(self, x, conv, bn, act, residual=None, link=None, bnb_own=None, bnb_feed=None):
         z = F.conv2d(_nchw(x), conv.weight, None, conv.stride, conv.padding)
         if bn.training and bn.num_batches_tracked is not None:
             bn.num_batches_tracked.add_(1)

@@ -139,6 +139,56 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   }
 }
 
+// BN backward from column partials produced elsewhere (the dgrad epilogue, mx_conv2d_dgrad_bnb):
+// part [2][mb][K] = per 64-row block sums of g and g*xhat -> sums (dbeta, dgamma) and the affine
+// coefficients of dx = a*g + b*x + c, exactly as bn_bwd_reduce_kernel's last block (f64 finish).
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ stats, int64_t mb, int64_t K,
+                                                              int64_t M, const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd,
+                                                              const float* __restrict__ gamma, float* __restrict__ sums,
+                                                              float* __restrict__ coef, unsigned* __restrict__ ctr,
+                                                              double* __restrict__ part) {
+  __shared__ double red[2][4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int64_t k = (int64_t)blockIdx.x * 64 + cl;
+  const int64_t RS = gridDim.y, per = (mb + RS - 1) / RS;
+  const int64_t r0 = (int64_t)blockIdx.y * per, r1 = min<int64_t>(mb, r0 + per);
+  double s0 = 0.0, s1 = 0.0, q0 = 0.0, q1 = 0.0;
+  if (k < K) {
+    int64_t r = r0 + rl;
+    for (; r + 4 < r1; r += 8) {
+      s0 += (double)stats[r * K + k];
+      q0 += (double)stats[(mb + r) * K + k];
+      s1 += (double)stats[(r + 4) * K + k];
+      q1 += (double)stats[(mb + r + 4) * K + k];
+    }
+    if (r < r1) {
+      s0 += (double)stats[r * K + k];
+      q0 += (double)stats[(mb + r) * K + k];
+    }
+  }
+  red[0][rl][cl] = s0 + s1;
+  red[1][rl][cl] = q0 + q1;
+  __syncthreads();
+  if (rl < 2 && k < K) {
+    const double v = (red[rl][0][cl] + red[rl][1][cl]) + (red[rl][2][cl] + red[rl][3][cl]);
+    st_sc1(part + ((int64_t)rl * RS + blockIdx.y) * K + k, v);
+  }
+  if (!arrive_last(ctr + blockIdx.x, (unsigned)RS)) return;
+  __shared__ double fin[2][64], scr[256];
+  last_sums<2>(part, RS, K, (int64_t)blockIdx.x * 64, fin, scr);
+  if (rl == 0 && k < K) {
+    const double sg = fin[0][cl], sgx = fin[1][cl];
+    sums[k] = (float)sg;
+    sums[K + k] = (float)sgx;
+    const float is = invstd[k], a = (gamma ? gamma[k] : 1.f) * is;
+    const float mg = (float)(sg / (double)M), mgx = (float)(sgx / (double)M);
+    coef[k] = a;
+    coef[K + k] = -a * is * mgx;
+    coef[2 * K + k] = -a * (mg - mean[k] * is * mgx);
+  }
+}
+
 // Thread t owns channel chunk c8 = t % K8 for its whole life (per-channel constants stay in
 // registers) and walks rows r = t / K8 + i * (T / K8): 16-B vector loads/stores, coalesced per row.
 template <typename T>
@@ -427,6 +477,21 @@ extern "C" int mx_bn_finalize_ex(const float* stats, int64_t mb, int64_t K, int6
   bn_finalize_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(stats, mb, K, count, gamma, beta, eps, momentum, rm, rv, mean,
                                                             invstd, scale, shift, (unsigned*)ws,
                                                             (double*)((char*)ws + CTR_BYTES));
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" int mx_bn_bwd_finalize(const float* part, int64_t mb, int64_t K, int64_t M, const float* mean,
+                                  const float* invstd, const float* gamma, float* sums, float* coef, void* ws,
+                                  size_t ws_bytes, mx_stream_t stream) {
+  MX_CHECK_ARG(mb > 0 && K > 0 && M > 0 && part && mean && invstd && sums && coef, "bn_bwd_finalize: bad arguments");
+  MX_CHECK_ARG(cdiv(K, 64) <= MAX_CHUNKS, "bn_bwd_finalize: K > %d", MAX_CHUNKS * 64);
+  const size_t need = mx_bn_finalize_workspace(mb, K);
+  MX_CHECK_ARG(ws && ws_bytes >= need, "bn_bwd_finalize: workspace of %zu bytes required (mx_bn_finalize_workspace)",
+               need);
+  dim3 grid((unsigned)cdiv(K, 64), (unsigned)fin_slices(mb));
+  bn_bwd_finalize_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(part, mb, K, M, mean, invstd, gamma, sums, coef,
+                                                                (unsigned*)ws, (double*)((char*)ws + CTR_BYTES));
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

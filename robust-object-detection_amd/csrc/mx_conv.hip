@@ -56,7 +56,22 @@ struct ConvP {
   int64_t rH, rW;
   // element counts of the A source and of the B operand (buffer-descriptor ranges)
   int64_t src_elems, wt_elems;
+  // dgrad feeding a train-mode BatchNorm backward (mx_conv2d_dgrad_bnb): per 64-row block column
+  // sums of g = bf16(dx) * act'(y) and g * (z - mean) * invstd -> bnb_part [2][mblocks64][Ncol]
+  const uint16_t* bnb_y;
+  const uint16_t* bnb_z;
+  const float* bnb_mean;
+  const float* bnb_invstd;
+  float* bnb_part;
+  int64_t bnb_mb;
+  int bnb_act;
 };
+
+__device__ __forceinline__ float bnb_act_grad(float y, int act) {
+  if (act == 1) return y > 0.f ? 1.f : 0.f;
+  if (act == 2) return y > 0.f ? 1.f : 0.2f;
+  return 1.f;
+}
 
 __device__ __forceinline__ int64_t out_row(const ConvP& p, int64_t m) {
   if (!p.remap) return m;
@@ -181,7 +196,38 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
   constexpr int LD = BN + 4;  // padded row (floats), keeps 16-B alignment
   float* Ct = (float*)smem;
   constexpr int CPR = BN / 8;  // 8-column chunks per row
+  constexpr int RL = NT / CPR;  // row lanes: a thread's column chunk (tid % CPR) is fixed
   const bool vec = (p.Ncol % 8) == 0;
+  // BN-backward partials (bnb): this thread's 8 columns, accumulated over its rows of a 64-row group
+  constexpr int BG = BMT / SROWS;  // 64-row statistics groups per tile
+  float bs[BG][8] = {}, bq[BG][8] = {}, bmu[8], bis[8];
+  const int64_t bcol0 = n0 + (tid % CPR) * 8;
+  if (p.bnb_part) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      bmu[t] = bcol0 + t < p.Ncol ? p.bnb_mean[bcol0 + t] : 0.f;
+      bis[t] = bcol0 + t < p.Ncol ? p.bnb_invstd[bcol0 + t] : 0.f;
+    }
+  }
+  auto bnb_flush = [&](int gi) {  // LDS reduce over the RL row lanes, one partial row per 64 rows
+    float* red = (float*)smem;       // [2][RL][BN] (aliases the drained staging tile)
+    __syncthreads();
+    const int rl = tid / CPR, cc = (tid % CPR) * 8;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      red[(0 * RL + rl) * BN + cc + t] = bs[gi][t];
+      red[(1 * RL + rl) * BN + cc + t] = bq[gi][t];
+    }
+    __syncthreads();
+    for (int c = tid; c < 2 * BN; c += NT) {
+      const int w = c / BN, col = c % BN;
+      float a = 0.f;
+      for (int r = 0; r < RL; ++r) a += red[(w * RL + r) * BN + col];
+      const int64_t srow = m0 / SROWS + gi;
+      if (n0 + col < p.Ncol && srow * SROWS < p.M) p.bnb_part[(w * p.bnb_mb + srow) * p.Ncol + n0 + col] = a;
+    }
+    __syncthreads();
+  };
 #pragma unroll
   for (int h = 0; h < HALVES; ++h) {
   if (HALVES == 1 || wm == h) {
@@ -228,6 +274,18 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
 #pragma unroll
         for (int t = 0; t < 8; ++t) wh[t] = f2bf(v[t]);
         *(uint4*)((uint16_t*)p.out + m * p.Ncol + col0) = w;
+        if (p.bnb_part) {  // the stored (bf16-rounded) gradient, as a separate reduce would read it
+          const uint4 yy = *(const uint4*)(p.bnb_y + m * p.Ncol + col0);
+          const uint4 zz = *(const uint4*)(p.bnb_z + m * p.Ncol + col0);
+          const uint16_t *yh = (const uint16_t*)&yy, *zh = (const uint16_t*)&zz;
+          const int gi = BG == 1 ? 0 : (int)((h * PR + row) / SROWS);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const float g = bf2f(wh[t]) * bnb_act_grad(bf2f(yh[t]), p.bnb_act);
+            bs[gi][t] += g;
+            bq[gi][t] += g * ((bf2f(zh[t]) - bmu[t]) * bis[t]);
+          }
+        }
       }
     } else {
       for (int t = 0; t < 8 && col0 + t < p.Ncol; ++t) {
@@ -241,6 +299,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
     }
   }
   if (HALVES > 1) __syncthreads();
+  }
+  if (p.bnb_part) {
+#pragma unroll
+    for (int gi = 0; gi < BG; ++gi) bnb_flush(gi);
   }
 }
 
@@ -756,6 +818,11 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
   const int64_t mt = blockIdx.x, col0 = (int64_t)blockIdx.y * CW + cl * 8;
   const bool cok = col0 < p.Ncol;
   float s2[2][8] = {}, q2[2][8] = {};
+  float b2[2][8] = {}, c2[2][8] = {}, bmu[8], bis[8];  // BN-backward partials (p.bnb_part)
+  if (p.bnb_part && cok) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) { bmu[t] = p.bnb_mean[col0 + t]; bis[t] = p.bnb_invstd[col0 + t]; }
+  }
   const int64_t stride = p.M * p.Ncol;
   // the rows' loads of one split plane are issued together (2*RPT x 16 B in flight per thread); the
   // per-element summation order over the splits is sequential
@@ -810,24 +877,42 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) wh[t] = f2bf(v[t]);
       *(uint4*)((uint16_t*)p.out + mo * p.Ncol + col0) = w;
+      if (p.bnb_part) {
+        const uint4 yy = *(const uint4*)(p.bnb_y + mo * p.Ncol + col0);
+        const uint4 zz = *(const uint4*)(p.bnb_z + mo * p.Ncol + col0);
+        const uint16_t *yh = (const uint16_t*)&yy, *zh = (const uint16_t*)&zz;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const float g = bf2f(wh[t]) * bnb_act_grad(bf2f(yh[t]), p.bnb_act);
+          b2[h][t] += g;
+          c2[h][t] += g * ((bf2f(zh[t]) - bmu[t]) * bis[t]);
+        }
+      }
     }
   }
-  if (!p.stats) return;
   // 64-row statistics rows: half h = rows [64h, 64h+64) of this 128-row block
+  for (int pass = 0; pass < 2; ++pass) {
+    float* dst = pass == 0 ? p.stats : p.bnb_part;
+    if (!dst) continue;
+    const int64_t mbk = pass == 0 ? p.mblocks : p.bnb_mb;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) { red[0][rl][cl * 8 + t] = s2[h][t]; red[1][rl][cl * 8 + t] = q2[h][t]; }
-    __syncthreads();
-    if (tid < 2 * CW) {
-      const int w = tid / CW, c = tid % CW;
-      float a = 0.f;
-      for (int r = 0; r < RL; ++r) a += red[w][r][c];
-      const int64_t col = (int64_t)blockIdx.y * CW + c;
-      const int64_t srow = 2 * mt + h;
-      if (col < p.Ncol && srow * SROWS < p.M) p.stats[(w * p.mblocks + srow) * p.Ncol + col] = a;
+      for (int t = 0; t < 8; ++t) {
+        red[0][rl][cl * 8 + t] = pass == 0 ? s2[h][t] : b2[h][t];
+        red[1][rl][cl * 8 + t] = pass == 0 ? q2[h][t] : c2[h][t];
+      }
+      __syncthreads();
+      if (tid < 2 * CW) {
+        const int w = tid / CW, c = tid % CW;
+        float a = 0.f;
+        for (int r = 0; r < RL; ++r) a += red[w][r][c];
+        const int64_t col = (int64_t)blockIdx.y * CW + c;
+        const int64_t srow = 2 * mt + h;
+        if (col < p.Ncol && srow * SROWS < p.M) dst[(w * mbk + srow) * p.Ncol + col] = a;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -1921,9 +2006,36 @@ extern "C" int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, con
   return mx_conv2d_dgrad_ex(s, dy, wt, nullptr, dx, ws, ws_bytes, stream);
 }
 
+struct BnbArgs {
+  const uint16_t *y, *z;
+  const float *mean, *invstd;
+  int act;
+  float* part;
+  int64_t mb;
+};
+
+static int dgrad_impl(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, const uint16_t* residual,
+                      uint16_t* dx, const BnbArgs* bnb, void* ws, size_t ws_bytes, mx_stream_t stream);
+
 extern "C" int mx_conv2d_dgrad_ex(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt,
                                   const uint16_t* residual, uint16_t* dx, void* ws, size_t ws_bytes,
                                   mx_stream_t stream) {
+  return dgrad_impl(s, dy, wt, residual, dx, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int mx_conv2d_dgrad_bnb(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt,
+                                   const uint16_t* residual, uint16_t* dx, const uint16_t* y, const uint16_t* z,
+                                   const float* mean, const float* invstd, int act, float* part, int64_t part_mb,
+                                   void* ws, size_t ws_bytes, mx_stream_t stream) {
+  MX_CHECK_ARG(s && s->stride_h == 1 && s->stride_w == 1, "conv dgrad bnb: stride 1 only");
+  MX_CHECK_ARG(y && z && mean && invstd && part && act >= 0 && act <= 2, "conv dgrad bnb: bad BN arguments");
+  MX_CHECK_ARG(part_mb == cdiv(s->N * s->H * s->W, 64), "conv dgrad bnb: part rows must be cdiv(N*H*W, 64)");
+  BnbArgs b{y, z, mean, invstd, act, part, part_mb};
+  return dgrad_impl(s, dy, wt, residual, dx, &b, ws, ws_bytes, stream);
+}
+
+static int dgrad_impl(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, const uint16_t* residual,
+                      uint16_t* dx, const BnbArgs* bnb, void* ws, size_t ws_bytes, mx_stream_t stream) {
   MX_CHECK_ARG(!residual || (s && s->stride_h == 1 && s->stride_w == 1),
                "conv dgrad: a residual (gradient accumulated in the epilogue) needs stride 1");
   int rc = conv_check(s);
@@ -1945,6 +2057,10 @@ extern "C" int mx_conv2d_dgrad_ex(const mx_conv_shape* s, const uint16_t* dy, co
     p.OH = c.Hc; p.OW = c.Wc; p.IH = s->Ho; p.IW = s->Wo; p.IC = s->K;
     p.R = std::max(c.Rc, 1); p.S = std::max(c.Sc, 1); p.st_h = 1; p.st_w = 1; p.pad_h = c.dh; p.pad_w = c.dw;
     p.out = dx; p.out_f32 = 0; p.act = 0; p.residual = residual;
+    if (bnb) {
+      p.bnb_y = bnb->y; p.bnb_z = bnb->z; p.bnb_mean = bnb->mean; p.bnb_invstd = bnb->invstd;
+      p.bnb_act = bnb->act; p.bnb_part = bnb->part; p.bnb_mb = bnb->mb;
+    }
     p.remap = remap; p.rst_h = s->stride_h; p.rst_w = s->stride_w; p.rph = c.ph; p.rpw = c.pw;
     p.rH = s->H; p.rW = s->W;
     p.src_elems = s->N * s->Ho * s->Wo * s->K; p.wt_elems = p.Ncol * p.Kdim;

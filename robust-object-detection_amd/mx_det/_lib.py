@@ -72,6 +72,9 @@ _SIGS = {
     "mx_conv_dgrad_weight_elems": (ctypes.c_size_t, [c_vp, c_i64, c_i64]),
     "mx_conv_pack_plan_bytes": (ctypes.c_size_t, [c_i64]),
     "mx_conv_pack_batched": (c_int, [c_vp, c_i64, c_vp, ctypes.c_size_t, c_int, c_vp]),
+    "mx_conv2d_dgrad_bnb": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                    c_vp, c_i64, c_vp, c_sz, c_vp]),
+    "mx_bn_bwd_finalize": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_conv2d_dgrad_ex": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_conv2d_dgrad_t": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_maxpool_fwd": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp]),

@@ -94,12 +94,16 @@ class HipBackend:
         mc.count_batches([b for b in bns if b.training] if model.training else [])
 
     # ---- dense ---------------------------------------------------------------------------
-    def conv_bn(self, x, conv, bn, act, residual=None, link=None):
-        return mc.conv_bn(x, conv, bn, act, residual, link)
+    def conv_bn(self, x, conv, bn, act, residual=None, link=None, bnb_own=None, bnb_feed=None):
+        return mc.conv_bn(x, conv, bn, act, residual, link, bnb_own, bnb_feed)
 
     @staticmethod
     def res_link():
         return mc.ResLink()
+
+    @staticmethod
+    def bnb_link():
+        return mc.BNBLink()
 
     def conv(self, x, weight, bias, stride, pad, act, out_dtype=torch.bfloat16):
         return mc.ConvAct.apply(x, weight, bias, stride, pad, act, out_dtype)

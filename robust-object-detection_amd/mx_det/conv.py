@@ -239,7 +239,7 @@ def _is_dense(x_shape, R, S, stride, pad):
     return (x_shape[1], x_shape[2]) == (R, S) and tuple(pad) == (0, 0) and R * S > 1
 
 
-def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None):
+def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
     """dy NHWC bf16 [N,Ho,Wo,K] (K = the wt's padded output channels), wt from
     pack_weight(dgrad=True) -> dx NHWC bf16 [N,H,W,C] (+ residual, a bf16 tensor of dx's shape added
     in the epilogue; stride 1)."""
@@ -255,7 +255,14 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None):
     t0 = _timer.start() if _timer else None
     if residual is not None:
         assert residual.dtype == torch.bfloat16 and residual.shape == dx.shape and residual.is_contiguous()
-    call("mx_conv2d_dgrad_ex", ctypes.byref(sh), _p(dyc), _p(wt), _p(residual), _p(dx), _p(ws), wsb, _s())
+    if bnb is not None:  # dx is the gradient of a train-mode BN output: its backward partials too
+        mb = (N * H * W + 63) // 64
+        part = torch.empty((2, mb, C), dtype=torch.float32, device=dy.device)
+        call("mx_conv2d_dgrad_bnb", ctypes.byref(sh), _p(dyc), _p(wt), _p(residual), _p(dx), _p(bnb.y), _p(bnb.z),
+             _p(bnb.mean), _p(bnb.invstd), int(bnb.act), _p(part), mb, _p(ws), wsb, _s())
+        bnb.part = part
+    else:
+        call("mx_conv2d_dgrad_ex", ctypes.byref(sh), _p(dyc), _p(wt), _p(residual), _p(dx), _p(ws), wsb, _s())
     if _timer:
         _timer.stop("dgrad", 2.0 * N * Ho * Wo * K * R * S * C, t0, _tag(N, H, W, C, K, R, S, stride))
     return dx
@@ -419,9 +426,11 @@ class ConvBNAct(torch.autograd.Function):
     """y = act(BN_train(conv(x, w)) (+ residual)). Updates running stats in place."""
 
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, residual, rmean, rvar, stride, pad, act, eps, momentum, link=None):
+    def forward(ctx, x, w, gamma, beta, residual, rmean, rvar, stride, pad, act, eps, momentum, link=None,
+                bnb_own=None, bnb_feed=None):
         need_dx = ctx.needs_input_grad[0]
         ctx.link, ctx.role = link if link is not None else (None, None)
+        ctx.bnb_own, ctx.bnb_feed = bnb_own, bnb_feed
         wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(w.shape[0]), need_dx)
         z, st = conv_fwd(x, wk, stride, pad, stats=True)
         K = wk.shape[0]
@@ -441,6 +450,8 @@ class ConvBNAct(torch.autograd.Function):
             _timer.stop("bn_apply", M * K * (4 + (2 if res is not None else 0)), t0, f"{M}x{K}")
         ctx.save_for_backward(x, wt if need_dx else None, z, y, mean, invstd, gamma)
         ctx.cfg = (stride, pad, act, w.shape, residual is not None)
+        if bnb_own is not None:  # the next conv's dgrad will produce this BN's backward partials
+            bnb_own.y, bnb_own.z, bnb_own.mean, bnb_own.invstd, bnb_own.act = y, z, mean, invstd, act
         ctx.wref, ctx.uses = weakref.ref(w), _count_use(w)
         return y
 
@@ -453,13 +464,21 @@ class ConvBNAct(torch.autograd.Function):
         gy = gy.to(torch.bfloat16).contiguous()
         sums = torch.empty((2, K), dtype=torch.float32, device=z.device)
         coef = torch.empty((3, K), dtype=torch.float32, device=z.device)
-        wsb = _lib.load().mx_bn_bwd_workspace(M, K)
-        ws = bn_scratch(wsb, z.device)
-        t0 = _timer.start() if _timer else None
-        call("mx_bn_bwd_reduce_ex", _p(gy), _p(y), _p(z), M, K, int(act), _p(mean), _p(invstd), _p(gamma.detach()),
-             _p(ws), ws.numel(), _p(sums), _p(coef), _s())
-        if _timer:
-            _timer.stop("bn_bwd_reduce", M * K * (6 if act else 4), t0, f"{M}x{K}")
+        own = ctx.bnb_own
+        if own is not None and own.part is not None:  # partials from the next conv's dgrad epilogue
+            part, own.part = own.part, None
+            mb = part.shape[1]
+            ws = bn_scratch(_lib.load().mx_bn_finalize_workspace(mb, K), z.device)
+            call("mx_bn_bwd_finalize", _p(part), mb, K, M, _p(mean), _p(invstd), _p(gamma.detach()), _p(sums),
+                 _p(coef), _p(ws), ws.numel(), _s())
+        else:
+            wsb = _lib.load().mx_bn_bwd_workspace(M, K)
+            ws = bn_scratch(wsb, z.device)
+            t0 = _timer.start() if _timer else None
+            call("mx_bn_bwd_reduce_ex", _p(gy), _p(y), _p(z), M, K, int(act), _p(mean), _p(invstd),
+                 _p(gamma.detach()), _p(ws), ws.numel(), _p(sums), _p(coef), _s())
+            if _timer:
+                _timer.stop("bn_bwd_reduce", M * K * (6 if act else 4), t0, f"{M}x{K}")
         dz = torch.empty_like(z)
         dres = torch.empty_like(z) if has_res else None
         t0 = _timer.start() if _timer else None
@@ -474,12 +493,15 @@ class ConvBNAct(torch.autograd.Function):
             res = None
             if ctx.role == "src":
                 res, link.dres = link.dres, None
-            dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad, residual=res)
+            feed = ctx.bnb_feed
+            bnb = feed if (feed is not None and feed.y is not None and tuple(stride) == (1, 1)
+                           and feed.y.shape == x.shape) else None
+            dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad, residual=res, bnb=bnb)
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad(dz, x, K, R, S, stride, pad, cin=wshape[1], side=side_wgrad_enabled(ctx))
         dgamma = sums[1] if ctx.needs_input_grad[2] else None
         dbeta = sums[0] if ctx.needs_input_grad[3] else None
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
 
 
 class Conv2d(torch.nn.Module):
@@ -541,14 +563,26 @@ class ResLink:
         return (self, role)
 
 
-def conv_bn(x, conv, bn, act, residual=None, link=None):
+class BNBLink:
+    """BN-backward hand-off between a ConvBNAct (the owner, whose BN output y feeds exactly one conv)
+    and that next conv (the feeder): the feeder's dgrad IS the owner's incoming gradient, so its
+    epilogue also emits the owner's BN-backward column partials (mx_conv2d_dgrad_bnb) and the
+    owner's backward finishes them with one small launch (mx_bn_bwd_finalize) instead of a full
+    bn_bwd_reduce pass over (dy, y, z). Feeder backward always runs first (it is downstream)."""
+
+    def __init__(self):
+        self.y = self.z = self.mean = self.invstd = self.part = None
+        self.act = 0
+
+
+def conv_bn(x, conv, bn, act, residual=None, link=None, bnb_own=None, bnb_feed=None):
     """Conv2d(bias=False) + BatchNorm2d (+ residual) + activation as one fused unit. Train mode:
     batch statistics + running-stat update (nn.BatchNorm2d semantics); eval: BN folded into the conv."""
     if bn.training:
         if bn.num_batches_tracked is not None and id(bn) not in _nbt_batched:
             bn.num_batches_tracked.add_(1)
         return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
-                               conv.stride, conv.padding, act, bn.eps, bn.momentum, link)
+                               conv.stride, conv.padding, act, bn.eps, bn.momentum, link, bnb_own, bnb_feed)
     return eval_conv_bn(x, conv, bn, act, residual)
 
 

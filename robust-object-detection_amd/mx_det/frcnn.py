@@ -49,12 +49,17 @@ class Bottleneck(nn.Module):
         # no downsample: the identity gradient is added inside conv1's dgrad (HIP backend, training)
         link = be.res_link() if (self.downsample is None and self.training and x.requires_grad
                                  and hasattr(be, "res_link")) else None
-        out = be.conv_bn(x, self.conv1, self.bn1, ACT_RELU, link=link and link.bind("src"))
-        out = be.conv_bn(out, self.conv2, self.bn2, ACT_RELU)
+        # bn1 / bn2 backward partials from conv2's / conv3's dgrad epilogue (HIP backend, training)
+        b1 = b2 = None
+        if self.training and hasattr(be, "bnb_link") and torch.is_grad_enabled() and _bnb_enabled():
+            b1, b2 = be.bnb_link(), be.bnb_link()
+        out = be.conv_bn(x, self.conv1, self.bn1, ACT_RELU, link=link and link.bind("src"), bnb_own=b1)
+        out = be.conv_bn(out, self.conv2, self.bn2, ACT_RELU, bnb_own=b2, bnb_feed=b1)
         identity = x
         if self.downsample is not None:
             identity = be.conv_bn(x, self.downsample[0], self.downsample[1], ACT_NONE)
-        return be.conv_bn(out, self.conv3, self.bn3, ACT_RELU, residual=identity, link=link and link.bind("sink"))
+        return be.conv_bn(out, self.conv3, self.bn3, ACT_RELU, residual=identity, link=link and link.bind("sink"),
+                          bnb_feed=b2)
 
 
 class ResNet50Body(nn.Module):
@@ -691,6 +696,11 @@ class FasterRCNN(nn.Module):
             losses.update(rpn_losses)
             return losses
         return self.transform.postprocess(detections, il.image_sizes, original)
+
+
+def _bnb_enabled():
+    import os
+    return os.environ.get("MX_BNB", "1") != "0"
 
 
 def _graphs_enabled():

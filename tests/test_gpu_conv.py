@@ -333,3 +333,45 @@ def test_pack_weight_layouts(dev, K, C, k, cp, kp):
     reft = torch.zeros(k, k, cp, kp, dtype=torch.bfloat16, device=dev)
     reft[:, :, :C, :K] = w.permute(2, 3, 1, 0).bfloat16()
     assert torch.equal(wt.view(k, k, cp, kp), reft)
+
+
+def test_bn_backward_partials_from_dgrad_epilogue(dev, monkeypatch):
+    """A bottleneck (no downsample and stride-2 downsample variants) trained one step with the BN
+    backward partials produced in the next conv's dgrad epilogue (BNBLink: mx_conv2d_dgrad_bnb +
+    mx_bn_bwd_finalize) and with the separate bn_bwd_reduce pass: same gradients up to f32
+    summation order (and the bf16 roundings that order can flip)."""
+    from mx_det import frcnn
+    from mx_det.backend import default_backend
+    be = default_backend()
+    for inplanes, planes, stride in ((256, 64, 1), (256, 128, 2)):
+        torch.manual_seed(0)
+        ds = None
+        if stride != 1 or inplanes != planes * 4:
+            from mx_det.conv import BatchNorm2d, Conv2d
+            ds = torch.nn.Sequential(Conv2d(inplanes, planes * 4, 1, stride, bias=False), BatchNorm2d(planes * 4))
+        blk = frcnn.Bottleneck(inplanes, planes, stride, ds).to(dev).train()
+        x0 = torch.randn(2, 40, 56, inplanes, device=dev).bfloat16()
+        gy = None
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("MX_BNB", mode)
+            from mx_det import conv as mc
+            pk = mc.WeightPacker()
+            for m in blk.modules():
+                if isinstance(m, mc.Conv2d):
+                    pk.register(m.weight, m.stride, m.padding, True)
+            mc.set_packer(pk)
+            pk.refresh()
+            for p in blk.parameters():
+                p.grad = None
+            x = x0.clone().requires_grad_(True)
+            y = blk(x, be)
+            if gy is None:
+                gy = torch.randn_like(y.float()).bfloat16()
+            y.backward(gy)
+            res[mode] = (x.grad.float(), {n: p.grad.clone() for n, p in blk.named_parameters()})
+            mc.set_packer(None)
+        rel = lambda a, b: ((a - b).norm() / b.norm().clamp_min(1e-12)).item()  # noqa: E731
+        assert rel(res["1"][0], res["0"][0]) < 2e-3
+        for n in res["0"][1]:
+            assert rel(res["1"][1][n], res["0"][1][n]) < 2e-3, n
