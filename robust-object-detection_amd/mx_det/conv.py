@@ -600,9 +600,11 @@ class ConvNormAct(torch.nn.Sequential):
             super().__init__(conv, torch.nn.ReLU() if act == ACT_RELU else torch.nn.Identity())
         self.norm, self.act_code = norm, act
 
-    def forward(self, x, be, residual=None):
+    def forward(self, x, be, residual=None, bnb_own=None, bnb_feed=None):
         if self.norm:
-            return be.conv_bn(x, self[0], self[1], self.act_code, residual)
+            if bnb_own is None and bnb_feed is None:
+                return be.conv_bn(x, self[0], self[1], self.act_code, residual)
+            return be.conv_bn(x, self[0], self[1], self.act_code, residual, bnb_own=bnb_own, bnb_feed=bnb_feed)
         c = self[0]
         return be.conv(x, c.weight, c.bias, c.stride, c.padding, c.act, c.out_dtype)
 

@@ -45,21 +45,28 @@ class Bottleneck(nn.Module):
         self.bn3 = BatchNorm2d(planes * 4)
         self.downsample = downsample
 
-    def forward(self, x, be):
+    def forward(self, x, be, feed=None, own_out=False):
+        """feed: the previous block's bn3 BNBLink (this block's conv1 dgrad, identity gradient included,
+        is that BN's whole incoming gradient); own_out: also return this block's bn3 link (or None)."""
         # no downsample: the identity gradient is added inside conv1's dgrad (HIP backend, training)
         link = be.res_link() if (self.downsample is None and self.training and x.requires_grad
                                  and hasattr(be, "res_link")) else None
         # bn1 / bn2 backward partials from conv2's / conv3's dgrad epilogue (HIP backend, training)
-        b1 = b2 = None
+        b1 = b2 = b3 = None
         if self.training and hasattr(be, "bnb_link") and torch.is_grad_enabled() and _bnb_enabled():
             b1, b2 = be.bnb_link(), be.bnb_link()
-        out = be.conv_bn(x, self.conv1, self.bn1, ACT_RELU, link=link and link.bind("src"), bnb_own=b1)
+            b3 = be.bnb_link() if own_out else None
+        if self.downsample is not None:
+            feed = None  # x also feeds the downsample conv: conv1's dgrad is not its whole gradient
+        out = be.conv_bn(x, self.conv1, self.bn1, ACT_RELU, link=link and link.bind("src"), bnb_own=b1,
+                         bnb_feed=feed)
         out = be.conv_bn(out, self.conv2, self.bn2, ACT_RELU, bnb_own=b2, bnb_feed=b1)
         identity = x
         if self.downsample is not None:
             identity = be.conv_bn(x, self.downsample[0], self.downsample[1], ACT_NONE)
-        return be.conv_bn(out, self.conv3, self.bn3, ACT_RELU, residual=identity, link=link and link.bind("sink"),
-                          bnb_feed=b2)
+        y = be.conv_bn(out, self.conv3, self.bn3, ACT_RELU, residual=identity, link=link and link.bind("sink"),
+                       bnb_feed=b2, bnb_own=b3)
+        return (y, b3) if own_out else y
 
 
 class ResNet50Body(nn.Module):
@@ -92,8 +99,14 @@ class ResNet50Body(nn.Module):
         x = be.maxpool(x, 3, 2, 1)
         out = OrderedDict()
         for i, name in enumerate(("layer1", "layer2", "layer3", "layer4")):
-            for blk in getattr(self, name):
-                x = blk(x, be)
+            blocks = list(getattr(self, name))
+            feed = None
+            for j, blk in enumerate(blocks):
+                # a block's output feeds only the next block of its layer (conv1 + identity); the
+                # layer output also feeds the next layer's downsample and the FPN -> no hand-off
+                own = j + 1 < len(blocks)
+                r = blk(x, be, feed=feed, own_out=own)
+                x, feed = r if own else (r, None)
             out[str(i)] = x
         return out
 
@@ -421,9 +434,16 @@ class FastRCNNConvFCHead(nn.Sequential):
 
     def forward(self, x, be):
         fcs = iter(self.fc_weight_views())
+        convs = [m for m in self if isinstance(m, ConvNormAct)]
+        # conv i's BN gets its backward partials from conv i+1's dgrad (3x3 stride 1 chain)
+        links = [None] * len(convs)
+        if self.training and hasattr(be, "bnb_link") and torch.is_grad_enabled() and _bnb_enabled():
+            links = [be.bnb_link() for _ in convs[:-1]] + [None]
+        ci = 0
         for m in self:
             if isinstance(m, ConvNormAct):
-                x = m(x, be)
+                x = m(x, be, bnb_own=links[ci], bnb_feed=links[ci - 1] if ci else None)
+                ci += 1
             elif isinstance(m, Linear):
                 _, w = next(fcs)
                 x = be.conv(x, w, m.bias, (1, 1), (0, 0), ACT_RELU)  # Linear + ReLU; [R,7,7,C] -> [R,1,1,1024]
