@@ -60,6 +60,8 @@ def train_step(model, opt, images, targets, augment=False, gen=None):
     losses = sum(loss for loss in loss_dict.values())
     opt.zero_grad(set_to_none=True)
     losses.backward()
+    if hasattr(model, "sync_gradients"):  # mx_det.dp.DataParallel
+        model.sync_gradients()
     opt.step()
     return float(losses.item())
 
@@ -170,18 +172,28 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device")
+    # MX_BENCH_REHEARSE=1: all ranks on cuda:0 over gloo -- exercises the multi-rank code path on a
+    # one-GPU box (not a performance measurement); the real N>1 run is one rank per GPU over RCCL
+    rehearse = os.environ.get("MX_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from mx_det.data import synth_batch
     torch.manual_seed(42)
     model = build_model(dev).train()
     ddp = model
     if world > 1:
-        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], broadcast_buffers=False,
-                                                        gradient_as_bucket_view=True, bucket_cap_mb=50)
+        # DDP semantics (rank-0 init, per-GPU BN, averaged gradients) with the HIP graphs kept on:
+        # gradients are all-reduced over RCCL after the backward (mx_det.dp.DataParallel)
+        from mx_det.dp import DataParallel
+        ddp = DataParallel(model)
     opt = make_optimizer(model)
     imgs, tg = synth_batch(rank * N_IMAGES_PER_RANK, N_IMAGES_PER_RANK, device=dev)
     gen = torch.Generator().manual_seed(1234 + rank)

@@ -277,6 +277,14 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
 # from its AccumulateGrad hook on the main stream, so multi-rank runs keep wgrad in order.
 _side = {}
 _pending = []
+_dp = False
+
+
+def set_data_parallel(flag):
+    """mx_det.dp.DataParallel (gradients averaged after the backward, not from AccumulateGrad hooks)
+    keeps the side stream legal in multi-rank runs."""
+    global _dp
+    _dp = bool(flag)
 
 
 class _Uses:
@@ -312,7 +320,7 @@ def side_wgrad_enabled(ctx):
     if w is None or not w.is_leaf or w.grad is not None or uses is None or uses.n != 1:
         return False
     import torch.distributed as dist
-    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+    return _dp or not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
 
 
 def _join_side():

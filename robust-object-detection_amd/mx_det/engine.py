@@ -169,9 +169,9 @@ def train_frcnn(cfg):
                             num_workers=cfg.get("NUM_WORKERS", 0), collate_fn=collate_fn, pin_memory=True)
     model = build_frcnn(7, cfg.get("WEIGHTS"), trainable_backbone_layers=cfg.get("TRAINABLE_LAYERS")).to(dev)
     ddp = model
-    if world > 1:
-        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index], broadcast_buffers=False,
-                                                        gradient_as_bucket_view=True)
+    if world > 1:  # DDP(broadcast_buffers=False) semantics, HIP graphs kept (gradients averaged after backward)
+        from .dp import DataParallel
+        ddp = DataParallel(model)
     params = [p for p in model.parameters() if p.requires_grad]
     from .optim import SGD
     optimizer = SGD(params, lr=cfg["LR"], momentum=cfg["MOMENTUM"], weight_decay=cfg["WEIGHT_DECAY"])
@@ -193,6 +193,8 @@ def train_frcnn(cfg):
             losses = sum(loss for loss in loss_dict.values())
             optimizer.zero_grad(set_to_none=True)
             losses.backward()
+            if world > 1:
+                ddp.sync_gradients()
             optimizer.step()
             epoch_loss += float(losses.item())
             if rank == 0 and ((i + 1) % 100 == 0 or (i + 1) == n_batches):

@@ -469,7 +469,7 @@ class RoIHeads(nn.Module):
         one shape recurs; at most 4 shapes are captured, others run eagerly (as do MX_GRAPHS=0,
         eval and non-HIP backends)."""
         import os
-        if not (x.is_cuda and getattr(be, "name", "") == "hip" and _graphs_enabled()
+        if not (x.is_cuda and getattr(be, "name", "") == "hip" and _graphs_enabled(self)
                 and os.environ.get("MX_HEAD_GRAPHS", "1") != "0"):
             return None
         key = (tuple(x.shape), x.dtype)
@@ -670,7 +670,7 @@ class FasterRCNN(nn.Module):
         instead of being issued op by op from Python (_Graphs; the op kernels are the same
         libmx_det launches, recorded on the capture stream). At most 8 input shapes are captured;
         further shapes, eval, MX_GRAPHS=0 and non-HIP backends run eagerly."""
-        if not (self.training and x.is_cuda and getattr(be, "name", "") == "hip" and _graphs_enabled()):
+        if not (self.training and x.is_cuda and getattr(be, "name", "") == "hip" and _graphs_enabled(self)):
             return None
         key = (tuple(x.shape), x.dtype)
         cache = self.__dict__.setdefault("_mx_graphs", {})
@@ -723,13 +723,15 @@ def _bnb_enabled():
     return os.environ.get("MX_BNB", "1") != "0"
 
 
-def _graphs_enabled():
+def _graphs_enabled(mod=None):
     import os
     if os.environ.get("MX_GRAPHS", "1") == "0":
         return False
+    if mod is not None and mod.__dict__.get("_mx_dp"):
+        return True  # mx_det.dp.DataParallel: gradients averaged after the backward
     import torch.distributed as dist
-    # under DDP the gradient all-reduce hooks live on the parameters' AccumulateGrad nodes, which the
-    # replayed backward graph bypasses: multi-rank training runs the trunk eagerly
+    # under torch DDP the gradient all-reduce hooks live on the parameters' AccumulateGrad nodes,
+    # which the replayed backward graph bypasses: such runs keep the trunk eager
     return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
 
 

@@ -1,6 +1,7 @@
-"""Data-parallel training path on CPU (gloo, world_size 2): DistributedDataParallel over the
-detection model with per-rank BatchNorm statistics (broadcast_buffers=False, as bench.py and
-mx_det.engine use it over RCCL on the GPUs) averages exactly the per-rank gradients; eval sharding
+"""Data-parallel training path on CPU (gloo, world_size 2): torch DistributedDataParallel over the
+detection model with per-rank BatchNorm statistics (broadcast_buffers=False) and mx_det.dp.DataParallel
+(same semantics, gradients averaged after the backward so the HIP graphs stay on -- what bench.py and
+mx_det.engine use over RCCL on the GPUs) both average exactly the per-rank gradients; eval sharding
 covers every image once. The model runs on the CPU restatement backend here."""
 import os
 import socket
@@ -56,8 +57,29 @@ def _worker(rank, world, port, out):
         dist.all_gather(g, local[n])
         avg = sum(g) / world
         worst = max(worst, ((p.grad - avg).abs().max() / (avg.abs().max() + 1e-12)).item())
+    # mx_det.dp.DataParallel (the graph-compatible path bench.py / engine use): rank-0 broadcast of
+    # a deliberately different init, then the same averaged gradients after sync_gradients()
+    from mx_det.dp import DataParallel
+    torch.manual_seed(0)
+    m2 = make()
+    if rank == 1:
+        with torch.no_grad():
+            for p in m2.parameters():
+                p.add_(1.0)  # must be overwritten by rank 0's values
+    dp = DataParallel(m2, bucket_mb=16)
+    torch.manual_seed(100 + rank)
+    sum(dp(imgs, tg).values()).backward()
+    dp.sync_gradients()
+    worst_dp = 0.0
+    for n, p in m2.named_parameters():
+        if n not in local:
+            continue
+        g = [torch.zeros_like(local[n]) for _ in range(world)]
+        dist.all_gather(g, local[n])
+        avg = sum(g) / world
+        worst_dp = max(worst_dp, ((p.grad - avg).abs().max() / (avg.abs().max() + 1e-12)).item())
     shard = list(ShardSampler(7, world, rank))
-    out[rank] = (worst, shard)
+    out[rank] = (max(worst, worst_dp), shard)
     dist.destroy_process_group()
 
 
