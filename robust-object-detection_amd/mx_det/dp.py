@@ -30,9 +30,19 @@ class DataParallel:
             for t in list(model.parameters()) + list(model.buffers()):
                 dist.broadcast(t.data, 0, group=group)
         self.params = [p for p in model.parameters() if p.requires_grad]
-        # buckets in reverse registration order (the backward produces the head's gradients first)
+        # the RoI head's gradients are complete as soon as its backward graph has replayed, before
+        # the trunk's (most of the step's backward): their all-reduce starts right then and overlaps
+        # the trunk backward (hook fired by frcnn._Graphs; without it they join the normal buckets)
+        rh = getattr(model, "roi_heads", None)
+        early = {id(p) for p in rh.parameters() if p.requires_grad} if rh is not None else set()
+        self.early = [p for p in self.params if id(p) in early]
+        self._early_work = None
+        if self.early:
+            rh.__dict__["_mx_grads_ready"] = self._early_reduce
+        rest = [p for p in self.params if id(p) not in early]
+        # buckets in reverse registration order (the backward produces the later layers' first)
         self.buckets, cur, size = [], [], 0
-        for p in reversed(self.params):
+        for p in reversed(rest):
             cur.append(p)
             size += p.numel() * 4
             if size >= bucket_mb * 2 ** 20:
@@ -56,19 +66,29 @@ class DataParallel:
         return self
 
     @torch.no_grad()
+    def _start(self, params):
+        grads = []
+        for p in params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            grads.append(p.grad)
+        flat = _flatten_dense_tensors(grads)
+        return dist.all_reduce(flat, group=self.group, async_op=True), flat, grads
+
+    def _early_reduce(self):
+        if self._early_work is None:
+            self._early_work = self._start(self.early)
+
+    @torch.no_grad()
     def sync_gradients(self):
         """Average the trainable gradients over all ranks (call after backward, before step). A
         parameter without a gradient on this rank contributes zeros (and gets the average)."""
         pending = []
+        if self.early:
+            pending.append(self._early_work if self._early_work is not None else self._start(self.early))
+            self._early_work = None
         for b in self.buckets:
-            grads = []
-            for p in b:
-                if p.grad is None:
-                    p.grad = torch.zeros_like(p)
-                grads.append(p.grad)
-            flat = _flatten_dense_tensors(grads)
-            work = dist.all_reduce(flat, group=self.group, async_op=True)
-            pending.append((work, flat, grads))
+            pending.append(self._start(b))
         for work, flat, grads in pending:
             work.wait()
             flat.mul_(1.0 / self.world)

@@ -480,6 +480,7 @@ class RoIHeads(nn.Module):
                 return None
             head = _Head(self, be)
             g = cache[key] = _Graphs(head, head.parameters(), self, x, input_grad=True)
+        g.on_ready = self.__dict__.get("_mx_grads_ready")
         return g
 
     def _scales(self, feats, image_sizes):
@@ -793,6 +794,7 @@ class _Graphs:
             for k, v in saved.items():
                 sd[k].copy_(v)
         self.anchor = torch.zeros((), device=x.device, requires_grad=True)
+        self.on_ready = None
 
     def __call__(self, x):
         return _GraphFn.apply(x, self.anchor, self)
@@ -823,6 +825,8 @@ class _GraphFn(torch.autograd.Function):
                 p.grad = g
             else:
                 p.grad.add_(g)
+        if tg.on_ready is not None:  # e.g. mx_det.dp.DataParallel starts this unit's all-reduce
+            tg.on_ready()
         # the input gradient is the graph's static buffer: consumed by the producer's backward in
         # this same backward pass, before the next replay overwrites it
         return (tg.static_xgrad if tg.input_grad else None), None, None
