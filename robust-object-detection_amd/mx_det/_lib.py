@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmx_det.so")
+# MX_DET_LIB: an alternative build of the same ABI (A/B timing of kernel changes); default in-tree
+LIB_PATH = os.environ.get("MX_DET_LIB") or os.path.join(_HERE, "libmx_det.so")
 
 c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
