@@ -277,16 +277,19 @@ class RegionProposalNetwork(nn.Module):
         dev = proposals.device
         ob = objectness.detach()
         pre = self.pre_nms_top_n()
-        tops, lvls, off = [], [], 0
-        for i, n in enumerate(num_per_level):
-            k = min(pre, n)
-            _, ti = ob[:, off:off + n].topk(k, dim=1)
+        tops, off = [], 0
+        for n in num_per_level:
+            _, ti = ob[:, off:off + n].topk(min(pre, n), dim=1)
             tops.append(ti + off)
-            lvls.append(torch.full((k,), i, dtype=torch.int64, device=dev))
             off += n
         top = torch.cat(tops, 1)
-        lvl = torch.cat(lvls).unsqueeze(0).expand(N, -1)
-        bi = torch.arange(N, device=dev)[:, None]
+        ckey = ("lvl", tuple(num_per_level), pre, N, dev)
+        cached = self._hw.get(ckey)
+        if cached is None:  # level id per top-k slot and image index column: shape constants
+            lv = torch.cat([torch.full((min(pre, n),), i, dtype=torch.int64, device=dev)
+                            for i, n in enumerate(num_per_level)])
+            cached = self._hw[ckey] = (lv.unsqueeze(0).expand(N, -1), torch.arange(N, device=dev)[:, None])
+        lvl, bi = cached
         prob = torch.sigmoid(ob[bi, top])
         boxes = proposals[bi, top]
         key = (tuple(map(tuple, image_sizes)), dev)
