@@ -375,3 +375,16 @@ def test_bn_backward_partials_from_dgrad_epilogue(dev, monkeypatch):
         assert rel(res["1"][0], res["0"][0]) < 2e-3
         for n in res["0"][1]:
             assert rel(res["1"][1][n], res["0"][1][n]) < 2e-3, n
+
+
+@pytest.mark.parametrize("ci", range(6))
+@pytest.mark.parametrize("N,H,W,C,K,k,st,pd", [c for c in CASES if c[4] % 8 == 0])
+def test_conv_tuner_candidates(dev, monkeypatch, ci, N, H, W, C, K, k, st, pd):
+    """Every launch configuration the per-shape tuner may pick (block tile x split cap for fwd /
+    dgrad, block target for wgrad) gives the torch results on every test shape."""
+    from mx_det import conv as mc
+    monkeypatch.setenv("MX_CONV_TUNE", "0")
+    monkeypatch.setattr(mc, "_FD_CANDS", (mc._FD_CANDS[ci],))
+    monkeypatch.setattr(mc, "_WG_CANDS", (mc._WG_CANDS[ci % len(mc._WG_CANDS)],))
+    test_conv_fwd(dev, 7, N, H, W, C, K, k, st, pd)
+    test_conv_dgrad_wgrad(dev, 7, N, H, W, C, K, k, st, pd)
