@@ -190,15 +190,45 @@ __global__ void __launch_bounds__(256) nms_scan_lds_kernel(const uint64_t* __res
     }
     for (int w = tid; w < W; w += 256) removed[w] = 0;
     int kept_total = 0;
+    // the next 64-row block's mask words are loaded into registers while this block is resolved
+    // (when they fit: <= 8 words per thread), hiding the global-load latency of each step
+    constexpr int PF = 8;
+    uint64_t pre[PF];
+    auto fetch = [&](int b) {
+      const int64_t rb = s0 + (int64_t)b * 64;
+      const int c = (int)min<int64_t>(64, len - (int64_t)b * 64), nw_ = W - b;
+#pragma unroll
+      for (int i = 0; i < PF; ++i) {
+        const int e = tid + i * 256;
+        if (e < c * nw_) {
+          const int t = e / nw_, w = b + (e - t * nw_);
+          pre[i] = mask[(rb + t) * Wm + w];
+        }
+      }
+    };
+    auto fits = [&](int b) { return b < W && (int)min<int64_t>(64, len - (int64_t)b * 64) * (W - b) <= PF * 256; };
+    if (fits(0)) fetch(0);
     for (int blk = 0; blk < W; ++blk) {
       const int64_t rbase = s0 + (int64_t)blk * 64;
       const int cnt = (int)min<int64_t>(64, len - (int64_t)blk * 64);
       const int nw = W - blk;  // words blk..W-1
-      for (int e = tid; e < cnt * nw; e += 256) {
-        const int t = e / nw, w = blk + (e - t * nw);
-        rows[t * Wm + w] = mask[(rbase + t) * Wm + w];
+      if (fits(blk)) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+          const int e = tid + i * 256;
+          if (e < cnt * nw) {
+            const int t = e / nw, w = blk + (e - t * nw);
+            rows[t * Wm + w] = pre[i];
+          }
+        }
+      } else {
+        for (int e = tid; e < cnt * nw; e += 256) {
+          const int t = e / nw, w = blk + (e - t * nw);
+          rows[t * Wm + w] = mask[(rbase + t) * Wm + w];
+        }
       }
       __syncthreads();
+      if (fits(blk + 1)) fetch(blk + 1);
       if (tid < 64) {
         const uint64_t diag = lane < cnt ? rows[lane * Wm + blk] : 0ull;
         uint64_t cur = removed[blk];
@@ -218,15 +248,18 @@ __global__ void __launch_bounds__(256) nms_scan_lds_kernel(const uint64_t* __res
       __syncthreads();
       const uint64_t kept = kept_s;
       if (tid == 0) kept_total += __popcll(kept);
-      for (int w = blk + 1 + tid; w < W; w += 256) {
-        uint64_t acc = removed[w];
-        uint64_t k = kept;
+      // OR the kept rows into `removed`: (word, 1/8 of the kept rows) per thread, combined with LDS
+      // atomic ORs -- 8x shorter dependent LDS-read chains than one thread per word
+      for (int e = tid; e < (W - blk - 1) * 8; e += 256) {
+        const int w = blk + 1 + (e >> 3), part = e & 7;
+        uint64_t k = kept & (0x0101010101010101ull << part);
+        uint64_t acc = 0;
         while (k) {
           const int t = __ffsll((unsigned long long)k) - 1;
           k &= k - 1;
           acc |= rows[t * Wm + w];
         }
-        removed[w] = acc;
+        if (acc) atomicOr((unsigned long long*)&removed[w], (unsigned long long)acc);
       }
       __syncthreads();
     }
