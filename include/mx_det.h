@@ -268,6 +268,18 @@ int mx_bn_finalize(const float* stats, int64_t mblocks, int64_t K, int64_t count
  * zero-kept. */
 int mx_bn_bwd_finalize(const float* part, int64_t mb, int64_t K, int64_t M, const float* mean, const float* invstd,
                        const float* gamma, float* sums, float* coef, void* ws, size_t ws_bytes, mx_stream_t stream);
+/* RegionProposalNetwork.compute_loss over N*A anchors (objectness [n], deltas / targets [n][4] f32,
+ * labels [n] (1 fg / 0 bg / -1), pos / neg sampler masks [n] u8): out[0] = mean BCE-with-logits over
+ * the sampled anchors, out[1] = smooth-L1(beta) summed over the positives / number sampled,
+ * out[2] = number sampled. Deterministic (fixed-order f64 finish). Workspace counters zero-kept. */
+size_t mx_rpn_loss_workspace(int64_t n);
+int mx_rpn_loss_fwd(const float* objectness, const float* deltas, const float* labels, const float* targets,
+                    const uint8_t* pos, const uint8_t* neg, int64_t n, float beta, float* out, void* ws,
+                    size_t ws_bytes, mx_stream_t stream);
+/* Gradients of (out[0], out[1]) scaled by grad[0..1] (device) w.r.t. objectness and deltas. */
+int mx_rpn_loss_bwd(const float* objectness, const float* deltas, const float* labels, const float* targets,
+                    const uint8_t* pos, const uint8_t* neg, int64_t n, float beta, const float* out, const float* grad,
+                    float* grad_objectness, float* grad_deltas, mx_stream_t stream);
 size_t mx_bn_finalize_workspace(int64_t mblocks, int64_t K);
 int mx_bn_finalize_ex(const float* stats, int64_t mblocks, int64_t K, int64_t count, const float* gamma,
                       const float* beta, float eps, float momentum, float* running_mean, float* running_var,

@@ -456,6 +456,86 @@ static BwdGeo bwd_geo(int64_t M, int64_t K) {
 
 static int64_t fin_slices(int64_t mb) { return std::max<int64_t>(1, std::min<int64_t>(64, cdiv(mb, 32))); }
 
+// ---- RPN losses (RegionProposalNetwork.compute_loss) -------------------------------------------
+// Over all N*A anchors with the sampler's masks: sum_sampled BCE-with-logits(x, y) and
+// sum_positive smooth-L1(beta)(d - t) (summed over the 4 coordinates), each / number sampled.
+// Per-block f64 partials, last block finishes in a fixed order (deterministic); BCE restated as
+// torch's binary_cross_entropy_with_logits: (1 - y) x + m + log(exp(-m) + exp(-x - m)), m = max(-x, 0).
+__device__ __forceinline__ float smooth_l1(float u, float beta) {
+  const float a = fabsf(u);
+  return a < beta ? 0.5f * u * u / beta : a - 0.5f * beta;
+}
+
+__global__ void __launch_bounds__(256) rpn_loss_fwd_kernel(const float* __restrict__ x, const float4* __restrict__ d,
+                                                           const float* __restrict__ y, const float4* __restrict__ t,
+                                                           const uint8_t* __restrict__ pm, const uint8_t* __restrict__ nm,
+                                                           int64_t n, float beta, unsigned* __restrict__ ctr,
+                                                           double* __restrict__ part, float* __restrict__ out) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const bool p = pm[i], s = p || nm[i];
+    if (!s) continue;
+    const float xi = x[i], yi = y[i] > 0.f ? 1.f : 0.f;
+    const float m = fmaxf(-xi, 0.f);
+    a0 += (double)((1.f - yi) * xi + m + logf(expf(-m) + expf(-xi - m)));
+    a2 += 1.0;
+    if (p) {
+      const float4 di = d[i], ti = t[i];
+      a1 += (double)(smooth_l1(di.x - ti.x, beta) + smooth_l1(di.y - ti.y, beta) + smooth_l1(di.z - ti.z, beta) +
+                     smooth_l1(di.w - ti.w, beta));
+    }
+  }
+  __shared__ double red[3][256];
+  red[0][threadIdx.x] = a0;
+  red[1][threadIdx.x] = a1;
+  red[2][threadIdx.x] = a2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      for (int w = 0; w < 3; ++w) red[w][threadIdx.x] += red[w][threadIdx.x + o];
+    __syncthreads();
+  }
+  const int64_t RB = gridDim.x;
+  if (threadIdx.x < 3) st_sc1(part + threadIdx.x * RB + blockIdx.x, red[threadIdx.x][0]);
+  if (!arrive_last(ctr, (unsigned)RB)) return;
+  __shared__ double fin[3][64], scr[256];
+  last_sums<3>(part, RB, 1, 0, fin, scr);
+  if (threadIdx.x == 0) {
+    const double cnt = fin[2][0];
+    out[0] = (float)(fin[0][0] / cnt);  // loss_objectness
+    out[1] = (float)(fin[1][0] / cnt);  // loss_rpn_box_reg
+    out[2] = (float)cnt;
+  }
+}
+
+// d loss / d x = (sigmoid(x) - y) / cnt * g0 on sampled anchors; d loss / d d = smooth-L1'(d - t) / cnt
+// * g1 on positives; zero elsewhere.
+__global__ void __launch_bounds__(256) rpn_loss_bwd_kernel(const float* __restrict__ x, const float4* __restrict__ d,
+                                                           const float* __restrict__ y, const float4* __restrict__ t,
+                                                           const uint8_t* __restrict__ pm, const uint8_t* __restrict__ nm,
+                                                           int64_t n, float beta, const float* __restrict__ stats,
+                                                           const float* __restrict__ g, float* __restrict__ gx,
+                                                           float4* __restrict__ gd) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float inv = 1.f / stats[2];
+  const bool p = pm[i], s = p || nm[i];
+  float gxi = 0.f;
+  float4 gdi = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (s) {
+    const float xi = x[i], yi = y[i] > 0.f ? 1.f : 0.f;
+    gxi = (1.f / (1.f + expf(-xi)) - yi) * inv * g[0];
+  }
+  if (p) {
+    const float4 di = d[i], ti = t[i];
+    const float sc = inv * g[1];
+    auto dl = [&](float u) { return (fabsf(u) < beta ? u / beta : (u > 0.f ? 1.f : (u < 0.f ? -1.f : 0.f))) * sc; };
+    gdi = make_float4(dl(di.x - ti.x), dl(di.y - ti.y), dl(di.z - ti.z), dl(di.w - ti.w));
+  }
+  gx[i] = gxi;
+  gd[i] = gdi;
+}
+
 }  // namespace mx
 
 using namespace mx;
@@ -654,6 +734,35 @@ extern "C" int mx_act_bias_bwd(const void* gy, const void* y, int dtype, int64_t
   hipStream_t st = (hipStream_t)stream;
   if (dtype == MX_BF16) launch_act_bias<uint16_t>(gy, y, M, (int)K, (int)K8, act, g_, g, db, ctr, part, st);
   else launch_act_bias<float>(gy, y, M, (int)K, (int)K8, act, g_, g, db, ctr, part, st);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" size_t mx_rpn_loss_workspace(int64_t n) {
+  (void)n;
+  return CTR_BYTES + sizeof(double) * 3 * 1024;
+}
+
+extern "C" int mx_rpn_loss_fwd(const float* objectness, const float* deltas, const float* labels, const float* targets,
+                               const uint8_t* pos, const uint8_t* neg, int64_t n, float beta, float* out, void* ws,
+                               size_t ws_bytes, mx_stream_t stream) {
+  MX_CHECK_ARG(n > 0 && objectness && deltas && labels && targets && pos && neg && out, "rpn_loss: bad arguments");
+  MX_CHECK_ARG(ws && ws_bytes >= mx_rpn_loss_workspace(n), "rpn_loss: workspace too small");
+  const unsigned blocks = (unsigned)std::min<int64_t>(1024, cdiv(n, 256 * 4));
+  rpn_loss_fwd_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(objectness, (const float4*)deltas, labels,
+                                                               (const float4*)targets, pos, neg, n, beta,
+                                                               (unsigned*)ws, (double*)((char*)ws + CTR_BYTES), out);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" int mx_rpn_loss_bwd(const float* objectness, const float* deltas, const float* labels, const float* targets,
+                               const uint8_t* pos, const uint8_t* neg, int64_t n, float beta, const float* out,
+                               const float* grad, float* grad_objectness, float* grad_deltas, mx_stream_t stream) {
+  MX_CHECK_ARG(n > 0 && out && grad && grad_objectness && grad_deltas, "rpn_loss bwd: bad arguments");
+  rpn_loss_bwd_kernel<<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(
+      objectness, (const float4*)deltas, labels, (const float4*)targets, pos, neg, n, beta, out, grad, grad_objectness,
+      (float4*)grad_deltas);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

@@ -124,6 +124,9 @@ class HipBackend:
     def batched_nms(self, boxes, scores, idxs, thr, group=None, max_seg=None, mode=0):
         return ops.batched_nms(boxes, scores, idxs, thr, group=group, max_seg=max_seg, mode=mode)
 
+    def rpn_loss(self, objectness, deltas, labels, targets, pos, neg, beta):
+        return ops.rpn_loss(objectness, deltas, labels, targets, pos, neg, beta)
+
     def proposal_nms(self, boxes, scores, lvl, group, G, L, thr, max_seg):
         return ops.batched_nms_grouped(boxes, scores, lvl, group, G, L, thr, max_seg)
 

@@ -348,14 +348,18 @@ class RegionProposalNetwork(nn.Module):
             lab = torch.stack(labels)                     # [N, A] 1 / 0 / -1
             rt = torch.stack(reg_targets)                 # [N, A, 4]
             pm, nm = self.fg_bg_sampler(lab)
-            sm = pm | nm
-            cnt = sm.sum()
             # torchvision: BCE mean over the sampled anchors; smooth-L1 (beta 1/9) sum over the sampled
             # positives / number sampled
-            obj = F.binary_cross_entropy_with_logits(objectness, lab.clamp(min=0), reduction="none")
-            bl = F.smooth_l1_loss(pred_deltas, rt, beta=1.0 / 9, reduction="none").sum(-1)
-            losses = {"loss_objectness": torch.where(sm, obj, 0.0).sum() / cnt,
-                      "loss_rpn_box_reg": torch.where(pm, bl, 0.0).sum() / cnt}
+            if hasattr(be, "rpn_loss"):  # HIP: one fused launch each way
+                lo, lb = be.rpn_loss(objectness, pred_deltas, lab, rt, pm, nm, 1.0 / 9)
+                losses = {"loss_objectness": lo, "loss_rpn_box_reg": lb}
+            else:
+                sm = pm | nm
+                cnt = sm.sum()
+                obj = F.binary_cross_entropy_with_logits(objectness, lab.clamp(min=0), reduction="none")
+                bl = F.smooth_l1_loss(pred_deltas, rt, beta=1.0 / 9, reduction="none").sum(-1)
+                losses = {"loss_objectness": torch.where(sm, obj, 0.0).sum() / cnt,
+                          "loss_rpn_box_reg": torch.where(pm, bl, 0.0).sum() / cnt}
         proposals = be.box_decode(pred_deltas.detach().reshape(-1, 4), anchors.repeat(N, 1), RPN_WEIGHTS)
         proposals = proposals.view(N, A, 4)
         if self.training:  # padded (boxes, scores, valid): the RoI sampler works on the device

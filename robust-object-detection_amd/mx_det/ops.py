@@ -296,3 +296,46 @@ def normalize_pad(images, padded_hw, channels=3, dtype=torch.float32, mean=IMAGE
     call("mx_normalize_pad", _p(x), B, H, W, (ctypes.c_float * 3)(*mean), (ctypes.c_float * 3)(*std), Hp, Wp,
          channels, _dtype_code(out), _p(out), _stream())
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+class _RPNLoss(torch.autograd.Function):
+    """RegionProposalNetwork.compute_loss fused (mx_rpn_loss_fwd / _bwd): two launches instead of the
+    ~25 elementwise / reduction ops (and their autograd nodes) of the torch formulation."""
+
+    @staticmethod
+    def forward(ctx, objectness, deltas, labels, targets, pos, neg, beta):
+        from .conv import bn_scratch
+        x = objectness.detach().float().contiguous()
+        d = deltas.detach().float().contiguous()
+        y = labels.float().contiguous()
+        t = targets.float().contiguous()
+        pm = pos.to(torch.uint8).contiguous()
+        nm = neg.to(torch.uint8).contiguous()
+        n = x.numel()
+        out = torch.empty(3, dtype=torch.float32, device=x.device)
+        ws = bn_scratch(_lib.load().mx_rpn_loss_workspace(n), x.device)
+        call("mx_rpn_loss_fwd", _p(x), _p(d), _p(y), _p(t), _p(pm), _p(nm), n, float(beta), _p(out), _p(ws),
+             ws.numel(), _stream())
+        ctx.save_for_backward(x, d, y, t, pm, nm, out)
+        ctx.beta = beta
+        ctx.shapes = (objectness.shape, deltas.shape)
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, g0, g1):
+        x, d, y, t, pm, nm, out = ctx.saved_tensors
+        z = torch.zeros((), dtype=torch.float32, device=x.device)
+        g = torch.stack([g0 if g0 is not None else z, g1 if g1 is not None else z]).float().contiguous()
+        gx = torch.empty_like(x)
+        gd = torch.empty_like(d)
+        call("mx_rpn_loss_bwd", _p(x), _p(d), _p(y), _p(t), _p(pm), _p(nm), x.numel(), float(ctx.beta), _p(out),
+             _p(g), _p(gx), _p(gd), _stream())
+        return gx.view(ctx.shapes[0]), gd.view(ctx.shapes[1]), None, None, None, None, None
+
+
+def rpn_loss(objectness, deltas, labels, targets, pos, neg, beta=1.0 / 9):
+    """(loss_objectness, loss_rpn_box_reg) of torchvision's RegionProposalNetwork.compute_loss given
+    the sampler's masks; objectness [N, A], deltas / targets [N, A, 4], labels [N, A] (1/0/-1)."""
+    _dev(objectness, deltas)
+    return _RPNLoss.apply(objectness, deltas, labels, targets, pos, neg, beta)

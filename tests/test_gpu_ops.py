@@ -338,3 +338,32 @@ def test_multiscale_roi_align_bf16_tiled(dev, C):
         r = orc.roi_align_backward(gn[sel], rois[sel], scales[l], fn[l].shape, 2, False)
         gg = ft[l].grad.float().permute(0, 3, 1, 2).cpu().numpy()
         np.testing.assert_allclose(gg, r, rtol=1e-2, atol=1e-2)
+
+
+def test_rpn_loss_fused_matches_torch(dev):
+    """mx_rpn_loss_fwd / _bwd == torchvision's compute_loss formulation (BCE-with-logits mean over the
+    sampled anchors, smooth-L1 beta 1/9 over positives / number sampled) and its autograd gradients."""
+    import torch.nn.functional as F
+    from mx_det import ops
+    g = torch.Generator().manual_seed(5)
+    N, A = 2, 70001
+    x = (torch.randn(N, A, generator=g) * 3).to(dev).requires_grad_(True)
+    d = torch.randn(N, A, 4, generator=g).to(dev).requires_grad_(True)
+    t = torch.randn(N, A, 4, generator=g).to(dev)
+    lab = (torch.randint(-1, 2, (N, A), generator=g)).float().to(dev)
+    r = torch.rand(N, A, generator=g).to(dev)
+    pm = (lab == 1) & (r < 0.01)
+    nm = (lab == 0) & (r < 0.02)
+    lo, lb = ops.rpn_loss(x, d, lab, t, pm, nm, 1.0 / 9)
+    (lo * 1.5 + lb * 0.5).backward()
+    gx, gd = x.grad.clone(), d.grad.clone()
+    x.grad = d.grad = None
+    sm = pm | nm
+    cnt = sm.sum()
+    ro = torch.where(sm, F.binary_cross_entropy_with_logits(x, lab.clamp(min=0), reduction="none"), 0.0).sum() / cnt
+    rb = torch.where(pm, F.smooth_l1_loss(d, t, beta=1.0 / 9, reduction="none").sum(-1), 0.0).sum() / cnt
+    (ro * 1.5 + rb * 0.5).backward()
+    torch.testing.assert_close(lo, ro, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(lb, rb, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(gx, x.grad, rtol=1e-4, atol=1e-8)
+    torch.testing.assert_close(gd, d.grad, rtol=1e-4, atol=1e-8)
