@@ -280,6 +280,16 @@ int mx_rpn_loss_fwd(const float* objectness, const float* deltas, const float* l
 int mx_rpn_loss_bwd(const float* objectness, const float* deltas, const float* labels, const float* targets,
                     const uint8_t* pos, const uint8_t* neg, int64_t n, float beta, const float* out, const float* grad,
                     float* grad_objectness, float* grad_deltas, mx_stream_t stream);
+/* fastrcnn_loss over R sampled RoIs: logits [R][ldl] (C classes), box regression [R][ldr] (4 per
+ * class), labels [R] int64, targets [R][4]: out[0] = mean cross-entropy, out[1] = smooth-L1(beta) of
+ * the labelled class's box over positive RoIs / R. Workspace: mx_rpn_loss_workspace(R). Backward:
+ * grad_logits [R][C], grad_reg [R][4C] (dense) for upstream grad[0..1]. */
+int mx_roi_loss_fwd(const float* logits, int64_t ldl, int C, const float* reg, int64_t ldr, const int64_t* labels,
+                    const float* targets, int64_t R, float beta, float* out, void* ws, size_t ws_bytes,
+                    mx_stream_t stream);
+int mx_roi_loss_bwd(const float* logits, int64_t ldl, int C, const float* reg, int64_t ldr, const int64_t* labels,
+                    const float* targets, int64_t R, float beta, const float* grad, float* grad_logits,
+                    float* grad_reg, mx_stream_t stream);
 size_t mx_bn_finalize_workspace(int64_t mblocks, int64_t K);
 int mx_bn_finalize_ex(const float* stats, int64_t mblocks, int64_t K, int64_t count, const float* gamma,
                       const float* beta, float eps, float momentum, float* running_mean, float* running_var,

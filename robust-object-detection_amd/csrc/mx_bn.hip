@@ -536,6 +536,83 @@ __global__ void __launch_bounds__(256) rpn_loss_bwd_kernel(const float* __restri
   gd[i] = gdi;
 }
 
+// ---- Fast R-CNN losses (roi_heads.fastrcnn_loss) ---------------------------------------------------
+// logits [R][ldl] (first C columns), reg [R][ldr] (4 per class), labels [R] int64, targets [R][4]:
+// out[0] = mean cross-entropy, out[1] = sum over positive RoIs of smooth-L1(beta)(reg[r, 4*label:+4]
+// - targets[r]) / R. One thread per RoI, fixed-order f64 finish in the last block.
+__global__ void __launch_bounds__(256) roi_loss_fwd_kernel(const float* __restrict__ logits, int64_t ldl, int C,
+                                                           const float* __restrict__ reg, int64_t ldr,
+                                                           const int64_t* __restrict__ labels,
+                                                           const float* __restrict__ targets, int64_t R, float beta,
+                                                           unsigned* __restrict__ ctr, double* __restrict__ part,
+                                                           float* __restrict__ out) {
+  double a0 = 0.0, a1 = 0.0;
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r < R) {
+    const float* l = logits + r * ldl;
+    const int64_t lab = labels[r];
+    float mx = l[0];
+    for (int c = 1; c < C; ++c) mx = fmaxf(mx, l[c]);
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += expf(l[c] - mx);
+    a0 = (double)(logf(se) + mx - l[lab]);
+    if (lab > 0) {
+      const float* q = reg + r * ldr + 4 * lab;
+      const float* tt = targets + r * 4;
+      a1 = (double)(smooth_l1(q[0] - tt[0], beta) + smooth_l1(q[1] - tt[1], beta) + smooth_l1(q[2] - tt[2], beta) +
+                    smooth_l1(q[3] - tt[3], beta));
+    }
+  }
+  __shared__ double red[2][256];
+  red[0][threadIdx.x] = a0;
+  red[1][threadIdx.x] = a1;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  const int64_t RB = gridDim.x;
+  if (threadIdx.x < 2) st_sc1(part + threadIdx.x * RB + blockIdx.x, red[threadIdx.x][0]);
+  if (!arrive_last(ctr, (unsigned)RB)) return;
+  __shared__ double fin[2][64], scr[256];
+  last_sums<2>(part, RB, 1, 0, fin, scr);
+  if (threadIdx.x == 0) {
+    out[0] = (float)(fin[0][0] / (double)R);
+    out[1] = (float)(fin[1][0] / (double)R);
+  }
+}
+
+__global__ void __launch_bounds__(256) roi_loss_bwd_kernel(const float* __restrict__ logits, int64_t ldl, int C,
+                                                           const float* __restrict__ reg, int64_t ldr,
+                                                           const int64_t* __restrict__ labels,
+                                                           const float* __restrict__ targets, int64_t R, float beta,
+                                                           const float* __restrict__ g, float* __restrict__ gl,
+                                                           float* __restrict__ gr) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= R) return;
+  const float* l = logits + r * ldl;
+  const int64_t lab = labels[r];
+  const float s0 = g[0] / (float)R, s1 = g[1] / (float)R;
+  float mx = l[0];
+  for (int c = 1; c < C; ++c) mx = fmaxf(mx, l[c]);
+  float se = 0.f;
+  for (int c = 0; c < C; ++c) se += expf(l[c] - mx);
+  for (int c = 0; c < C; ++c) gl[r * C + c] = (expf(l[c] - mx) / se - (c == lab ? 1.f : 0.f)) * s0;
+  float* q = gr + r * (4 * C);
+  for (int j = 0; j < 4 * C; ++j) q[j] = 0.f;
+  if (lab > 0) {
+    const float* p = reg + r * ldr + 4 * lab;
+    const float* tt = targets + r * 4;
+    for (int j = 0; j < 4; ++j) {
+      const float u = p[j] - tt[j];
+      q[4 * lab + j] = (fabsf(u) < beta ? u / beta : (u > 0.f ? 1.f : (u < 0.f ? -1.f : 0.f))) * s1;
+    }
+  }
+}
+
 }  // namespace mx
 
 using namespace mx;
@@ -763,6 +840,30 @@ extern "C" int mx_rpn_loss_bwd(const float* objectness, const float* deltas, con
   rpn_loss_bwd_kernel<<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(
       objectness, (const float4*)deltas, labels, (const float4*)targets, pos, neg, n, beta, out, grad, grad_objectness,
       (float4*)grad_deltas);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" int mx_roi_loss_fwd(const float* logits, int64_t ldl, int C, const float* reg, int64_t ldr,
+                               const int64_t* labels, const float* targets, int64_t R, float beta, float* out, void* ws,
+                               size_t ws_bytes, mx_stream_t stream) {
+  MX_CHECK_ARG(R > 0 && C > 0 && ldl >= C && ldr >= 4 * C && logits && reg && labels && targets && out,
+               "roi_loss: bad arguments");
+  const int64_t blocks = cdiv(R, 256);
+  MX_CHECK_ARG(blocks <= 1024 && ws && ws_bytes >= mx_rpn_loss_workspace(R), "roi_loss: workspace / size");
+  roi_loss_fwd_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(logits, ldl, C, reg, ldr, labels, targets, R,
+                                                                         beta, (unsigned*)ws,
+                                                                         (double*)((char*)ws + CTR_BYTES), out);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" int mx_roi_loss_bwd(const float* logits, int64_t ldl, int C, const float* reg, int64_t ldr,
+                               const int64_t* labels, const float* targets, int64_t R, float beta, const float* grad,
+                               float* grad_logits, float* grad_reg, mx_stream_t stream) {
+  MX_CHECK_ARG(R > 0 && C > 0 && grad && grad_logits && grad_reg, "roi_loss bwd: bad arguments");
+  roi_loss_bwd_kernel<<<(unsigned)cdiv(R, 256), 256, 0, (hipStream_t)stream>>>(logits, ldl, C, reg, ldr, labels, targets,
+                                                                               R, beta, grad, grad_logits, grad_reg);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

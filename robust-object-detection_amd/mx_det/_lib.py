@@ -78,6 +78,8 @@ _SIGS = {
     "mx_rpn_loss_workspace": (c_sz, [c_i64]),
     "mx_rpn_loss_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_sz, c_vp]),
     "mx_rpn_loss_bwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mx_roi_loss_fwd": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_sz, c_vp]),
+    "mx_roi_loss_bwd": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp]),
     "mx_bn_bwd_finalize": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_conv2d_dgrad_ex": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_conv2d_dgrad_t": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),

@@ -124,6 +124,9 @@ class HipBackend:
     def batched_nms(self, boxes, scores, idxs, thr, group=None, max_seg=None, mode=0):
         return ops.batched_nms(boxes, scores, idxs, thr, group=group, max_seg=max_seg, mode=mode)
 
+    def roi_loss(self, class_logits, box_regression, labels, targets, beta):
+        return ops.roi_loss(class_logits, box_regression, labels, targets, beta)
+
     def rpn_loss(self, objectness, deltas, labels, targets, pos, neg, beta):
         return ops.rpn_loss(objectness, deltas, labels, targets, pos, neg, beta)
 

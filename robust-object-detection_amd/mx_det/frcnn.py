@@ -540,12 +540,15 @@ class RoIHeads(nn.Module):
         if self.training:
             lab = torch.cat(labels)
             rt = torch.cat(tgts)
-            loss_cls = F.cross_entropy(class_logits, lab)
-            R = class_logits.shape[0]
-            reg = box_regression.reshape(R, -1, 4)[torch.arange(R, device=dev), lab]
-            # torchvision: smooth-L1 (beta 1/9) summed over the positive RoIs / number of sampled RoIs
-            bl = F.smooth_l1_loss(reg, rt, beta=1.0 / 9, reduction="none").sum(-1)
-            loss_box = torch.where(lab > 0, bl, 0.0).sum() / lab.numel()
+            if hasattr(be, "roi_loss"):  # HIP: one fused launch each way
+                loss_cls, loss_box = be.roi_loss(class_logits, box_regression, lab, rt, 1.0 / 9)
+            else:
+                loss_cls = F.cross_entropy(class_logits, lab)
+                R = class_logits.shape[0]
+                reg = box_regression.reshape(R, -1, 4)[torch.arange(R, device=dev), lab]
+                # torchvision: smooth-L1 (beta 1/9) summed over the positive RoIs / number of sampled RoIs
+                bl = F.smooth_l1_loss(reg, rt, beta=1.0 / 9, reduction="none").sum(-1)
+                loss_box = torch.where(lab > 0, bl, 0.0).sum() / lab.numel()
             return [], {"loss_classifier": loss_cls, "loss_box_reg": loss_box}
         return self.postprocess_detections(class_logits, box_regression, proposals, image_sizes, be), {}
 

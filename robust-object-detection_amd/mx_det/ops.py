@@ -339,3 +339,45 @@ def rpn_loss(objectness, deltas, labels, targets, pos, neg, beta=1.0 / 9):
     the sampler's masks; objectness [N, A], deltas / targets [N, A, 4], labels [N, A] (1/0/-1)."""
     _dev(objectness, deltas)
     return _RPNLoss.apply(objectness, deltas, labels, targets, pos, neg, beta)
+
+
+class _RoILoss(torch.autograd.Function):
+    """fastrcnn_loss fused (mx_roi_loss_fwd / _bwd): cross-entropy + class-indexed smooth-L1."""
+
+    @staticmethod
+    def forward(ctx, logits, reg, labels, targets, beta):
+        from .conv import bn_scratch
+        lg = logits.detach().float()
+        rg = reg.detach().float()
+        if lg.stride(1) != 1:
+            lg = lg.contiguous()
+        if rg.stride(1) != 1:
+            rg = rg.contiguous()
+        lab = labels.to(torch.int64).contiguous()
+        t = targets.float().contiguous()
+        R, C = lg.shape
+        out = torch.empty(2, dtype=torch.float32, device=lg.device)
+        ws = bn_scratch(_lib.load().mx_rpn_loss_workspace(R), lg.device)
+        call("mx_roi_loss_fwd", _p(lg), lg.stride(0), C, _p(rg), rg.stride(0), _p(lab), _p(t), R, float(beta),
+             _p(out), _p(ws), ws.numel(), _stream())
+        ctx.save_for_backward(lg, rg, lab, t)
+        ctx.beta = beta
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, g0, g1):
+        lg, rg, lab, t = ctx.saved_tensors
+        R, C = lg.shape
+        z = torch.zeros((), dtype=torch.float32, device=lg.device)
+        g = torch.stack([g0 if g0 is not None else z, g1 if g1 is not None else z]).float().contiguous()
+        gl = torch.empty((R, C), dtype=torch.float32, device=lg.device)
+        gr = torch.empty((R, 4 * C), dtype=torch.float32, device=lg.device)
+        call("mx_roi_loss_bwd", _p(lg), lg.stride(0), C, _p(rg), rg.stride(0), _p(lab), _p(t), R, float(ctx.beta),
+             _p(g), _p(gl), _p(gr), _stream())
+        return gl, gr, None, None, None
+
+
+def roi_loss(class_logits, box_regression, labels, regression_targets, beta=1.0 / 9):
+    """(loss_classifier, loss_box_reg) of torchvision's fastrcnn_loss for the sampled RoIs."""
+    _dev(class_logits, box_regression)
+    return _RoILoss.apply(class_logits, box_regression, labels, regression_targets, beta)

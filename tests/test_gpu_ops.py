@@ -367,3 +367,28 @@ def test_rpn_loss_fused_matches_torch(dev):
     torch.testing.assert_close(lb, rb, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(gx, x.grad, rtol=1e-4, atol=1e-8)
     torch.testing.assert_close(gd, d.grad, rtol=1e-4, atol=1e-8)
+
+
+def test_roi_loss_fused_matches_torch(dev):
+    """mx_roi_loss_fwd / _bwd == fastrcnn_loss (cross-entropy mean; class-indexed smooth-L1 beta 1/9
+    over positives / R) and its gradients, on strided views of one predictor output as in the model."""
+    import torch.nn.functional as F
+    from mx_det import ops
+    g = torch.Generator().manual_seed(6)
+    R, C = 1000, 7
+    o = torch.randn(R, 5 * C, generator=g).to(dev).requires_grad_(True)
+    lab = torch.randint(0, C, (R,), generator=g).to(dev)
+    lab[torch.rand(R, generator=g).to(dev) < 0.7] = 0
+    t = torch.randn(R, 4, generator=g).to(dev)
+    lc, lb = ops.roi_loss(o[:, :C], o[:, C:], lab, t, 1.0 / 9)
+    (lc * 0.7 + lb * 1.3).backward()
+    go = o.grad.clone()
+    o.grad = None
+    cl, br = o[:, :C], o[:, C:]
+    rc = F.cross_entropy(cl, lab)
+    reg = br.reshape(R, -1, 4)[torch.arange(R, device=dev), lab]
+    rb = torch.where(lab > 0, F.smooth_l1_loss(reg, t, beta=1.0 / 9, reduction="none").sum(-1), 0.0).sum() / R
+    (rc * 0.7 + rb * 1.3).backward()
+    torch.testing.assert_close(lc, rc, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(lb, rb, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(go, o.grad, rtol=1e-4, atol=1e-7)
