@@ -92,7 +92,7 @@ def weight_krsc(w, cin_pad=None):
 # on the launch stream (outputs are pure functions of the inputs, so re-running is harmless) and
 # the winner is reused (and baked into the captured graphs). MX_CONV_TUNE=0: library defaults.
 _FD_CANDS = ((0, 0, 0), (0, 0, 1), (0, 0, 2), (64, 64, 0), (64, 64, 1), (128, 128, 1))
-_WG_CANDS = (0, 512, 1024, 384)
+_WG_CANDS = ((3, 0), (3, 512), (3, 1024), (3, 384), (2, 0), (0, 0))  # (wgrad kernel variant, block target)
 _tune_cache = {}
 
 
@@ -106,15 +106,22 @@ def _apply_fd(cfg):
     call("mx_conv_set_max_splits", cfg[2])
 
 
-def _apply_wg(t):
-    call("mx_conv_set_wgrad_target", int(t))
+def _apply_wg(c):
+    call("mx_conv_set_wgrad_variant", int(c[0]))
+    call("mx_conv_set_wgrad_target", int(c[1]))
 
 
-def _tuned(key, cands, apply, run):
-    """Launch `run` under the cached best candidate for `key` (timing the candidates at first use)."""
+_FD_DEFAULT, _WG_DEFAULT = (0, 0, 0), (3, 0)  # the library's own settings (restored after each launch)
+
+
+def _tuned(key, cands, apply, run, default):
+    """Launch `run` under the cached best candidate for `key` (timing the candidates at first use).
+    MX_CONV_TUNE=0 leaves the library's launch settings untouched (defaults or mx_conv_set_*)."""
+    if not _tune_on():
+        return run()
     cfg = _tune_cache.get(key)
     if cfg is None:
-        if not _tune_on() or _timer is not None or torch.cuda.is_current_stream_capturing():
+        if _timer is not None or torch.cuda.is_current_stream_capturing():
             cfg = cands[0]
         else:
             best = None
@@ -136,7 +143,7 @@ def _tuned(key, cands, apply, run):
     try:
         return run()
     finally:
-        apply(cands[0])
+        apply(default)
 
 
 def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dtype=torch.bfloat16, stats=False):
@@ -161,7 +168,7 @@ def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dty
              1 if out_dtype == torch.bfloat16 else 0, _p(st), _p(ws), wsb, _s())
 
     key = ("fwd", sh.N, sh.H, sh.W, C, K, R, S, tuple(stride), tuple(pad), residual is not None, out_dtype)
-    _tuned(key, _FD_CANDS, _apply_fd, run)
+    _tuned(key, _FD_CANDS, _apply_fd, run, _FD_DEFAULT)
     if _timer:
         _timer.stop("fwd128" if K > 64 else "fwd64", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * C, t0,
                     _tag(sh.N, sh.H, sh.W, C, K, R, S, stride))
@@ -326,7 +333,7 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
             call("mx_conv2d_dgrad_ex", ctypes.byref(sh), _p(dyc), _p(wt), _p(residual), _p(dx), _p(ws), wsb, _s())
 
     key = ("dgrad", N, H, W, C, K, R, S, tuple(stride), tuple(pad), residual is not None, part is not None)
-    _tuned(key, _FD_CANDS, _apply_fd, run)
+    _tuned(key, _FD_CANDS, _apply_fd, run, _FD_DEFAULT)
     if part is not None:
         bnb.part = part
     if _timer:
@@ -412,8 +419,10 @@ def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False):
             wsb_ = _lib.load().mx_conv_workspace(ctypes.byref(sh), 2)
             ws_ = torch.empty(wsb_, dtype=torch.uint8, device=x.device) if wsb_ else None
             call("mx_conv2d_wgrad_ex", ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws_), wsb_, _s())
-        _tuned(key, _WG_CANDS, _apply_wg, trial)
-    _apply_wg(_tune_cache.get(key, 0))
+        _tuned(key, _WG_CANDS, _apply_wg, trial, _WG_DEFAULT)
+    tune = _tune_on()
+    if tune:
+        _apply_wg(_tune_cache.get(key, _WG_DEFAULT))
     wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 2)
     ws = torch.empty(wsb, dtype=torch.uint8, device=x.device) if wsb else None
     stream = _s()
@@ -424,7 +433,8 @@ def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False):
         st.wait_stream(torch.cuda.current_stream())
         stream = st.cuda_stream
     call("mx_conv2d_wgrad_ex", ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws), wsb, stream)
-    _apply_wg(0)
+    if tune:
+        _apply_wg(_WG_DEFAULT)
     if side:
         ev = torch.cuda.Event()
         ev.record(st)

@@ -34,12 +34,19 @@ def variant(request):
     variants (mx_conv_set_wgrad_variant)."""
     from mx_det import _lib
     v, loader, wv = request.param
+    import os
+    tune = os.environ.get("MX_CONV_TUNE")
+    os.environ["MX_CONV_TUNE"] = "0"  # exactly the forced variants, not the per-shape tuner's picks
     old = _lib.load().mx_conv_get_variant()
     oldw = _lib.load().mx_conv_get_wgrad_variant()
     _lib.call("mx_conv_set_variant", v)
     _lib.call("mx_conv_set_loader", loader)
     _lib.call("mx_conv_set_wgrad_variant", wv)
     yield v
+    if tune is None:
+        os.environ.pop("MX_CONV_TUNE", None)
+    else:
+        os.environ["MX_CONV_TUNE"] = tune
     _lib.call("mx_conv_set_variant", old)
     _lib.call("mx_conv_set_loader", 1)
     _lib.call("mx_conv_set_wgrad_variant", oldw)
@@ -381,9 +388,10 @@ def test_bn_backward_partials_from_dgrad_epilogue(dev, monkeypatch):
 @pytest.mark.parametrize("N,H,W,C,K,k,st,pd", [c for c in CASES if c[4] % 8 == 0])
 def test_conv_tuner_candidates(dev, monkeypatch, ci, N, H, W, C, K, k, st, pd):
     """Every launch configuration the per-shape tuner may pick (block tile x split cap for fwd /
-    dgrad, block target for wgrad) gives the torch results on every test shape."""
+    dgrad, kernel variant x block target for wgrad) gives the torch results on every test shape."""
     from mx_det import conv as mc
-    monkeypatch.setenv("MX_CONV_TUNE", "0")
+    monkeypatch.setenv("MX_CONV_TUNE", "1")
+    monkeypatch.setattr(mc, "_tune_cache", {})  # single candidates: the tuner must pick exactly them
     monkeypatch.setattr(mc, "_FD_CANDS", (mc._FD_CANDS[ci],))
     monkeypatch.setattr(mc, "_WG_CANDS", (mc._WG_CANDS[ci % len(mc._WG_CANDS)],))
     test_conv_fwd(dev, 7, N, H, W, C, K, k, st, pd)
