@@ -384,7 +384,7 @@ def test_bn_backward_partials_from_dgrad_epilogue(dev, monkeypatch):
             assert rel(res["1"][1][n], res["0"][1][n]) < 2e-3, n
 
 
-@pytest.mark.parametrize("ci", range(6))
+@pytest.mark.parametrize("ci", range(9))
 @pytest.mark.parametrize("N,H,W,C,K,k,st,pd", [c for c in CASES if c[4] % 8 == 0])
 def test_conv_tuner_candidates(dev, monkeypatch, ci, N, H, W, C, K, k, st, pd):
     """Every launch configuration the per-shape tuner may pick (block tile x split cap for fwd /
