@@ -157,6 +157,94 @@ def conv_roofline(model, opt, imgs, tg):
                                        for k, v in s.items()}}}
 
 
+def _roi_footprint_bytes(feats, rois, scales, k_min, C, esize):
+    """Distinct feature bytes MultiScaleRoIAlign must read: per level, the union over its RoIs of the
+    pixel rectangles the bilinear taps can touch ([floor(start), floor(end)+1] clipped; aligned=False,
+    torchvision roi_align_kernel.cpp), times C * element size. LevelMapper as torchvision poolers.py."""
+    import numpy as np
+    r = rois.detach().float().cpu().numpy()
+    b = r[:, 1:]
+    s = np.sqrt(np.maximum(b[:, 2] - b[:, 0], 0) * np.maximum(b[:, 3] - b[:, 1], 0))
+    lv = np.clip(np.floor(4 + np.log2(s / 224 + 1e-30) + 1e-6), k_min, k_min + len(feats) - 1).astype(int) - k_min
+    total = 0
+    for l, f in enumerate(feats):
+        H, W = f.shape[1], f.shape[2]
+        m = np.zeros((H, W), bool)
+        for x1, y1, x2, y2 in b[lv == l] * scales[l]:
+            ys, ye = max(int(np.floor(y1)), 0), min(int(np.floor(max(y2, y1 + 1))) + 1, H - 1)
+            xs, xe = max(int(np.floor(x1)), 0), min(int(np.floor(max(x2, x1 + 1))) + 1, W - 1)
+            m[ys:ye + 1, xs:xe + 1] = True
+        total += int(m.sum()) * C * esize
+    return total
+
+
+def hbm_ops_roofline(model, opt, imgs, tg, reps=20):
+    """RoIAlign forward and the proposal NMS on the inputs of a real train step, timed with HIP events
+    on their launch stream (torch's current stream), against the 8 TB/s HBM peak. Algorithmic bytes:
+    RoIAlign = output K*7*7*C + distinct feature footprint (_roi_footprint_bytes); NMS = boxes (16 B),
+    score (4), level (8), image (4) read + kept index (8) written per box (its masks stay in L2/LDS)."""
+    from mx_det import ops
+    from mx_det.backend import HipBackend
+    cap = {}
+    o_ra, o_nms = HipBackend.multiscale_roi_align, HipBackend.proposal_nms
+
+    def ra(self, feats, rois, scales, k_min, output_size=(7, 7), sampling_ratio=2):
+        cap["ra"] = ([f.detach() for f in feats], rois.detach().clone(), list(scales), k_min)
+        return o_ra(self, feats, rois, scales, k_min, output_size, sampling_ratio)
+
+    def pn(self, boxes, scores, lvl, group, G, L, thr, max_seg):
+        cap["nms"] = (boxes.detach().clone(), scores.detach().clone(), lvl.clone(), group.clone(), G, L, thr, max_seg)
+        return o_nms(self, boxes, scores, lvl, group, G, L, thr, max_seg)
+
+    HipBackend.multiscale_roi_align, HipBackend.proposal_nms = ra, pn
+    graphs = os.environ.get("MX_GRAPHS")
+    os.environ["MX_GRAPHS"] = "0"  # eager: the RoI head graph would replay past the hook
+    try:
+        train_step(model, opt, imgs, tg)
+    finally:
+        HipBackend.multiscale_roi_align, HipBackend.proposal_nms = o_ra, o_nms
+        if graphs is None:
+            del os.environ["MX_GRAPHS"]
+        else:
+            os.environ["MX_GRAPHS"] = graphs
+    torch.cuda.synchronize()
+
+    def timed(fn):
+        fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps * 1e3  # us
+
+    res = {}
+    if "ra" in cap:
+        feats, rois, scales, k_min = cap["ra"]
+        K, C, es = rois.shape[0], feats[0].shape[3], feats[0].element_size()
+        with torch.no_grad():
+            us = timed(lambda: ops.multiscale_roi_align(feats, rois, scales, k_min))
+        byts = K * 49 * C * es + _roi_footprint_bytes(feats, rois, scales, k_min, C, es)
+        gbs = byts / (us * 1e-6) / 1e9
+        res["roi_align_fwd"] = {"kernel": "roi_align_fwd_v8_kernel", "rois": K, "channels": C,
+                                "dtype": str(feats[0].dtype).replace("torch.", ""), "avg_launch_us": round(us, 2),
+                                "algorithmic_mb": round(byts / 1e6, 2), "achieved": round(gbs, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    if "nms" in cap:
+        boxes, scores, lvl, group, G, L, thr, max_seg = cap["nms"]
+        n = boxes.shape[0]
+        us = timed(lambda: ops.batched_nms_grouped(boxes, scores, lvl, group, G, L, thr, max_seg))
+        byts = n * (16 + 4 + 8 + 4 + 8)
+        gbs = byts / (us * 1e-6) / 1e9
+        res["proposal_nms"] = {"kernel": "mx_batched_nms_grouped (mask + scan)", "boxes": n, "images": G,
+                               "avg_call_us": round(us, 2), "algorithmic_mb": round(byts / 1e6, 3),
+                               "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(gbs / HBM_PEAK_GBS, 5), "bound": "latency (dependent scan)"}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -239,6 +327,7 @@ def main():
     }
     if rank == 0 and not args.no_roofline:
         rec["roofline"] = conv_roofline(ddp, opt, imgs[0:2], tg[0:2])
+        rec["hbm_ops"] = hbm_ops_roofline(ddp, opt, imgs[0:2], tg[0:2])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(model)
     if rank == 0:
