@@ -76,6 +76,14 @@ size_t mx_nms_grouped_workspace(int64_t n, int64_t G, int64_t max_seg);
 int mx_batched_nms_grouped(const float* boxes, const float* scores, const int64_t* lvl, const int32_t* group,
                            int64_t n, int64_t G, int64_t L, int64_t max_seg, double iou_threshold, int64_t* keep,
                            int64_t* num_keep, void* ws, size_t ws_bytes, mx_stream_t stream);
+/* RegionProposalNetwork._get_top_n_idx (torchvision rpn.py:221-233, reached from
+ * train_frcnn_baseline.py:171): for each image row of scores [N, row_stride] and each level l
+ * (columns level_off[l] .. +level_n[l]), the indices of the min(k, level_n[l]) largest scores,
+ * value descending (ties: index ascending; the set at a tied threshold takes the lowest indices),
+ * plus level_off[l]; levels concatenated: out_idx [N, sum_l min(k, level_n[l])] int64.
+ * 1 <= nlev <= 8, min(k, level_n[l]) <= 4096. */
+int mx_level_topk(const float* scores, int64_t N, int64_t row_stride, int nlev, const int64_t* level_off,
+                  const int64_t* level_n, int64_t k, int64_t* out_idx, mx_stream_t stream);
 size_t mx_nms_workspace(int64_t n, int64_t max_seg);
 int mx_batched_nms(const float* boxes, const float* scores, const int64_t* idxs, const int32_t* group, int64_t n,
                    int64_t max_seg, double iou_threshold, int mode, int64_t* keep, int64_t* num_keep, void* ws,

@@ -132,6 +132,16 @@ class CpuBackend:
             out.append(sel[k])
         return torch.from_numpy(np.concatenate(out) if out else np.zeros(0, np.int64))
 
+    def level_topk(self, scores, num_per_level, k):
+        """RegionProposalNetwork._get_top_n_idx (torchvision rpn.py): per level topk(min(k, n)) on the
+        CPU, level offset added, levels concatenated."""
+        tops, off = [], 0
+        for n in num_per_level:
+            _, ti = scores[:, off:off + n].topk(min(k, n), dim=1)
+            tops.append(ti + off)
+            off += n
+        return torch.cat(tops, 1)
+
     def proposal_nms(self, boxes, scores, lvl, group, G, L, thr, max_seg):
         """Per image (group g < G), torchvision's batched_nms with its CPU dispatch rule; output padded
         to n with num_keep as a 1-element tensor (the HIP entry's contract)."""

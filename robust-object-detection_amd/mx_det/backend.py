@@ -130,6 +130,9 @@ class HipBackend:
     def rpn_loss(self, objectness, deltas, labels, targets, pos, neg, beta):
         return ops.rpn_loss(objectness, deltas, labels, targets, pos, neg, beta)
 
+    def level_topk(self, scores, num_per_level, k):
+        return ops.level_topk(scores, num_per_level, k)
+
     def proposal_nms(self, boxes, scores, lvl, group, G, L, thr, max_seg):
         return ops.batched_nms_grouped(boxes, scores, lvl, group, G, L, thr, max_seg)
 

@@ -277,12 +277,7 @@ class RegionProposalNetwork(nn.Module):
         dev = proposals.device
         ob = objectness.detach()
         pre = self.pre_nms_top_n()
-        tops, off = [], 0
-        for n in num_per_level:
-            _, ti = ob[:, off:off + n].topk(min(pre, n), dim=1)
-            tops.append(ti + off)
-            off += n
-        top = torch.cat(tops, 1)
+        top = be.level_topk(ob, num_per_level, pre)  # [N, sum_l min(pre, n_l)], level offsets added
         ckey = ("lvl", tuple(num_per_level), pre, N, dev)
         cached = self._hw.get(ckey)
         if cached is None:  # level id per top-k slot and image index column: shape constants

@@ -145,6 +145,26 @@ def batched_nms_grouped(boxes, scores, lvl, group, G, L, iou_threshold, max_seg)
     return keep, nk
 
 
+def level_topk(scores, num_per_level, k):
+    """RegionProposalNetwork._get_top_n_idx (torchvision rpn.py): per image row of scores [N, A] and
+    per level, the indices of the min(k, n_l) largest scores (value descending, ties by index) plus
+    the level offset, levels concatenated -> [N, sum_l min(k, n_l)] int64 (mx_level_topk; one launch)."""
+    _dev(scores)
+    _check(scores.dim() == 2, f"scores should be [N, A], got {tuple(scores.shape)}")
+    s = scores.float().contiguous()
+    N, A = s.shape
+    L = len(num_per_level)
+    offs = [0]
+    for n in num_per_level[:-1]:
+        offs.append(offs[-1] + int(n))
+    _check(offs[-1] + int(num_per_level[-1]) <= A, "level_topk: levels exceed the row")
+    tot = sum(min(int(k), int(n)) for n in num_per_level)
+    out = torch.empty((N, tot), dtype=torch.int64, device=s.device)
+    call("mx_level_topk", _p(s), N, A, L, (ctypes.c_int64 * L)(*offs),
+         (ctypes.c_int64 * L)(*[int(n) for n in num_per_level]), int(k), _p(out), _stream())
+    return out
+
+
 def nms(boxes, scores, iou_threshold):
     """torchvision.ops.nms: kept indices sorted by decreasing score."""
     return batched_nms(boxes, scores, None, iou_threshold)

@@ -392,3 +392,53 @@ def test_roi_loss_fused_matches_torch(dev):
     torch.testing.assert_close(lc, rc, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(lb, rb, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(go, o.grad, rtol=1e-4, atol=1e-7)
+
+
+def _level_topk_np(scores, num_per_level, k):
+    """_get_top_n_idx by definition: per level the min(k, n) largest, value descending, ties by
+    index ascending (the set at a tied threshold takes the lowest indices), + level offset."""
+    out, off = [], 0
+    for n in num_per_level:
+        seg = scores[:, off:off + n]
+        rows = []
+        for r in seg:
+            o = np.lexsort((np.arange(n), -r.astype(np.float64)))[:min(k, n)]
+            rows.append(o + off)
+        out.append(np.stack(rows) if rows else np.zeros((scores.shape[0], 0), np.int64))
+        off += n
+    return np.concatenate(out, 1)
+
+
+@pytest.mark.parametrize("case", ["train", "ties", "edges"])
+def test_level_topk(dev, case):
+    """mx_level_topk == the per-level topk of RegionProposalNetwork._get_top_n_idx: exact indices vs
+    the definition (value desc, index asc) and exact values vs torch.topk on the CPU."""
+    from mx_det import ops
+    rng = np.random.default_rng(21)
+    if case == "train":  # bs=2 at 1344x800: P2..P6 anchors per level, pre_nms_top_n=2000
+        levels, k = [201600, 50400, 12600, 3150, 819], 2000
+        s = rng.standard_normal((2, sum(levels))).astype(np.float32)
+    elif case == "ties":  # heavy ties at every threshold (quantised logits), eval k=1000
+        levels, k = [40000, 10000, 2500, 700], 1000
+        s = (np.round(rng.standard_normal((3, sum(levels))) * 4) / 4).astype(np.float32)
+        s[1, :] = 0.5  # a row of one value: every level is one tie
+        s[2, ::7] = -0.0  # -0.0 and +0.0 compare equal: ties
+    else:  # tiny / empty levels, k=1, infinities, k > n
+        levels, k = [5, 0, 3000, 1, 64], 1
+        s = rng.standard_normal((2, sum(levels))).astype(np.float32)
+        s[0, 10:20] = np.inf
+        s[1, 5:3005] = -np.inf
+        s[1, 7] = -3.0
+    ref = _level_topk_np(s, levels, k)
+    st = torch.from_numpy(s)
+    got = ops.level_topk(st.to(dev), levels, k).cpu().numpy()
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref)
+    tv, off = [], 0
+    for n in levels:
+        tv.append(st[:, off:off + n].topk(min(k, n), dim=1).values)
+        off += n
+    assert torch.equal(torch.gather(st, 1, torch.from_numpy(got)), torch.cat(tv, 1))
+    if case == "edges":
+        got2 = ops.level_topk(st.to(dev), levels, 5000).cpu().numpy()  # k >= every n: full sorts
+        assert np.array_equal(got2, _level_topk_np(s, levels, 5000))
