@@ -3,19 +3,19 @@
 // torchvision 0.20.1 rpn.py _get_top_n_idx: for every feature level, ob[:, off:off+n].topk(min(pre, n))
 // and the level offset added; the levels' index lists are concatenated. Here one launch covers every
 // (level, image) pair: one 1024-thread workgroup each (grid = levels x images). Per workgroup:
-//   1. radix select of the k-th largest value on order-preserving u32 keys, four 8-bit digit passes
-//      (MSB first) with an LDS histogram; the first pass (sign + exponent bits, which cluster) counts
-//      with wave-aggregated atomics (one LDS atomic per distinct digit per wave);
+//   1. radix select of the k-th largest value on order-preserving u32 keys, three digit passes of
+//      11/11/10 bits (MSB first) into LDS histograms (4 copies by wave group, summed by the scan: the
+//      first digit -- sign, exponent, 2 mantissa bits -- clusters); 16 loads in flight per thread;
 //   2. the k winners -- every key above the threshold T, then the keys equal to T in index order
 //      (torch's gatherTopK tie rule) -- are gathered into LDS as (~key << 32 | index);
 //   3. an LDS bitonic sort orders them by value descending, index ascending (sorted=True), and the
 //      indices + level offset are written to out[image, level slot].
-// Reads a level's scores 5 times (4 select passes + gather), the later passes from L2.
+// Reads a level's scores 4 times (3 select passes + gather), the later passes from L2.
 #include "mx_common.h"
 
 namespace mx {
 
-static constexpr int TK_THREADS = 1024, TK_MAXK = 4096, TK_MAXL = 8;
+static constexpr int TK_THREADS = 1024, TK_MAXK = 4096, TK_MAXL = 8, TK_UNROLL = 16, TK_HCOPIES = 4, TK_BINS = 2048;
 
 struct TopkLv {
   int64_t off[TK_MAXL], n[TK_MAXL], oofs[TK_MAXL];
@@ -46,7 +46,7 @@ __device__ __forceinline__ int wave_append(bool take, uint32_t* ctr) {
 
 __global__ void __launch_bounds__(TK_THREADS) level_topk_kernel(const float* __restrict__ sc, int64_t rs, TopkLv P,
                                                                 int64_t* __restrict__ out) {
-  __shared__ uint32_t hist[256];
+  __shared__ uint32_t hist[TK_HCOPIES * TK_BINS];  // per-wave-group copies: fewer same-address atomics
   __shared__ uint64_t keys[TK_MAXK];
   __shared__ uint32_t s_digit, s_above, s_eq, s_cnt;
   __shared__ uint32_t wsum[TK_THREADS / 64];
@@ -57,67 +57,69 @@ __global__ void __launch_bounds__(TK_THREADS) level_topk_kernel(const float* __r
   int64_t* o = out + img * P.out_stride + P.oofs[l];
   if (k <= 0) return;
 
-  // 1. radix select
+  // 1. radix select: digits of 11, 11 and 10 bits, most significant first
   uint32_t prefix = 0, pmask = 0;
   uint32_t krem = (uint32_t)k;  // winners still to place at or below the current prefix
   uint32_t ceq = 0;
-  for (int pass = 0; pass < 4; ++pass) {
-    const int shift = 24 - 8 * pass;
-    if (tid < 256) hist[tid] = 0;
+  for (int pass = 0; pass < 3; ++pass) {
+    const int nbits = pass < 2 ? 11 : 10, shift = 21 - 11 * pass < 0 ? 0 : 21 - 11 * pass;
+    const int NB = 1 << nbits, per = NB / 64;
+    const uint32_t dmask = (uint32_t)NB - 1;
+    for (int i = tid; i < TK_HCOPIES * TK_BINS; i += TK_THREADS) hist[i] = 0;
     __syncthreads();
-    for (int64_t i0 = 0; i0 < n; i0 += TK_THREADS) {
-      const int64_t i = i0 + tid;
-      const bool in = i < n;
-      const uint32_t u = in ? ord_f32(x[i]) : 0u;
-      const bool m = in && (u & pmask) == prefix;
-      const uint32_t d = (u >> shift) & 255u;
-      if (pass == 0) {
-        bool pending = m;
-        for (;;) {
-          const uint64_t pm = __ballot(pending);
-          if (!pm) break;
-          const int leader = __ffsll((unsigned long long)pm) - 1;
-          const uint32_t dl = (uint32_t)__shfl((int)d, leader);
-          const uint64_t same = __ballot(pending && d == dl);
-          if (lane == leader) atomicAdd(&hist[dl], (uint32_t)__popcll(same));
-          if (pending && d == dl) pending = false;
-        }
-      } else if (m) {
-        atomicAdd(&hist[d], 1u);
+    uint32_t* hh = hist + (wid & (TK_HCOPIES - 1)) * TK_BINS;
+    for (int64_t i0 = 0; i0 < n; i0 += TK_THREADS * TK_UNROLL) {
+      // TK_UNROLL independent loads in flight per thread before the first is consumed
+      float xv[TK_UNROLL];
+#pragma unroll
+      for (int r = 0; r < TK_UNROLL; ++r) {
+        const int64_t i = i0 + r * TK_THREADS + tid;
+        xv[r] = i < n ? x[i] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < TK_UNROLL; ++r) {
+        const bool in = i0 + r * TK_THREADS + tid < n;
+        const uint32_t u = ord_f32(xv[r]);
+        if (in && (u & pmask) == prefix) atomicAdd(&hh[(u >> shift) & dmask], 1u);
       }
     }
     __syncthreads();
     if (wid == 0) {
-      // lane j owns bins 255-4j .. 252-4j (descending); inclusive scan of the lane sums
-      uint32_t c[4], s = 0;
+      // lane j owns bins NB-1-per*j .. NB-per*(j+1) (descending); inclusive scan of the lane sums
+      uint32_t sum = 0;
+      for (int q = 0; q < per; ++q) {
+        const int bin = NB - 1 - per * lane - q;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) { c[q] = hist[255 - 4 * lane - q]; s += c[q]; }
-      uint32_t inc = s;
+        for (int h = 0; h < TK_HCOPIES; ++h) sum += hist[h * TK_BINS + bin];
+      }
+      uint32_t inc = sum;
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
         const uint32_t v = (uint32_t)__shfl_up((int)inc, off);
         if (lane >= off) inc += v;
       }
-      const uint32_t exc = inc - s;
       const uint64_t hit = __ballot(inc >= krem);
       const int j = __ffsll((unsigned long long)hit) - 1;  // first lane crossing krem (exists: total >= krem)
       if (lane == j) {
-        uint32_t acc = exc;
+        uint32_t acc = inc - sum;
+        for (int q = 0; q < per; ++q) {
+          const int bin = NB - 1 - per * lane - q;
+          uint32_t c = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (acc + c[q] >= krem) {
-            s_digit = 255 - 4 * lane - q;
+          for (int h = 0; h < TK_HCOPIES; ++h) c += hist[h * TK_BINS + bin];
+          if (acc + c >= krem) {
+            s_digit = (uint32_t)bin;
             s_above = acc;
-            s_eq = c[q];
+            s_eq = c;
             break;
           }
-          acc += c[q];
+          acc += c;
         }
       }
     }
     __syncthreads();
     prefix |= s_digit << shift;
-    pmask |= 255u << shift;
+    pmask |= dmask << shift;
     krem -= s_above;
     ceq = s_eq;
     __syncthreads();
@@ -129,12 +131,21 @@ __global__ void __launch_bounds__(TK_THREADS) level_topk_kernel(const float* __r
   // 2. gather the winners
   if (tid == 0) s_cnt = 0;
   __syncthreads();
-  for (int64_t i0 = 0; i0 < n; i0 += TK_THREADS) {
-    const int64_t i = i0 + tid;
-    const uint32_t u = i < n ? ord_f32(x[i]) : 0u;
-    const bool take = i < n && (u > T || (take_all_eq && u == T));
-    const int pos = wave_append(take, &s_cnt);
-    if (take) keys[pos] = ((uint64_t)(~u) << 32) | (uint64_t)(uint32_t)i;
+  for (int64_t i0 = 0; i0 < n; i0 += TK_THREADS * TK_UNROLL) {
+    float xv[TK_UNROLL];
+#pragma unroll
+    for (int r = 0; r < TK_UNROLL; ++r) {
+      const int64_t i = i0 + r * TK_THREADS + tid;
+      xv[r] = i < n ? x[i] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < TK_UNROLL; ++r) {
+      const int64_t i = i0 + r * TK_THREADS + tid;
+      const uint32_t u = ord_f32(xv[r]);
+      const bool take = i < n && (u > T || (take_all_eq && u == T));
+      const int pos = wave_append(take, &s_cnt);
+      if (take) keys[pos] = ((uint64_t)(~u) << 32) | (uint64_t)(uint32_t)i;
+    }
   }
   if (!take_all_eq) {
     // ties at T: the first krem of them in index order, slots ngt.. (rare path)
