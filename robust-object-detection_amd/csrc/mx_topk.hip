@@ -6,16 +6,20 @@
 //   1. radix select of the k-th largest value on order-preserving u32 keys, three digit passes of
 //      11/11/10 bits (MSB first) into LDS histograms (4 copies by wave group, summed by the scan: the
 //      first digit -- sign, exponent, 2 mantissa bits -- clusters); 16 loads in flight per thread;
-//   2. the k winners -- every key above the threshold T, then the keys equal to T in index order
+//      After the first pass the elements whose first digit reaches the threshold digit (at most
+//      TK_CAND of them, else the passes stay on global memory) are compacted into LDS, and the
+//      remaining passes and the gather read only them;
+//   2. the k winners -- every key above the threshold T, then the keys equal to T by lowest index
 //      (torch's gatherTopK tie rule) -- are gathered into LDS as (~key << 32 | index);
 //   3. an LDS bitonic sort orders them by value descending, index ascending (sorted=True), and the
 //      indices + level offset are written to out[image, level slot].
-// Reads a level's scores 4 times (3 select passes + gather), the later passes from L2.
+// Reads a level's scores twice from global memory (first pass + compaction) in the common case.
 #include "mx_common.h"
 
 namespace mx {
 
-static constexpr int TK_THREADS = 1024, TK_MAXK = 4096, TK_MAXL = 8, TK_UNROLL = 16, TK_HCOPIES = 4, TK_BINS = 2048;
+static constexpr int TK_THREADS = 1024, TK_MAXK = 4096, TK_MAXL = 8, TK_UNROLL = 16, TK_HCOPIES = 4, TK_BINS = 2048,
+                     TK_CAND = 8192;
 
 struct TopkLv {
   int64_t off[TK_MAXL], n[TK_MAXL], oofs[TK_MAXL];
@@ -48,7 +52,8 @@ __global__ void __launch_bounds__(TK_THREADS) level_topk_kernel(const float* __r
                                                                 int64_t* __restrict__ out) {
   __shared__ uint32_t hist[TK_HCOPIES * TK_BINS];  // per-wave-group copies: fewer same-address atomics
   __shared__ uint64_t keys[TK_MAXK];
-  __shared__ uint32_t s_digit, s_above, s_eq, s_cnt;
+  __shared__ uint2 cand[TK_CAND];                  // (key, index) of the first pass's survivors
+  __shared__ uint32_t s_digit, s_above, s_eq, s_cnt, s_ncand;
   __shared__ uint32_t wsum[TK_THREADS / 64];
   const int l = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t n = P.n[l];
@@ -57,32 +62,49 @@ __global__ void __launch_bounds__(TK_THREADS) level_topk_kernel(const float* __r
   int64_t* o = out + img * P.out_stride + P.oofs[l];
   if (k <= 0) return;
 
+  // visits every element (valid flag, key, index) of the level -- from global memory (16 loads in
+  // flight per thread) or, once compacted, from the LDS candidate list; wave-uniform trip counts
+  bool use_lds = false;
+  uint32_t ncand = 0;
+  auto visit = [&](auto&& f) {
+    if (use_lds) {
+      for (uint32_t j0 = 0; j0 < ncand; j0 += TK_THREADS) {
+        const uint32_t j = j0 + tid;
+        const bool in = j < ncand;
+        const uint2 c = in ? cand[j] : make_uint2(0u, 0u);
+        f(in, c.x, (int64_t)c.y);
+      }
+    } else {
+      for (int64_t i0 = 0; i0 < n; i0 += TK_THREADS * TK_UNROLL) {
+        float xv[TK_UNROLL];
+#pragma unroll
+        for (int r = 0; r < TK_UNROLL; ++r) {
+          const int64_t i = i0 + r * TK_THREADS + tid;
+          xv[r] = i < n ? x[i] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < TK_UNROLL; ++r) {
+          const int64_t i = i0 + r * TK_THREADS + tid;
+          f(i < n, ord_f32(xv[r]), i);
+        }
+      }
+    }
+  };
+
   // 1. radix select: digits of 11, 11 and 10 bits, most significant first
   uint32_t prefix = 0, pmask = 0;
   uint32_t krem = (uint32_t)k;  // winners still to place at or below the current prefix
   uint32_t ceq = 0;
   for (int pass = 0; pass < 3; ++pass) {
-    const int nbits = pass < 2 ? 11 : 10, shift = 21 - 11 * pass < 0 ? 0 : 21 - 11 * pass;
+    const int nbits = pass < 2 ? 11 : 10, shift = pass < 2 ? 21 - 11 * pass : 0;
     const int NB = 1 << nbits, per = NB / 64;
     const uint32_t dmask = (uint32_t)NB - 1;
     for (int i = tid; i < TK_HCOPIES * TK_BINS; i += TK_THREADS) hist[i] = 0;
     __syncthreads();
     uint32_t* hh = hist + (wid & (TK_HCOPIES - 1)) * TK_BINS;
-    for (int64_t i0 = 0; i0 < n; i0 += TK_THREADS * TK_UNROLL) {
-      // TK_UNROLL independent loads in flight per thread before the first is consumed
-      float xv[TK_UNROLL];
-#pragma unroll
-      for (int r = 0; r < TK_UNROLL; ++r) {
-        const int64_t i = i0 + r * TK_THREADS + tid;
-        xv[r] = i < n ? x[i] : 0.f;
-      }
-#pragma unroll
-      for (int r = 0; r < TK_UNROLL; ++r) {
-        const bool in = i0 + r * TK_THREADS + tid < n;
-        const uint32_t u = ord_f32(xv[r]);
-        if (in && (u & pmask) == prefix) atomicAdd(&hh[(u >> shift) & dmask], 1u);
-      }
-    }
+    visit([&](bool in, uint32_t u, int64_t) {
+      if (in && (u & pmask) == prefix) atomicAdd(&hh[(u >> shift) & dmask], 1u);
+    });
     __syncthreads();
     if (wid == 0) {
       // lane j owns bins NB-1-per*j .. NB-per*(j+1) (descending); inclusive scan of the lane sums
@@ -123,32 +145,35 @@ __global__ void __launch_bounds__(TK_THREADS) level_topk_kernel(const float* __r
     krem -= s_above;
     ceq = s_eq;
     __syncthreads();
+    if (pass == 0 && (uint32_t)k - krem + ceq <= (uint32_t)TK_CAND) {
+      // every later winner has a first digit >= the threshold digit: keep just those (key >= prefix)
+      if (tid == 0) s_ncand = 0;
+      __syncthreads();
+      visit([&](bool in, uint32_t u, int64_t i) {
+        const bool take = in && u >= prefix;
+        const int pos = wave_append(take, &s_ncand);
+        if (take) cand[pos] = make_uint2(u, (uint32_t)i);
+      });
+      __syncthreads();
+      ncand = s_ncand;
+      use_lds = true;
+    }
   }
   const uint32_t T = prefix;
   const uint32_t ngt = (uint32_t)k - krem;  // keys strictly above T
-  const bool take_all_eq = ceq == krem;
+  // every key tied at T fits the sort buffer: take them all and let the (value, index) sort keep
+  // the lowest indices; otherwise place the first krem ties in index order (global, rare path)
+  const bool all_ties = ngt + ceq <= (uint32_t)TK_MAXK;
 
   // 2. gather the winners
   if (tid == 0) s_cnt = 0;
   __syncthreads();
-  for (int64_t i0 = 0; i0 < n; i0 += TK_THREADS * TK_UNROLL) {
-    float xv[TK_UNROLL];
-#pragma unroll
-    for (int r = 0; r < TK_UNROLL; ++r) {
-      const int64_t i = i0 + r * TK_THREADS + tid;
-      xv[r] = i < n ? x[i] : 0.f;
-    }
-#pragma unroll
-    for (int r = 0; r < TK_UNROLL; ++r) {
-      const int64_t i = i0 + r * TK_THREADS + tid;
-      const uint32_t u = ord_f32(xv[r]);
-      const bool take = i < n && (u > T || (take_all_eq && u == T));
-      const int pos = wave_append(take, &s_cnt);
-      if (take) keys[pos] = ((uint64_t)(~u) << 32) | (uint64_t)(uint32_t)i;
-    }
-  }
-  if (!take_all_eq) {
-    // ties at T: the first krem of them in index order, slots ngt.. (rare path)
+  visit([&](bool in, uint32_t u, int64_t i) {
+    const bool take = in && (u > T || (all_ties && u == T));
+    const int pos = wave_append(take, &s_cnt);
+    if (take) keys[pos] = ((uint64_t)(~u) << 32) | (uint64_t)(uint32_t)i;
+  });
+  if (!all_ties) {
     uint32_t taken = 0;
     for (int64_t i0 = 0; i0 < n && taken < krem; i0 += TK_THREADS) {
       const int64_t i = i0 + tid;
@@ -168,10 +193,11 @@ __global__ void __launch_bounds__(TK_THREADS) level_topk_kernel(const float* __r
       __syncthreads();
     }
   }
-  // 3. bitonic sort (ascending key = value descending, index ascending)
+  // 3. bitonic sort (ascending key = value descending, index ascending); the first k are the output
+  const int nsort = all_ties ? (int)(ngt + ceq) : k;
   int P2 = 1;
-  while (P2 < k) P2 <<= 1;
-  for (int i = k + tid; i < P2; i += TK_THREADS) keys[i] = ~0ull;
+  while (P2 < nsort) P2 <<= 1;
+  for (int i = nsort + tid; i < P2; i += TK_THREADS) keys[i] = ~0ull;
   for (int size = 2; size <= P2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       __syncthreads();
