@@ -29,6 +29,13 @@ def main():
         torch.cuda.synchronize()
     print(prof.key_averages().table(sort_by="count", row_limit=40))
     print(prof.key_averages(group_by_stack_n=4).table(sort_by="count", row_limit=25))
+    # where the device copies come from (aten::copy_ / to / contiguous call sites, 6 frames)
+    for ev in prof.key_averages(group_by_stack_n=6):
+        if ev.key in ("aten::copy_", "aten::clone", "aten::_to_copy", "aten::cat", "aten::index", "aten::nonzero",
+                      "aten::item", "aten::_local_scalar_dense"):
+            print(f"{ev.key} x{ev.count}")
+            for fr in ev.stack[:6]:
+                print("    ", fr)
 
 
 if __name__ == "__main__":
