@@ -231,16 +231,22 @@ __global__ void __launch_bounds__(256) nms_scan_lds_kernel(const uint64_t* __res
       if (fits(blk + 1)) fetch(blk + 1);
       if (tid < 64) {
         const uint64_t diag = lane < cnt ? rows[lane * Wm + blk] : 0ull;
-        uint64_t cur = removed[blk];
+        const uint64_t rm = removed[blk];
+        // wave-uniform scalar walk over the not-yet-suppressed boxes only (s_ff1 jumps to the next
+        // survivor; suppressed ones cost nothing): same greedy result as testing all cnt bits
+        const uint64_t valid = cnt >= 64 ? ~0ull : ((1ull << cnt) - 1);
+        uint64_t cur = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(rm >> 32)) << 32) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)rm);
         uint64_t kept = 0;
         const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
-        for (int t = 0; t < cnt; ++t) {
-          if (!((cur >> t) & 1ull)) {
-            kept |= 1ull << t;
-            const uint64_t row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, t) << 32) |
-                                 (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, t);
-            cur |= row;
-          }
+        uint64_t avail = ~cur & valid;
+        while (avail) {
+          const int t = __builtin_ctzll(avail);
+          kept |= 1ull << t;
+          const uint64_t row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, t) << 32) |
+                               (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, t);
+          cur |= row;
+          avail = ~cur & valid & ~((2ull << t) - 1ull);  // bits above t (t = 63: none)
         }
         if (lane < cnt && ((kept >> lane) & 1ull)) flags[svals[rbase + lane]] = 1;
         if (lane == 0) kept_s = kept;
