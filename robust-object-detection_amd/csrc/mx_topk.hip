@@ -5,7 +5,7 @@
 // (level, image) pair: one 1024-thread workgroup each (grid = levels x images). Per workgroup:
 //   1. radix select of the k-th largest value on order-preserving u32 keys, three digit passes of
 //      11/11/10 bits (MSB first) into LDS histograms (4 copies by wave group, summed by the scan: the
-//      first digit -- sign, exponent, 2 mantissa bits -- clusters); 16 loads in flight per thread;
+//      first digit -- sign, exponent, 2 mantissa bits -- clusters); 8 float4 loads in flight per thread;
 //      After the first pass the elements whose first digit reaches the threshold digit (at most
 //      TK_CAND of them, else the passes stay on global memory) are compacted into LDS, and the
 //      remaining passes and the gather read only them;
@@ -18,7 +18,7 @@
 
 namespace mx {
 
-static constexpr int TK_THREADS = 1024, TK_MAXK = 4096, TK_MAXL = 8, TK_UNROLL = 16, TK_HCOPIES = 4, TK_BINS = 2048,
+static constexpr int TK_THREADS = 1024, TK_MAXK = 4096, TK_MAXL = 8, TK_UNROLL4 = 8, TK_HCOPIES = 4, TK_BINS = 2048,
                      TK_CAND = 8192;
 
 struct TopkLv {
@@ -62,8 +62,8 @@ __global__ void __launch_bounds__(TK_THREADS) level_topk_kernel(const float* __r
   int64_t* o = out + img * P.out_stride + P.oofs[l];
   if (k <= 0) return;
 
-  // visits every element (valid flag, key, index) of the level -- from global memory (16 loads in
-  // flight per thread) or, once compacted, from the LDS candidate list; wave-uniform trip counts
+  // visits every element (valid flag, key, index) of the level -- from global memory (8 float4
+  // loads in flight per thread) or, once compacted, from the LDS candidate list; wave-uniform trip counts
   bool use_lds = false;
   uint32_t ncand = 0;
   auto visit = [&](auto&& f) {
@@ -75,19 +75,32 @@ __global__ void __launch_bounds__(TK_THREADS) level_topk_kernel(const float* __r
         f(in, c.x, (int64_t)c.y);
       }
     } else {
-      for (int64_t i0 = 0; i0 < n; i0 += TK_THREADS * TK_UNROLL) {
-        float xv[TK_UNROLL];
+      // scalar head up to the first 16-B boundary, float4 body (TK_UNROLL4 loads in flight per
+      // thread), scalar tail
+      const int64_t h = min<int64_t>((int64_t)((16 - ((uintptr_t)x & 15)) & 15) >> 2, n);
+      f(tid < h, tid < h ? ord_f32(x[tid]) : 0u, (int64_t)tid);
+      const int64_t nb4 = (n - h) >> 2;
+      const float4* x4 = (const float4*)(x + h);
+      for (int64_t q0 = 0; q0 < nb4; q0 += TK_THREADS * TK_UNROLL4) {
+        float4 xv[TK_UNROLL4];
 #pragma unroll
-        for (int r = 0; r < TK_UNROLL; ++r) {
-          const int64_t i = i0 + r * TK_THREADS + tid;
-          xv[r] = i < n ? x[i] : 0.f;
+        for (int r = 0; r < TK_UNROLL4; ++r) {
+          const int64_t q = q0 + r * TK_THREADS + tid;
+          xv[r] = q < nb4 ? x4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
-        for (int r = 0; r < TK_UNROLL; ++r) {
-          const int64_t i = i0 + r * TK_THREADS + tid;
-          f(i < n, ord_f32(xv[r]), i);
+        for (int r = 0; r < TK_UNROLL4; ++r) {
+          const int64_t q = q0 + r * TK_THREADS + tid;
+          const bool in = q < nb4;
+          const int64_t i = h + 4 * q;
+          f(in, ord_f32(xv[r].x), i);
+          f(in, ord_f32(xv[r].y), i + 1);
+          f(in, ord_f32(xv[r].z), i + 2);
+          f(in, ord_f32(xv[r].w), i + 3);
         }
       }
+      const int64_t t0 = h + 4 * nb4;
+      f(t0 + tid < n, t0 + tid < n ? ord_f32(x[t0 + tid]) : 0u, t0 + tid);
     }
   };
 
