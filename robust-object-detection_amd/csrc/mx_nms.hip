@@ -372,26 +372,25 @@ __global__ void nms_group_final_keys_kernel(const float* __restrict__ scores, co
                                             uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint64_t k = ~0ull;
+  // live: (group, score desc); removed / dead: the sentinel (G, max), above every live key, so the
+  // sort only needs the low 32 + bit_length(G) bits
+  uint64_t k = ((uint64_t)G << 32) | 0xffffffffull;
   const int g = group[i];
-  if (flags[i] && g >= 0 && g < G) {
-    k = ((uint64_t)ord_i32(g) << 32) | (uint64_t)(~ord_f32(scores[i]));
-    if (k == ~0ull) k = ~0ull - 1;
-  }
+  if (flags[i] && g >= 0 && g < G) k = ((uint64_t)g << 32) | (uint64_t)(~ord_f32(scores[i]));
   keys[i] = k;
   vals[i] = (int32_t)i;
 }
 
 // keep = survivors by (group, score desc, index); num_keep = number of non-sentinel keys
 __global__ void nms_group_out_kernel(const uint64_t* __restrict__ skeys, const int32_t* __restrict__ vals, int64_t n,
-                                     const int32_t* __restrict__ nk32, int64_t* __restrict__ keep,
+                                     uint64_t dead, const int32_t* __restrict__ nk32, int64_t* __restrict__ keep,
                                      int64_t* __restrict__ num_keep) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   keep[i] = vals[i];
-  const bool live = skeys[i] != ~0ull;
+  const bool live = skeys[i] != dead;
   // -1: a segment exceeded max_seg (the scan's overflow flag)
-  if (live && (i == n - 1 || skeys[i + 1] == ~0ull)) *num_keep = *nk32 < 0 ? -1 : i + 1;
+  if (live && (i == n - 1 || skeys[i + 1] == dead)) *num_keep = *nk32 < 0 ? -1 : i + 1;
   if (i == 0 && !live) *num_keep = *nk32 < 0 ? -1 : 0;
 }
 
@@ -538,8 +537,10 @@ extern "C" int mx_batched_nms_grouped(const float* boxes, const float* scores, c
   nms_group_keys_kernel<<<nb, T, 0, s>>>((const float4*)boxes, scores, lvl, group, n, (int)G, (int)L, w.gcnt, w.gmax,
                                          w.k0, w.v0, w.obox, w.flags, w.nk);
   MX_LAUNCH_CHECK();
+  // segment keys: hi < G*(L+1) + n, so only the low 32 + bit_length of that bound are sorted
+  const int end1 = std::min(64, 32 + (64 - __builtin_clzll((unsigned long long)(G * (L + 1) + n))));
   size_t cb = w.cub_bytes;
-  MX_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.k0, w.k1, w.v0, w.v1, (int)n, 0, 64, s));
+  MX_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.k0, w.k1, w.v0, w.v1, (int)n, 0, end1, s));
   nms_gather_kernel<<<nb, T, 0, s>>>(w.k1, w.v1, w.obox, n, w.sbox, w.sarea, w.head);
   MX_LAUNCH_CHECK();
   cb = w.cub_bytes;
@@ -558,9 +559,11 @@ extern "C" int mx_batched_nms_grouped(const float* boxes, const float* scores, c
   MX_LAUNCH_CHECK();
   nms_group_final_keys_kernel<<<nb, T, 0, s>>>(scores, group, w.flags, n, (int)G, w.k0, w.v0);
   MX_LAUNCH_CHECK();
+  const uint64_t dead = ((uint64_t)G << 32) | 0xffffffffull;
+  const int end2 = 32 + (64 - __builtin_clzll((unsigned long long)G));
   cb = w.cub_bytes;
-  MX_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.k0, w.k1, w.v0, w.v1, (int)n, 0, 64, s));
-  nms_group_out_kernel<<<nb, T, 0, s>>>(w.k1, w.v1, n, w.nk, keep, num_keep);
+  MX_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.k0, w.k1, w.v0, w.v1, (int)n, 0, end2, s));
+  nms_group_out_kernel<<<nb, T, 0, s>>>(w.k1, w.v1, n, dead, w.nk, keep, num_keep);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }
