@@ -232,20 +232,27 @@ class BalancedPositiveNegativeSampler:
     def __init__(self, batch_size_per_image, positive_fraction):
         self.batch, self.frac = batch_size_per_image, positive_fraction
 
-    def __call__(self, lab):
+    def __call__(self, lab, be=None):
+        """be: a backend with level_topk draws the k smallest keys with it (used for the RoI sampler's
+        ~2k-wide rows; the RPN's 268k-anchor rows stay on torch.topk, which splits a row over many
+        workgroups)."""
         L = lab.shape[1]
         pos, neg = lab >= 1, lab == 0
         P = int(self.batch * self.frac)
         num_pos = pos.sum(1).clamp(max=P)
         num_neg = torch.minimum(neg.sum(1), self.batch - num_pos)
         r = torch.rand(lab.shape, device=lab.device)
-        return self._pick(pos, r, min(P, L), num_pos), self._pick(neg, r, min(self.batch, L), num_neg)
+        return self._pick(pos, r, min(P, L), num_pos, be), self._pick(neg, r, min(self.batch, L), num_neg, be)
 
     @staticmethod
-    def _pick(cand, r, k, num):
+    def _pick(cand, r, k, num, be=None):
         m = torch.zeros_like(cand)
         if k > 0:
-            _, idx = torch.where(cand, r, 2.0).topk(k, dim=1, largest=False)  # ascending keys
+            if be is not None and hasattr(be, "level_topk"):
+                # the k largest of -key = the k smallest keys, value order (one mx_level_topk launch)
+                idx = be.level_topk(torch.where(cand, -r, -2.0), [cand.shape[1]], k)
+            else:
+                _, idx = torch.where(cand, r, 2.0).topk(k, dim=1, largest=False)  # ascending keys
             m.scatter_(1, idx, torch.arange(k, device=cand.device)[None, :] < num[:, None])
         return m
 
@@ -516,7 +523,7 @@ class RoIHeads(nn.Module):
                 val_l.append(torch.cat([pvalid[i], gslot < gt.shape[0]]))
             lab_p = torch.where(torch.stack(val_l), torch.stack(lab_l), -1)
             tg_p = torch.stack(tg_l)
-            pos_m, neg_m = self.fg_bg_sampler(lab_p)
+            pos_m, neg_m = self.fg_bg_sampler(lab_p, be)
             sm = (pos_m | neg_m).flatten()
             idx = _compact(sm, int(sm.sum()))             # per image ascending, as torch.where per image
             cm = lab_p.shape[1]

@@ -442,3 +442,31 @@ def test_level_topk(dev, case):
     if case == "edges":
         got2 = ops.level_topk(st.to(dev), levels, 5000).cpu().numpy()  # k >= every n: full sorts
         assert np.array_equal(got2, _level_topk_np(s, levels, 5000))
+
+
+def test_sampler_draw_via_level_topk(dev):
+    """BalancedPositiveNegativeSampler with the HIP backend (RoI-head rows: the k smallest uniform
+    keys drawn with mx_level_topk): per image exactly min(#pos, 128) positives and min(#neg,
+    512 - pos) negatives, each a subset of its candidates; a fresh draw differs; rows with fewer
+    candidates than k (the non-candidate key ties) included."""
+    from mx_det.backend import HipBackend
+    from mx_det.frcnn import BalancedPositiveNegativeSampler
+    torch.manual_seed(3)
+    L = 2100
+    lab = torch.full((3, L), -1, dtype=torch.int64)
+    lab[0, torch.randperm(L)[:40]] = 1            # fewer positives than k=128
+    lab[0, torch.randperm(L)[:1500]] = 0
+    lab[1, :700] = 1
+    lab[1, 700:] = 0
+    lab[2, :100] = 0                              # fewer negatives than 512 - 0
+    lab = lab.to(dev)
+    s = BalancedPositiveNegativeSampler(512, 0.25)
+    be = HipBackend()
+    pm, nm = s(lab, be)
+    pos, neg = lab >= 1, lab == 0
+    npos = pos.sum(1).clamp(max=128)
+    nneg = torch.minimum(neg.sum(1), 512 - npos)
+    assert torch.equal(pm.sum(1), npos) and torch.equal(nm.sum(1), nneg)
+    assert not (pm & ~pos).any() and not (nm & ~neg).any()
+    pm2, _ = s(lab, be)
+    assert not torch.equal(pm2[1], pm[1])  # 128 of 700 positives redrawn
