@@ -7,6 +7,12 @@ step + loss.item()), on synthetic VisDrone-shaped uint8 images resident in HBM (
 random-init weights of the same architecture, trainable_backbone_layers=3 as in the reference run.
 `--augment` adds the on-GPU 50% noise/blur/low-res corruption of configs[2].
 
+Arithmetic: the headline runs the reference's precision -- an fp32 model (train_frcnn_baseline.py:139-176,
+no autocast; TF32 convs on its Ampere GPU): HipBackend("f32"), f32 activations / gradients / BN /
+RoIAlign, every conv product as the bf16x3 split on MFMA (~2^-16 relative, finer than TF32's 2^-11;
+tests/test_gpu_x3.py). The bf16 mode (bf16 activations and operands) is timed after it and reported
+inside the same line under "bf16_variant" (--precision f32|bf16 picks one mode only).
+
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
@@ -29,15 +35,20 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+# f32-equivalent peak of the bf16x3 conv path: three bf16 MFMAs per f32 product
+X3_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 3
 HBM_PEAK_GBS = 8000.0
 N_IMAGES_PER_RANK = 8
 
 
-def build_model(device, trainable=3, backend=None):
+def build_model(device, trainable=3, backend=None, precision=None):
     from mx_det import frcnn
     model = frcnn.fasterrcnn_resnet50_fpn_v2(weights=None)
     model.roi_heads.box_predictor = frcnn.FastRCNNPredictor(model.roi_heads.box_predictor.cls_score.in_features, 7)
     frcnn.set_trainable_layers(model.backbone.body, trainable)
+    if backend is None and precision is not None:
+        from mx_det.backend import HipBackend
+        backend = HipBackend(precision)
     if backend is not None:
         model.set_backend(backend)
     return model.to(device)
@@ -90,10 +101,14 @@ def cpu_baseline(gpu_model, seconds_hint=30.0):
             "sample": f"{n} train step(s) x 2 images 1333x800 on {cores} CPU threads ({dt:.1f} s)"}
 
 
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_traffic.json")
+TRAFFIC_FILE = os.environ.get("MX_TRAFFIC_FILE", os.path.join(ROOT, "profiles", "r02_traffic.json"))
 # kernels of one op: outer list = the op's sequential kernels (summed), inner = alternative template
 # instances of one kernel (launch-weighted mean)
-KIND_KERNELS = {"wgrad": [["mx::conv_wgrad_buf_kernel"], ["mx::wgrad_reduce_kernel"]],
+KIND_KERNELS = {"x3_wgrad": [["mx::conv_wgrad_x3_kernel"], ["mx::wgrad_reduce_kernel"]],
+                "x3_fwd128": [["mx::conv_x3_kernel<128, 0", "mx::conv_x3_kernel<64, 0"]],
+                "x3_fwd64": [["mx::conv_x3_kernel<64, 0"]],
+                "x3_dgrad": [["mx::conv_x3_kernel<128, 1", "mx::conv_x3_kernel<64, 1"]],
+                "wgrad": [["mx::conv_wgrad_buf_kernel"], ["mx::wgrad_reduce_kernel"]],
                 "fwd128": [["mx::conv_igemm_buf_kernel<128, 0", "mx::conv_igemm_buf_kernel<256, 0"]],
                 "dgrad": [["mx::conv_igemm_buf_kernel<128, 1", "mx::conv_igemm_buf_kernel<256, 1",
                            "mx::conv_igemm_buf_kernel<64, 1"]],
@@ -119,9 +134,10 @@ def pmc_traffic(kind):
     return round(tot / 1e6, 2) if hit else None
 
 
-def conv_roofline(model, opt, imgs, tg):
+def conv_roofline(model, opt, imgs, tg, peak=X3_PEAK_TFLOPS):
     """Live HIP-event timing of every conv kernel launch in one train step; the dominant kernel kind
-    (largest total time) is reported against the bf16 MFMA peak with its algorithmic FLOPs."""
+    (largest total time) is reported with its algorithmic FLOPs (2 * M * N * K per conv, f32-equivalent
+    for the bf16x3 path) against the peak of the arithmetic it runs (bf16 dense / 3 for bf16x3)."""
     from mx_det import conv as mc
     t = mc.KernelTimer()
     mc.set_timer(t)
@@ -141,13 +157,17 @@ def conv_roofline(model, opt, imgs, tg):
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
     allf = sum(v["flops"] for v in s.values())
     allms = sum(v["ms"] for v in s.values())
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(dom),
-            "traffic_unit": "MB per launch (HBM, rocprofv3 PMC, profiles/r01_traffic.json)",
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom),
+            "traffic_unit": "MB per launch (HBM, rocprofv3 PMC, " + os.path.relpath(TRAFFIC_FILE, ROOT) + ")",
             "kernel": {"fwd128": "conv_igemm_buf_kernel<128|256,0,*> (+ conv_splitk_reduce_kernel)",
                        "fwd64": "conv_igemm_buf_kernel<64,0,*> (+ conv_splitk_reduce_kernel)",
                        "dgrad": "conv_igemm_buf_kernel<*,1,*> (+ conv_splitk_reduce_kernel)",
-                       "wgrad": "conv_wgrad_buf_kernel (+ wgrad_reduce_kernel)"}[dom],
+                       "wgrad": "conv_wgrad_buf_kernel (+ wgrad_reduce_kernel)",
+                       "x3_fwd128": "conv_x3_kernel<*,0,*> (+ conv_splitk_reduce_kernel<*,float>)",
+                       "x3_fwd64": "conv_x3_kernel<64,0,*> (+ conv_splitk_reduce_kernel<*,float>)",
+                       "x3_dgrad": "conv_x3_kernel<*,1,*> (+ conv_splitk_reduce_kernel<*,float>)",
+                       "x3_wgrad": "conv_wgrad_x3_kernel (+ wgrad_reduce_kernel)"}[dom],
             "launches_per_step": d["launches"], "avg_launch_us": round(1000 * d["ms"] / d["launches"], 2),
             "gflop_per_launch": round(d["flops"] / d["launches"] / 1e9, 3),
             "conv_stack": {"tflops": round(allf / (allms * 1e-3) / 1e12, 2), "gflop_per_step": round(allf / 1e9, 1),
@@ -245,12 +265,60 @@ def hbm_ops_roofline(model, opt, imgs, tg, reps=20):
     return res
 
 
+def _time_precision(precision, args, world, rank, dev, imgs, tg):
+    """Build the model in one arithmetic mode, run W warmup steps, time exactly K steps between
+    barrier + synchronize pairs; returns (model, ddp, opt, seconds over K steps, max over ranks)."""
+    torch.manual_seed(42)
+    model = build_model(dev, precision=precision).train()
+    ddp = model
+    if world > 1:
+        # DDP semantics (rank-0 init, per-GPU BN, averaged gradients) with the HIP graphs kept on:
+        # gradients are all-reduced over RCCL after the backward (mx_det.dp.DataParallel)
+        from mx_det.dp import DataParallel
+        ddp = DataParallel(model)
+    opt = make_optimizer(model)
+    gen = torch.Generator().manual_seed(1234 + rank)
+
+    def step(i):
+        j = (2 * i) % N_IMAGES_PER_RANK
+        return train_step(ddp, opt, imgs[j:j + 2], tg[j:j + 2], args.augment, gen)
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    from mx_det import _lib
+    _lib.trace_marker(1)  # timed-region markers for the rocprofv3 kernel trace (tools/prof_steps.py)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    _lib.trace_marker(2)
+    if world > 1:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    return model, ddp, opt, dt
+
+
+DTYPE_TEXT = {"f32": "f32", "bf16": "bf16"}
+ARITH_TEXT = {"f32": "f32 activations/gradients/BN/RoIAlign; conv products as bf16x3 MFMA (hi*hi + hi*lo + lo*hi, "
+                     "f32 accumulate, ~2^-16 rel. per product vs TF32 2^-11)",
+              "bf16": "bf16 activations and conv operands, f32 accumulate"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--augment", action="store_true")
+    ap.add_argument("--precision", choices=("both", "f32", "bf16"), default="both",
+                    help="both (default): the f32 headline, then the bf16 variant in the same JSON line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     args = ap.parse_args()
@@ -274,38 +342,10 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
 
     from mx_det.data import synth_batch
-    torch.manual_seed(42)
-    model = build_model(dev).train()
-    ddp = model
-    if world > 1:
-        # DDP semantics (rank-0 init, per-GPU BN, averaged gradients) with the HIP graphs kept on:
-        # gradients are all-reduced over RCCL after the backward (mx_det.dp.DataParallel)
-        from mx_det.dp import DataParallel
-        ddp = DataParallel(model)
-    opt = make_optimizer(model)
     imgs, tg = synth_batch(rank * N_IMAGES_PER_RANK, N_IMAGES_PER_RANK, device=dev)
-    gen = torch.Generator().manual_seed(1234 + rank)
-
-    def step(i):
-        j = (2 * i) % N_IMAGES_PER_RANK
-        return train_step(ddp, opt, imgs[j:j + 2], tg[j:j + 2], args.augment, gen)
-
-    for i in range(args.warmup):
-        step(i)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    precs = ["f32", "bf16"] if args.precision == "both" else [args.precision]
+    head = precs[0]
+    model, ddp, opt, dt = _time_precision(head, args, world, rank, dev, imgs, tg)
     images = 2 * args.steps * world
     rec = {
         "metric": "images/sec FRCNN-R50-FPN train @1333x800 bs=2/GPU",
@@ -318,18 +358,31 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": DTYPE_TEXT[head],
+        "arithmetic": ARITH_TEXT[head],
         "data": "synthetic VisDrone-shaped uint8 1333x800 (G~Poisson(55)), random-init weights",
         "config": {"workload": "configs[1]: FRCNN R50-FPN v2 baseline train step" + (" + 50% on-GPU corruption"
                                                                                    if args.augment else ""),
                    "global_batch": 2 * world, "per_gpu_batch": 2, "image": "1333x800 (padded 1344x800)",
                    "parallelism": f"dp{world}", "trainable_backbone_layers": 3},
     }
+    peak = {"f32": X3_PEAK_TFLOPS, "bf16": BF16_PEAK_TFLOPS}
     if rank == 0 and not args.no_roofline:
-        rec["roofline"] = conv_roofline(ddp, opt, imgs[0:2], tg[0:2])
+        rec["roofline"] = conv_roofline(ddp, opt, imgs[0:2], tg[0:2], peak[head])
         rec["hbm_ops"] = hbm_ops_roofline(ddp, opt, imgs[0:2], tg[0:2])
+    cpu_model = model  # the CPU baseline starts from the headline model's weights
+    for p in precs[1:]:
+        del ddp, opt
+        torch.cuda.empty_cache()
+        m2, ddp, opt, dt2 = _time_precision(p, args, world, rank, dev, imgs, tg)
+        var = {"dtype": DTYPE_TEXT[p], "arithmetic": ARITH_TEXT[p], "value": round(images / dt2, 3),
+               "ms_per_step": round(1000 * dt2 / args.steps, 3)}
+        if rank == 0 and not args.no_roofline:
+            var["roofline"] = conv_roofline(ddp, opt, imgs[0:2], tg[0:2], peak[p])
+        rec[p + "_variant"] = var
+        del m2
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline(model)
+        rec["cpu_baseline"] = cpu_baseline(cpu_model)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

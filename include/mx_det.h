@@ -34,6 +34,8 @@ typedef void* mx_stream_t; /* hipStream_t */
 
 int mx_version(void);
 const char* mx_last_error(void);
+/* Launches an empty kernel (trace_marker_kernel) on `stream`: a marker in rocprofv3 kernel traces. */
+int mx_trace_marker(int id, mx_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Anchor assignment: torchvision box_iou + Matcher (+ label/target construction), fused.
@@ -185,13 +187,13 @@ int mx_conv_get_variant(void);
 int mx_conv_set_wgrad_variant(int variant);
 int mx_conv_get_wgrad_variant(void);
 /* Per-step weight preparation from the f32 master parameter w[Kout][Cin][R][S] (torch layout) in
- * one pass: wk = [Kout][R][S][s->C] bf16 (input channels zero-padded to s->C; nullable) and
+ * one pass (split != 0: every layout as hi / lo bf16 planes, see mx_pack_desc.flags bit 1): wk = [Kout][R][S][s->C] bf16 (input channels zero-padded to s->C; nullable) and
  * wt = the dgrad operand (nullable): for each tap-parity class (r0, s0) = (r % st_h, s % st_w), in
  * order r0*st_w + s0, a contiguous block [s->C][Rc][Sc][s->K] (output channels zero-padded to s->K);
  * for stride 1 this is the plain [C][R][S][K] transpose. Uses s->C, K, R, S, strides, pads.
  * Replaces the per-step .to(bfloat16) weight casts of the reference's autocast-free fp32 model. */
 int mx_conv_pack_weight(const mx_conv_shape* s, const float* w, int64_t Cin, int64_t Kout, uint16_t* wk, uint16_t* wt,
-                        mx_stream_t stream);
+                        int split, mx_stream_t stream);
 size_t mx_conv_dgrad_weight_elems(const mx_conv_shape* s, int64_t Cpad, int64_t Kpad);
 /* The same packing for a list of weights in ONE launch (per-step operand preparation of a whole
  * model). A job: f32 w[Kout][Cin][R][S] -> wk [Kout][R][S][Cpad] (nullable) and wt, the dgrad layout
@@ -205,7 +207,10 @@ typedef struct {
   int64_t Cin, Kout, Cpad, Kpad;
   int32_t R, S, stride_h, stride_w, pad_h, pad_w;
   int32_t flags; /* bit 0: "dense" dgrad layout [R][S][Cpad][Kpad] for a conv whose output is 1x1 (FC6 as a
-                    valid 7x7 conv): its dgrad runs as the 1x1 GEMM dX[N, R*S*C] = dY[N, K] * W */
+                    valid 7x7 conv): its dgrad runs as the 1x1 GEMM dX[N, R*S*C] = dY[N, K] * W;
+                    bit 1: split -- each layout written as two bf16 planes, hi = bf16(w) then
+                    lo = bf16(w - hi) (the bf16x3 operands of the *_x3 convolutions; buffers twice
+                    the size) */
 } mx_pack_desc;
 size_t mx_conv_pack_plan_bytes(int64_t njobs);
 int mx_conv_pack_batched(const mx_pack_desc* jobs, int64_t njobs, void* plan, size_t plan_bytes, int upload,
@@ -245,20 +250,41 @@ int mx_conv_set_max_splits(int max_splits);
 int mx_conv_set_stages(int stages);
 int mx_conv_set_wgrad_target(int64_t blocks);
 
-/* NHWC pooling / resampling (bf16, C % 8 == 0).
+/* ---------------------------------------------------------------------------------------------
+ * Precision-faithful convolution (bf16x3): the reference trains and evaluates its convs in fp32
+ * (TF32 on Ampere; train_frcnn_baseline.py:139-176, no autocast; U-Net restore_testsets.py:64-68).
+ * Activations, gradients and outputs are f32 NHWC; every product is computed as
+ * hi*hi + hi*lo + lo*hi of the operands' bf16 hi/lo split (three v_mfma_f32_16x16x32_bf16 per
+ * K-step, f32 accumulation; ~2^-16 relative per product against TF32's 2^-11). Weights are the
+ * split planes written by mx_conv_pack_weight / mx_conv_pack_batched with split set: w [2][K][R][S][C]
+ * (fwd), wt [2][dgrad layout] (dgrad). Same shapes, epilogues, BN statistics, split-K workspaces
+ * (mx_conv_workspace_x3) and layouts as the bf16 entries above.
+ *   dgrad_x3: part != NULL adds the mx_conv2d_dgrad_bnb BN-backward partials (y, z, mean, invstd, act
+ *   of the BN whose output gradient dx is; stride 1), else those arguments are ignored.
+ * ------------------------------------------------------------------------------------------- */
+size_t mx_conv_workspace_x3(const mx_conv_shape* s, int pass);
+int mx_conv2d_fwd_x3(const mx_conv_shape* s, const float* x, const uint16_t* w, const float* bias, const float* residual,
+                     int act, float* y, float* stats, void* ws, size_t ws_bytes, mx_stream_t stream);
+int mx_conv2d_dgrad_x3(const mx_conv_shape* s, const float* dy, const uint16_t* wt, const float* residual, float* dx,
+                       const float* y, const float* z, const float* mean, const float* invstd, int act, float* part,
+                       int64_t part_mb, void* ws, size_t ws_bytes, mx_stream_t stream);
+int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const float* x, float* dw, int64_t Kout, int64_t Cin,
+                       int layout, void* ws, size_t ws_bytes, mx_stream_t stream);
+
+/* NHWC pooling / resampling (dtype MX_BF16 or MX_F32 storage, C % 8 == 0).
  * maxpool: F.max_pool2d (ResNet stem k3 s2 p1 — torchvision resnet50 reached at
  *   train_frcnn_baseline.py:139; U-Net MaxPool2d(2), restoration_net.py:39); argmax (nullable,
  *   int32 [N,Ho,Wo,C]) feeds the gather-form backward.
  * upsample_nearest: F.interpolate(mode="nearest", size=(Ho,Wo)) of the FPN top-down path, fused with
  *   the lateral add (y = up(x) + add, add nullable); backward sums each source's destinations. */
-int mx_maxpool_fwd(const uint16_t* x, int64_t N, int64_t H, int64_t W, int64_t C, int k, int stride, int pad,
-                   uint16_t* y, int32_t* argmax, mx_stream_t stream);
-int mx_maxpool_bwd(const uint16_t* gy, const int32_t* argmax, int64_t N, int64_t H, int64_t W, int64_t C, int k,
-                   int stride, int pad, uint16_t* gx, mx_stream_t stream);
-int mx_upsample_nearest_fwd(const uint16_t* x, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo,
-                            const uint16_t* add, uint16_t* y, mx_stream_t stream);
-int mx_upsample_nearest_bwd(const uint16_t* gy, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo,
-                            uint16_t* gx, mx_stream_t stream);
+int mx_maxpool_fwd(const void* x, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, int k, int stride, int pad,
+                   void* y, int32_t* argmax, mx_stream_t stream);
+int mx_maxpool_bwd(const void* gy, int dtype, const int32_t* argmax, int64_t N, int64_t H, int64_t W, int64_t C, int k,
+                   int stride, int pad, void* gx, mx_stream_t stream);
+int mx_upsample_nearest_fwd(const void* x, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo,
+                            const void* add, void* y, mx_stream_t stream);
+int mx_upsample_nearest_bwd(const void* gy, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo,
+                            void* gx, mx_stream_t stream);
 
 /* Train-mode BatchNorm2d around the conv (torch.nn.BatchNorm2d semantics, momentum 0.1,
  * unbiased running_var). finalize: reduce stats partials -> mean/invstd (f64 accumulation), fold
@@ -303,8 +329,9 @@ int mx_bn_finalize_ex(const float* stats, int64_t mblocks, int64_t K, int64_t co
                       const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                       float* mean_out, float* invstd_out, float* scale_out, float* shift_out, void* ws,
                       size_t ws_bytes, mx_stream_t stream);
+/* apply: x of xdtype, residual and y of ydtype (bf16 -> bf16, f32 -> bf16, f32 -> f32). */
 int mx_bn_apply(const void* x, int xdtype, int64_t M, int64_t K, const float* scale, const float* shift,
-                const uint16_t* residual, int act, uint16_t* y, mx_stream_t stream);
+                const void* residual, int act, void* y, int ydtype, mx_stream_t stream);
 /* Hot-path backward: reduce_ex = one launch of per-row-block partials (no float atomics) whose last
  * block per 64-channel chunk does the f64 column reduce, writing sums[2][K] = (sum g, sum g*xhat) =
  * (dbeta, dgamma) and coef[3][K], the per-channel affine form dx = coef0*g + coef1*x + coef2;
@@ -312,19 +339,19 @@ int mx_bn_apply(const void* x, int xdtype, int64_t M, int64_t K, const float* sc
  * use, left zero: see mx_bn_finalize_ex). apply_ex streams dx (and dres = g, nullable).
  * g = dy * act'(y); y may be null when act == 0. */
 size_t mx_bn_bwd_workspace(int64_t M, int64_t K);
-int mx_bn_bwd_reduce_ex(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
+int mx_bn_bwd_reduce_ex(const void* dy, const void* y, const void* x, int dtype, int64_t M, int64_t K, int act,
                         const float* mean, const float* invstd, const float* gamma, void* ws, size_t ws_bytes,
                         float* sums, float* coef, mx_stream_t stream);
-int mx_bn_bwd_apply_ex(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
-                       const float* coef, uint16_t* dx, uint16_t* dres, mx_stream_t stream);
+int mx_bn_bwd_apply_ex(const void* dy, const void* y, const void* x, int dtype, int64_t M, int64_t K, int act,
+                       const float* coef, void* dx, void* dres, mx_stream_t stream);
 /* Backward head of conv (+bias) (+act) (the ConvAct layers: RPN head convs, cls/bbox heads, FC6/FC7,
- * predictor): g[M][K8] bf16 = gy * act'(y) (columns K..K8-1 zero), db[K] f32 = column sums of the
+ * predictor): g[M][K8] (gdtype: bf16, or f32 for the bf16x3 path) = gy * act'(y) (columns K..K8-1 zero), db[K] f32 = column sums of the
  * unrounded g (nullable). gy, y: [M][K] of dtype MX_BF16 / MX_F32 (y nullable when act == 0).
  * ws = mx_act_bias_bwd_workspace(M, K) bytes with the zero-kept counters of mx_bn_finalize_ex
  * (needed only when db is given). */
 size_t mx_act_bias_bwd_workspace(int64_t M, int64_t K);
 int mx_act_bias_bwd(const void* gy, const void* y, int dtype, int64_t M, int64_t K, int64_t K8, int act,
-                    uint16_t* g, float* db, void* ws, size_t ws_bytes, mx_stream_t stream);
+                    void* g, int gdtype, float* db, void* ws, size_t ws_bytes, mx_stream_t stream);
 /* Convenience forms (allocate per call): sums[2][K] is overwritten. */
 int mx_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
                      const float* mean, const float* invstd, float* sums, mx_stream_t stream);
@@ -351,8 +378,8 @@ int mx_sgd_step(float* const* params, const float* const* grads, float* const* m
  * ------------------------------------------------------------------------------------------- */
 int mx_reflect_pad_u8(const uint8_t* src, int64_t B, int64_t H, int64_t W, int64_t C, int64_t Hp, int64_t Wp,
                       uint8_t* dst, mx_stream_t stream);
-int mx_up_concat(const uint16_t* up, const uint16_t* skip, int64_t N, int64_t H, int64_t W, int64_t Cu, int64_t Cs,
-                 uint16_t* out, mx_stream_t stream);
+int mx_up_concat(const void* up, const void* skip, int dtype, int64_t N, int64_t H, int64_t W, int64_t Cu, int64_t Cs,
+                 void* out, mx_stream_t stream);
 int mx_restore_finish(const uint8_t* img_padded, int64_t B, int64_t Hp, int64_t Wp, const float* residual, int64_t H,
                       int64_t W, uint8_t* out, mx_stream_t stream);
 

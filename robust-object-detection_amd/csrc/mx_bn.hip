@@ -191,10 +191,10 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
 
 // Thread t owns channel chunk c8 = t % K8 for its whole life (per-channel constants stay in
 // registers) and walks rows r = t / K8 + i * (T / K8): 16-B vector loads/stores, coalesced per row.
-template <typename T>
+template <typename T, typename TY>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, int64_t M, int64_t K, const float* __restrict__ scale,
-                                const float* __restrict__ shift, const uint16_t* __restrict__ res, int act,
-                                uint16_t* __restrict__ y) {
+                                const float* __restrict__ shift, const TY* __restrict__ res, int act,
+                                TY* __restrict__ y) {
   const int64_t K8 = K / 8;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t rstride = ((int64_t)gridDim.x * blockDim.x) / K8;
@@ -206,27 +206,13 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
   for (int64_t r = t / K8; r < M; r += rstride) {
     const int64_t e = r * K8 + c8;
     float v[8];
-    if constexpr (sizeof(T) == 2) {
-      uint4 u = *(const uint4*)(x + e * 8);
-      const uint16_t* h = (const uint16_t*)&u;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = bf2f(h[q]);
-    } else {
-      *(float4*)&v[0] = *(const float4*)(x + e * 8);
-      *(float4*)&v[4] = *(const float4*)(x + e * 8 + 4);
-    }
+    ld8(x + e * 8, v);
     float rv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (res) {
-      uint4 u = *(const uint4*)(res + e * 8);
-      const uint16_t* h = (const uint16_t*)&u;
+    if (res) ld8(res + e * 8, rv);
+    float o[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) rv[q] = bf2f(h[q]);
-    }
-    uint4 o;
-    uint16_t* oh = (uint16_t*)&o;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) oh[q] = f2bf(actf(v[q] * sc[q] + sh[q] + rv[q], act));
-    *(uint4*)(y + e * 8) = o;
+    for (int q = 0; q < 8; ++q) o[q] = actf(v[q] * sc[q] + sh[q] + rv[q], act);
+    st8(y + e * 8, o);
   }
 }
 
@@ -245,9 +231,9 @@ __device__ __forceinline__ float act_grad(float y) {
 // block = 64 channels (8 chunk lanes x 8 channels) x 32 row lanes over a row range; grid (RB, gy).
 // f32 per-thread sums over the block's rows, f32 partial per block, f64 across blocks in the last
 // block of the channel chunk, which also writes sums[2][K] and the affine coefficients.
-template <int ACT>
-__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
-                                                            const uint16_t* __restrict__ x, int64_t M, int64_t K,
+template <int ACT, typename T>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                            const T* __restrict__ x, int64_t M, int64_t K,
                                                             int64_t rows_per_block, const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, const float* __restrict__ gamma,
                                                             unsigned* __restrict__ ctr, float* __restrict__ part,
@@ -269,25 +255,25 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const uint16_t* __re
     // step would leave a single load set in flight per thread); per-row summation order unchanged
     constexpr int U = 4;
     for (int64_t rb = r0 + rl; rb < r1; rb += 32 * U) {
-      uint4 ud[U], ux[U], uy[U];
+      float vd[U][8], vx[U][8], vy[U][8];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t r = rb + 32 * u;
-        ud[u] = ux[u] = uy[u] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) vd[u][t] = vx[u][t] = vy[u][t] = 0.f;
         if (r < r1) {
-          ud[u] = *(const uint4*)(dy + r * K + c0);
-          ux[u] = *(const uint4*)(x + r * K + c0);
-          if (ACT) uy[u] = *(const uint4*)(y + r * K + c0);
+          ld8(dy + r * K + c0, vd[u]);
+          ld8(x + r * K + c0, vx[u]);
+          if (ACT) ld8(y + r * K + c0, vy[u]);
         }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (rb + 32 * u >= r1) break;
-        const uint16_t *hd = (const uint16_t*)&ud[u], *hy = (const uint16_t*)&uy[u], *hx = (const uint16_t*)&ux[u];
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-          const float g = bf2f(hd[t]) * act_grad<ACT>(bf2f(hy[t]));
-          const float xh = (bf2f(hx[t]) - mu[t]) * is[t];
+          const float g = vd[u][t] * act_grad<ACT>(vy[u][t]);
+          const float xh = (vx[u][t] - mu[t]) * is[t];
           s[t] += g;
           q[t] += g * xh;
         }
@@ -330,9 +316,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const uint16_t* __re
 // the narrow RPN / predictor heads are padded to 8), and db = column sums of the unrounded g
 // (torch: bias grad = grad_out.sum over N,H,W). Block = 64 columns (8 lanes x 8) x 32 row lanes;
 // grid (RB, cdiv(K8, 64)); the last block per column chunk sums the RB partials (f64) into db.
-template <typename T, int ACT>
+template <typename T, int ACT, typename TG>
 __global__ void __launch_bounds__(256) act_bias_bwd_kernel(const T* __restrict__ gy, const T* __restrict__ y, int64_t M,
-                                                           int K, int K8, int64_t rows_per_block, uint16_t* __restrict__ g,
+                                                           int K, int K8, int64_t rows_per_block, TG* __restrict__ g,
                                                            float* __restrict__ db, unsigned* __restrict__ ctr,
                                                            float* __restrict__ part) {
   __shared__ float red[32][65];
@@ -341,18 +327,17 @@ __global__ void __launch_bounds__(256) act_bias_bwd_kernel(const T* __restrict__
   const int64_t RB = gridDim.x;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c0 < K8) {
-    const bool vec = sizeof(T) == 2 && (K % 8) == 0;
+    const bool vec = (K % 8) == 0;
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = min<int64_t>(M, r0 + rows_per_block);
     for (int64_t r = r0 + rl; r < r1; r += 32) {
       float v[8];
       if (vec) {
-        const uint4 ug = *(const uint4*)(gy + r * K + c0);
-        uint4 uy = make_uint4(0, 0, 0, 0);
-        if (ACT) uy = *(const uint4*)(y + r * K + c0);
-        const uint16_t *hg = (const uint16_t*)&ug, *hy = (const uint16_t*)&uy;
+        float vg[8], vy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        ld8(gy + r * K + c0, vg);
+        if (ACT) ld8(y + r * K + c0, vy);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = bf2f(hg[t]) * act_grad<ACT>(bf2f(hy[t]));
+        for (int t = 0; t < 8; ++t) v[t] = vg[t] * act_grad<ACT>(vy[t]);
       } else {
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -360,14 +345,9 @@ __global__ void __launch_bounds__(256) act_bias_bwd_kernel(const T* __restrict__
           v[t] = c < K ? io<T>::ld(gy + r * K + c) * (ACT ? act_grad<ACT>(io<T>::ld(y + r * K + c)) : 1.f) : 0.f;
         }
       }
-      uint4 o;
-      uint16_t* oh = (uint16_t*)&o;
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        s[t] += v[t];
-        oh[t] = f2bf(v[t]);
-      }
-      *(uint4*)(g + r * K8 + c0) = o;
+      for (int t = 0; t < 8; ++t) s[t] += v[t];
+      st8(g + r * K8 + c0, v);
     }
   }
   if (!db) return;
@@ -389,36 +369,33 @@ __global__ void __launch_bounds__(256) act_bias_bwd_kernel(const T* __restrict__
 }
 
 // one 8-channel chunk of one row per thread
-template <int ACT>
-__global__ void __launch_bounds__(256) bn_bwd_apply2_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
-                                                            const uint16_t* __restrict__ x, int64_t n8, int K8,
-                                                            const float* __restrict__ coef, uint16_t* __restrict__ dx,
-                                                            uint16_t* __restrict__ dres) {
+template <int ACT, typename T>
+__global__ void __launch_bounds__(256) bn_bwd_apply2_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                            const T* __restrict__ x, int64_t n8, int K8,
+                                                            const float* __restrict__ coef, T* __restrict__ dx,
+                                                            T* __restrict__ dres) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= n8) return;
   const int K = K8 * 8;
   const int c0 = (int)(e % K8) * 8;
-  const uint4 ud = *(const uint4*)(dy + e * 8), ux = *(const uint4*)(x + e * 8);
-  uint4 uy = make_uint4(0, 0, 0, 0);
-  if (ACT) uy = *(const uint4*)(y + e * 8);
+  float vd[8], vx[8], vy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  ld8(dy + e * 8, vd);
+  ld8(x + e * 8, vx);
+  if (ACT) ld8(y + e * 8, vy);
   const float4 a0 = *(const float4*)(coef + c0), a1 = *(const float4*)(coef + c0 + 4);
   const float4 b0 = *(const float4*)(coef + K + c0), b1 = *(const float4*)(coef + K + c0 + 4);
   const float4 d0 = *(const float4*)(coef + 2 * K + c0), d1 = *(const float4*)(coef + 2 * K + c0 + 4);
   const float A[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
   const float B[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
   const float C[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-  const uint16_t *hd = (const uint16_t*)&ud, *hy = (const uint16_t*)&uy, *hx = (const uint16_t*)&ux;
-  uint4 o, orr;
-  uint16_t* oh = (uint16_t*)&o;
-  uint16_t* orh = (uint16_t*)&orr;
+  float o[8], og[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const float g = bf2f(hd[q]) * act_grad<ACT>(bf2f(hy[q]));
-    oh[q] = f2bf(A[q] * g + B[q] * bf2f(hx[q]) + C[q]);
-    orh[q] = f2bf(g);
+    og[q] = vd[q] * act_grad<ACT>(vy[q]);
+    o[q] = A[q] * og[q] + B[q] * vx[q] + C[q];
   }
-  *(uint4*)(dx + e * 8) = o;
-  if (dres) *(uint4*)(dres + e * 8) = orr;
+  st8(dx + e * 8, o);
+  if (dres) st8(dres + e * 8, og);
 }
 
 // sums -> coef for the legacy mx_bn_bwd_apply entry
@@ -669,15 +646,23 @@ extern "C" int mx_bn_finalize(const float* stats, int64_t mb, int64_t K, int64_t
 }
 
 extern "C" int mx_bn_apply(const void* x, int xdtype, int64_t M, int64_t K, const float* scale, const float* shift,
-                           const uint16_t* residual, int act, uint16_t* y, mx_stream_t stream) {
+                           const void* residual, int act, void* y, int ydtype, mx_stream_t stream) {
   MX_CHECK_ARG(K % 8 == 0, "bn_apply: K %% 8 != 0");
+  MX_CHECK_ARG((xdtype == MX_BF16 || xdtype == MX_F32) && (ydtype == MX_BF16 || ydtype == MX_F32), "bn_apply: bad dtype");
   if (M == 0) return MX_OK;
-  if (xdtype == MX_BF16)
-    bn_apply_kernel<uint16_t><<<grid_rows(M, K / 8), 256, 0, (hipStream_t)stream>>>((const uint16_t*)x, M, K, scale, shift,
-                                                                                     residual, act, y);
+  const unsigned grid = grid_rows(M, K / 8);
+  hipStream_t st = (hipStream_t)stream;
+  if (xdtype == MX_BF16 && ydtype == MX_BF16)
+    bn_apply_kernel<uint16_t, uint16_t><<<grid, 256, 0, st>>>((const uint16_t*)x, M, K, scale, shift,
+                                                             (const uint16_t*)residual, act, (uint16_t*)y);
+  else if (xdtype == MX_F32 && ydtype == MX_BF16)
+    bn_apply_kernel<float, uint16_t><<<grid, 256, 0, st>>>((const float*)x, M, K, scale, shift, (const uint16_t*)residual,
+                                                          act, (uint16_t*)y);
+  else if (xdtype == MX_F32 && ydtype == MX_F32)
+    bn_apply_kernel<float, float><<<grid, 256, 0, st>>>((const float*)x, M, K, scale, shift, (const float*)residual, act,
+                                                       (float*)y);
   else
-    bn_apply_kernel<float><<<grid_rows(M, K / 8), 256, 0, (hipStream_t)stream>>>((const float*)x, M, K, scale, shift,
-                                                                                  residual, act, y);
+    MX_CHECK_ARG(false, "bn_apply: bf16 input with f32 output is not a supported combination");
   MX_LAUNCH_CHECK();
   return MX_OK;
 }
@@ -688,7 +673,21 @@ extern "C" size_t mx_bn_bwd_workspace(int64_t M, int64_t K) {
   return CTR_BYTES + sizeof(float) * 2 * (size_t)g.RB * K;
 }
 
-extern "C" int mx_bn_bwd_reduce_ex(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
+template <typename T>
+static void bn_bwd_reduce_launch(const void* dy, const void* y, const void* x, int64_t M, int64_t K, int act,
+                                 const BwdGeo& g, const float* mean, const float* invstd, const float* gamma, unsigned* ctr,
+                                 float* part, float* sums, float* coef, hipStream_t st) {
+  dim3 grid((unsigned)g.RB, (unsigned)g.gy);
+  const T *d = (const T*)dy, *yy = (const T*)y, *xx = (const T*)x;
+  if (act == 1)
+    bn_bwd_reduce_kernel<1, T><<<grid, 256, 0, st>>>(d, yy, xx, M, K, g.rows_per_block, mean, invstd, gamma, ctr, part, sums, coef);
+  else if (act == 2)
+    bn_bwd_reduce_kernel<2, T><<<grid, 256, 0, st>>>(d, yy, xx, M, K, g.rows_per_block, mean, invstd, gamma, ctr, part, sums, coef);
+  else
+    bn_bwd_reduce_kernel<0, T><<<grid, 256, 0, st>>>(d, yy, xx, M, K, g.rows_per_block, mean, invstd, gamma, ctr, part, sums, coef);
+}
+
+extern "C" int mx_bn_bwd_reduce_ex(const void* dy, const void* y, const void* x, int dtype, int64_t M, int64_t K, int act,
                                    const float* mean, const float* invstd, const float* gamma, void* ws, size_t ws_bytes,
                                    float* sums, float* coef, mx_stream_t stream) {
   MX_CHECK_ARG(K % 8 == 0 && K > 0 && M > 0, "bn_bwd_reduce: K must be a positive multiple of 8, M > 0");
@@ -698,32 +697,32 @@ extern "C" int mx_bn_bwd_reduce_ex(const uint16_t* dy, const uint16_t* y, const 
   const size_t need = mx_bn_bwd_workspace(M, K);
   MX_CHECK_ARG(ws && ws_bytes >= need, "bn_bwd_reduce: workspace of %zu bytes required (mx_bn_bwd_workspace)", need);
   MX_CHECK_ARG(g.gy <= MAX_CHUNKS && g.RB < 65536, "bn_bwd_reduce: K > %d", MAX_CHUNKS * 64);
-  hipStream_t st = (hipStream_t)stream;
   unsigned* ctr = (unsigned*)ws;
   float* part = (float*)((char*)ws + CTR_BYTES);
-  dim3 grid((unsigned)g.RB, (unsigned)g.gy);
-  if (act == 1)
-    bn_bwd_reduce_kernel<1><<<grid, 256, 0, st>>>(dy, y, x, M, K, g.rows_per_block, mean, invstd, gamma, ctr, part, sums, coef);
-  else if (act == 2)
-    bn_bwd_reduce_kernel<2><<<grid, 256, 0, st>>>(dy, y, x, M, K, g.rows_per_block, mean, invstd, gamma, ctr, part, sums, coef);
-  else
-    bn_bwd_reduce_kernel<0><<<grid, 256, 0, st>>>(dy, y, x, M, K, g.rows_per_block, mean, invstd, gamma, ctr, part, sums, coef);
+  MX_DT_DISPATCH(dtype, bn_bwd_reduce_launch, dy, y, x, M, K, act, g, mean, invstd, gamma, ctr, part, sums, coef,
+                 (hipStream_t)stream);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }
 
-extern "C" int mx_bn_bwd_apply_ex(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
-                                  const float* coef, uint16_t* dx, uint16_t* dres, mx_stream_t stream) {
+template <typename T>
+static void bn_bwd_apply_launch(const void* dy, const void* y, const void* x, int64_t n8, int K8, int act, const float* coef,
+                                void* dx, void* dres, hipStream_t st) {
+  const unsigned blocks = (unsigned)cdiv(n8, 256);
+  const T *d = (const T*)dy, *yy = (const T*)y, *xx = (const T*)x;
+  if (act == 1) bn_bwd_apply2_kernel<1, T><<<blocks, 256, 0, st>>>(d, yy, xx, n8, K8, coef, (T*)dx, (T*)dres);
+  else if (act == 2) bn_bwd_apply2_kernel<2, T><<<blocks, 256, 0, st>>>(d, yy, xx, n8, K8, coef, (T*)dx, (T*)dres);
+  else bn_bwd_apply2_kernel<0, T><<<blocks, 256, 0, st>>>(d, yy, xx, n8, K8, coef, (T*)dx, (T*)dres);
+}
+
+extern "C" int mx_bn_bwd_apply_ex(const void* dy, const void* y, const void* x, int dtype, int64_t M, int64_t K, int act,
+                                  const float* coef, void* dx, void* dres, mx_stream_t stream) {
   MX_CHECK_ARG(K % 8 == 0 && K > 0 && K < (1 << 24), "bn_bwd_apply: K must be a positive multiple of 8");
   MX_CHECK_ARG(act >= 0 && act <= 2, "bn_bwd_apply: act 0/1/2");
   MX_CHECK_ARG(act == 0 || y, "bn_bwd_apply: y required for an activation");
   if (M == 0) return MX_OK;
   const int64_t n8 = M * (K / 8);
-  const unsigned blocks = (unsigned)cdiv(n8, 256);
-  hipStream_t st = (hipStream_t)stream;
-  if (act == 1) bn_bwd_apply2_kernel<1><<<blocks, 256, 0, st>>>(dy, y, x, n8, (int)(K / 8), coef, dx, dres);
-  else if (act == 2) bn_bwd_apply2_kernel<2><<<blocks, 256, 0, st>>>(dy, y, x, n8, (int)(K / 8), coef, dx, dres);
-  else bn_bwd_apply2_kernel<0><<<blocks, 256, 0, st>>>(dy, y, x, n8, (int)(K / 8), coef, dx, dres);
+  MX_DT_DISPATCH(dtype, bn_bwd_apply_launch, dy, y, x, n8, (int)(K / 8), act, coef, dx, dres, (hipStream_t)stream);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }
@@ -740,7 +739,7 @@ extern "C" int mx_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uin
   MX_HIP(hipMallocAsync(&ws, wsb, st));
   MX_HIP(hipMemsetAsync(ws, 0, CTR_BYTES, st));
   MX_HIP(hipMallocAsync((void**)&coef, sizeof(float) * 3 * K, st));
-  int rc = mx_bn_bwd_reduce_ex(dy, y, x, M, K, act, mean, invstd, nullptr, ws, wsb, sums, coef, stream);
+  int rc = mx_bn_bwd_reduce_ex(dy, y, x, MX_BF16, M, K, act, mean, invstd, nullptr, ws, wsb, sums, coef, stream);
   MX_HIP(hipFreeAsync(ws, st));
   MX_HIP(hipFreeAsync(coef, st));
   return rc;
@@ -757,7 +756,7 @@ extern "C" int mx_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint
   bn_coef_from_sums_kernel<<<(unsigned)cdiv(K, 256), 256, 0, st>>>(sums, K, M, mean, invstd, gamma, coef);
   int rc = MX_OK;
   if (hipGetLastError() != hipSuccess) rc = MX_EHIP;
-  if (!rc) rc = mx_bn_bwd_apply_ex(dy, y, x, M, K, act, coef, dx, dres, stream);
+  if (!rc) rc = mx_bn_bwd_apply_ex(dy, y, x, MX_BF16, M, K, act, coef, dx, dres, stream);
   MX_HIP(hipFreeAsync(coef, st));
   return rc;
 }
@@ -777,23 +776,25 @@ extern "C" size_t mx_act_bias_bwd_workspace(int64_t M, int64_t K) {
   return CTR_BYTES + sizeof(float) * (size_t)g.RB * K;
 }
 
-template <typename T>
+template <typename T, typename TG>
 static void launch_act_bias(const void* gy, const void* y, int64_t M, int K, int K8, int act, const BwdGeo& g,
-                            uint16_t* out, float* db, unsigned* ctr, float* part, hipStream_t st) {
+                            void* out_, float* db, unsigned* ctr, float* part, hipStream_t st) {
   dim3 grid((unsigned)g.RB, (unsigned)g.gy);
+  TG* out = (TG*)out_;
   if (act == 1)
-    act_bias_bwd_kernel<T, 1><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr, part);
+    act_bias_bwd_kernel<T, 1, TG><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr, part);
   else if (act == 2)
-    act_bias_bwd_kernel<T, 2><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr, part);
+    act_bias_bwd_kernel<T, 2, TG><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr, part);
   else
-    act_bias_bwd_kernel<T, 0><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr, part);
+    act_bias_bwd_kernel<T, 0, TG><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr, part);
 }
 
 extern "C" int mx_act_bias_bwd(const void* gy, const void* y, int dtype, int64_t M, int64_t K, int64_t K8, int act,
-                               uint16_t* g, float* db, void* ws, size_t ws_bytes, mx_stream_t stream) {
+                               void* g, int gdtype, float* db, void* ws, size_t ws_bytes, mx_stream_t stream) {
   MX_CHECK_ARG(M >= 0 && K > 0 && K8 >= K && K8 % 8 == 0 && K8 < (1 << 24), "act_bias_bwd: need 0 < K <= K8, K8 %% 8 == 0");
   MX_CHECK_ARG(act >= 0 && act <= 2 && (act == 0 || y), "act_bias_bwd: act 0/1/2 (y required for 1/2)");
   MX_CHECK_ARG(dtype == MX_BF16 || dtype == MX_F32, "act_bias_bwd: dtype bf16 or f32");
+  MX_CHECK_ARG(gdtype == MX_BF16 || gdtype == MX_F32, "act_bias_bwd: gdtype bf16 or f32");
   if (M == 0) {
     if (db) MX_HIP(hipMemsetAsync(db, 0, sizeof(float) * K, (hipStream_t)stream));
     return MX_OK;
@@ -809,8 +810,14 @@ extern "C" int mx_act_bias_bwd(const void* gy, const void* y, int dtype, int64_t
     part = (float*)((char*)ws + CTR_BYTES);
   }
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MX_BF16) launch_act_bias<uint16_t>(gy, y, M, (int)K, (int)K8, act, g_, g, db, ctr, part, st);
-  else launch_act_bias<float>(gy, y, M, (int)K, (int)K8, act, g_, g, db, ctr, part, st);
+  if (dtype == MX_BF16 && gdtype == MX_BF16)
+    launch_act_bias<uint16_t, uint16_t>(gy, y, M, (int)K, (int)K8, act, g_, g, db, ctr, part, st);
+  else if (dtype == MX_F32 && gdtype == MX_BF16)
+    launch_act_bias<float, uint16_t>(gy, y, M, (int)K, (int)K8, act, g_, g, db, ctr, part, st);
+  else if (dtype == MX_F32 && gdtype == MX_F32)
+    launch_act_bias<float, float>(gy, y, M, (int)K, (int)K8, act, g_, g, db, ctr, part, st);
+  else
+    MX_CHECK_ARG(false, "act_bias_bwd: bf16 input with f32 gradient output is not a supported combination");
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

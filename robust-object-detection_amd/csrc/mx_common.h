@@ -48,6 +48,76 @@ template <> struct io<uint16_t> {
   static __device__ __forceinline__ void st(uint16_t* p, float v) { *p = f2bf(v); }
 };
 
+// 8 consecutive activation elements of storage type T (bf16 bits or f32) <-> float[8]: one 16-B
+// access for bf16, two for f32 (NHWC rows are 8-element aligned everywhere: C % 8 == 0)
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const uint4 u = *(const uint4*)p;
+    const uint16_t* h = (const uint16_t*)&u;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = bf2f(h[q]);
+  } else {
+    *(float4*)&v[0] = *(const float4*)p;
+    *(float4*)&v[4] = *(const float4*)(p + 4);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    uint4 u;
+    uint16_t* h = (uint16_t*)&u;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) h[q] = f2bf(v[q]);
+    *(uint4*)p = u;
+  } else {
+    *(float4*)p = *(const float4*)&v[0];
+    *(float4*)(p + 4) = *(const float4*)&v[4];
+  }
+}
+// storage element as stored (no rounding when T is f32)
+template <typename T>
+__device__ __forceinline__ float ld1(const T* p) {
+  if constexpr (sizeof(T) == 2) return bf2f(*p);
+  else return *p;
+}
+template <typename T>
+__device__ __forceinline__ void st1(T* p, float v) {
+  if constexpr (sizeof(T) == 2) *p = f2bf(v);
+  else *p = v;
+}
+
+// bf16x3 split of f32 operands (precision-faithful conv mode): x = hi + lo + O(2^-17 |x|), hi = RNE
+// bf16(x), lo = RNE bf16(x - hi); products hi*hi + hi*lo + lo*hi in f32 accumulation differ from the
+// f32 product by O(2^-16) relative (TF32 rounds each operand to 2^-11). One v_cvt_pk_bf16_f32 per
+// pair and plane.
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+  const b2_t r = __builtin_convertvector((f2_t){a, b}, b2_t);
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = pk_bf16(a, b);
+  const float ha = __uint_as_float(hi << 16), hb = __uint_as_float(hi & 0xffff0000u);
+  lo = pk_bf16(a - ha, b - hb);
+}
+// 8 f32 -> 8 bf16 hi (16 B) + 8 bf16 lo (16 B)
+__device__ __forceinline__ void split8(const float4 a, const float4 b, uint4& hi, uint4& lo) {
+  split2(a.x, a.y, hi.x, lo.x);
+  split2(a.z, a.w, hi.y, lo.y);
+  split2(b.x, b.y, hi.z, lo.z);
+  split2(b.z, b.w, hi.w, lo.w);
+}
+
+// host: call F<uint16_t> (MX_BF16) or F<float> (MX_F32) with the arguments; other codes -> MX_EINVAL
+#define MX_DT_DISPATCH(dt, F, ...)                                   \
+  do {                                                              \
+    MX_CHECK_ARG((dt) == MX_BF16 || (dt) == MX_F32, "bad dtype %d", (int)(dt)); \
+    if ((dt) == MX_BF16) F<uint16_t>(__VA_ARGS__);                  \
+    else F<float>(__VA_ARGS__);                                     \
+  } while (0)
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t v, size_t a = 256) { return (v + a - 1) / a * a; }
 

@@ -37,9 +37,9 @@ struct ConvP {
   int64_t OH, OW;       // row grid (n, oh, ow) of the GEMM rows
   int64_t IH, IW, IC;   // gathered source grid
   int R, S, st_h, st_w, pad_h, pad_w;
-  // epilogue
+  // epilogue (residual / bnb_y / bnb_z: activation storage, bf16 or f32 per the kernel's TA)
   const float* bias;
-  const uint16_t* residual;
+  const void* residual;
   int act;
   void* out;
   int out_f32;
@@ -56,10 +56,13 @@ struct ConvP {
   int64_t rH, rW;
   // element counts of the A source and of the B operand (buffer-descriptor ranges)
   int64_t src_elems, wt_elems;
+  // bf16x3 (f32 activation) kernels: the lo plane of the split weight operand starts wt_plane
+  // elements after the hi plane (wt)
+  int64_t wt_plane;
   // dgrad feeding a train-mode BatchNorm backward (mx_conv2d_dgrad_bnb): per 64-row block column
   // sums of g = bf16(dx) * act'(y) and g * (z - mean) * invstd -> bnb_part [2][mblocks64][Ncol]
-  const uint16_t* bnb_y;
-  const uint16_t* bnb_z;
+  const void* bnb_y;
+  const void* bnb_z;
   const float* bnb_mean;
   const float* bnb_invstd;
   float* bnb_part;
@@ -116,7 +119,7 @@ __device__ __forceinline__ bool gather_pos(const ConvP& p, int oh, int ow, int r
 // granularity: stats[2][ceil(M/64)][Ncol] (row = m / 64).
 static constexpr int SROWS = 64;
 
-template <int BN, int HALVES = 1, int BMT = BM>
+template <int BN, int HALVES = 1, int BMT = BM, typename TA = uint16_t>
 __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT / 32][BN / 32], char* smem, int64_t m0,
                                               int64_t n0, int64_t mt, int wm, int wn, int lane, int tid, int split) {
   constexpr int WN = BN / 2, TJ = WN / 16, WM = BMT / 2, TI = BMT / 32;
@@ -257,10 +260,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
         for (int t = 0; t < 8; ++t) v[t] += p.bias[col0 + t];
       }
       if (p.residual) {
-        uint4 rr = *(const uint4*)(p.residual + m * p.Ncol + col0);
-        const uint16_t* rh = (const uint16_t*)&rr;
+        float rr[8];
+        ld8((const TA*)p.residual + m * p.Ncol + col0, rr);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] += bf2f(rh[t]);
+        for (int t = 0; t < 8; ++t) v[t] += rr[t];
       }
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], p.act);
@@ -268,6 +271,18 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
         float* o = (float*)p.out + m * p.Ncol + col0;
         *(float4*)o = *(float4*)&v[0];
         *(float4*)(o + 4) = *(float4*)&v[4];
+        if (sizeof(TA) == 4 && p.bnb_part) {  // f32 activations: the stored gradient is v itself
+          float yy[8], zz[8];
+          ld8((const TA*)p.bnb_y + m * p.Ncol + col0, yy);
+          ld8((const TA*)p.bnb_z + m * p.Ncol + col0, zz);
+          const int gi = BG == 1 ? 0 : (int)((h * PR + row) / SROWS);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const float g = v[t] * bnb_act_grad(yy[t], p.bnb_act);
+            bs[gi][t] += g;
+            bq[gi][t] += g * ((zz[t] - bmu[t]) * bis[t]);
+          }
+        }
       } else {
         uint4 w;
         uint16_t* wh = (uint16_t*)&w;
@@ -275,8 +290,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
         for (int t = 0; t < 8; ++t) wh[t] = f2bf(v[t]);
         *(uint4*)((uint16_t*)p.out + m * p.Ncol + col0) = w;
         if (p.bnb_part) {  // the stored (bf16-rounded) gradient, as a separate reduce would read it
-          const uint4 yy = *(const uint4*)(p.bnb_y + m * p.Ncol + col0);
-          const uint4 zz = *(const uint4*)(p.bnb_z + m * p.Ncol + col0);
+          const uint4 yy = *(const uint4*)((const uint16_t*)p.bnb_y + m * p.Ncol + col0);
+          const uint4 zz = *(const uint4*)((const uint16_t*)p.bnb_z + m * p.Ncol + col0);
           const uint16_t *yh = (const uint16_t*)&yy, *zh = (const uint16_t*)&zz;
           const int gi = BG == 1 ? 0 : (int)((h * PR + row) / SROWS);
 #pragma unroll
@@ -291,7 +306,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
       for (int t = 0; t < 8 && col0 + t < p.Ncol; ++t) {
         float x = v[t];
         if (p.bias) x += p.bias[col0 + t];
-        if (p.residual) x += bf2f(p.residual[m * p.Ncol + col0 + t]);
+        if (p.residual) x += ld1((const TA*)p.residual + m * p.Ncol + col0 + t);
         x = act_f(x, p.act);
         if (p.out_f32) ((float*)p.out)[m * p.Ncol + col0 + t] = x;
         else ((uint16_t*)p.out)[m * p.Ncol + col0 + t] = f2bf(x);
@@ -810,7 +825,7 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_buf_kernel(ConvP p) {
 // maps, where 64-column blocks would leave most CUs idle). Sums the splits' f32 partials, then
 // bias / residual / activation / store and the BN statistics partials of the 128-row block (same
 // [2][mblocks][Ncol] layout as the fused epilogue).
-template <int CG>
+template <int CG, typename TA = uint16_t>
 __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
   constexpr int RL = 256 / CG, RPT = BM / RL, CW = 8 * CG;
   __shared__ float red[2][RL][CW + 1];
@@ -860,10 +875,10 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
     }
     const int64_t mo = out_row(p, m);
     if (p.residual) {
-      uint4 r4 = *(const uint4*)(p.residual + mo * p.Ncol + col0);
-      const uint16_t* rh = (const uint16_t*)&r4;
+      float rr[8];
+      ld8((const TA*)p.residual + mo * p.Ncol + col0, rr);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] += bf2f(rh[t]);
+      for (int t = 0; t < 8; ++t) v[t] += rr[t];
     }
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], p.act);
@@ -871,6 +886,17 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
       float* o = (float*)p.out + mo * p.Ncol + col0;
       *(float4*)o = *(float4*)&v[0];
       *(float4*)(o + 4) = *(float4*)&v[4];
+      if (sizeof(TA) == 4 && p.bnb_part) {
+        float yy[8], zz[8];
+        ld8((const TA*)p.bnb_y + mo * p.Ncol + col0, yy);
+        ld8((const TA*)p.bnb_z + mo * p.Ncol + col0, zz);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const float g = v[t] * bnb_act_grad(yy[t], p.bnb_act);
+          b2[h][t] += g;
+          c2[h][t] += g * ((zz[t] - bmu[t]) * bis[t]);
+        }
+      }
     } else {
       uint4 w;
       uint16_t* wh = (uint16_t*)&w;
@@ -878,8 +904,8 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
       for (int t = 0; t < 8; ++t) wh[t] = f2bf(v[t]);
       *(uint4*)((uint16_t*)p.out + mo * p.Ncol + col0) = w;
       if (p.bnb_part) {
-        const uint4 yy = *(const uint4*)(p.bnb_y + mo * p.Ncol + col0);
-        const uint4 zz = *(const uint4*)(p.bnb_z + mo * p.Ncol + col0);
+        const uint4 yy = *(const uint4*)((const uint16_t*)p.bnb_y + mo * p.Ncol + col0);
+        const uint4 zz = *(const uint4*)((const uint16_t*)p.bnb_z + mo * p.Ncol + col0);
         const uint16_t *yh = (const uint16_t*)&yy, *zh = (const uint16_t*)&zz;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -1363,6 +1389,311 @@ __global__ void __launch_bounds__(NT, 3) conv_wgrad_buf_kernel(WgP p) {
 #endif
 }
 
+// ------------------------------------------------------------------------------------------------
+// bf16x3 implicit GEMM (precision-faithful mode: f32 activations, f32 accumulate). The reference
+// trains its convs in fp32 (TF32 on Ampere; train_frcnn_baseline.py:139-176, no autocast). gfx950
+// has no xf32 MFMA and its f32 MFMA runs at 1/16 of the bf16 rate, so each f32 operand is split
+// into bf16 hi + lo planes and a K-step issues hi*hi + hi*lo + lo*hi (three bf16 MFMAs, f32
+// accumulation): ~2^-16 relative per product (TF32 rounds each operand to 2^-11) at 1/3 of the
+// bf16 MFMA rate. Weights arrive pre-split (mx_conv_pack_* split mode, planes p.wt / p.wt +
+// p.wt_plane); activations are read as f32 by register-staged loads and split once per block while
+// they are written to LDS (each element is read by two waves, so splitting at staging halves the
+// VALU work of splitting fragments). Tile BMT x BN x 32, 4 waves (2x2), double-buffered LDS of
+// [A hi | A lo | B hi | B lo] bf16 tiles (64-B rows, tile_swz<4> chunk swizzle: conflict-free
+// ds_read_b128 fragment reads and ds_write_b128 stores). Any C % 8 == 0 (a lane's 8-channel chunk
+// stays inside one tap): the stem's 8-channel input included.
+template <int BN, int MODE, int BMT>
+__global__ void __launch_bounds__(NT, 2) conv_x3_kernel(ConvP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BKT = 32, RB = BKT * 2;
+  constexpr int APL = BMT * RB, BPL = BN * RB, STAGE = 2 * (APL + BPL);
+  constexpr int WN = BN / 2, TJ = WN / 16, WM = BMT / 2, TI = WM / 16;
+  constexpr int ACH = BMT * 4 / NT, BCH = BN * 4 / NT, RPS = NT / 4;  // chunks per thread; rows per sweep
+  static_assert(ACH >= 1 && BCH >= 1, "tile shape");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t ntiles_n = (p.Ncol + BN - 1) / BN;
+  const int64_t gid = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int split = (int)(gid % p.splits);
+  const int64_t bid = gid / p.splits;
+  const int64_t mt = bid / ntiles_n, nt = bid % ntiles_n;
+  const int64_t m0 = mt * BMT, n0 = nt * BN;
+  const float* __restrict__ src = (const float*)p.src;
+  const uint16_t* __restrict__ whi = p.wt;
+  const uint16_t* __restrict__ wlo = p.wt + p.wt_plane;
+  const int IH = (int)p.IH, IW = (int)p.IW, IC = (int)p.IC, S = p.S, Kd = (int)p.Kdim;
+  const int kc = tid & 3;  // this thread's 8-element K chunk of every A and B row it stages
+  int a_h0[ACH], a_w0[ACH];
+  int64_t a_pix[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int64_t m = m0 + (tid >> 2) + RPS * i;
+    const bool ok = m < p.M;
+    const int64_t mm = ok ? m : 0;
+    const int ow = (int)(mm % p.OW);
+    const int64_t t = mm / p.OW;
+    const int oh = (int)(t % p.OH);
+    const int n = (int)(t / p.OH);
+    // MODE 0: ih = oh*st - pad + r; MODE 1 (dgrad parity class): ih = hh + dh - ri
+    a_h0[i] = MODE == 0 ? oh * p.st_h - p.pad_h : oh + p.pad_h;
+    a_w0[i] = MODE == 0 ? ow * p.st_w - p.pad_w : ow + p.pad_w;
+    if (!ok) a_h0[i] = -(1 << 28);
+    a_pix[i] = ((int64_t)n * IH + a_h0[i]) * IW + a_w0[i];
+  }
+  int64_t b_row[BCH];
+#pragma unroll
+  for (int i = 0; i < BCH; ++i) b_row[i] = n0 + (tid >> 2) + RPS * i;
+  const int64_t nk = (p.Kdim + BKT - 1) / BKT;
+  const int64_t kbeg = (int64_t)split * p.kt_per_split;
+  const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
+  // K position of this thread's chunk (k -> tap (cr, cq), channel cc), walked incrementally
+  int ik = (int)(kbeg * BKT) + kc * 8;
+  int cc, cr, cq;
+  {
+    const int tap = ik / IC;
+    cc = ik - tap * IC;
+    cr = tap / S;
+    cq = tap - cr * S;
+  }
+  float4 ra[ACH][2];
+  uint4 rbh[BCH], rbl[BCH];
+  auto load = [&]() {
+    const int k = ik;
+    const bool kin = k < Kd;
+    const int dr = MODE == 0 ? cr : -cr, ds = MODE == 0 ? cq : -cq, c = cc;
+    ik += BKT;
+    cc += BKT;
+    while (cc >= IC) {
+      cc -= IC;
+      if (++cq == S) { cq = 0; ++cr; }
+    }
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int ih = a_h0[i] + dr, iw = a_w0[i] + ds;
+      if (kin && (unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW) {
+        const float* sp = src + (a_pix[i] + (int64_t)dr * IW + ds) * IC + c;
+        ra[i][0] = *(const float4*)sp;
+        ra[i][1] = *(const float4*)(sp + 4);
+      } else {
+        ra[i][0] = ra[i][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      if (kin && b_row[i] < p.Ncol) {
+        rbh[i] = *(const uint4*)(whi + b_row[i] * p.Kdim + k);
+        rbl[i] = *(const uint4*)(wlo + b_row[i] * p.Kdim + k);
+      } else {
+        rbh[i] = rbl[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    char* Ah = smem + buf * STAGE;
+    char* Al = Ah + APL;
+    char* Bh = Al + APL;
+    char* Bl = Bh + BPL;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int row = (tid >> 2) + RPS * i;
+      const int off = row * RB + ((kc ^ tile_swz<4>(row)) << 4);
+      uint4 h, l;
+      split8(ra[i][0], ra[i][1], h, l);
+      *(uint4*)(Ah + off) = h;
+      *(uint4*)(Al + off) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int row = (tid >> 2) + RPS * i;
+      const int off = row * RB + ((kc ^ tile_swz<4>(row)) << 4);
+      *(uint4*)(Bh + off) = rbh[i];
+      *(uint4*)(Bl + off) = rbl[i];
+    }
+  };
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (ntk > 0) {
+    load();
+    store(0);
+  }
+  __syncthreads();
+  for (int64_t t = 0; t < ntk; ++t) {
+    const int buf = (int)(t & 1);
+    if (t + 1 < ntk) load();
+    const char* Ah = smem + buf * STAGE;
+    const char* Al = Ah + APL;
+    const char* Bh = Al + APL;
+    const char* Bl = Bh + BPL;
+    const int ch = lane >> 4;
+    bf16x8 ah[TI], al[TI], bh[TJ], bl[TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int row = wm * WM + i * 16 + (lane & 15);
+      const int off = row * RB + ((ch ^ tile_swz<4>(row)) << 4);
+      ah[i] = *(const bf16x8*)(Ah + off);
+      al[i] = *(const bf16x8*)(Al + off);
+    }
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int row = wn * WN + j * 16 + (lane & 15);
+      const int off = row * RB + ((ch ^ tile_swz<4>(row)) << 4);
+      bh[j] = *(const bf16x8*)(Bh + off);
+      bl[j] = *(const bf16x8*)(Bl + off);
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+    if (t + 1 < ntk) store(buf ^ 1);
+    __syncthreads();
+  }
+  conv_epilogue<BN, 2, BMT, float>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
+}
+
+// bf16x3 wgrad: dw[k][(r,s,c)] = sum_p dy[p][k] * x[gather(p, r, s)][c] on f32 dy / x, both split
+// into hi / lo while staged (register loads, 32-pixel K-tiles, pixel-major bf16 LDS tiles with the
+// swz_w swizzle), fragments read transposed with ds_read_b64_tr_b16 as in conv_wgrad_buf_kernel;
+// 128 x 128 (k, col) block tiles, the pixel axis split into slab partials (wgrad_reduce_kernel).
+__global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int PXT = 32, OPB = PXT * 256, STAGE = 4 * OPB;  // planes: dy hi, dy lo, x hi, x lo
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t ntn = (p.Ncol + 127) / 128;
+  const int64_t tile = blockIdx.x;
+  const int64_t mt = tile / ntn, nt = tile % ntn;
+  const int64_t k0 = mt * 128, c0 = nt * 128;
+  const int64_t pbeg = (int64_t)blockIdx.y * p.kchunk;
+  const int64_t pend = min<int64_t>(p.P, pbeg + p.kchunk);
+  if (pbeg >= pend) return;
+  const float* __restrict__ dy = (const float*)p.dy;
+  const float* __restrict__ x = (const float*)p.x;
+  const int ch = tid & 15;  // this thread's 8-wide chunk of the k columns (dy) and of the (r,s,c) columns (x)
+  const int64_t col = c0 + ch * 8;
+  const bool col_ok = col < p.Ncol;
+  const int tap = col_ok ? (int)(col / p.C) : 0;
+  const int cc = col_ok ? (int)(col - (int64_t)tap * p.C) : 0;
+  const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
+  const bool k_ok = (k0 + ch * 8) < p.K;
+  const int OW = (int)p.OW, OH = (int)p.OH, H = (int)p.H, W = (int)p.W;
+  int px_n[2], px_oh[2], px_ow[2];
+  int64_t px_i[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    px_i[i] = pbeg + (tid >> 4) + 16 * i;
+    const int64_t t = px_i[i] / OW;
+    px_ow[i] = (int)(px_i[i] - t * OW);
+    px_oh[i] = (int)(t % OH);
+    px_n[i] = (int)(t / OH);
+  }
+  float4 rd[2][2], rx[2][2];
+  auto load = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t px = px_i[i];
+      rd[i][0] = rd[i][1] = rx[i][0] = rx[i][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (px < pend) {
+        if (k_ok) {
+          const float* sp = dy + px * p.K + k0 + ch * 8;
+          rd[i][0] = *(const float4*)sp;
+          rd[i][1] = *(const float4*)(sp + 4);
+        }
+        if (col_ok) {
+          const int ih = px_oh[i] * p.st_h - p.pad_h + r, iw = px_ow[i] * p.st_w - p.pad_w + s;
+          if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+            const float* sp = x + (((int64_t)px_n[i] * H + ih) * W + iw) * p.C + cc;
+            rx[i][0] = *(const float4*)sp;
+            rx[i][1] = *(const float4*)(sp + 4);
+          }
+        }
+      }
+      px_i[i] += PXT;
+      px_ow[i] += PXT;
+      if (px_ow[i] >= OW) {  // small maps wrap several rows per tile
+        const int q = px_ow[i] / OW;
+        px_ow[i] -= q * OW;
+        px_oh[i] += q;
+        if (px_oh[i] >= OH) {
+          const int q2 = px_oh[i] / OH;
+          px_oh[i] -= q2 * OH;
+          px_n[i] += q2;
+        }
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    char* Dh = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (tid >> 4) + 16 * i;
+      const int off = row * 256 + (swz_w(row, ch) << 4);
+      uint4 h, l;
+      split8(rd[i][0], rd[i][1], h, l);
+      *(uint4*)(Dh + off) = h;
+      *(uint4*)(Dh + OPB + off) = l;
+      split8(rx[i][0], rx[i][1], h, l);
+      *(uint4*)(Dh + 2 * OPB + off) = h;
+      *(uint4*)(Dh + 3 * OPB + off) = l;
+    }
+  };
+  auto tr_read = [&](const char* T, int prow0, int colbase) -> s16x4 {
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int row = prow0 + 8 * g + q;
+    const int colx = colbase + 4 * pp;
+    const int chunk = colx >> 3, within = (colx & 7) * 2;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(T + row * 256 + (swz_w(row, chunk) << 4) + within));
+  };
+  auto frag = [&](const char* T, int colbase) -> bf16x8 {
+    const s16x4 lo = tr_read(T, 0, colbase), hi = tr_read(T, 4, colbase);
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nk = (pend - pbeg + PXT - 1) / PXT;
+  load();
+  store(0);
+  __syncthreads();
+  for (int64_t it = 0; it < nk; ++it) {
+    const int buf = (int)(it & 1);
+    if (it + 1 < nk) load();
+    const char* Dh = smem + buf * STAGE;
+    bf16x8 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ah[i] = frag(Dh, wm * 64 + i * 16);
+      al[i] = frag(Dh + OPB, wm * 64 + i * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bh[j] = frag(Dh + 2 * OPB, wn * 64 + j * 16);
+      bl[j] = frag(Dh + 3 * OPB, wn * 64 + j * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+    if (it + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+  wgrad_store(p, acc, k0, c0, wm, wn, lane);
+#endif
+}
+
 __global__ void transpose_w_kernel(const uint16_t* __restrict__ w, int64_t K, int64_t RS, int64_t C, uint16_t* __restrict__ wt) {
   // w[K][RS][C] -> wt[C][RS][K]
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1385,6 +1716,10 @@ struct PackP {
   int64_t off[4];
   int Rc[4], Sc[4];
   int dense;  // wt as [R][S][Cpad][Kpad]: the 1x1-GEMM dgrad operand of a conv whose output is 1x1
+  // split: bf16x3 operands -- every layout is written twice, plane 0 = bf16(w) (hi) and plane 1 =
+  // bf16(w - hi) (lo), the lo plane wk_plane / wt_plane elements after the hi plane
+  int split;
+  int64_t wk_plane, wt_plane;
   // tiling (pack_plan): wk tiles = kr output rows x cw input channels x all taps (nwk of them, first),
   // then wt tiles = 64 output channels x tct input channels x all taps
   int kr, cw, tct;
@@ -1416,10 +1751,16 @@ __device__ __forceinline__ void st_bf2(uint16_t* d, uint16_t a, uint16_t b, bool
   }
 }
 
+// plane 0 (hi) / 1 (lo) of the bf16x3 split of an f32 weight
+__device__ __forceinline__ uint16_t plane_bf(float v, int plane) {
+  const uint16_t h = f2bf(v);
+  return plane ? f2bf(v - bf2f(h)) : h;
+}
+
 // T[row * ldt + j] = bf16(w[(k0 + row) * C * RS + c0 * RS + j]) for j < n_valid (zero past the real
-// input channels / output rows); ldt % 4 == 0
+// input channels / output rows); ldt % 4 == 0. plane 1: the lo part bf16(w - bf16(w)).
 __device__ __forceinline__ void pack_stage(const PackP& p, int64_t k0, int64_t c0, int rows, int width, int ldt,
-                                           uint16_t* T) {
+                                           uint16_t* T, int plane) {
   const int RS = p.R * p.S;
   const int64_t cend = p.C < c0 + width / RS ? p.C : c0 + width / RS;
   const int nvalid = cend > c0 ? (int)((cend - c0) * RS) : 0;
@@ -1445,8 +1786,9 @@ __device__ __forceinline__ void pack_stage(const PackP& p, int64_t k0, int64_t c
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (dst[u] >= 0)
-          *(uint2*)(T + dst[u]) = make_uint2((uint32_t)f2bf(v[u].x) | ((uint32_t)f2bf(v[u].y) << 16),
-                                             (uint32_t)f2bf(v[u].z) | ((uint32_t)f2bf(v[u].w) << 16));
+          *(uint2*)(T + dst[u]) =
+              make_uint2((uint32_t)plane_bf(v[u].x, plane) | ((uint32_t)plane_bf(v[u].y, plane) << 16),
+                         (uint32_t)plane_bf(v[u].z, plane) | ((uint32_t)plane_bf(v[u].w, plane) << 16));
     }
     __syncthreads();
     return;
@@ -1466,18 +1808,19 @@ __device__ __forceinline__ void pack_stage(const PackP& p, int64_t k0, int64_t c
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (dst[u] >= 0) T[dst[u]] = f2bf(v[u]);
+      if (dst[u] >= 0) T[dst[u]] = plane_bf(v[u], plane);
   }
   __syncthreads();
 }
 
-__device__ __forceinline__ void pack_wk_tile(const PackP& p, int64_t t, uint16_t* T) {
+__device__ __forceinline__ void pack_wk_tile(const PackP& p, int64_t t, uint16_t* T, int plane) {
   const int RS = p.R * p.S;
   const int64_t nc = (p.Cpad + p.cw - 1) / p.cw;
   const int64_t k0 = (t / nc) * p.kr, c0 = (t % nc) * p.cw;
   const int cwv = (int)(p.Cpad - c0 < p.cw ? p.Cpad - c0 : p.cw);
   const int width = cwv * RS, ldt = width + 4;
-  pack_stage(p, k0, c0, p.kr, width, ldt, T);
+  pack_stage(p, k0, c0, p.kr, width, ldt, T, plane);
+  uint16_t* wk = p.wk + plane * p.wk_plane;
   const int h = (cwv + 1) >> 1, per = RS * h;  // channel pairs per (row, tap)
   const float inv_per = 1.f / (float)per, inv_h = 1.f / (float)h;
   for (int e = threadIdx.x; e < p.kr * per; e += 256) {
@@ -1487,16 +1830,17 @@ __device__ __forceinline__ void pack_wk_tile(const PackP& p, int64_t t, uint16_t
     if (k >= p.K) continue;
     const int cc = 2 * c2;
     const uint16_t* tt = T + row * ldt + cc * RS + rs;
-    st_bf2(p.wk + (k * RS + rs) * p.Cpad + c0 + cc, tt[0], cc + 1 < cwv ? tt[RS] : (uint16_t)0, cc + 1 < cwv);
+    st_bf2(wk + (k * RS + rs) * p.Cpad + c0 + cc, tt[0], cc + 1 < cwv ? tt[RS] : (uint16_t)0, cc + 1 < cwv);
   }
 }
 
-__device__ __forceinline__ void pack_wt_tile(const PackP& p, int64_t t, uint16_t* T) {
+__device__ __forceinline__ void pack_wt_tile(const PackP& p, int64_t t, uint16_t* T, int plane) {
   const int RS = p.R * p.S;
   const int64_t nc = (p.Cpad + p.tct - 1) / p.tct;
   const int64_t k0 = (t / nc) * PK, c0 = (t % nc) * p.tct;
   const int width = p.tct * RS, ldt = width + 4;
-  pack_stage(p, k0, c0, PK, width, ldt, T);
+  pack_stage(p, k0, c0, PK, width, ldt, T, plane);
+  uint16_t* wt = p.wt + plane * p.wt_plane;
   constexpr int PK2 = PK / 2;
   const int per = RS * PK2;
   const float inv_per = 1.f / (float)per;
@@ -1514,14 +1858,20 @@ __device__ __forceinline__ void pack_wt_tile(const PackP& p, int64_t t, uint16_t
       const int q = (r % p.st_h) * p.st_w + (sx % p.st_w);
       dst = p.off[q] + ((c * p.Rc[q] + r / p.st_h) * p.Sc[q] + sx / p.st_w) * p.Kpad + k;
     }
-    st_bf2(p.wt + dst, tt[0], tt[ldt], k + 1 < p.Kpad);
+    st_bf2(wt + dst, tt[0], tt[ldt], k + 1 < p.Kpad);
   }
 }
 
+// tiles: [planes][nwk] wk tiles, then [planes][nwt] wt tiles (planes = 2 when split)
 __device__ __forceinline__ void pack_tile(const PackP& p, int64_t t) {
   __shared__ uint16_t T[PACK_LDS];
-  if (t < p.nwk) pack_wk_tile(p, t, T);
-  else pack_wt_tile(p, t - p.nwk, T);
+  const int np = p.split ? 2 : 1;
+  if (t < np * p.nwk) {
+    pack_wk_tile(p, t % p.nwk, T, (int)(t / p.nwk));
+  } else {
+    t -= np * p.nwk;
+    pack_wt_tile(p, t % p.nwt, T, (int)(t / p.nwt));
+  }
 }
 
 __global__ void __launch_bounds__(256) pack_weight_kernel(PackP p) { pack_tile(p, blockIdx.x); }
@@ -1555,6 +1905,8 @@ static int pack_plan(PackP& p) {
   p.kr = (int)kr;
   p.nwk = p.wk ? cdiv(p.K, p.kr) * cdiv(p.Cpad, p.cw) : 0;
   p.nwt = p.wt ? cdiv(p.Kpad, (int64_t)PK) * cdiv(p.Cpad, (int64_t)p.tct) : 0;
+  p.wk_plane = p.K * RS * p.Cpad;
+  p.wt_plane = p.Cpad * RS * p.Kpad;
   return MX_OK;
 }
 
@@ -1914,7 +2266,7 @@ extern "C" size_t mx_conv_dgrad_weight_elems(const mx_conv_shape* s, int64_t Cpa
 }
 
 extern "C" int mx_conv_pack_weight(const mx_conv_shape* s, const float* w, int64_t Cin, int64_t Kout, uint16_t* wk,
-                                   uint16_t* wt, mx_stream_t stream) {
+                                   uint16_t* wt, int split, mx_stream_t stream) {
   // s->C / s->K are the padded channel counts the kernels see (Cin <= s->C real input channels,
   // Kout <= s->K real output channels of the f32 parameter w[Kout][Cin][R][S])
   MX_CHECK_ARG(s && w && s->R > 0 && s->S > 0 && Cin > 0 && Kout > 0 && Cin <= s->C && Kout <= s->K,
@@ -1934,7 +2286,8 @@ extern "C" int mx_conv_pack_weight(const mx_conv_shape* s, const float* w, int64
   }
   // wk covers Kout rows only; wt also covers the zero-padded output channels up to s->K
   MX_CHECK_ARG(pack_plan(p) == MX_OK, "conv pack: at most 196 taps");
-  const int64_t tiles = p.nwk + p.nwt;
+  p.split = split ? 1 : 0;
+  const int64_t tiles = (p.nwk + p.nwt) * (split ? 2 : 1);
   MX_CHECK_ARG(tiles < (1ll << 31), "conv pack: too many tiles");
   pack_weight_kernel<<<(unsigned)tiles, 256, 0, (hipStream_t)stream>>>(p);
   MX_LAUNCH_CHECK();
@@ -1951,6 +2304,7 @@ static int make_pack(const mx_pack_desc& d, PackP& p, int64_t& tiles) {
   p.K = d.Kout; p.C = d.Cin; p.Cpad = d.Cpad; p.Kpad = d.Kpad;
   p.R = d.R; p.S = d.S; p.st_h = d.stride_h; p.st_w = d.stride_w;
   p.dense = d.flags & 1;
+  p.split = (d.flags >> 1) & 1;
   if (d.wt && !p.dense) {
     mx_conv_shape s{};
     s.C = d.Cpad; s.K = d.Kpad; s.R = d.R; s.S = d.S; s.H = 1; s.W = 1;
@@ -1961,7 +2315,7 @@ static int make_pack(const mx_pack_desc& d, PackP& p, int64_t& tiles) {
     p.st_h = p.st_w = 1;
   }
   MX_CHECK_ARG(pack_plan(p) == MX_OK, "conv pack: at most 196 taps");
-  tiles = p.nwk + p.nwt;
+  tiles = (p.nwk + p.nwt) * (p.split ? 2 : 1);
   return MX_OK;
 }
 
@@ -2225,4 +2579,223 @@ extern "C" int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const
   rc = mx_conv2d_wgrad_ex(s, dy, x, dw, s->K, s->C, 0, ws, wsb, stream);
   if (ws) MX_HIP(hipFreeAsync(ws, (hipStream_t)stream));
   return rc;
+}
+
+// ================================================================================================
+// bf16x3 (f32 activation) entry points: same GEMM decompositions as the bf16 path (fwd, dgrad per
+// stride-parity class, wgrad split over pixels), f32 activations / gradients, split weights.
+static Geo make_geo_x3(int64_t M, int64_t Ncol, int64_t Kdim) {
+  Geo g;
+  g.M = M; g.Ncol = Ncol; g.Kdim = Kdim;
+  g.narrow = Ncol <= 64;
+  g.bn = g.narrow ? 64 : 128;
+  const int64_t cus = num_cus();
+  // 2 blocks per CU: below two full rounds of 128-row tiles, 64-row tiles (twice the blocks)
+  g.bmt = 128;
+  g.tiles = cdiv(M, 128) * cdiv(Ncol, g.bn);
+  if (g.tiles < 2 * cus) {
+    g.bmt = 64;
+    g.tiles = cdiv(M, 64) * cdiv(Ncol, g.bn);
+  }
+  if (g_force_bmt) {
+    g.bmt = g_force_bmt;
+    g.bn = std::min(g_force_bn, 128);
+    g.narrow = g.bn == 64;
+    g.tiles = cdiv(M, g.bmt) * cdiv(Ncol, g.bn);
+  }
+  g.nk = cdiv(Kdim, 32);
+  g.splits = 1;
+  if (Ncol % 8 == 0 && g.tiles < 320 && g.nk >= 8) {
+    int64_t sp = std::min<int64_t>(std::min<int64_t>(cdiv(640, g.tiles), g.nk / 4), 16);
+    g.splits = (int)std::max<int64_t>(1, sp);
+  }
+  if (g_max_splits && g.splits > g_max_splits) g.splits = g_max_splits;
+  return g;
+}
+
+template <int BN, int MODE, int BMT>
+static void launch_x3(const ConvP& p, int64_t blocks, hipStream_t st) {
+  const size_t ring = (size_t)2 * 2 * (BMT + BN) * 64;
+  const size_t epi = (size_t)(BMT / 2) * (BN + 4) * 4;
+  conv_x3_kernel<BN, MODE, BMT><<<(unsigned)blocks, NT, std::max(ring, epi), st>>>(p);
+}
+
+template <int MODE>
+static int launch_igemm_x3(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipStream_t st) {
+  int64_t blocks = g.tiles;
+  MX_CHECK_ARG(g.Kdim < (1ll << 30) && p.IH < (1ll << 26) && p.IW < (1ll << 26) && p.IC < (1ll << 30),
+               "conv: GEMM K or spatial size too large");
+  MX_CHECK_ARG(p.IC % 8 == 0 && p.Kdim % 8 == 0, "conv x3: channel counts must be multiples of 8");
+  const int64_t nk = cdiv(g.Kdim, 32);
+  p.splits = 1;
+  p.kt_per_split = nk;
+  p.slab = nullptr;
+  if (g.splits > 1) {
+    const size_t need = sizeof(float) * (size_t)g.splits * g.M * g.Ncol;
+    MX_CHECK_ARG(ws && ws_bytes >= need, "conv: split-K workspace of %zu bytes required (mx_conv_workspace_x3)", need);
+    p.kt_per_split = cdiv(nk, (int64_t)g.splits);
+    p.splits = (int)cdiv(nk, p.kt_per_split);
+    p.slab = (float*)ws;
+    blocks *= p.splits;
+  }
+  MX_CHECK_ARG(blocks < (1ll << 31), "conv: grid too large");
+  if (g.bmt == 64) {
+    if (g.bn == 64) launch_x3<64, MODE, 64>(p, blocks, st);
+    else launch_x3<128, MODE, 64>(p, blocks, st);
+  } else {
+    if (g.bn == 64) launch_x3<64, MODE, 128>(p, blocks, st);
+    else launch_x3<128, MODE, 128>(p, blocks, st);
+  }
+  MX_LAUNCH_CHECK();
+  if (p.slab) {
+    if (cdiv(g.M, BM) * cdiv(g.Ncol, 64) >= 2 * (int64_t)num_cus()) {
+      dim3 rg((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.Ncol, 64));
+      conv_splitk_reduce_kernel<8, float><<<rg, 256, 0, st>>>(p);
+    } else {
+      dim3 rg((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.Ncol, 16));
+      conv_splitk_reduce_kernel<2, float><<<rg, 256, 0, st>>>(p);
+    }
+    MX_LAUNCH_CHECK();
+  }
+  return MX_OK;
+}
+
+static WGeo wgrad_geo_x3(const mx_conv_shape* s) {
+  WGeo g;
+  const int64_t P = s->N * s->Ho * s->Wo, Ncol = s->R * s->S * s->C;
+  g.tiles = cdiv(s->K, 128) * cdiv(Ncol, 128);
+  g.pxt = 32;
+  const int64_t slots = g_wgrad_target ? g_wgrad_target : (int64_t)num_cus() * 2;
+  int64_t splits = std::max<int64_t>(1, slots / g.tiles);
+  const int64_t max_splits = std::max<int64_t>(1, P / (g.pxt * 4));
+  splits = std::min(splits, max_splits);
+  g.kchunk = cdiv(cdiv(P, splits), g.pxt) * g.pxt;
+  g.splits = cdiv(P, g.kchunk);
+  return g;
+}
+
+extern "C" size_t mx_conv_workspace_x3(const mx_conv_shape* s, int pass) {
+  if (!s || pass < 0 || pass > 2) return 0;
+  if (pass == 2) {
+    bool dense;
+    const mx_conv_shape sd = wgrad_shape(s, &dense);
+    const WGeo g = wgrad_geo_x3(&sd);
+    return g.splits > 1 ? sizeof(float) * (size_t)g.splits * sd.K * sd.R * sd.S * sd.C : 0;
+  }
+  if (pass == 0) {
+    const Geo g = make_geo_x3(s->N * s->Ho * s->Wo, s->K, s->R * s->S * s->C);
+    return g.splits > 1 ? sizeof(float) * (size_t)g.splits * g.M * g.Ncol : 0;
+  }
+  if (s->stride_h < 1 || s->stride_h > 2 || s->stride_w < 1 || s->stride_w > 2) return 0;
+  DClass cl[4];
+  int64_t off[4];
+  int br[4], bs[4];
+  const int n = dgrad_classes(s, s->C, s->K, cl, off, br, bs);
+  size_t mx = 0;
+  for (int i = 0; i < n; ++i) {
+    const Geo g = make_geo_x3(s->N * cl[i].Hc * cl[i].Wc, s->C, (int64_t)cl[i].Rc * cl[i].Sc * s->K);
+    if (g.splits > 1) mx = std::max(mx, sizeof(float) * (size_t)g.splits * g.M * g.Ncol);
+  }
+  return mx;
+}
+
+extern "C" int mx_conv2d_fwd_x3(const mx_conv_shape* s, const float* x, const uint16_t* w, const float* bias,
+                                const float* residual, int act, float* y, float* stats, void* ws, size_t ws_bytes,
+                                mx_stream_t stream) {
+  int rc = conv_check(s);
+  if (rc) return rc;
+  MX_CHECK_ARG(s->C % 8 == 0, "conv fwd x3: C=%lld must be a multiple of 8 (pad the input channels)", (long long)s->C);
+  MX_CHECK_ARG(s->K % 8 == 0 || !residual, "conv fwd x3: residual needs K %% 8 == 0");
+  MX_CHECK_ARG(x && w && y, "conv fwd x3: null operand");
+  ConvP p{};
+  p.src = (const uint16_t*)(const void*)x; p.wt = w;
+  p.M = s->N * s->Ho * s->Wo; p.Ncol = s->K; p.Kdim = s->R * s->S * s->C;
+  p.OH = s->Ho; p.OW = s->Wo; p.IH = s->H; p.IW = s->W; p.IC = s->C;
+  p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
+  p.bias = bias; p.residual = residual; p.act = act; p.out = y; p.out_f32 = 1;
+  p.stats = stats; p.mblocks = cdiv(p.M, SROWS);
+  p.src_elems = s->N * s->H * s->W * s->C; p.wt_elems = p.Ncol * p.Kdim; p.wt_plane = p.Ncol * p.Kdim;
+  return launch_igemm_x3<0>(p, make_geo_x3(p.M, p.Ncol, p.Kdim), ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int mx_conv2d_dgrad_x3(const mx_conv_shape* s, const float* dy, const uint16_t* wt, const float* residual,
+                                  float* dx, const float* y, const float* z, const float* mean, const float* invstd,
+                                  int act, float* part, int64_t part_mb, void* ws, size_t ws_bytes, mx_stream_t stream) {
+  int rc = conv_check(s);
+  if (rc) return rc;
+  MX_CHECK_ARG(s->K % 8 == 0 && s->C % 8 == 0, "conv dgrad x3: K and C must be multiples of 8");
+  MX_CHECK_ARG(s->stride_h <= 2 && s->stride_w <= 2, "conv dgrad x3: strides 1 and 2 are supported");
+  MX_CHECK_ARG(!residual || (s->stride_h == 1 && s->stride_w == 1), "conv dgrad x3: a residual needs stride 1");
+  const bool bnb = part != nullptr;
+  if (bnb) {
+    MX_CHECK_ARG(s->stride_h == 1 && s->stride_w == 1, "conv dgrad x3 bnb: stride 1 only");
+    MX_CHECK_ARG(y && z && mean && invstd && act >= 0 && act <= 2, "conv dgrad x3 bnb: bad BN arguments");
+    MX_CHECK_ARG(part_mb == cdiv(s->N * s->H * s->W, 64), "conv dgrad x3 bnb: part rows must be cdiv(N*H*W, 64)");
+  }
+  DClass cl[4];
+  int64_t off[4];
+  int br[4], bs[4];
+  const int n = dgrad_classes(s, s->C, s->K, cl, off, br, bs);
+  const bool remap = s->stride_h > 1 || s->stride_w > 1;
+  const int64_t plane = s->C * s->R * s->S * s->K;
+  for (int i = 0; i < n; ++i) {
+    const DClass& c = cl[i];
+    if (c.Hc * c.Wc == 0) continue;
+    ConvP p{};
+    p.src = (const uint16_t*)(const void*)dy; p.wt = wt + c.off; p.wt_plane = plane;
+    p.M = s->N * c.Hc * c.Wc; p.Ncol = s->C; p.Kdim = (int64_t)c.Rc * c.Sc * s->K;
+    p.OH = c.Hc; p.OW = c.Wc; p.IH = s->Ho; p.IW = s->Wo; p.IC = s->K;
+    p.R = std::max(c.Rc, 1); p.S = std::max(c.Sc, 1); p.st_h = 1; p.st_w = 1; p.pad_h = c.dh; p.pad_w = c.dw;
+    p.out = dx; p.out_f32 = 1; p.act = 0; p.residual = residual;
+    if (bnb) {
+      p.bnb_y = y; p.bnb_z = z; p.bnb_mean = mean; p.bnb_invstd = invstd; p.bnb_act = act; p.bnb_part = part;
+      p.bnb_mb = part_mb;
+    }
+    p.remap = remap; p.rst_h = s->stride_h; p.rst_w = s->stride_w; p.rph = c.ph; p.rpw = c.pw;
+    p.rH = s->H; p.rW = s->W;
+    p.src_elems = s->N * s->Ho * s->Wo * s->K; p.wt_elems = p.Ncol * p.Kdim;
+    rc = launch_igemm_x3<1>(p, make_geo_x3(p.M, p.Ncol, p.Kdim), ws, ws_bytes, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return MX_OK;
+}
+
+extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const float* x, float* dw, int64_t Kout,
+                                  int64_t Cin, int layout, void* ws, size_t ws_bytes, mx_stream_t stream) {
+  int rc = conv_check(s);
+  if (rc) return rc;
+  MX_CHECK_ARG(s->K % 8 == 0 && s->C % 8 == 0, "conv wgrad x3: K and C must be multiples of 8");
+  MX_CHECK_ARG(Kout >= 1 && Kout <= s->K && Cin >= 1 && Cin <= s->C, "conv wgrad x3: Kout/Cin out of range");
+  MX_CHECK_ARG(layout == 0 || layout == 1, "conv wgrad x3: layout 0 (KRSC) or 1 (KCRS)");
+  MX_CHECK_ARG(s->K * s->R * s->S * s->C < (1ll << 31), "conv wgrad x3: weight too large");
+  hipStream_t st = (hipStream_t)stream;
+  const int dC = (int)s->C, dRS = (int)(s->R * s->S);
+  bool dense;
+  const mx_conv_shape sd = wgrad_shape(s, &dense);
+  s = &sd;
+  WgP p{};
+  p.dy = (const uint16_t*)(const void*)dy; p.x = (const uint16_t*)(const void*)x; p.dw = dw;
+  p.P = s->N * s->Ho * s->Wo; p.K = s->K; p.Ncol = s->R * s->S * s->C;
+  p.OH = s->Ho; p.OW = s->Wo; p.H = s->H; p.W = s->W; p.C = s->C; p.N = s->N;
+  p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
+  p.Kout = Kout; p.Cin = Cin; p.layout = layout;
+  p.dC = dC; p.dRS = dRS;
+  const WGeo g = wgrad_geo_x3(s);
+  p.kchunk = g.kchunk;
+  if (g.splits > 1) {
+    const size_t need = sizeof(float) * (size_t)g.splits * p.K * p.Ncol;
+    MX_CHECK_ARG(ws && ws_bytes >= need, "conv wgrad x3: split workspace of %zu bytes required (mx_conv_workspace_x3)",
+                 need);
+    p.slab = (float*)ws;
+  }
+  MX_CHECK_ARG(g.tiles < (1ll << 31) && g.splits < 65536, "conv wgrad x3: grid too large");
+  dim3 grid((unsigned)g.tiles, (unsigned)g.splits);
+  conv_wgrad_x3_kernel<<<grid, NT, 2 * 4 * 32 * 256, st>>>(p);
+  MX_LAUNCH_CHECK();
+  if (g.splits > 1) {
+    MX_CHECK_ARG(Kout < 65536, "conv wgrad x3: too many output channels for the split reduce");
+    wgrad_reduce_kernel<<<dim3((unsigned)cdiv(p.Ncol / 4, 64), (unsigned)Kout), 256, 0, st>>>(p, (int)g.splits);
+    MX_LAUNCH_CHECK();
+  }
+  return MX_OK;
 }

@@ -28,22 +28,26 @@ __global__ void reflect_pad_kernel(const uint8_t* __restrict__ src, int64_t B, i
   dst[i] = src[((b * H + reflect(y, H)) * W + reflect(x, W)) * C + c];
 }
 
-// up [N,H,W,4*Cu] (i,j,co) + skip [N,2H,2W,Cs] -> out [N,2H,2W,Cu+Cs]; 8 channels per thread
-__global__ void up_concat_kernel(const uint16_t* __restrict__ up, const uint16_t* __restrict__ skip, int64_t N, int64_t H,
-                                 int64_t W, int64_t Cu, int64_t Cs, uint16_t* __restrict__ out) {
+// up [N,H,W,4*Cu] (i,j,co) + skip [N,2H,2W,Cs] -> out [N,2H,2W,Cu+Cs]; 8 channels per thread (a copy:
+// bf16 or f32 storage, 16 or 32 B per thread)
+template <typename T>
+__global__ void up_concat_kernel(const T* __restrict__ up, const T* __restrict__ skip, int64_t N, int64_t H,
+                                 int64_t W, int64_t Cu, int64_t Cs, T* __restrict__ out) {
   const int64_t Co = Cu + Cs, C8 = Co / 8;
   int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= N * 2 * H * 2 * W * C8) return;
   int64_t c0 = (e % C8) * 8, p = e / C8;
   int64_t x = p % (2 * W), y = (p / (2 * W)) % (2 * H), n = p / (4 * H * W);
-  uint4 v;
+  const T* src;
   if (c0 < Cu) {
     int64_t q = (y & 1) * 2 + (x & 1);
-    v = *(const uint4*)(up + ((n * H + (y >> 1)) * W + (x >> 1)) * 4 * Cu + q * Cu + c0);
+    src = up + ((n * H + (y >> 1)) * W + (x >> 1)) * 4 * Cu + q * Cu + c0;
   } else {
-    v = *(const uint4*)(skip + p * Cs + (c0 - Cu));
+    src = skip + p * Cs + (c0 - Cu);
   }
-  *(uint4*)(out + p * Co + c0) = v;
+  constexpr int V = sizeof(T) / 2;  // 16-B vectors per 8 elements
+#pragma unroll
+  for (int i = 0; i < V; ++i) ((uint4*)(out + p * Co + c0))[i] = ((const uint4*)src)[i];
 }
 
 __global__ void restore_finish_kernel(const uint8_t* __restrict__ img, int64_t B, int64_t Hp, int64_t Wp, const float* __restrict__ res,
@@ -73,12 +77,18 @@ extern "C" int mx_reflect_pad_u8(const uint8_t* src, int64_t B, int64_t H, int64
   return MX_OK;
 }
 
-extern "C" int mx_up_concat(const uint16_t* up, const uint16_t* skip, int64_t N, int64_t H, int64_t W, int64_t Cu, int64_t Cs,
-                            uint16_t* out, mx_stream_t stream) {
+template <typename T>
+static void up_concat_launch(const void* up, const void* skip, int64_t N, int64_t H, int64_t W, int64_t Cu, int64_t Cs,
+                             void* out, int64_t n, hipStream_t s) {
+  up_concat_kernel<T><<<(unsigned)cdiv(n, 256), 256, 0, s>>>((const T*)up, (const T*)skip, N, H, W, Cu, Cs, (T*)out);
+}
+
+extern "C" int mx_up_concat(const void* up, const void* skip, int dtype, int64_t N, int64_t H, int64_t W, int64_t Cu,
+                            int64_t Cs, void* out, mx_stream_t stream) {
   MX_CHECK_ARG(Cu % 8 == 0 && Cs % 8 == 0, "up_concat: channel counts must be multiples of 8");
   int64_t n = N * 4 * H * W * ((Cu + Cs) / 8);
   if (n == 0) return MX_OK;
-  up_concat_kernel<<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(up, skip, N, H, W, Cu, Cs, out);
+  MX_DT_DISPATCH(dtype, up_concat_launch, up, skip, N, H, W, Cu, Cs, out, n, (hipStream_t)stream);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

@@ -29,6 +29,7 @@ class ConvShape(ctypes.Structure):
 _SIGS = {
     "mx_version": (c_int, []),
     "mx_last_error": (ctypes.c_char_p, []),
+    "mx_trace_marker": (c_int, [c_int, c_vp]),
     "mx_match_workspace": (c_sz, [c_i64, c_i64]),
     "mx_match_assign": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_f, c_f, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                 c_vp, c_sz, c_vp]),
@@ -70,7 +71,7 @@ _SIGS = {
     "mx_conv2d_wgrad_ex": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp,
                                    ctypes.c_size_t, c_vp]),
     "mx_conv_transpose_weight": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
-    "mx_conv_pack_weight": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "mx_conv_pack_weight": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_int, c_vp]),
     "mx_conv_dgrad_weight_elems": (ctypes.c_size_t, [c_vp, c_i64, c_i64]),
     "mx_conv_pack_plan_bytes": (ctypes.c_size_t, [c_i64]),
     "mx_conv_pack_batched": (c_int, [c_vp, c_i64, c_vp, ctypes.c_size_t, c_int, c_vp]),
@@ -84,12 +85,12 @@ _SIGS = {
     "mx_bn_bwd_finalize": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_conv2d_dgrad_ex": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_conv2d_dgrad_t": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
-    "mx_maxpool_fwd": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
-    "mx_maxpool_bwd": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp]),
-    "mx_upsample_nearest_fwd": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
-    "mx_upsample_nearest_bwd": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "mx_maxpool_fwd": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
+    "mx_maxpool_bwd": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp]),
+    "mx_upsample_nearest_fwd": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "mx_upsample_nearest_bwd": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mx_reflect_pad_u8": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
-    "mx_up_concat": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "mx_up_concat": (c_int, [c_vp, c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mx_restore_finish": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mx_bn_finalize": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_vp]),
@@ -97,16 +98,23 @@ _SIGS = {
     "mx_bn_finalize_ex": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                   c_vp, ctypes.c_size_t, c_vp]),
     "mx_act_bias_bwd_workspace": (ctypes.c_size_t, [c_i64, c_i64]),
-    "mx_act_bias_bwd": (c_int, [c_vp, c_vp, c_int, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, ctypes.c_size_t,
-                                c_vp]),
+    "mx_act_bias_bwd": (c_int, [c_vp, c_vp, c_int, c_i64, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp,
+                                ctypes.c_size_t, c_vp]),
     "mx_sgd_step": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_f, c_f, c_int, c_vp]),
-    "mx_bn_apply": (c_int, [c_vp, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "mx_bn_apply": (c_int, [c_vp, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
     "mx_bn_bwd_reduce": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
     "mx_bn_bwd_apply": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_bn_bwd_workspace": (ctypes.c_size_t, [c_i64, c_i64]),
-    "mx_bn_bwd_reduce_ex": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, ctypes.c_size_t,
-                                    c_vp, c_vp, c_vp]),
-    "mx_bn_bwd_apply_ex": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "mx_bn_bwd_reduce_ex": (c_int, [c_vp, c_vp, c_vp, c_int, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp,
+                                    ctypes.c_size_t, c_vp, c_vp, c_vp]),
+    "mx_bn_bwd_apply_ex": (c_int, [c_vp, c_vp, c_vp, c_int, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "mx_conv_workspace_x3": (c_sz, [ctypes.POINTER(ConvShape), c_int]),
+    "mx_conv2d_fwd_x3": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_sz,
+                                 c_vp]),
+    "mx_conv2d_dgrad_x3": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                   c_vp, c_i64, c_vp, c_sz, c_vp]),
+    "mx_conv2d_wgrad_x3": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_sz,
+                                   c_vp]),
 }
 
 _lib = None
@@ -168,3 +176,8 @@ def stream():
     """The current HIP stream of the current device as a raw pointer (the C entry points enqueue on it)."""
     import torch
     return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
+
+
+def trace_marker(marker_id):
+    """Enqueue the empty marker kernel (mx_trace_marker) on the current stream."""
+    call("mx_trace_marker", int(marker_id), stream())

@@ -1,11 +1,18 @@
 """Op backend the detection model is written against.
 
-`HipBackend` (this file) is the product path: every hot op is a libmx_det HIP kernel on NHWC bf16
+`HipBackend` (this file) is the product path: every hot op is a libmx_det HIP kernel on NHWC
 activations. The model never calls torch conv/pool/RoI ops itself; it calls `self.be.*`. (A CPU
 restatement of the same interface lives in oracle/cpu_backend.py for parity tests and the CPU
 baseline; the product never imports it.)
+
+Precision (`HipBackend(precision=...)`, default from MX_PRECISION, else "f32"):
+  "f32"   the reference's arithmetic (fp32 model, TF32 convs on Ampere; train_frcnn_baseline.py:139-176,
+          no autocast): f32 activations / gradients / BN / RoIAlign, convs as bf16x3 MFMA products
+          (~2^-16 relative, finer than TF32's 2^-11)
+  "bf16"  bf16 activations and conv operands with f32 accumulation (faster, 2^-8 per rounding)
 """
 import ctypes
+import os
 
 import torch
 
@@ -31,7 +38,7 @@ class _MaxPool(torch.autograd.Function):
         Ho, Wo = (H + 2 * pd - k) // st + 1, (W + 2 * pd - k) // st + 1
         y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
         arg = torch.empty((N, Ho, Wo, C), dtype=torch.int32, device=x.device) if x.requires_grad else None
-        call("mx_maxpool_fwd", _p(x), N, H, W, C, k, st, pd, _p(y), _p(arg), _s())
+        call("mx_maxpool_fwd", _p(x), mc.dcode(x), N, H, W, C, k, st, pd, _p(y), _p(arg), _s())
         ctx.save_for_backward(arg)
         ctx.cfg = (x.shape, k, st, pd)
         return y
@@ -40,8 +47,9 @@ class _MaxPool(torch.autograd.Function):
     def backward(ctx, gy):
         (arg,) = ctx.saved_tensors
         (N, H, W, C), k, st, pd = ctx.cfg
-        gx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=gy.device)
-        call("mx_maxpool_bwd", _p(gy.contiguous()), _p(arg), N, H, W, C, k, st, pd, _p(gx), _s())
+        gy = gy.contiguous()
+        gx = torch.empty((N, H, W, C), dtype=gy.dtype, device=gy.device)
+        call("mx_maxpool_bwd", _p(gy), mc.dcode(gy), _p(arg), N, H, W, C, k, st, pd, _p(gx), _s())
         return gx, None, None, None
 
 
@@ -54,7 +62,9 @@ class _UpsampleAdd(torch.autograd.Function):
         N, H, W, C = x.shape
         y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
         a = add.contiguous() if add is not None else None
-        call("mx_upsample_nearest_fwd", _p(x), N, H, W, C, Ho, Wo, _p(a), _p(y), _s())
+        if a is not None:
+            assert a.dtype == x.dtype
+        call("mx_upsample_nearest_fwd", _p(x), mc.dcode(x), N, H, W, C, Ho, Wo, _p(a), _p(y), _s())
         ctx.cfg = (x.shape, Ho, Wo, add is not None)
         return y
 
@@ -62,30 +72,44 @@ class _UpsampleAdd(torch.autograd.Function):
     def backward(ctx, gy):
         (N, H, W, C), Ho, Wo, has_add = ctx.cfg
         g = gy.contiguous()
-        gx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=gy.device)
-        call("mx_upsample_nearest_bwd", _p(g), N, H, W, C, Ho, Wo, _p(gx), _s())
+        gx = torch.empty((N, H, W, C), dtype=g.dtype, device=gy.device)
+        call("mx_upsample_nearest_bwd", _p(g), mc.dcode(g), N, H, W, C, Ho, Wo, _p(gx), _s())
         return gx, (g if has_add else None), None, None
+
+
+def default_precision():
+    p = os.environ.get("MX_PRECISION", "f32").lower()
+    if p not in ("f32", "bf16"):
+        raise ValueError(f"MX_PRECISION must be f32 or bf16, got {p!r}")
+    return p
 
 
 class HipBackend:
     name = "hip"
-    act_dtype = torch.bfloat16
-    stem_channels = 8  # RGB padded to 8 channels for the 16-B gather of the stem conv
+    stem_channels = 8  # RGB padded to 8 channels for the 8-channel gather of the stem conv
+
+    def __init__(self, precision=None):
+        self.precision = precision or default_precision()
+        if self.precision not in ("f32", "bf16"):
+            raise ValueError(f"precision must be 'f32' or 'bf16', got {self.precision!r}")
+        self.act_dtype = torch.float32 if self.precision == "f32" else torch.bfloat16
 
     def prepare(self, model):
         """Register every conv weight of the model with one WeightPacker (first call) and repack the
         changed ones in a single launch; the conv autograd functions then read the packed operands."""
-        pk = model.__dict__.get("_mx_packer")
+        key = "_mx_packer_" + self.precision
+        pk = model.__dict__.get(key)
         if pk is None:
             from .frcnn import FastRCNNConvFCHead
+            split = self.precision == "f32"
             pk = mc.WeightPacker()
             for m in model.modules():
                 if isinstance(m, mc.Conv2d):
-                    pk.register(m.weight, m.stride, m.padding, m.weight.requires_grad)
+                    pk.register(m.weight, m.stride, m.padding, m.weight.requires_grad, split=split)
                 elif isinstance(m, FastRCNNConvFCHead):
                     for i, (lin, w) in enumerate(m.fc_weight_views()):
-                        pk.register(w, (1, 1), (0, 0), lin.weight.requires_grad, dense=i == 0)
-            model.__dict__["_mx_packer"] = pk
+                        pk.register(w, (1, 1), (0, 0), lin.weight.requires_grad, dense=i == 0, split=split)
+            model.__dict__[key] = pk
         mc.set_packer(pk)
         pk.refresh()
         bns = model.__dict__.get("_mx_bns")
@@ -105,7 +129,7 @@ class HipBackend:
     def bnb_link():
         return mc.BNBLink()
 
-    def conv(self, x, weight, bias, stride, pad, act, out_dtype=torch.bfloat16):
+    def conv(self, x, weight, bias, stride, pad, act, out_dtype=None):
         return mc.ConvAct.apply(x, weight, bias, stride, pad, act, out_dtype)
 
     def maxpool(self, x, k, stride, pad):
@@ -146,11 +170,12 @@ class HipBackend:
         return ops.normalize_pad(images_u8, padded_hw, channels=self.stem_channels, dtype=self.act_dtype)
 
 
-_default = None
+_default = {}
 
 
 def default_backend():
-    global _default
-    if _default is None:
-        _default = HipBackend()
-    return _default
+    """The process's HipBackend for the current MX_PRECISION (one instance per precision)."""
+    p = default_precision()
+    if p not in _default:
+        _default[p] = HipBackend(p)
+    return _default[p]

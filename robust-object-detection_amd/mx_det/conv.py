@@ -1,11 +1,16 @@
-"""Convolution + BatchNorm + activation on libmx_det's MFMA implicit-GEMM kernels (NHWC, bf16).
+"""Convolution + BatchNorm + activation on libmx_det's MFMA implicit-GEMM kernels (NHWC).
 
+Two arithmetic modes, chosen by the activation dtype:
+  f32   precision-faithful (the reference's fp32/TF32 convs, train_frcnn_baseline.py:139-176): f32
+        activations and gradients, every product as the bf16x3 split hi*hi + hi*lo + lo*hi on MFMA
+        (mx_conv2d_*_x3; weights packed as hi/lo bf16 planes)
+  bf16  bf16 activations and operands, f32 accumulation (mx_conv2d_*_ex)
 Autograd functions:
   ConvAct      conv (+bias) (+act)                      - RPN head convs, predictor / FC layers
   ConvBNAct    conv -> train-mode BatchNorm2d (+residual) (+act) - ResNet-50 body, FPN, box head
 The parameters keep torchvision's shapes ([Cout, Cin, kh, kw] conv weights, BatchNorm affine and
 running buffers), so state_dicts load both ways; the kernels take KRSC bf16 copies
-made once per step.
+(split into hi / lo planes in f32 mode) made once per step.
 """
 import ctypes
 import weakref
@@ -16,6 +21,21 @@ from . import _lib
 from ._lib import call
 
 ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
+MX_F32, MX_BF16 = 0, 1
+
+
+def dcode(t):
+    """libmx_det dtype code of an activation tensor."""
+    if t.dtype == torch.float32:
+        return MX_F32
+    if t.dtype == torch.bfloat16:
+        return MX_BF16
+    raise RuntimeError(f"unsupported activation dtype {t.dtype}")
+
+
+def is_x3(t):
+    """f32 activations run the precision-faithful bf16x3 kernels."""
+    return t.dtype == torch.float32
 
 
 def _s():
@@ -95,6 +115,10 @@ def weight_krsc(w, cin_pad=None):
 _FD_CANDS = ((0, 0, 0, 0), (0, 0, 1, 0), (0, 0, 2, 0), (64, 64, 0, 0), (64, 64, 1, 0), (128, 128, 1, 0),
              (0, 0, 1, 4), (0, 0, 0, 4), (128, 128, 1, 4))
 _WG_CANDS = ((3, 0), (3, 512), (3, 1024), (3, 384), (2, 0), (0, 0))  # (wgrad kernel variant, block target)
+# bf16x3 kernels (one kernel family: block tile x split-K cap; wgrad block target)
+_FD_CANDS_X3 = ((0, 0, 0, 0), (0, 0, 1, 0), (0, 0, 2, 0), (64, 128, 0, 0), (128, 128, 1, 0), (64, 64, 0, 0),
+                (64, 128, 1, 0))
+_WG_CANDS_X3 = ((3, 0), (3, 256), (3, 768), (3, 1024))
 _tune_cache = {}
 
 
@@ -168,10 +192,19 @@ def _tuned(key, cands, apply, run, default):
         apply(default)
 
 
-def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dtype=torch.bfloat16, stats=False):
-    """x NHWC bf16, wk KRSC bf16 -> y NHWC (out_dtype); optional BN stat partials."""
-    assert x.dtype == torch.bfloat16 and wk.dtype == torch.bfloat16 and x.is_contiguous() and wk.is_contiguous()
-    K, R, S, C = wk.shape
+def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dtype=None, stats=False):
+    """x NHWC, wk KRSC bf16 -> y NHWC; optional BN stat partials. bf16 x: wk [K,R,S,C], output
+    out_dtype (default bf16). f32 x (bf16x3): wk [2,K,R,S,C] hi / lo planes, output and residual f32."""
+    x3 = is_x3(x)
+    assert wk.dtype == torch.bfloat16 and x.is_contiguous() and wk.is_contiguous()
+    if x3:
+        assert wk.dim() == 5 and wk.shape[0] == 2, wk.shape
+        K, R, S, C = wk.shape[1:]
+        out_dtype = torch.float32
+    else:
+        assert x.dtype == torch.bfloat16 and wk.dim() == 4
+        K, R, S, C = wk.shape
+        out_dtype = out_dtype or torch.bfloat16
     assert x.shape[3] == C, (x.shape, wk.shape)
     sh = shape(x, K, R, S, stride, pad)
     y = torch.empty((sh.N, sh.Ho, sh.Wo, K), dtype=out_dtype, device=x.device)
@@ -181,36 +214,47 @@ def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dty
         st = torch.empty((2, mb, K), dtype=torch.float32, device=x.device)
     if residual is not None:
         residual = residual.contiguous()
+        assert residual.dtype == (torch.float32 if x3 else torch.bfloat16), residual.dtype
     t0 = _timer.start() if _timer else None
 
     def run():
+        if x3:
+            wsb = _lib.load().mx_conv_workspace_x3(ctypes.byref(sh), 0)
+            ws = torch.empty(wsb, dtype=torch.uint8, device=x.device) if wsb else None
+            call("mx_conv2d_fwd_x3", ctypes.byref(sh), _p(x), _p(wk), _p(bias), _p(residual), int(act), _p(y), _p(st),
+                 _p(ws), wsb, _s())
+            return
         wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 0)
         ws = torch.empty(wsb, dtype=torch.uint8, device=x.device) if wsb else None
         call("mx_conv2d_fwd_ex", ctypes.byref(sh), _p(x), _p(wk), _p(bias), _p(residual), int(act), _p(y),
              1 if out_dtype == torch.bfloat16 else 0, _p(st), _p(ws), wsb, _s())
 
-    key = ("fwd", sh.N, sh.H, sh.W, C, K, R, S, tuple(stride), tuple(pad), residual is not None, out_dtype)
-    _tuned(key, _FD_CANDS, _apply_fd, run, _FD_DEFAULT)
+    key = ("fwd", x.dtype, sh.N, sh.H, sh.W, C, K, R, S, tuple(stride), tuple(pad), residual is not None, out_dtype)
+    _tuned(key, _FD_CANDS_X3 if x3 else _FD_CANDS, _apply_fd, run, _FD_DEFAULT)
     if _timer:
-        _timer.stop("fwd128" if K > 64 else "fwd64", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * C, t0,
-                    _tag(sh.N, sh.H, sh.W, C, K, R, S, stride))
+        kind = ("x3_" if x3 else "") + ("fwd128" if K > 64 else "fwd64")
+        _timer.stop(kind, 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * C, t0, _tag(sh.N, sh.H, sh.W, C, K, R, S, stride))
     return (y, st) if stats else y
 
 
-def pack_weight(w, cin_pad=None, stride=(1, 1), pad=(0, 0), kpad=None, krsc=True, dgrad=False):
+def pack_weight(w, cin_pad=None, stride=(1, 1), pad=(0, 0), kpad=None, krsc=True, dgrad=False, split=False):
     """f32 [K,C,R,S] device parameter -> (wk, wt) in one kernel (mx_conv_pack_weight):
     wk [K,R,S,Cpad] bf16 (fwd operand) and wt, the dgrad operand (taps grouped by stride-parity
-    class, output channels zero-padded to kpad); either can be skipped."""
+    class, output channels zero-padded to kpad); either can be skipped. split: bf16x3 operands,
+    wk [2,K,R,S,Cpad] and wt [2 * Cpad*R*S*kpad] as hi / lo planes."""
     w = w.detach()
     if w.dtype != torch.float32 or not w.is_contiguous():
         w = w.float().contiguous()
     K, C, R, S = w.shape
     cp = cin_pad or C
     kp = kpad or K
+    np_ = 2 if split else 1
     sh = _lib.ConvShape(1, 1, 1, cp, kp, R, S, 1, 1, stride[0], stride[1], pad[0], pad[1])
-    wk = torch.empty((K, R, S, cp), dtype=torch.bfloat16, device=w.device) if krsc else None
-    wt = torch.empty(cp * R * S * kp, dtype=torch.bfloat16, device=w.device) if dgrad else None
-    call("mx_conv_pack_weight", ctypes.byref(sh), _p(w), C, K, _p(wk), _p(wt), _s())
+    wk = None
+    if krsc:
+        wk = torch.empty(((2,) if split else ()) + (K, R, S, cp), dtype=torch.bfloat16, device=w.device)
+    wt = torch.empty(np_ * cp * R * S * kp, dtype=torch.bfloat16, device=w.device) if dgrad else None
+    call("mx_conv_pack_weight", ctypes.byref(sh), _p(w), C, K, _p(wk), _p(wt), int(split), _s())
     return wk, wt
 
 
@@ -226,14 +270,15 @@ class PackDesc(ctypes.Structure):
 
 
 class _Entry:
-    __slots__ = ("w", "cp", "kp", "stride", "pad", "wk", "wt", "version", "dense")
+    __slots__ = ("w", "cp", "kp", "stride", "pad", "wk", "wt", "version", "dense", "split")
 
 
 class WeightPacker:
     """Per-step bf16 conv operands of a whole model, packed in ONE launch (mx_conv_pack_batched).
 
     Weights are registered once (f32 parameter or a view of one, its padded channel counts, stride,
-    pad, whether the dgrad layout is needed); `refresh()` repacks exactly the entries whose version
+    pad, whether the dgrad layout is needed, bf16x3 hi/lo planes or not); `refresh()` repacks
+    exactly the entries whose version
     counter moved since they were packed (optimizer step, load_state_dict) -- frozen layers are
     packed once. ConvAct / ConvBNAct take their operands from here when registered and fall back
     to a per-call pack_weight otherwise. Buffers are rewritten in place on the stream, so a
@@ -247,15 +292,15 @@ class WeightPacker:
         self._descs = None
 
     @staticmethod
-    def key(w, cp, kp, stride, pad):
-        return (w.data_ptr(), tuple(w.shape), cp, kp, tuple(stride), tuple(pad))
+    def key(w, cp, kp, stride, pad, split=False):
+        return (w.data_ptr(), tuple(w.shape), cp, kp, tuple(stride), tuple(pad), bool(split))
 
-    def register(self, w, stride, pad, dgrad, dense=False):
+    def register(self, w, stride, pad, dgrad, dense=False, split=False):
         """dense: the conv covers its whole input (output 1x1, e.g. FC6 as a 7x7 conv on the RoI tile);
-        its dgrad operand is laid out for the 1x1-GEMM form."""
+        its dgrad operand is laid out for the 1x1-GEMM form. split: bf16x3 hi / lo planes."""
         K, C, R, S = w.shape
         cp, kp = _ceil8(C), _ceil8(K)
-        k = self.key(w, cp, kp, stride, pad)
+        k = self.key(w, cp, kp, stride, pad, split)
         if k in self.entries:
             return
         e = _Entry()
@@ -263,8 +308,10 @@ class WeightPacker:
         # FC7) must not keep its autograd node -- and the parameter's AccumulateGrad node, bound to
         # the stream it was created on -- alive across steps and graph captures
         e.w, e.cp, e.kp, e.stride, e.pad, e.dense = w.detach(), cp, kp, tuple(stride), tuple(pad), bool(dense)
-        e.wk = torch.empty((K, R, S, cp), dtype=torch.bfloat16, device=w.device)
-        e.wt = torch.empty(cp * R * S * kp, dtype=torch.bfloat16, device=w.device) if dgrad else None
+        e.split = bool(split)
+        np_ = 2 if split else 1
+        e.wk = torch.empty(((2,) if split else ()) + (K, R, S, cp), dtype=torch.bfloat16, device=w.device)
+        e.wt = torch.empty(np_ * cp * R * S * kp, dtype=torch.bfloat16, device=w.device) if dgrad else None
         e.version = None
         self.entries[k] = e
         self.order.append(k)
@@ -281,7 +328,7 @@ class WeightPacker:
                 K, C, R, S = e.w.shape
                 descs[i] = PackDesc(e.w.data_ptr(), e.wk.data_ptr(), e.wt.data_ptr() if e.wt is not None else None,
                                     C, K, e.cp, e.kp, R, S, e.stride[0], e.stride[1], e.pad[0], e.pad[1],
-                                    1 if e.dense else 0)
+                                    (1 if e.dense else 0) | (2 if e.split else 0))
             nb = _lib.load().mx_conv_pack_plan_bytes(len(dirty))
             self._plan = torch.empty(nb, dtype=torch.uint8, device=self.entries[dirty[0]].w.device)
             self._descs = descs
@@ -292,8 +339,8 @@ class WeightPacker:
             e = self.entries[k]
             e.version = e.w._version
 
-    def lookup(self, w, cp, kp, stride, pad, dgrad, dense=False):
-        e = self.entries.get(self.key(w, cp, kp, stride, pad))
+    def lookup(self, w, cp, kp, stride, pad, dgrad, dense=False, split=False):
+        e = self.entries.get(self.key(w, cp, kp, stride, pad, split))
         if e is None or e.version != w._version or (dgrad and (e.wt is None or e.dense != dense)):
             return None
         return e.wk, e.wt
@@ -307,19 +354,20 @@ def set_packer(p):
     _packer = p
 
 
-def operands(w, cin_pad, stride, pad, kpad, dgrad, dense=False):
+def operands(w, cin_pad, stride, pad, kpad, dgrad, dense=False, split=False):
     """(wk, wt) for a conv weight: from the model's WeightPacker when registered and current, else
     packed now (one launch; the dense dgrad layout by a transpose of wk)."""
     if _packer is not None:
-        r = _packer.lookup(w, cin_pad, kpad, stride, pad, dgrad, dense)
+        r = _packer.lookup(w, cin_pad, kpad, stride, pad, dgrad, dense, split)
         if r is not None:
             return r
     if dense and dgrad:
-        wk, _ = pack_weight(w, cin_pad, stride, pad)
-        K = wk.shape[0]
-        wt = torch.nn.functional.pad(wk.reshape(K, -1).t(), (0, kpad - K)).contiguous().view(-1)
+        wk, _ = pack_weight(w, cin_pad, stride, pad, split=split)
+        K = w.shape[0]
+        planes = wk.view(2 if split else 1, K, -1)
+        wt = torch.nn.functional.pad(planes.transpose(1, 2), (0, kpad - K)).contiguous().view(-1)
         return wk, wt
-    return pack_weight(w, cin_pad, stride, pad, kpad=kpad, dgrad=dgrad)
+    return pack_weight(w, cin_pad, stride, pad, kpad=kpad, dgrad=dgrad, split=split)
 
 
 def _is_dense(x_shape, R, S, stride, pad):
@@ -328,24 +376,33 @@ def _is_dense(x_shape, R, S, stride, pad):
 
 
 def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
-    """dy NHWC bf16 [N,Ho,Wo,K] (K = the wt's padded output channels), wt from
-    pack_weight(dgrad=True) -> dx NHWC bf16 [N,H,W,C] (+ residual, a bf16 tensor of dx's shape added
-    in the epilogue; stride 1)."""
+    """dy NHWC [N,Ho,Wo,K] (K = the wt's padded output channels), wt from pack_weight(dgrad=True)
+    -> dx NHWC [N,H,W,C] of dy's dtype (+ residual, a tensor of dx's shape and dtype added in the
+    epilogue; stride 1). f32 dy: bf16x3 kernels on the split wt."""
     N, H, W, C = x_shape
     K = dy.shape[3]
-    assert wt.numel() == C * R * S * K, (wt.numel(), C, R, S, K)
+    x3 = is_x3(dy)
+    assert wt.numel() == (2 if x3 else 1) * C * R * S * K, (wt.numel(), C, R, S, K)
     Ho, Wo = out_hw(H, W, R, S, stride, pad)
     sh = _lib.ConvShape(N, H, W, C, K, R, S, Ho, Wo, stride[0], stride[1], pad[0], pad[1])
-    dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=dy.device)
+    dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
     dyc = dy.contiguous()
     t0 = _timer.start() if _timer else None
     if residual is not None:
-        assert residual.dtype == torch.bfloat16 and residual.shape == dx.shape and residual.is_contiguous()
+        assert residual.dtype == dy.dtype and residual.shape == dx.shape and residual.is_contiguous()
     part, mb = None, (N * H * W + 63) // 64
     if bnb is not None:  # dx is the gradient of a train-mode BN output: its backward partials too
         part = torch.empty((2, mb, C), dtype=torch.float32, device=dy.device)
 
     def run():
+        if x3:
+            wsb = _lib.load().mx_conv_workspace_x3(ctypes.byref(sh), 1)
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dy.device) if wsb else None
+            b = bnb if part is not None else None
+            call("mx_conv2d_dgrad_x3", ctypes.byref(sh), _p(dyc), _p(wt), _p(residual), _p(dx),
+                 _p(b.y) if b else None, _p(b.z) if b else None, _p(b.mean) if b else None,
+                 _p(b.invstd) if b else None, int(b.act) if b else 0, _p(part), mb, _p(ws), wsb, _s())
+            return
         wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 1)
         ws = torch.empty(wsb, dtype=torch.uint8, device=dy.device) if wsb else None
         if part is not None:
@@ -354,12 +411,13 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
         else:
             call("mx_conv2d_dgrad_ex", ctypes.byref(sh), _p(dyc), _p(wt), _p(residual), _p(dx), _p(ws), wsb, _s())
 
-    key = ("dgrad", N, H, W, C, K, R, S, tuple(stride), tuple(pad), residual is not None, part is not None)
-    _tuned(key, _FD_CANDS, _apply_fd, run, _FD_DEFAULT)
+    key = ("dgrad", dy.dtype, N, H, W, C, K, R, S, tuple(stride), tuple(pad), residual is not None, part is not None)
+    _tuned(key, _FD_CANDS_X3 if x3 else _FD_CANDS, _apply_fd, run, _FD_DEFAULT)
     if part is not None:
         bnb.part = part
     if _timer:
-        _timer.stop("dgrad", 2.0 * N * Ho * Wo * K * R * S * C, t0, _tag(N, H, W, C, K, R, S, stride))
+        _timer.stop(("x3_" if x3 else "") + "dgrad", 2.0 * N * Ho * Wo * K * R * S * C, t0,
+                    _tag(N, H, W, C, K, R, S, stride))
     return dx
 
 
@@ -426,26 +484,31 @@ def _join_side():
 
 
 def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False):
-    """dy NHWC bf16 [N,Ho,Wo,K], x NHWC bf16 -> dW f32 [kout, cin, R, S] (torch weight layout; the
-    zero-padded channels K > kout, C > cin are dropped). side=True (inside a backward pass only):
-    launched on the side stream, joined at the end of the backward."""
+    """dy NHWC [N,Ho,Wo,K], x NHWC (both bf16, or both f32 -> bf16x3 kernels) -> dW f32
+    [kout, cin, R, S] (torch weight layout; the zero-padded channels K > kout, C > cin are dropped).
+    side=True (inside a backward pass only): launched on the side stream, joined at the end of the
+    backward."""
     sh = shape(x, K, R, S, stride, pad)
     kout = kout or K
     cin = cin or x.shape[3]
+    x3 = is_x3(x)
+    assert dy.dtype == x.dtype, (dy.dtype, x.dtype)
+    wsfn = "mx_conv_workspace_x3" if x3 else "mx_conv_workspace"
+    entry = "mx_conv2d_wgrad_x3" if x3 else "mx_conv2d_wgrad_ex"
     dw = torch.empty((kout, cin, R, S), dtype=torch.float32, device=x.device)
     dyc = dy.contiguous()
     t0 = _timer.start() if _timer else None
-    key = ("wgrad", sh.N, sh.H, sh.W, x.shape[3], K, R, S, tuple(stride), tuple(pad))
+    key = ("wgrad", x.dtype, sh.N, sh.H, sh.W, x.shape[3], K, R, S, tuple(stride), tuple(pad))
     if key not in _tune_cache and _tune_on() and _timer is None and not torch.cuda.is_current_stream_capturing():
         def trial():  # timed on the current stream; the real launch below may go to the side stream
-            wsb_ = _lib.load().mx_conv_workspace(ctypes.byref(sh), 2)
+            wsb_ = getattr(_lib.load(), wsfn)(ctypes.byref(sh), 2)
             ws_ = torch.empty(wsb_, dtype=torch.uint8, device=x.device) if wsb_ else None
-            call("mx_conv2d_wgrad_ex", ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws_), wsb_, _s())
-        _tuned(key, _WG_CANDS, _apply_wg, trial, _WG_DEFAULT)
+            call(entry, ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws_), wsb_, _s())
+        _tuned(key, _WG_CANDS_X3 if x3 else _WG_CANDS, _apply_wg, trial, _WG_DEFAULT)
     tune = _tune_on()
     if tune:
         _apply_wg(_tune_cache.get(key, _WG_DEFAULT))
-    wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 2)
+    wsb = getattr(_lib.load(), wsfn)(ctypes.byref(sh), 2)
     ws = torch.empty(wsb, dtype=torch.uint8, device=x.device) if wsb else None
     stream = _s()
     if side:
@@ -454,7 +517,7 @@ def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False):
             st = _side[x.device] = torch.cuda.Stream(device=x.device)
         st.wait_stream(torch.cuda.current_stream())
         stream = st.cuda_stream
-    call("mx_conv2d_wgrad_ex", ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws), wsb, stream)
+    call(entry, ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws), wsb, stream)
     if tune:
         _apply_wg(_WG_DEFAULT)
     if side:
@@ -466,30 +529,32 @@ def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False):
         # reference (an extra one makes it clone dw on the main stream, before the side kernel ran)
         _pending.append((ev, (dyc, x, ws)))
     if _timer:
-        _timer.stop("wgrad", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * x.shape[3], t0,
+        _timer.stop(("x3_" if x3 else "") + "wgrad", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * x.shape[3], t0,
                     _tag(sh.N, sh.H, sh.W, x.shape[3], K, R, S, stride))
     return dw
 
 
-def act_bias_bwd(gy, y, act, K8, need_db):
-    """(g, db): g = gy * act'(y) as bf16 [..., K8] (zero-padded columns), db = sum of g over all but
-    the last dim (f32, or None) -- one launch (mx_act_bias_bwd)."""
+def act_bias_bwd(gy, y, act, K8, need_db, g_dtype=torch.bfloat16):
+    """(g, db): g = gy * act'(y) as g_dtype [..., K8] (zero-padded columns; the dgrad/wgrad operand:
+    bf16, or f32 for the bf16x3 path), db = sum of g over all but the last dim (f32, or None) --
+    one launch (mx_act_bias_bwd)."""
     K = gy.shape[-1]
     gy = gy.contiguous()
     M = gy.numel() // K
     assert gy.dtype in (torch.bfloat16, torch.float32) and y.dtype == gy.dtype and y.shape == gy.shape
-    g = torch.empty(gy.shape[:-1] + (K8,), dtype=torch.bfloat16, device=gy.device)
+    g = torch.empty(gy.shape[:-1] + (K8,), dtype=g_dtype, device=gy.device)
     db = torch.empty(K, dtype=torch.float32, device=gy.device) if need_db else None
     ws = None
     if need_db:
         ws = bn_scratch(_lib.load().mx_act_bias_bwd_workspace(M, K), gy.device)
-    call("mx_act_bias_bwd", _p(gy), _p(y.contiguous()) if act else None, 1 if gy.dtype == torch.bfloat16 else 0,
-         M, K, K8, int(act), _p(g), _p(db), _p(ws), ws.numel() if ws is not None else 0, _s())
+    call("mx_act_bias_bwd", _p(gy), _p(y.contiguous()) if act else None, dcode(gy), M, K, K8, int(act), _p(g),
+         dcode(g), _p(db), _p(ws), ws.numel() if ws is not None else 0, _s())
     return g, db
 
 
 class ConvAct(torch.autograd.Function):
-    """y = act(conv(x, w) + b). x NHWC bf16; w [K,C,R,S] f32 parameter; b f32 [K] or None."""
+    """y = act(conv(x, w) + b). x NHWC (bf16, or f32: bf16x3); w [K,C,R,S] f32 parameter; b f32 [K]
+    or None."""
 
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, act, out_dtype):
@@ -497,7 +562,7 @@ class ConvAct(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         dense = _is_dense(x.shape, w.shape[2], w.shape[3], stride, pad)
         # narrow heads (RPN cls+box 15, predictor 35): the dgrad operand is zero-padded to K8
-        wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(K), need_dx, dense)
+        wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(K), need_dx, dense, split=is_x3(x))
         y = conv_fwd(x, wk, stride, pad, bias=b.detach() if b is not None else None, act=act, out_dtype=out_dtype)
         ctx.save_for_backward(x, y, wt if need_dx else None)
         ctx.cfg = (stride, pad, act, w.shape, b is not None)
@@ -511,7 +576,7 @@ class ConvAct(torch.autograd.Function):
         K, _, R, S = wshape
         dx = dw = db = None
         K8 = (K + 7) // 8 * 8
-        gk, db = act_bias_bwd(gy, y, act, K8, has_b and ctx.needs_input_grad[2])
+        gk, db = act_bias_bwd(gy, y, act, K8, has_b and ctx.needs_input_grad[2], g_dtype=x.dtype)
         if ctx.needs_input_grad[0]:
             if _is_dense(x.shape, R, S, stride, pad):  # 1x1-GEMM form: dX[N, R*S*C] = dY[N, K8] wt
                 N, H, W, C = x.shape
@@ -546,9 +611,9 @@ class ConvBNAct(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         ctx.link, ctx.role = link if link is not None else (None, None)
         ctx.bnb_own, ctx.bnb_feed = bnb_own, bnb_feed
-        wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(w.shape[0]), need_dx)
+        wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(w.shape[0]), need_dx, split=is_x3(x))
         z, st = conv_fwd(x, wk, stride, pad, stats=True)
-        K = wk.shape[0]
+        K = w.shape[0]
         M = z.numel() // K
         mean = torch.empty(K, dtype=torch.float32, device=x.device)
         invstd, scale, shift = torch.empty_like(mean), torch.empty_like(mean), torch.empty_like(mean)
@@ -560,9 +625,9 @@ class ConvBNAct(torch.autograd.Function):
         y = torch.empty_like(z)
         res = residual.contiguous() if residual is not None else None
         t0 = _timer.start() if _timer else None
-        call("mx_bn_apply", _p(z), 1, M, K, _p(scale), _p(shift), _p(res), int(act), _p(y), _s())
+        call("mx_bn_apply", _p(z), dcode(z), M, K, _p(scale), _p(shift), _p(res), int(act), _p(y), dcode(y), _s())
         if _timer:  # bn kinds record algorithmic HBM bytes instead of FLOPs
-            _timer.stop("bn_apply", M * K * (4 + (2 if res is not None else 0)), t0, f"{M}x{K}")
+            _timer.stop("bn_apply", M * K * z.element_size() * (2 + (1 if res is not None else 0)), t0, f"{M}x{K}")
         ctx.save_for_backward(x, wt if need_dx else None, z, y, mean, invstd, gamma)
         ctx.cfg = (stride, pad, act, w.shape, residual is not None)
         if bnb_own is not None:  # the next conv's dgrad will produce this BN's backward partials
@@ -576,7 +641,7 @@ class ConvBNAct(torch.autograd.Function):
         stride, pad, act, wshape, has_res = ctx.cfg
         K, _, R, S = wshape
         M = z.numel() // K
-        gy = gy.to(torch.bfloat16).contiguous()
+        gy = gy.to(z.dtype).contiguous()
         sums = torch.empty((2, K), dtype=torch.float32, device=z.device)
         coef = torch.empty((3, K), dtype=torch.float32, device=z.device)
         own = ctx.bnb_own
@@ -590,16 +655,16 @@ class ConvBNAct(torch.autograd.Function):
             wsb = _lib.load().mx_bn_bwd_workspace(M, K)
             ws = bn_scratch(wsb, z.device)
             t0 = _timer.start() if _timer else None
-            call("mx_bn_bwd_reduce_ex", _p(gy), _p(y), _p(z), M, K, int(act), _p(mean), _p(invstd),
+            call("mx_bn_bwd_reduce_ex", _p(gy), _p(y), _p(z), dcode(z), M, K, int(act), _p(mean), _p(invstd),
                  _p(gamma.detach()), _p(ws), ws.numel(), _p(sums), _p(coef), _s())
             if _timer:
-                _timer.stop("bn_bwd_reduce", M * K * (6 if act else 4), t0, f"{M}x{K}")
+                _timer.stop("bn_bwd_reduce", M * K * z.element_size() * (3 if act else 2), t0, f"{M}x{K}")
         dz = torch.empty_like(z)
         dres = torch.empty_like(z) if has_res else None
         t0 = _timer.start() if _timer else None
-        call("mx_bn_bwd_apply_ex", _p(gy), _p(y), _p(z), M, K, int(act), _p(coef), _p(dz), _p(dres), _s())
+        call("mx_bn_bwd_apply_ex", _p(gy), _p(y), _p(z), dcode(z), M, K, int(act), _p(coef), _p(dz), _p(dres), _s())
         if _timer:
-            _timer.stop("bn_bwd_apply", M * K * (8 + (2 if has_res else 0)), t0, f"{M}x{K}")
+            _timer.stop("bn_bwd_apply", M * K * z.element_size() * (4 + (1 if has_res else 0)), t0, f"{M}x{K}")
         dx = dw = None
         link = ctx.link
         if ctx.role == "sink" and dres is not None:
@@ -620,9 +685,10 @@ class ConvBNAct(torch.autograd.Function):
 
 
 class Conv2d(torch.nn.Module):
-    """nn.Conv2d-compatible parameters (state_dict keys weight/bias), NHWC bf16 activations."""
+    """nn.Conv2d-compatible parameters (state_dict keys weight/bias), NHWC activations. out_dtype None:
+    the activation dtype of the input (bf16 or f32)."""
 
-    def __init__(self, cin, cout, k, stride=1, padding=0, bias=True, act=ACT_NONE, out_dtype=torch.bfloat16):
+    def __init__(self, cin, cout, k, stride=1, padding=0, bias=True, act=ACT_NONE, out_dtype=None):
         super().__init__()
         k = (k, k) if isinstance(k, int) else tuple(k)
         self.stride = (stride, stride) if isinstance(stride, int) else tuple(stride)
@@ -736,5 +802,5 @@ def fold_bn(conv, bn):
 
 def eval_conv_bn(x, conv, bn, act, residual=None):
     w, b = fold_bn(conv, bn)
-    wk, _ = pack_weight(w, x.shape[3], conv.stride, conv.padding)
+    wk, _ = pack_weight(w, x.shape[3], conv.stride, conv.padding, split=is_x3(x))
     return conv_fwd(x.contiguous(), wk, conv.stride, conv.padding, bias=b, residual=residual, act=act)

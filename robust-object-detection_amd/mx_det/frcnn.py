@@ -1,4 +1,5 @@
-"""Faster R-CNN ResNet-50-FPN v2 on the libmx_det HIP backend (NHWC, bf16 activations).
+"""Faster R-CNN ResNet-50-FPN v2 on the libmx_det HIP backend (NHWC activations: f32 with bf16x3 conv
+products by default, or bf16; mx_det.backend).
 
 Drop-in for what the reference builds at scripts/train_frcnn_baseline.py:139-143 and
 scripts/eval_all.py:79-87:
@@ -227,10 +228,13 @@ class BalancedPositiveNegativeSampler:
     per image min(#pos, B*frac) positives (label >= 1) and min(#neg, B - num_pos) negatives (label 0),
     each drawn uniformly without replacement. The draw takes the k smallest of i.i.d. uniform keys (a
     uniform random subset, as randperm(n)[:k] is) and keeps the counts on the device, so sampling
-    never waits for the GPU. labels: [N, L] (padding -1) -> boolean masks (pos, neg) of that shape."""
+    never waits for the GPU. labels: [N, L] (padding -1) -> boolean masks (pos, neg) of that shape.
+    `rand(shape, device)` draws the keys (default torch.rand on the device generator); a parity test
+    injects the same key stream into two backends, as SURVEY.md §7 prescribes for the randperm."""
 
     def __init__(self, batch_size_per_image, positive_fraction):
         self.batch, self.frac = batch_size_per_image, positive_fraction
+        self.rand = None
 
     def __call__(self, lab, be=None):
         """be: a backend with level_topk draws the k smallest keys with it (used for the RoI sampler's
@@ -241,7 +245,7 @@ class BalancedPositiveNegativeSampler:
         P = int(self.batch * self.frac)
         num_pos = pos.sum(1).clamp(max=P)
         num_neg = torch.minimum(neg.sum(1), self.batch - num_pos)
-        r = torch.rand(lab.shape, device=lab.device)
+        r = self.rand(lab.shape, lab.device) if self.rand is not None else torch.rand(lab.shape, device=lab.device)
         return self._pick(pos, r, min(P, L), num_pos, be), self._pick(neg, r, min(self.batch, L), num_neg, be)
 
     @staticmethod

@@ -2,7 +2,8 @@
 
 Same module tree and state_dict keys as the reference (down1.conv.block.{0,1,3,4}.*, up4.up.*,
 out_conv.*; 118 entries incl. BN buffers), so experiments/restoration/best.pth loads unchanged.
-Eval forward, NHWC bf16 activations:
+Eval forward, NHWC activations: f32 with bf16x3 conv products (precision "f32", the default: the
+reference runs the U-Net in fp32, restore_testsets.py:64-68) or bf16 ("bf16"):
   ConvBlock  = 2 x [conv3x3 with eval-BN folded into weights+bias, LeakyReLU(0.2) fused in the epilogue]
   MaxPool2d(2), ConvTranspose2d(2, s2) as a 1x1 MFMA conv to 4*Cout channels + fused pixel-shuffle/concat,
   out_conv 1x1 (f32 out) + clamp(x + residual, 0, 1).
@@ -29,6 +30,14 @@ def _p(t):
     return t.data_ptr() if t is not None else None
 
 
+def _wk(w, cin, x):
+    """The conv operand of an f32 [K,C,R,S] weight for activations like x: hi/lo split planes
+    (device pack kernel) for f32 x, a KRSC bf16 copy for bf16 x."""
+    if mc.is_x3(x):
+        return mc.pack_weight(w.contiguous(), cin, split=True)[0]
+    return mc.weight_krsc(w, cin)
+
+
 class ConvBlock(nn.Module):
     def __init__(self, in_ch, out_ch):
         super().__init__()
@@ -40,14 +49,14 @@ class ConvBlock(nn.Module):
         for ci, bi in ((0, 1), (3, 4)):
             c, b = self.block[ci], self.block[bi]
             w, bias = mc.fold_bn(c, b)
-            x = mc.conv_fwd(x, mc.weight_krsc(w, x.shape[3]), c.stride, c.padding, bias=bias, act=mc.ACT_LEAKY)
+            x = mc.conv_fwd(x, _wk(w, x.shape[3], x), c.stride, c.padding, bias=bias, act=mc.ACT_LEAKY)
         return x
 
 
 def _maxpool2(x):
     N, H, W, C = x.shape
     y = torch.empty((N, H // 2, W // 2, C), dtype=x.dtype, device=x.device)
-    call("mx_maxpool_fwd", _p(x.contiguous()), N, H, W, C, 2, 2, 0, _p(y), None, _s())
+    call("mx_maxpool_fwd", _p(x.contiguous()), mc.dcode(x), N, H, W, C, 2, 2, 0, _p(y), None, _s())
     return y
 
 
@@ -74,10 +83,11 @@ class UpBlock(nn.Module):
         Cout = wt.shape[1]
         w1 = wt.permute(2, 3, 1, 0).reshape(4 * Cout, C, 1, 1)  # output channel = (i, j, co)
         b1 = self.up.bias.detach().repeat(4).float().contiguous()
-        u = mc.conv_fwd(x, mc.weight_krsc(w1), (1, 1), (0, 0), bias=b1)   # [N, H, W, 4*Cout]
+        u = mc.conv_fwd(x, _wk(w1, C, x), (1, 1), (0, 0), bias=b1)   # [N, H, W, 4*Cout]
         if (2 * H, 2 * W) == (skip.shape[1], skip.shape[2]):
             cat = torch.empty((N, 2 * H, 2 * W, Cout + skip.shape[3]), dtype=x.dtype, device=x.device)
-            call("mx_up_concat", _p(u), _p(skip.contiguous()), N, H, W, Cout, skip.shape[3], _p(cat), _s())
+            call("mx_up_concat", _p(u), _p(skip.contiguous()), mc.dcode(x), N, H, W, Cout, skip.shape[3], _p(cat),
+                 _s())
         else:
             # odd spatial size (restoration_net.py:53-55): bilinear fix-up of the upsampled map
             up = u.view(N, H, W, 2, 2, Cout).permute(0, 1, 3, 2, 4, 5).reshape(N, 2 * H, 2 * W, Cout)
@@ -88,8 +98,11 @@ class UpBlock(nn.Module):
 
 
 class RestorationUNet(nn.Module):
-    def __init__(self, channels=(32, 64, 128, 256)):
+    def __init__(self, channels=(32, 64, 128, 256), precision=None):
         super().__init__()
+        from .backend import default_precision
+        self.precision = precision or default_precision()
+        self.act_dtype = torch.float32 if self.precision == "f32" else torch.bfloat16
         c1, c2, c3, c4 = channels
         self.down1 = DownBlock(3, c1)
         self.down2 = DownBlock(c1, c2)
@@ -103,7 +116,8 @@ class RestorationUNet(nn.Module):
         self.out_conv = nn.Conv2d(c1, 3, 1)
 
     def residual_nhwc(self, x8):
-        """x8: NHWC bf16 [N,H,W,8] (image in [0,1] in channels 0..2) -> residual f32 [N,H,W,3]."""
+        """x8: NHWC [N,H,W,8] of the activation dtype (image in [0,1] in channels 0..2) -> residual f32
+        [N,H,W,3]."""
         d1, s1 = self.down1(x8)
         d2, s2 = self.down2(d1)
         d3, s3 = self.down3(d2)
@@ -111,13 +125,13 @@ class RestorationUNet(nn.Module):
         b = self.bottleneck(d4)
         u = self.up1(self.up2(self.up3(self.up4(b, s4), s3), s2), s1)
         oc = self.out_conv
-        return mc.conv_fwd(u, mc.weight_krsc(oc.weight.detach()), (1, 1), (0, 0), bias=oc.bias.detach().float(),
+        return mc.conv_fwd(u, _wk(oc.weight.detach(), u.shape[3], u), (1, 1), (0, 0), bias=oc.bias.detach().float(),
                            out_dtype=torch.float32)
 
     @torch.no_grad()
     def forward(self, x):
         """Reference contract: x [N,3,H,W] f32 in [0,1] -> clamp(x + residual, 0, 1) [N,3,H,W] f32."""
-        x8 = F.pad(x.permute(0, 2, 3, 1), (0, 5)).to(torch.bfloat16).contiguous()
+        x8 = F.pad(x.permute(0, 2, 3, 1), (0, 5)).to(self.act_dtype).contiguous()
         r = self.residual_nhwc(x8)
         return torch.clamp(x + r.permute(0, 3, 1, 2), 0.0, 1.0)
 
@@ -132,7 +146,7 @@ class RestorationUNet(nn.Module):
             pad = torch.empty((B, Hp, Wp, 3), dtype=torch.uint8, device=img_u8.device)
             call("mx_reflect_pad_u8", _p(src), B, H, W, 3, Hp, Wp, _p(pad), _s())
             src = pad
-        x8 = ops.normalize_pad(src, (Hp, Wp), channels=8, dtype=torch.bfloat16, mean=(0.0, 0.0, 0.0),
+        x8 = ops.normalize_pad(src, (Hp, Wp), channels=8, dtype=self.act_dtype, mean=(0.0, 0.0, 0.0),
                                std=(1.0, 1.0, 1.0))
         r = self.residual_nhwc(x8)
         out = torch.empty((B, H, W, 3), dtype=torch.uint8, device=img_u8.device)

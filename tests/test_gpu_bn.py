@@ -34,18 +34,18 @@ def test_bn_backward_matches_torch(dev, M, K, act):
     ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)  # arrival counters start (and stay) zero
     sums = torch.empty(2, K, device=dev)
     coef = torch.empty(3, K, device=dev)
-    _lib.call("mx_bn_bwd_reduce_ex", _p(dyd), _p(yd), _p(zd), M, K, act, _p(meand), _p(invd), _p(gd), _p(ws), wsb,
+    _lib.call("mx_bn_bwd_reduce_ex", _p(dyd), _p(yd), _p(zd), 1, M, K, act, _p(meand), _p(invd), _p(gd), _p(ws), wsb,
               _p(sums), _p(coef), _s())
     # second launch on the same workspace: the counters were left zero, results identical
     sums_b, coef_b = torch.empty_like(sums), torch.empty_like(coef)
-    _lib.call("mx_bn_bwd_reduce_ex", _p(dyd), _p(yd), _p(zd), M, K, act, _p(meand), _p(invd), _p(gd), _p(ws), wsb,
+    _lib.call("mx_bn_bwd_reduce_ex", _p(dyd), _p(yd), _p(zd), 1, M, K, act, _p(meand), _p(invd), _p(gd), _p(ws), wsb,
               _p(sums_b), _p(coef_b), _s())
     torch.cuda.synchronize()
     assert torch.equal(sums, sums_b) and torch.equal(coef, coef_b)
     assert int(ws[:256].sum()) == 0
     dx = torch.empty_like(zd)
     dres = torch.empty_like(zd)
-    _lib.call("mx_bn_bwd_apply_ex", _p(dyd), _p(yd), _p(zd), M, K, act, _p(coef), _p(dx), _p(dres), _s())
+    _lib.call("mx_bn_bwd_apply_ex", _p(dyd), _p(yd), _p(zd), 1, M, K, act, _p(coef), _p(dx), _p(dres), _s())
     torch.cuda.synchronize()
     # the activation mask of the device path is the one of the bf16 y it was given
     mask = (y.float() > 0).float() if act == 1 else torch.where(y.float() > 0, 1.0, 0.2) if act == 2 else 1.0

@@ -45,15 +45,15 @@ def main():
         out = torch.empty_like(z)
         out2 = torch.empty_like(z)
         res = []
-        t = timeit(lambda: call("mx_bn_apply", _p(z), 1, M, K, _p(invstd), _p(mean), None, 1, _p(out), _s()))
+        t = timeit(lambda: call("mx_bn_apply", _p(z), 1, M, K, _p(invstd), _p(mean), None, 1, _p(out), 1, _s()))
         res.append(("apply", t, M * K * 4))
         wsb = _lib.load().mx_bn_bwd_workspace(M, K)
         ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
         coef = torch.empty(3, K, device=dev)
-        t = timeit(lambda: call("mx_bn_bwd_reduce_ex", _p(dy), _p(y), _p(z), M, K, 1, _p(mean), _p(invstd),
+        t = timeit(lambda: call("mx_bn_bwd_reduce_ex", _p(dy), _p(y), _p(z), 1, M, K, 1, _p(mean), _p(invstd),
                                 _p(gamma), _p(ws), wsb, _p(sums), _p(coef), _s()))
         res.append(("bwd_reduce", t, M * K * 6))
-        t = timeit(lambda: call("mx_bn_bwd_apply_ex", _p(dy), _p(y), _p(z), M, K, 1, _p(coef), _p(out), _p(out2),
+        t = timeit(lambda: call("mx_bn_bwd_apply_ex", _p(dy), _p(y), _p(z), 1, M, K, 1, _p(coef), _p(out), _p(out2),
                                 _s()))
         res.append(("bwd_apply", t, M * K * 10))
         mb = (M + 63) // 64

@@ -25,7 +25,7 @@ def main():
     m = m.to(dev).train()
     imgs, tg = synth_batch(0, 2, device=dev)
     sum(m(imgs, tg).values()).backward()
-    pk = m.__dict__["_mx_packer"]
+    pk = m.__dict__["_mx_packer_" + m.be.precision]
     es = [pk.entries[k] for k in pk.order]
     ws = [e.w for e in es]
     nbytes = sum(e.w.numel() * 4 + e.wk.numel() * 2 + (e.wt.numel() * 2 + e.w.numel() * 4 if e.wt is not None else 0)
