@@ -136,6 +136,14 @@ int mx_box_decode(const float* rel, const float* boxes, int64_t n, int64_t ncls,
 int mx_corrupt_u8(const uint8_t* img, int64_t B, int64_t H, int64_t W, int64_t C, const int32_t* ops_host,
                   float sigma, uint64_t seed, const float* noise, double factor, uint8_t* tmp, uint8_t* out,
                   mx_stream_t stream);
+/* apply_motion_blur at any kernel size / angle (augmentations.py:21-38): cv2.filter2D(img, -1, kernel)
+ * on uint8 [B,H,W,C] with the non-zero taps of the k x k float kernel given as ntaps (dy, dx, coef)
+ * triples (row-major kernel order, offsets from the anchor = kernel centre), BORDER_REFLECT_101,
+ * f32 sum, round half to even. The kernel itself (getRotationMatrix2D + warpAffine of the centre row,
+ * normalised) is built on the host (mx_det.augment.motion_blur_kernel). ntaps <= 128; not in place.
+ * Low-res (op 3) takes OpenCV's exact-x2 INTER_AREA fast path when W == 2*nw and H == 2*nh. */
+int mx_filter2d_u8(const uint8_t* img, int64_t B, int64_t H, int64_t W, int64_t C, const float* taps_host, int ntaps,
+                   uint8_t* out, mx_stream_t stream);
 /* GeneralizedRCNNTransform (normalize, zero-pad to /32) fused with ToDtype(scale=True):
  * u8 HWC [B,H,W,3] -> NHWC [B, Hp, Wp, Cp] dtype, (x/255 - mean)/std, zero padding; Cp >= 3 (extra
  * channels zero, for the conv stem's 8-channel gather). */

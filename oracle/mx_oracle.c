@@ -462,12 +462,64 @@ void orc_resize_linear_u8(const uint8_t* src, int64_t sh, int64_t sw, int64_t C,
   free(xo); free(yo); free(xa); free(ya);
 }
 
+/* OpenCV resize, INTER_AREA with is_area_fast (both scales exactly the integer 2): resizeAreaFast_.
+ * ResizeAreaFastVec_SIMD_8u (128-bit x86-64 baseline) handles the first elements of each destination
+ * row: cn 3 in steps of 48 (3 x 16 lanes, v_load_deinterleave), cn 1 in steps of 8, cn 4 in steps of
+ * 16, each as v_rshr_pack<2>: (a + b + c + d + 2) >> 2. The remaining elements of the row take the
+ * scalar loop: saturate_cast<uchar>(sum * (1.f / area)) = cvRound, half to even. */
+void orc_resize_area_fast2_u8(const uint8_t* src, int64_t sh, int64_t sw, int64_t C, uint8_t* dst, int64_t dh,
+                              int64_t dw) {
+  const int64_t w = dw * C;
+  const int64_t step = C == 1 ? 8 : (C == 3 ? 48 : (C == 4 ? 16 : 0));
+  const int64_t vec = step ? (w / step) * step : 0;
+  (void)sh;
+  for (int64_t dy = 0; dy < dh; ++dy)
+    for (int64_t e = 0; e < w; ++e) {
+      const int64_t c = e % C, dx = e / C;
+      const uint8_t* s0 = src + ((2 * dy) * sw + 2 * dx) * C + c;
+      const uint8_t* s1 = s0 + sw * C;
+      const int sum = (int)s0[0] + (int)s0[C] + (int)s1[0] + (int)s1[C];
+      uint8_t v;
+      if (e < vec) {
+        v = (uint8_t)((sum + 2) >> 2);
+      } else {
+        const float r = rintf((float)sum * 0.25f);
+        v = (uint8_t)(r > 255.f ? 255.f : r);
+      }
+      dst[dy * w + e] = v;
+    }
+}
+
 void orc_lowres_u8(const uint8_t* img, int64_t H, int64_t W, int64_t C, double factor, uint8_t* tmp, uint8_t* out) {
   int64_t nw = (int64_t)(W * factor), nh = (int64_t)(H * factor);
   if (nw < 1) nw = 1;
   if (nh < 1) nh = 1;
-  orc_resize_area_u8(img, H, W, C, tmp, nh, nw);
+  if (W == 2 * nw && H == 2 * nh)  /* cv::resize: scale_x == scale_y == 2 exactly -> fast area path */
+    orc_resize_area_fast2_u8(img, H, W, C, tmp, nh, nw);
+  else
+    orc_resize_area_u8(img, H, W, C, tmp, nh, nw);
   orc_resize_linear_u8(tmp, nh, nw, C, out, H, W);
+}
+
+/* cv2.filter2D(src, -1, kernel), 8U -> 8U, direct (non-DFT) path, anchor at the kernel centre,
+ * BORDER_REFLECT_101 (BORDER_DEFAULT): the taps are the kernel's non-zero coefficients in row-major
+ * order (preprocess2DKernel), each output = saturate_cast<uchar>(sum_t coef_t * src_t) with the sum in
+ * f32 starting at delta = 0 (mul and add rounded separately: -ffp-contract=off). taps: ntaps triples
+ * (dy, dx, coef) relative to the anchor. */
+void orc_filter2d_u8(const uint8_t* img, int64_t H, int64_t W, int64_t C, const float* taps, int ntaps, uint8_t* out) {
+  for (int64_t y = 0; y < H; ++y)
+    for (int64_t x = 0; x < W; ++x)
+      for (int64_t c = 0; c < C; ++c) {
+        float s = 0.f;
+        for (int k = 0; k < ntaps; ++k) {
+          const int64_t yy = refl101(y + (int64_t)taps[3 * k], H), xx = refl101(x + (int64_t)taps[3 * k + 1], W);
+          s += taps[3 * k + 2] * (float)img[(yy * W + xx) * C + c];
+        }
+        float r = rintf(s);
+        if (r < 0) r = 0;
+        if (r > 255) r = 255;
+        out[(y * W + x) * C + c] = (uint8_t)r;
+      }
 }
 
 /* BORDER_REFLECT: fedcba|abcdefgh|hgfedcb */
@@ -481,4 +533,70 @@ void orc_reflect_pad_u8(const uint8_t* src, int64_t H, int64_t W, int64_t C, int
   for (int64_t y = 0; y < H + ph; ++y)
     for (int64_t x = 0; x < W2; ++x)
       for (int64_t c = 0; c < C; ++c) dst[(y * W2 + x) * C + c] = src[(refl(y, H) * W + refl(x, W)) * C + c];
+}
+
+/* ---- augmentations.py:21-27 _motion_blur_kernel(k, angle) ----------------------------------------
+ * kernel = zeros(k, k) f32, row k//2 = 1; M = cv2.getRotationMatrix2D((k/2 - 0.5, k/2 - 0.5), angle, 1);
+ * kernel = cv2.warpAffine(kernel, M, (k, k)) (INTER_LINEAR, BORDER_CONSTANT 0); kernel /= kernel.sum() +
+ * 1e-8 (numpy 2 scalar rules: all f32). warpAffine restated from OpenCV imgwarp.cpp: M inverted in
+ * double, source coordinates in 1/32-pixel fixed point (AB_BITS 10, INTER_BITS 5, round_delta 16),
+ * bilinear weights from the f32 table (1-ay)(1-ax), (1-ay)ax, ay(1-ax), ay*ax (remapBilinear, f32
+ * sum in tap order), constant-0 border per tap. The sum is numpy's pairwise float32 sum (blocks of 8
+ * partial sums for n <= 128). */
+static int cv_round(double v) { return (int)lrint(v); }
+
+static float np_pairwise_sum_f32(const float* a, int n) {
+  if (n < 8) {
+    float r = 0.f;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  float r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+void orc_motion_blur_kernel(int k, double angle_deg, float* out /* k*k */) {
+  float* src = (float*)calloc((size_t)k * k, sizeof(float));
+  for (int x = 0; x < k; ++x) src[(k / 2) * k + x] = 1.f;
+  const double cx = k / 2.0 - 0.5, cy = k / 2.0 - 0.5;
+  const double ang = angle_deg * 3.14159265358979323846 / 180.0;
+  const double alpha = cos(ang), beta = sin(ang);
+  double M[6] = {alpha, beta, (1 - alpha) * cx - beta * cy, -beta, alpha, beta * cx + (1 - alpha) * cy};
+  double D = M[0] * M[4] - M[1] * M[3];
+  D = D != 0 ? 1. / D : 0;
+  const double A11 = M[4] * D, A22 = M[0] * D;
+  M[0] = A11; M[1] *= -D; M[3] *= -D; M[4] = A22;
+  const double b1 = -M[0] * M[2] - M[1] * M[5], b2 = -M[3] * M[2] - M[4] * M[5];
+  M[2] = b1; M[5] = b2;
+  for (int y = 0; y < k; ++y) {
+    const int X0 = cv_round((M[1] * y + M[2]) * 1024) + 16;
+    const int Y0 = cv_round((M[4] * y + M[5]) * 1024) + 16;
+    for (int x = 0; x < k; ++x) {
+      const int X = (X0 + cv_round(M[0] * x * 1024)) >> 5;
+      const int Y = (Y0 + cv_round(M[3] * x * 1024)) >> 5;
+      const int sx = X >> 5, sy = Y >> 5;
+      const float ax = (float)(X & 31) * (1.f / 32), ay = (float)(Y & 31) * (1.f / 32);
+      const float w0 = (1.f - ay) * (1.f - ax), w1 = (1.f - ay) * ax, w2 = ay * (1.f - ax), w3 = ay * ax;
+      float v;
+      if (sx >= k || sx + 1 < 0 || sy >= k || sy + 1 < 0) {
+        v = 0.f;
+      } else {
+        const float v0 = (sx >= 0 && sy >= 0 && sx < k && sy < k) ? src[sy * k + sx] : 0.f;
+        const float v1 = (sx + 1 >= 0 && sy >= 0 && sx + 1 < k && sy < k) ? src[sy * k + sx + 1] : 0.f;
+        const float v2 = (sx >= 0 && sy + 1 >= 0 && sx < k && sy + 1 < k) ? src[(sy + 1) * k + sx] : 0.f;
+        const float v3 = (sx + 1 >= 0 && sy + 1 >= 0 && sx + 1 < k && sy + 1 < k) ? src[(sy + 1) * k + sx + 1] : 0.f;
+        v = v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3;
+      }
+      out[y * k + x] = v;
+    }
+  }
+  const float den = np_pairwise_sum_f32(out, k * k) + 1e-8f;
+  for (int i = 0; i < k * k; ++i) out[i] = out[i] / den;
+  free(src);
 }

@@ -171,3 +171,40 @@ def reflect_pad_u8(img, ph, pw):
     out = np.empty((H + ph, W + pw, C), np.uint8)
     lib().orc_reflect_pad_u8(_p(img, U8), i64(H), i64(W), i64(C), i64(ph), i64(pw), _p(out, U8))
     return out
+
+
+def motion_blur_kernel(k, angle_deg):
+    """augmentations.py:21-27 restated in C (orc_motion_blur_kernel)."""
+    out = np.empty((k, k), np.float32)
+    lib().orc_motion_blur_kernel(int(k), ctypes.c_double(angle_deg), _p(out, F32))
+    return out
+
+
+def kernel_taps(kernel):
+    """Non-zero taps of a k x k kernel, row-major, as (dy, dx, coef) relative to the centre anchor."""
+    k = kernel.shape[0]
+    ys, xs = np.nonzero(kernel)
+    return np.stack([ys - k // 2, xs - k // 2, kernel[ys, xs]], 1).astype(np.float32)
+
+
+def filter2d_u8(img, kernel):
+    """cv2.filter2D(img, -1, kernel) on HxWxC uint8 (direct path, BORDER_REFLECT_101)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W, C = img.shape
+    taps = np.ascontiguousarray(kernel_taps(np.asarray(kernel, np.float32)))
+    out = np.empty_like(img)
+    lib().orc_filter2d_u8(_p(img, U8), i64(H), i64(W), i64(C), _p(taps, F32), ctypes.c_int(len(taps)), _p(out, U8))
+    return out
+
+
+def motion_blur_u8(img, k=9, angle_deg=0.0):
+    """apply_motion_blur (augmentations.py:36-38)."""
+    return filter2d_u8(img, motion_blur_kernel(k, angle_deg))
+
+
+def resize_area_fast2_u8(img):
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W, C = img.shape
+    out = np.empty((H // 2, W // 2, C), np.uint8)
+    lib().orc_resize_area_fast2_u8(_p(img, U8), i64(H), i64(W), i64(C), _p(out, U8), i64(H // 2), i64(W // 2))
+    return out

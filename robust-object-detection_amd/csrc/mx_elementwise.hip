@@ -94,6 +94,51 @@ __global__ void blur_kernel(const uint8_t* __restrict__ img, int64_t H, int64_t 
   out[i] = (uint8_t)r;
 }
 
+// filter2D(src, -1, kernel) for a general k x k float kernel (apply_motion_blur at any angle,
+// augmentations.py:21-38): the non-zero taps in row-major kernel order (OpenCV preprocess2DKernel),
+// sum = sum_t coef_t * src in f32 from 0 (delta), BORDER_REFLECT_101, saturate_cast<uchar> (round half
+// to even). This file is built -ffp-contract=off: one rounding per multiply and per add, like the
+// scalar / SSE path (an AVX2 build of OpenCV fuses them; results can differ only at exact .5 ties).
+struct FilterTaps {
+  int n;
+  int dy[128], dx[128];
+  float c[128];
+};
+
+__global__ void filter2d_kernel(const uint8_t* __restrict__ img, int64_t H, int64_t W, int64_t C, FilterTaps t,
+                                uint8_t* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= H * W * C) return;
+  int64_t c = i % C, x = (i / C) % W, y = i / (C * W);
+  float s = 0.f;
+  for (int k = 0; k < t.n; ++k) s += t.c[k] * (float)img[(refl101(y + t.dy[k], H) * W + refl101(x + t.dx[k], W)) * C + c];
+  float r = rintf(s);
+  r = r < 0.f ? 0.f : (r > 255.f ? 255.f : r);
+  out[i] = (uint8_t)r;
+}
+
+// INTER_AREA with an exact integer scale of 2 in both axes (OpenCV resize's is_area_fast branch,
+// resizeAreaFast_): the vectorised part (ResizeAreaFastVec_SIMD_8u, 3 channels: 48 output elements per
+// 128-bit iteration, the x86-64 baseline) computes (a + b + c + d + 2) >> 2; the scalar tail of each
+// row (the last dw*C mod 48 elements) computes saturate_cast<uchar>((a + b + c + d) * 0.25f), which
+// rounds exact halves to even. vec_elems = elements per row taken by the vector loop.
+__global__ void area_fast2_kernel(const uint8_t* __restrict__ src, int64_t sw, int64_t C, uint8_t* __restrict__ dst,
+                                  int64_t dh, int64_t dw, int64_t vec_elems) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= dh * dw * C) return;
+  const int64_t e = i % (dw * C), dy = i / (dw * C);
+  const int64_t c = e % C, dx = e / C;
+  const uint8_t* s0 = src + ((2 * dy) * sw + 2 * dx) * C + c;
+  const uint8_t* s1 = s0 + sw * C;
+  const int sum = (int)s0[0] + (int)s0[C] + (int)s1[0] + (int)s1[C];
+  if (e < vec_elems) {
+    dst[i] = (uint8_t)((sum + 2) >> 2);
+  } else {
+    const float r = rintf((float)sum * 0.25f);
+    dst[i] = (uint8_t)(r > 255.f ? 255.f : r);
+  }
+}
+
 // OpenCV computeResizeAreaTab for one destination index: up to 3 (src, alpha) entries
 __device__ int area_entries(int64_t ssize, int64_t d, double scale, int64_t* si, float* al) {
   int k = 0;
@@ -217,6 +262,33 @@ extern "C" int mx_box_decode(const float* rel, const float* boxes, int64_t n, in
   return MX_OK;
 }
 
+// elements per destination row that ResizeAreaFastVec_SIMD_8u (scale 2, 128-bit vectors) handles:
+// cn 1: 8 per step, cn 3: 48 per step, cn 4: 16 per step; other channel counts: none (scalar)
+static int64_t area_fast2_vec_elems(int64_t dw, int64_t C) {
+  const int64_t w = dw * C;
+  const int64_t step = C == 1 ? 8 : (C == 3 ? 48 : (C == 4 ? 16 : 0));
+  return step ? (w / step) * step : 0;
+}
+
+extern "C" int mx_filter2d_u8(const uint8_t* img, int64_t B, int64_t H, int64_t W, int64_t C, const float* taps_host,
+                              int ntaps, uint8_t* out, mx_stream_t stream) {
+  MX_CHECK_ARG(B >= 0 && H > 0 && W > 0 && C > 0 && img != out, "mx_filter2d_u8: bad shape or in-place call");
+  MX_CHECK_ARG(ntaps >= 0 && ntaps <= 128, "mx_filter2d_u8: at most 128 non-zero taps");
+  FilterTaps t{};
+  t.n = ntaps;
+  for (int k = 0; k < ntaps; ++k) {
+    t.dy[k] = (int)taps_host[3 * k];
+    t.dx[k] = (int)taps_host[3 * k + 1];
+    t.c[k] = taps_host[3 * k + 2];
+  }
+  const int64_t per = H * W * C;
+  for (int64_t b = 0; b < B; ++b) {
+    filter2d_kernel<<<(unsigned)cdiv(per, 256), 256, 0, (hipStream_t)stream>>>(img + b * per, H, W, C, t, out + b * per);
+    MX_LAUNCH_CHECK();
+  }
+  return MX_OK;
+}
+
 extern "C" int mx_corrupt_u8(const uint8_t* img, int64_t B, int64_t H, int64_t W, int64_t C, const int32_t* ops, float sigma,
                              uint64_t seed, const float* noise, double factor, uint8_t* tmp, uint8_t* out,
                              mx_stream_t stream) {
@@ -244,7 +316,12 @@ extern "C" int mx_corrupt_u8(const uint8_t* img, int64_t B, int64_t H, int64_t W
       case 3: {
         MX_CHECK_ARG(tmp != nullptr, "mx_corrupt_u8: low-res needs tmp");
         uint8_t* t = tmp + b * nh * nw * C;
-        area_kernel<<<(unsigned)cdiv(nh * nw * C, 256), 256, 0, s>>>(src, H, W, C, t, nh, nw);
+        if (W == 2 * nw && H == 2 * nh) {  // exact x2: OpenCV's fast INTER_AREA path
+          area_fast2_kernel<<<(unsigned)cdiv(nh * nw * C, 256), 256, 0, s>>>(src, W, C, t, nh, nw,
+                                                                             area_fast2_vec_elems(nw, C));
+        } else {
+          area_kernel<<<(unsigned)cdiv(nh * nw * C, 256), 256, 0, s>>>(src, H, W, C, t, nh, nw);
+        }
         linear_kernel<<<(unsigned)cdiv(per, 256), 256, 0, s>>>(t, nh, nw, C, dst, H, W);
         break;
       }

@@ -51,6 +51,7 @@ _SIGS = {
     "mx_anchors_level": (c_int, [c_f, c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mx_box_decode": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_f, c_vp, c_vp]),
     "mx_corrupt_u8": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_f, c_u64, c_vp, c_d, c_vp, c_vp, c_vp]),
+    "mx_filter2d_u8": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp]),
     "mx_normalize_pad": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp]),
     "mx_conv_mblocks": (c_i64, [ctypes.POINTER(ConvShape)]),
     "mx_conv2d_fwd": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),

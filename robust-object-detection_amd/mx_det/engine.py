@@ -10,8 +10,15 @@ Behaviour follows the reference entry points:
     stats[0]/[1], per-class AP50 from precision[0, :, k, 0, 2].
 MI355X-side differences: images stay uint8 until the device (ToImage/ToDtype scaling, corruption and
 normalisation run as HIP kernels); with WORLD_SIZE > 1 (torchrun) every rank trains on its shard of
-each epoch's permutation (DistributedSampler) with RCCL gradient all-reduce, and evaluation shards
-images by rank and gathers detections to rank 0.
+each epoch's permutation (DistributedSampler, drop_last: no padded duplicates in the loss sum) with
+RCCL gradient all-reduce, and evaluation shards images by rank and gathers detections to rank 0.
+
+Multi-GPU recipe: each rank keeps the reference's BATCH_SIZE (2) so every GPU's
+BatchNorm sees the reference's bs-2 statistics; the global batch is 2 x world and an epoch has 1/world
+as many optimizer steps. LR_SCALING (cfg key, or env MX_LR_SCALING) chooses the learning rate:
+"none" (default) keeps the reference's 0.005 (its per-image gradient scale, StepLR(8) per epoch);
+"linear" uses LR x world with a linear warm-up over WARMUP_ITERS (default 500) optimizer steps (the
+large-batch rule). The choice changes mAP; neither is the reference's single-GPU run.
 """
 import json
 import os
@@ -161,7 +168,8 @@ def train_frcnn(cfg):
             print("Mode: AUGMENTED training (corruption p=0.5, on GPU)\n", flush=True)
     train_ds = COCODetectionDataset(str(cfg["TRAIN_IMG"]), str(cfg["TRAIN_ANN"]), transforms=uint8_transform)
     val_ds = COCODetectionDataset(str(cfg["VAL_IMG"]), str(cfg["VAL_ANN"]), transforms=uint8_transform)
-    sampler = DistributedSampler(train_ds, world, rank, shuffle=True, seed=cfg["SEED"]) if world > 1 else None
+    sampler = (DistributedSampler(train_ds, world, rank, shuffle=True, seed=cfg["SEED"], drop_last=True)
+               if world > 1 else None)
     train_loader = DataLoader(train_ds, batch_size=cfg["BATCH_SIZE"], shuffle=sampler is None, sampler=sampler,
                               num_workers=cfg.get("NUM_WORKERS", 0), collate_fn=collate_fn, pin_memory=True)
     val_sampler = ShardSampler(len(val_ds), world, rank) if world > 1 else None
@@ -172,10 +180,19 @@ def train_frcnn(cfg):
     if world > 1:  # DDP(broadcast_buffers=False) semantics, HIP graphs kept (gradients averaged after backward)
         from .dp import DataParallel
         ddp = DataParallel(model)
+        # parameters are identical on every rank now (rank-0 broadcast); the per-rank random streams
+        # (corruption choice / noise seeds, RPN and RoI sampler keys) must not be
+        set_seed(cfg["SEED"] + rank)
     params = [p for p in model.parameters() if p.requires_grad]
     from .optim import SGD
-    optimizer = SGD(params, lr=cfg["LR"], momentum=cfg["MOMENTUM"], weight_decay=cfg["WEIGHT_DECAY"])
+    scaling = cfg.get("LR_SCALING", os.environ.get("MX_LR_SCALING", "none"))
+    if scaling not in ("none", "linear"):
+        raise ValueError(f"LR_SCALING must be 'none' or 'linear', got {scaling!r}")
+    lr = cfg["LR"] * (world if scaling == "linear" else 1)
+    warmup = int(cfg.get("WARMUP_ITERS", 500)) if (scaling == "linear" and world > 1) else 0
+    optimizer = SGD(params, lr=lr, momentum=cfg["MOMENTUM"], weight_decay=cfg["WEIGHT_DECAY"])
     sched = torch.optim.lr_scheduler.StepLR(optimizer, step_size=8, gamma=0.1)
+    it_global = 0
     corrupt = RandomCorruptionGPU(p=0.5) if cfg.get("AUGMENT") else None
     history, best_ckpt, last_ckpt = out_dir / "history.jsonl", out_dir / "best.pth", out_dir / "last.pth"
     t0 = time.time()
@@ -195,6 +212,10 @@ def train_frcnn(cfg):
             losses.backward()
             if world > 1:
                 ddp.sync_gradients()
+            if it_global < warmup:  # linear warm-up of the scaled LR (epoch 1 only at the default length)
+                for gr in optimizer.param_groups:
+                    gr["lr"] = lr * (it_global + 1) / warmup
+            it_global += 1
             optimizer.step()
             epoch_loss += float(losses.item())
             if rank == 0 and ((i + 1) % 100 == 0 or (i + 1) == n_batches):

@@ -833,12 +833,18 @@ class _GraphFn(torch.autograd.Function):
                 s.zero_()
             else:
                 s.copy_(g)
+        # A .grad still aliasing the graph's static buffer (adopted by the previous replay, kept by
+        # zero_grad(set_to_none=False) or gradient accumulation) gets its own storage first: the
+        # replay below overwrites the static buffer.
+        for p, g in zip(tg.params, tg.static_grads):
+            if g is not None and p.grad is g:
+                p.grad = g.clone()
         tg.bwd.replay()
         for p, g in zip(tg.params, tg.static_grads):
             if g is None:
                 continue
             if p.grad is None:
-                p.grad = g
+                p.grad = g  # adopted without a copy (the usual zero_grad(set_to_none=True) step)
             else:
                 p.grad.add_(g)
         if tg.on_ready is not None:  # e.g. mx_det.dp.DataParallel starts this unit's all-reduce

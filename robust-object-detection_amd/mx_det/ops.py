@@ -302,6 +302,20 @@ def corrupt_u8(images, ops, sigma=15.0, seed=0, noise=None, factor=0.5):
     return out
 
 
+def filter2d_u8(images, taps):
+    """cv2.filter2D(img, -1, kernel) on uint8 [B,H,W,C] device images; taps = the kernel's non-zero
+    coefficients as (dy, dx, coef) rows relative to the centre anchor, row-major (mx_filter2d_u8)."""
+    _dev(images)
+    _check(images.dtype == torch.uint8 and images.dim() == 4, "images must be uint8 [B,H,W,C]")
+    x = images.contiguous()
+    B, H, W, C = x.shape
+    t = [float(v) for row in taps for v in row]
+    _check(len(t) % 3 == 0 and len(t) // 3 <= 128, "filter2d_u8: at most 128 (dy, dx, coef) taps")
+    out = torch.empty_like(x)
+    call("mx_filter2d_u8", _p(x), B, H, W, C, (ctypes.c_float * max(len(t), 1))(*t), len(t) // 3, _p(out), _stream())
+    return out
+
+
 IMAGE_MEAN = (0.485, 0.456, 0.406)
 IMAGE_STD = (0.229, 0.224, 0.225)
 

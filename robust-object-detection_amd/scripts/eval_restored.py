@@ -1,11 +1,15 @@
 """Evaluate the baseline Faster R-CNN on U-Net-restored test sets — `python -m scripts.eval_restored`.
 
 Reference: eval_restored.py (FRCNN branch :60-113, :164-184) reads JPEGs written by restore_testsets.py.
-Default here (MX_RESTORE_ON_DEVICE=1) is the fused MI355X pipeline of the north star: each corrupted
-test image is restored by the HIP U-Net on the GPU (reflect pad, /255, U-Net, *255, clip, truncate,
-crop) and fed straight to detection — no host round trip, no JPEG re-encode. Set
-MX_RESTORE_ON_DEVICE=0 to evaluate pre-restored images from data/testsets/coco6_restored instead.
-Output: experiments/eval_restored_results.json (reference schema).
+Default (MX_RESTORE_ON_DEVICE=0): the reference's pipeline -- pre-restored JPEGs from
+data/testsets/coco6_restored (written by `python -m scripts.restore_testsets`, which runs the U-Net
+on the device in the reference's fp32 precision and re-encodes JPEG like restore_testsets.py:101),
+results in experiments/eval_restored_results.json (reference schema).
+MX_RESTORE_ON_DEVICE=1: the fused MI355X pipeline of the north star -- each corrupted test image is
+restored by the HIP U-Net on the GPU (reflect pad, /255, U-Net, *255, clip, truncate, crop) and fed
+straight to detection, no host round trip and no JPEG re-encode. That skips the reference's JPEG
+round trip, so its mAP is not the reference's number: it goes to
+experiments/eval_restored_results_fused.json instead.
 """
 import os
 from pathlib import Path
@@ -33,7 +37,7 @@ def load_unet(dev, ckpt=None):
 
 def main():
     dev, world, rank = eval_all.init_device()
-    on_device = os.environ.get("MX_RESTORE_ON_DEVICE", "1") != "0"
+    on_device = os.environ.get("MX_RESTORE_ON_DEVICE", "0") != "0"
     restorer = load_unet(dev) if on_device else None
     root = CORRUPTED_ROOT if on_device else RESTORED_ROOT
     results = {}
@@ -43,7 +47,8 @@ def main():
             results[name] = r
     if rank == 0:
         OUT_DIR.mkdir(parents=True, exist_ok=True)
-        eval_all.save_json(results, OUT_DIR / "eval_restored_results.json")
+        name = "eval_restored_results_fused.json" if on_device else "eval_restored_results.json"
+        eval_all.save_json(results, OUT_DIR / name)
     return results
 
 

@@ -14,9 +14,16 @@ What is pinned, and by which reference code:
                        noise field it drew (so the restatement can be fed the same field).
   * dataset_target.json - scripts/coco_detection_dataset.py:18-67 target construction for a small
                        COCO json with a zero-width box, a zero-height box and an image with no boxes.
+  * random_corruption.npz - scripts/augmentations.py:60-74 RandomCorruption(p=0.5) on a PIL RGB image
+                       under random.seed(s) / np.random.seed(s): the keep decision, the choice and,
+                       for the seeds whose choice is noise (or keep), the output image -- the noise
+                       field lands on the BGR view (cvtColor RGB2BGR, :72) and the result is flipped
+                       back (:74).
 
 cv2 and pycocotools are not installed here; they are stubbed only where the pinned function never
-calls them (apply_noise uses numpy alone; the dataset uses COCO as a plain index).
+calls them (apply_noise uses numpy alone; the dataset uses COCO as a plain index) or with exact
+equivalents (cv2.cvtColor RGB2BGR / BGR2RGB on HxWx3 uint8 is the channel reversal). A seed whose
+choice is blur or low-res needs real cv2 and is recorded without an output.
 """
 import json
 import os
@@ -35,6 +42,12 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 def _stub_modules():
     cv2 = types.ModuleType("cv2")
     cv2.__stub__ = True
+    cv2.COLOR_RGB2BGR, cv2.COLOR_BGR2RGB = 4, 4
+
+    def cvtColor(a, code):  # RGB <-> BGR for 3-channel uint8: the channel reversal
+        assert code == 4 and a.ndim == 3 and a.shape[2] == 3
+        return np.ascontiguousarray(a[..., ::-1])
+    cv2.cvtColor = cvtColor
     sys.modules.setdefault("cv2", cv2)
 
     class COCO:  # minimal index with the calls coco_detection_dataset.py:11-26 makes
@@ -122,6 +135,45 @@ def make_noise():
     print("noise: changed px", int((out != img).sum()))
 
 
+def make_random_corruption():
+    import random
+
+    from PIL import Image
+    from scripts import augmentations as aug
+
+    rng = np.random.RandomState(11)
+    img = rng.randint(0, 256, size=(23, 31, 3)).astype(np.uint8)
+    seeds, ops, outs = [], [], []
+    for s in range(40):
+        chosen = []
+        orig = {n: getattr(aug, n) for n in ("apply_noise", "apply_motion_blur", "apply_lowres")}
+
+        def spy(name):
+            def f(*a, **k):
+                chosen.append(name)
+                return orig[name](*a, **k)
+            return f
+        for n in orig:
+            setattr(aug, n, spy(n))
+        random.seed(s)
+        np.random.seed(s)
+        try:
+            out = np.asarray(aug.RandomCorruption(p=0.5)(Image.fromarray(img)))
+        except AttributeError:  # blur / low-res: real cv2 needed
+            out = None
+        finally:
+            for n, f in orig.items():
+                setattr(aug, n, f)
+        op = chosen[0] if chosen else "keep"
+        seeds.append(s)
+        ops.append(op)
+        outs.append(out if out is not None else np.zeros_like(img))
+    ops_a = np.array(ops)
+    np.savez_compressed(os.path.join(OUT, "random_corruption.npz"), img=img, seeds=np.array(seeds), ops=ops_a,
+                        outs=np.stack(outs), pinned=np.isin(ops_a, ["keep", "apply_noise"]))
+    print("random_corruption:", {o: int((ops_a == o).sum()) for o in set(ops)})
+
+
 def make_dataset():
     from PIL import Image
     from scripts.coco_detection_dataset import COCODetectionDataset, collate_fn
@@ -169,4 +221,5 @@ if __name__ == "__main__":
     _stub_modules()
     make_unet()
     make_noise()
+    make_random_corruption()
     make_dataset()

@@ -470,3 +470,45 @@ def test_sampler_draw_via_level_topk(dev):
     assert not (pm & ~pos).any() and not (nm & ~neg).any()
     pm2, _ = s(lab, be)
     assert not torch.equal(pm2[1], pm[1])  # 128 of 700 positives redrawn
+
+
+@pytest.mark.parametrize("k,angle", [(9, 0), (9, 45), (9, 90), (7, 30), (11, 135), (5, -20)])
+def test_motion_blur_any_angle(dev, k, angle):
+    """apply_motion_blur at any kernel size / angle (augmentations.py:21-38): the device filter2D on
+    the restated kernel equals the oracle's filter2D restatement bit for bit."""
+    from mx_det import augment as aug
+    rng = np.random.default_rng(k * 100 + angle % 360)
+    img = _img(rng, 61, 87)
+    got = aug.apply_motion_blur(img, k, angle)
+    assert np.array_equal(got, orc.motion_blur_u8(img, k, angle))
+
+
+@pytest.mark.parametrize("H,W", [(96, 134), (80, 132), (64, 2 * 81)])
+def test_lowres_even_frames_take_the_area_fast_path(dev, H, W):
+    """Even x even frames (VisDrone 1920x1080, 2000x1500) take OpenCV's exact-x2 INTER_AREA path."""
+    from mx_det import ops
+    rng = np.random.default_rng(H + W)
+    img = np.stack([_img(rng, H, W), _img(rng, H, W)])
+    got = ops.corrupt_u8(torch.from_numpy(img).to(dev), [3, 3]).cpu().numpy()
+    for b in range(2):
+        small = orc.resize_area_fast2_u8(img[b])
+        assert np.array_equal(got[b], orc.resize_linear_u8(small, H, W))
+        assert np.array_equal(got[b], orc.lowres_u8(img[b], 0.5))
+
+
+def test_random_corruption_matches_reference_golden(dev):
+    """RandomCorruption(p=0.5) (PIL transform) under the reference's seeded random / numpy streams:
+    identical output to the reference for every seed whose reference output needs no OpenCV
+    (keep or noise on the BGR view; tests/golden/random_corruption.npz)."""
+    import random
+    from PIL import Image
+    from mx_det import augment as aug
+    d = np.load("tests/golden/random_corruption.npz")
+    img = Image.fromarray(d["img"])
+    for s, out, pinned in zip(d["seeds"], d["outs"], d["pinned"]):
+        if not pinned:
+            continue
+        random.seed(int(s))
+        np.random.seed(int(s))
+        got = np.asarray(aug.RandomCorruption(p=0.5)(img))
+        assert np.array_equal(got, out), int(s)

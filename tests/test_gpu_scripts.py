@@ -1,6 +1,7 @@
 """Drop-in entry points end to end on a tiny synthetic VisDrone-COCO dataset written to disk
 (the reference's config #1 plumbing case, on MI355X): train_frcnn_baseline / _augmented (1 epoch),
-eval_all (4 variants) and eval_restored (fused device U-Net) with the reference's output schemas."""
+eval_all (4 variants) and eval_restored (reference pipeline, and the fused device U-Net) with the
+reference's output schemas."""
 import json
 
 import numpy as np
@@ -75,8 +76,15 @@ def test_train_eval_scripts(dev, tmp_path, monkeypatch):
     monkeypatch.setattr(eval_restored, "CORRUPTED_ROOT", ts)
     monkeypatch.setattr(eval_restored, "OUT_DIR", tmp_path / "experiments")
     monkeypatch.setattr(eval_restored, "CKPTS", {"FasterRCNN": tmp_path / "frcnn/baseline_clean/best.pth"})
+    # default: the reference's pipeline (pre-restored images; here the plumbing test set itself)
+    monkeypatch.setattr(eval_restored, "RESTORED_ROOT", ts)
     eval_restored.main()
     out = json.load(open(tmp_path / "experiments/eval_restored_results.json"))
+    assert set(out["FasterRCNN"]) == set(eval_all.VARIANTS)
+    # fused on-device restoration: reported separately (not the reference's JPEG round trip)
+    monkeypatch.setenv("MX_RESTORE_ON_DEVICE", "1")
+    eval_restored.main()
+    out = json.load(open(tmp_path / "experiments/eval_restored_results_fused.json"))
     assert set(out["FasterRCNN"]) == set(eval_all.VARIANTS)
 
 

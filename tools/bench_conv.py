@@ -10,6 +10,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "robust-object-detection_amd")]
 
+os.environ.setdefault("MX_CONV_TUNE", "0")  # the forced launch settings below, not the tuner's picks
+
 import torch  # noqa: E402
 
 from mx_det import conv as mc  # noqa: E402
@@ -75,6 +77,8 @@ def main():
     ap.add_argument("--splits", default="0", help="comma list of fwd/dgrad split-K caps, 0 = auto")
     ap.add_argument("--stages", default="0", help="comma list of buffer-kernel ring depths, 0 = auto")
     ap.add_argument("--graph", action="store_true", help="time launches replayed from a HIP graph")
+    ap.add_argument("--dtype", default="bf16", choices=("bf16", "f32"),
+                    help="f32: the precision-faithful bf16x3 kernels (TFLOP/s are f32-equivalent, peak 833)")
     args = ap.parse_args()
     global GRAPH
     GRAPH = args.graph
@@ -103,11 +107,12 @@ def run(args):
     for name, N, H, W, C, K, k, st, pd in SHAPES:
         if args.only and args.only not in name:
             continue
-        x = torch.randn(N, H, W, C, device=dev).bfloat16()
+        dt = torch.float32 if args.dtype == "f32" else torch.bfloat16
+        x = torch.randn(N, H, W, C, device=dev).to(dt)
         w = (torch.randn(K, C, k, k, device=dev) * 0.05)
-        wk, wt = mc.pack_weight(w, C, (st, st), (pd, pd), dgrad=True)
+        wk, wt = mc.pack_weight(w, C, (st, st), (pd, pd), dgrad=True, split=args.dtype == "f32")
         Ho, Wo = mc.out_hw(H, W, k, k, (st, st), (pd, pd))
-        dy = torch.randn(N, Ho, Wo, K, device=dev).bfloat16()
+        dy = torch.randn(N, Ho, Wo, K, device=dev).to(dt)
         fl = 2.0 * N * Ho * Wo * K * k * k * C
         res = []
         for kind, fn in (("fwd", lambda: mc.conv_fwd(x, wk, (st, st), (pd, pd), stats=True)),
