@@ -256,6 +256,9 @@ int mx_conv_set_tile(int block_rows, int block_cols);
 int mx_conv_set_max_splits(int max_splits);
 /* LDS ring depth of the 64x128 / 128x128 buffer-descriptor kernels (0 = automatic; tuning only). */
 int mx_conv_set_stages(int stages);
+/* K-tile order of the buffer-descriptor conv kernels: 0 tap-major, 1 (default) channel-major (all taps
+   of a 32-channel chunk before the next chunk: cross-tap re-reads of the gathered rows hit L2). */
+int mx_conv_set_korder(int order);
 int mx_conv_set_wgrad_target(int64_t blocks);
 
 /* ---------------------------------------------------------------------------------------------

@@ -59,6 +59,11 @@ struct ConvP {
   // bf16x3 (f32 activation) kernels: the lo plane of the split weight operand starts wt_plane
   // elements after the hi plane (wt)
   int64_t wt_plane;
+  // K-tile order of the buffer-descriptor kernels: 0 tap-major (all channel chunks of a tap, then
+  // the next tap), 1 channel-major (all taps of a 32-channel chunk, then the next chunk): the rows a
+  // block gathers between two visits of the same cache line shrink from BMT full pixel rows to the
+  // tap window of one chunk, so the re-reads across taps stay in L2
+  int korder;
   // dgrad feeding a train-mode BatchNorm backward (mx_conv2d_dgrad_bnb): per 64-row block column
   // sums of g = bf16(dx) * act'(y) and g * (z - mean) * invstd -> bnb_part [2][mblocks64][Ncol]
   const void* bnb_y;
@@ -119,11 +124,15 @@ __device__ __forceinline__ bool gather_pos(const ConvP& p, int oh, int ow, int r
 // granularity: stats[2][ceil(M/64)][Ncol] (row = m / 64).
 static constexpr int SROWS = 64;
 
-template <int BN, int HALVES = 1, int BMT = BM, typename TA = uint16_t>
-__device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT / 32][BN / 32], char* smem, int64_t m0,
-                                              int64_t n0, int64_t mt, int wm, int wn, int lane, int tid, int split) {
-  constexpr int WN = BN / 2, TJ = WN / 16, WM = BMT / 2, TI = BMT / 32;
+// WR = wave-rows of the block (2: 4 waves in 2x2, 4: 8 waves in 4x2; HALVES == WR then stages one
+// wave-row per pass).
+template <int BN, int HALVES = 1, int BMT = BM, typename TA = uint16_t, int WR = 2>
+__device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT / (16 * WR)][BN / 32], char* smem,
+                                              int64_t m0, int64_t n0, int64_t mt, int wm, int wn, int lane, int tid,
+                                              int split) {
+  constexpr int WN = BN / 2, TJ = WN / 16, WM = BMT / WR, TI = WM / 16, NT = 128 * WR;
   constexpr int PR = BMT / HALVES;  // rows staged per pass
+  static_assert(WR == 2 || (HALVES == WR && WM == SROWS), "8-wave tiles: one 64-row wave-row per pass");
   (void)mt;
   if (p.slab) {  // split-K partial: f32 tile to the slab, epilogue deferred to the reduce kernel
     constexpr int LD = BN + 4;
@@ -155,7 +164,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
   // ---- BatchNorm batch statistics from the f32 accumulators --------------------------------
   // C/D map (16x16): col = lane & 15, row = (lane >> 4) * 4 + reg
   if (p.stats) {
-    float* red = (float*)smem;  // [2 wm][2 (sum,sq)][BN]
+    float* red = (float*)smem;  // [WR wm][2 (sum,sq)][BN]
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       float s = 0.f, q = 0.f;
@@ -182,7 +191,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
       int64_t col = n0 + c;
       if (col >= p.Ncol) continue;
       if (WM == SROWS) {  // each wave-row is one statistics row
-        for (int w = 0; w < 2; ++w)
+        for (int w = 0; w < WR; ++w)
           if (m0 + w * WM < p.M) {
             p.stats[(srow + w) * p.Ncol + col] = red[(w * 2) * BN + c];
             p.stats[(p.mblocks + srow + w) * p.Ncol + col] = red[(w * 2 + 1) * BN + c];
@@ -754,18 +763,22 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_buf_kernel(ConvP p) {
   const int64_t nk = p.Kdim / BKT;
   const int64_t kbeg = (int64_t)split * p.kt_per_split;
   const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
-  // wave-uniform K position of the next tile to issue: tap (r, q), channel c
-  int ck = (int)(kbeg * BKT);
-  int ctap = ck / IC;
-  int cc = ck - ctap * IC;
-  int cr = ctap / S, cq = ctap - (ctap / S) * S;
+  // wave-uniform K position of the next tile to issue: tap (r, q), channel c (p.korder: K-tile order)
+  int cc, cr, cq;
+  {
+    const int RS = R * S, kb = (int)kbeg;
+    const int ctap = p.korder ? kb % RS : kb * BKT / IC;
+    cc = p.korder ? kb / RS * BKT : kb * BKT - ctap * IC;
+    cr = ctap / S;
+    cq = ctap - cr * S;
+  }
   auto issue = [&](int buf) {
     char* A = smem + buf * STAGE;
     char* B = A + A_BYTES;
     const int rr = MODE == 0 ? cr : R - 1 - cr, qq = MODE == 0 ? cq : S - 1 - cq;
     const uint32_t a_soff = (uint32_t)(((rr * IW + qq) * IC + cc) * 2);
-    const uint32_t b_soff = (uint32_t)(ck * 2);
     const int tap = cr * S + cq;
+    const uint32_t b_soff = (uint32_t)((tap * IC + cc) * 2);
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       // the whole offset in voffset (the origin may be negative; the tap offset brings it in range)
@@ -776,9 +789,12 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_buf_kernel(ConvP p) {
     for (int i = 0; i < BI; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (LDS_AS void*)(B + (wave * (BN / 4) + i * RPI) * RB), 16, b_voff[i],
                                                b_soff, 0, 0);
-    ck += BKT;
-    cc += BKT;
-    if (cc == IC) {
+    if (p.korder) {
+      if (++cq == S) {
+        cq = 0;
+        if (++cr == R) { cr = 0; cc += BKT; }
+      }
+    } else if ((cc += BKT) == IC) {
       cc = 0;
       if (++cq == S) { cq = 0; ++cr; }
     }
@@ -1557,6 +1573,174 @@ __global__ void __launch_bounds__(NT, 2) conv_x3_kernel(ConvP p) {
   conv_epilogue<BN, 2, BMT, float>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
 }
 
+// Chunk swizzle of the f32 A half-tiles of conv_x3_buf_kernel (64-B rows = 4 chunks of 4 f32): the
+// Gray code of the row's quarter within its 16-row fragment. A 16x16x32 fragment lane reads chunks
+// 2*(g&1) and 2*(g&1)+1 of half g>>1 (g = lane>>4), so each 16-lane ds_read_b128 group holds rows
+// 0..15 once, a quarter of them on the other chunk pair; with phys = logical ^ gray(quarter) the 16
+// lanes land on 16 distinct 4-bank groups (tile_swz<4> would collide rows 0-3 with 4-7).
+__device__ __forceinline__ int x3_swz(int row) {
+  const int g = (row >> 2) & 3;
+  return g ^ (g >> 1);
+}
+
+// bf16x3 implicit GEMM with an LDS-DMA ring (IC % 32 == 0, R*S <= 64, operands < 2 GiB): the f32 A
+// tile (BMT rows x 32 channels, one tap) lands as two 16-channel half-tiles of 64-B rows through
+// buffer_load_dwordx4 ... lds with wave-uniform tap offsets and per-row validity masks (as in
+// conv_igemm_buf_kernel); the pre-split weight planes land the same way. A fragments are split into
+// hi / lo in registers at read time (6 VALU per pair, ~2 per MFMA, hidden in the MFMA issue gaps),
+// so no register staging or ds_write sits on the critical path and STAGES-1 K-tiles stay in flight.
+template <int BN, int MODE, int STAGES, int OCC, int BMT, int WR = 2>
+__global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int RB = 64, RPI = 16;  // bytes per LDS row; rows landed per wave instruction
+  constexpr int NW = 2 * WR;  // waves: WR rows x 2 columns of wave tiles
+  constexpr int AR = BMT / NW, AI = AR / RPI, BR = BN / NW, BI = BR / RPI;
+  constexpr int LOADS = 2 * AI + 2 * BI;  // vmem instructions per K-tile per wave
+  constexpr int AH = BMT * RB, BP = BN * RB, STAGE = 2 * AH + 2 * BP;
+  constexpr int WN = BN / 2, TJ = WN / 16, WM = BMT / WR, TI = WM / 16;
+  static_assert(AI >= 1 && BI >= 1 && STAGES >= 2, "tile shape");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t ntiles_n = (p.Ncol + BN - 1) / BN;
+  const int64_t gid = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int split = (int)(gid % p.splits);
+  const int64_t bid = gid / p.splits;
+  const int64_t mt = bid / ntiles_n, nt = bid % ntiles_n;
+  const int64_t m0 = mt * BMT, n0 = nt * BN;
+  const int lrow = lane >> 2, pc = lane & 3;  // landing row within the instruction, physical chunk
+  const int qa = pc ^ x3_swz(lrow), qb = pc ^ tile_swz<4>(lrow);  // logical chunks fetched
+  const int IH = (int)p.IH, IW = (int)p.IW, IC = (int)p.IC, R = p.R, S = p.S;
+  uint32_t a_voff[AI];
+  uint64_t a_mask[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int64_t m = m0 + wave * AR + i * RPI + lrow;
+    uint64_t mask = 0;
+    int32_t off = 0;
+    if (m < p.M) {
+      const int ow = (int)(m % p.OW);
+      const int64_t t = m / p.OW;
+      const int oh = (int)(t % p.OH);
+      const int n = (int)(t / p.OH);
+      const int h0 = MODE == 0 ? oh * p.st_h - p.pad_h : oh + p.pad_h - (R - 1);
+      const int w0 = MODE == 0 ? ow * p.st_w - p.pad_w : ow + p.pad_w - (S - 1);
+      off = ((n * IH + h0) * IW + w0) * IC + qa * 4;
+      for (int r = 0; r < R; ++r)
+        for (int q = 0; q < S; ++q) {
+          const int rr = MODE == 0 ? r : R - 1 - r, qq = MODE == 0 ? q : S - 1 - q;
+          if ((unsigned)(h0 + rr) < (unsigned)IH && (unsigned)(w0 + qq) < (unsigned)IW) mask |= 1ull << (r * S + q);
+        }
+    }
+    a_voff[i] = (uint32_t)off * 4u;
+    a_mask[i] = mask;
+  }
+  uint32_t b_voff[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int64_t n = n0 + wave * BR + i * RPI + lrow;
+    b_voff[i] = n < p.Ncol ? (uint32_t)((n * p.Kdim + qb * 8) * 2) : kOOB;
+  }
+  const __amdgpu_buffer_rsrc_t arsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.src, (short)0, (int)(p.src_elems * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t bhrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.wt, (short)0, (int)(p.wt_elems * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t blrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.wt + p.wt_plane), (short)0, (int)(p.wt_elems * 2), 0x00020000);
+  const int64_t nk = p.Kdim / 32;
+  const int64_t kbeg = (int64_t)split * p.kt_per_split;
+  const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
+  // wave-uniform K position of the next tile to issue: tap (cr, cq), channel cc
+  int cc, cr, cq;
+  {
+    const int RS = R * S, kb = (int)kbeg;
+    const int ctap = p.korder ? kb % RS : kb * 32 / IC;
+    cc = p.korder ? kb / RS * 32 : kb * 32 - ctap * IC;
+    cr = ctap / S;
+    cq = ctap - cr * S;
+  }
+  auto issue = [&](int buf) {
+    char* A = smem + buf * STAGE;
+    char* B = A + 2 * AH;
+    const int rr = MODE == 0 ? cr : R - 1 - cr, qq = MODE == 0 ? cq : S - 1 - cq;
+    const uint32_t a_soff = (uint32_t)(((rr * IW + qq) * IC + cc) * 4);
+    const int tap = cr * S + cq;
+    const uint32_t b_soff = (uint32_t)((tap * IC + cc) * 2);
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const bool ok = (a_mask[i] >> tap) & 1ull;
+      const uint32_t v = a_voff[i] + a_soff;
+      char* dst = A + (wave * AR + i * RPI) * RB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (LDS_AS void*)dst, 16, ok ? v : kOOB, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (LDS_AS void*)(dst + AH), 16, ok ? v + 64u : kOOB, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      char* dst = B + (wave * BR + i * RPI) * RB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(bhrsrc, (LDS_AS void*)dst, 16, b_voff[i], b_soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(blrsrc, (LDS_AS void*)(dst + BP), 16, b_voff[i], b_soff, 0, 0);
+    }
+    if (p.korder) {
+      if (++cq == S) {
+        cq = 0;
+        if (++cr == R) { cr = 0; cc += 32; }
+      }
+    } else if ((cc += 32) == IC) {
+      cc = 0;
+      if (++cq == S) { cq = 0; ++cr; }
+    }
+  };
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < STAGES - 1; ++st)
+    if (st < ntk) issue(st);
+  const int g = lane >> 4, q0 = (g & 1) * 2;
+  for (int64_t t = 0; t < ntk; ++t) {
+    if (t + STAGES - 2 < ntk) wait_vmcnt<LOADS * (STAGES - 2)>();
+    else wait_vmcnt<0>();
+    block_barrier();
+    if (t + STAGES - 1 < ntk) issue((int)((t + STAGES - 1) % STAGES));
+    const char* A = smem + (int)(t % STAGES) * STAGE;
+    const char* Ag = A + (g >> 1) * AH;
+    const char* Bh = A + 2 * AH;
+    const char* Bl = Bh + BP;
+    bf16x8 ah[TI], al[TI], bh[TJ], bl[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int row = wn * WN + j * 16 + (lane & 15);
+      const int off = row * RB + ((g ^ tile_swz<4>(row)) << 4);
+      bh[j] = *(const bf16x8*)(Bh + off);
+      bl[j] = *(const bf16x8*)(Bl + off);
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int row = wm * WM + i * 16 + (lane & 15);
+      const int f = x3_swz(row);
+      const float4 u = *(const float4*)(Ag + row * RB + ((q0 ^ f) << 4));
+      const float4 w = *(const float4*)(Ag + row * RB + (((q0 + 1) ^ f) << 4));
+      uint4 h, l;
+      split8(u, w, h, l);
+      ah[i] = __builtin_bit_cast(bf16x8, h);
+      al[i] = __builtin_bit_cast(bf16x8, l);
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+  }
+  __syncthreads();
+  conv_epilogue<BN, WR, BMT, float, WR>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
+#endif
+}
+
 // bf16x3 wgrad: dw[k][(r,s,c)] = sum_p dy[p][k] * x[gather(p, r, s)][c] on f32 dy / x, both split
 // into hi / lo while staged (register loads, 32-pixel K-tiles, pixel-major bf16 LDS tiles with the
 // swz_w swizzle), fragments read transposed with ds_read_b64_tr_b16 as in conv_wgrad_buf_kernel;
@@ -1954,8 +2138,8 @@ struct Geo {
 static int num_cus();
 static int g_force_bmt = 0, g_force_bn = 0;  // mx_conv_set_tile (0 = automatic)
 extern "C" int mx_conv_set_tile(int bmt, int bn) {
-  MX_CHECK_ARG((bmt == 0 && bn == 0) || ((bmt == 64 || bmt == 128) && (bn == 64 || bn == 128 || bn == 256)),
-               "mx_conv_set_tile: (0,0) auto, or bmt 64/128 x bn 64/128/256");
+  MX_CHECK_ARG((bmt == 0 && bn == 0) || ((bmt == 64 || bmt == 128 || bmt == 256) && (bn == 64 || bn == 128 || bn == 256)),
+               "mx_conv_set_tile: (0,0) auto, or bmt 64/128/256 (256: bf16x3 kernels only) x bn 64/128/256");
   g_force_bmt = bmt;
   g_force_bn = bn;
   return MX_OK;
@@ -1963,8 +2147,14 @@ extern "C" int mx_conv_set_tile(int bmt, int bn) {
 
 static int g_buf_stages = 0;  // mx_conv_set_stages: LDS ring depth of the 64x128 / 128x128 buffer kernels
 extern "C" int mx_conv_set_stages(int n) {
-  MX_CHECK_ARG(n == 0 || n == 3 || n == 4 || n == 6, "mx_conv_set_stages: 0 (auto), 3, 4 or 6");
+  MX_CHECK_ARG(n == 0 || n == 3 || n == 4 || n == 6, "mx_conv_set_stages: 0 (auto), 3, 4 or 6 (x3 kernels: 3 = alternative ring)");
   g_buf_stages = n;
+  return MX_OK;
+}
+static int g_conv_korder = 1;  // mx_conv_set_korder: K-tile order of the buffer kernels (ConvP::korder)
+extern "C" int mx_conv_set_korder(int v) {
+  MX_CHECK_ARG(v == 0 || v == 1, "mx_conv_set_korder: 0 tap-major, 1 channel-major");
+  g_conv_korder = v;
   return MX_OK;
 }
 static int g_max_splits = 0;  // mx_conv_set_max_splits (0 = automatic, 1 = never split K)
@@ -2011,7 +2201,7 @@ static Geo make_geo(int64_t M, int64_t Ncol, int64_t Kdim) {
     g.tiles = cdiv(g.M, 64) * ntn;
   }
   if (g_force_bmt) {
-    g.bmt = g_force_bmt;
+    g.bmt = std::min(g_force_bmt, 128);
     g.bn = g_force_bn;
     g.narrow = g.bn == 64;
     g.tiles = cdiv(g.M, g.bmt) * cdiv(g.Ncol, g.bn);
@@ -2171,6 +2361,7 @@ static int launch_igemm(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipSt
     blocks *= p.splits;
   }
   if (buf) {
+    p.korder = g_conv_korder;
     if (g_conv_loader == 2) p.src_elems = 0;
     if (g_conv_loader == 3) p.wt_elems = 0;
     if (g.bmt == 64) {
@@ -2591,6 +2782,9 @@ static Geo make_geo_x3(int64_t M, int64_t Ncol, int64_t Kdim) {
   g.bn = g.narrow ? 64 : 128;
   const int64_t cus = num_cus();
   // 2 blocks per CU: below two full rounds of 128-row tiles, 64-row tiles (twice the blocks)
+  // 128 x 128 at 2 blocks per CU; below two full rounds, 64-row tiles. (256 x 128 tiles -- 8 waves,
+  // one block per CU, 25 % fewer LDS-DMA pieces per MFMA -- measured 15 % slower on the P2 3x3; a
+  // tuner candidate only.)
   g.bmt = 128;
   g.tiles = cdiv(M, 128) * cdiv(Ncol, g.bn);
   if (g.tiles < 2 * cus) {
@@ -2600,6 +2794,7 @@ static Geo make_geo_x3(int64_t M, int64_t Ncol, int64_t Kdim) {
   if (g_force_bmt) {
     g.bmt = g_force_bmt;
     g.bn = std::min(g_force_bn, 128);
+    if (g.bmt == 256) g.bn = 128;
     g.narrow = g.bn == 64;
     g.tiles = cdiv(M, g.bmt) * cdiv(Ncol, g.bn);
   }
@@ -2620,8 +2815,22 @@ static void launch_x3(const ConvP& p, int64_t blocks, hipStream_t st) {
   conv_x3_kernel<BN, MODE, BMT><<<(unsigned)blocks, NT, std::max(ring, epi), st>>>(p);
 }
 
+template <int BN, int MODE, int STAGES, int OCC, int BMT, int WR = 2>
+static void launch_x3_buf(const ConvP& p, int64_t blocks, hipStream_t st) {
+  const size_t ring = (size_t)STAGES * 2 * (BMT + BN) * 64;
+  const size_t epi = (size_t)(BMT / WR) * (BN + 4) * 4;
+  conv_x3_buf_kernel<BN, MODE, STAGES, OCC, BMT, WR><<<(unsigned)blocks, 128 * WR, std::max(ring, epi), st>>>(p);
+}
+
 template <int MODE>
-static int launch_igemm_x3(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hipStream_t st) {
+static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, hipStream_t st) {
+  const bool buf = g_conv_loader >= 1 && p.IC % 32 == 0 && p.R * p.S <= 64 && p.Kdim % 32 == 0 && p.src_elems > 0 &&
+                   p.src_elems * 4 < (1ll << 31) && p.wt_elems > 0 && p.wt_plane + p.wt_elems < (1ll << 30);
+  Geo g = g0;
+  if (g.bmt == 256 && !buf) {  // 256-row tiles exist only as the buffer kernel
+    g.bmt = 128;
+    g.tiles = cdiv(g.M, 128) * cdiv(g.Ncol, g.bn);
+  }
   int64_t blocks = g.tiles;
   MX_CHECK_ARG(g.Kdim < (1ll << 30) && p.IH < (1ll << 26) && p.IW < (1ll << 26) && p.IC < (1ll << 30),
                "conv: GEMM K or spatial size too large");
@@ -2639,7 +2848,20 @@ static int launch_igemm_x3(ConvP& p, const Geo& g, void* ws, size_t ws_bytes, hi
     blocks *= p.splits;
   }
   MX_CHECK_ARG(blocks < (1ll << 31), "conv: grid too large");
-  if (g.bmt == 64) {
+  if (buf) {
+    // ring depth x blocks per CU; mx_conv_set_stages(3) picks the alternative of each tile shape
+    const bool alt = g_buf_stages == 3;
+    p.korder = g_conv_korder;
+    if (g.bmt == 256) {
+      alt ? launch_x3_buf<128, MODE, 2, 1, 256, 4>(p, blocks, st) : launch_x3_buf<128, MODE, 3, 1, 256, 4>(p, blocks, st);
+    } else if (g.bmt == 64) {
+      if (g.bn == 64) alt ? launch_x3_buf<64, MODE, 4, 2, 64>(p, blocks, st) : launch_x3_buf<64, MODE, 3, 3, 64>(p, blocks, st);
+      else alt ? launch_x3_buf<128, MODE, 2, 3, 64>(p, blocks, st) : launch_x3_buf<128, MODE, 3, 2, 64>(p, blocks, st);
+    } else {
+      if (g.bn == 64) alt ? launch_x3_buf<64, MODE, 2, 3, 128>(p, blocks, st) : launch_x3_buf<64, MODE, 3, 2, 128>(p, blocks, st);
+      else alt ? launch_x3_buf<128, MODE, 3, 1, 128>(p, blocks, st) : launch_x3_buf<128, MODE, 2, 2, 128>(p, blocks, st);
+    }
+  } else if (g.bmt == 64) {
     if (g.bn == 64) launch_x3<64, MODE, 64>(p, blocks, st);
     else launch_x3<128, MODE, 64>(p, blocks, st);
   } else {

@@ -66,6 +66,7 @@ _SIGS = {
     "mx_conv_set_tile": (c_int, [c_int, c_int]),
     "mx_conv_set_max_splits": (c_int, [c_int]),
     "mx_conv_set_stages": (c_int, [c_int]),
+    "mx_conv_set_korder": (c_int, [c_int]),
     "mx_conv_set_wgrad_variant": (c_int, [c_int]),
     "mx_conv_get_wgrad_variant": (c_int, []),
     "mx_conv_set_wgrad_target": (c_int, [c_i64]),

@@ -133,9 +133,21 @@ def test_x3_dgrad_wgrad(dev, N, H, W, C, K, k, st, pd):
     _check(dw, wr.grad, wt_.grad)
 
 
-def test_x3_dgrad_residual_and_bn_partials(dev):
+@pytest.mark.parametrize("tile", [(0, 0), (256, 128), (64, 64)])
+def test_x3_dgrad_residual_and_bn_partials(dev, tile, monkeypatch):
     """dgrad epilogue extras on f32: + residual (bottleneck identity gradient) and the BN-backward
-    column partials of g = dx * act'(y), g * (z - mean) * invstd per 64-row block."""
+    column partials of g = dx * act'(y), g * (z - mean) * invstd per 64-row block; auto and forced
+    block tiles (the 256-row tile stages its 8-wave epilogue one wave-row at a time)."""
+    from mx_det._lib import call
+    monkeypatch.setenv("MX_CONV_TUNE", "0")  # the forced tile, not the tuner's pick
+    call("mx_conv_set_tile", *tile)
+    try:
+        _dgrad_residual_and_bn_partials(dev)
+    finally:
+        call("mx_conv_set_tile", 0, 0)
+
+
+def _dgrad_residual_and_bn_partials(dev):
     from mx_det import conv as mc
     g = torch.Generator().manual_seed(3)
     N, H, W, C, K = 2, 20, 24, 64, 128
@@ -244,7 +256,7 @@ def test_x3_act_bias_bwd_f32(dev, M, K, act):
     torch.testing.assert_close(db.cpu(), ref.double().sum(0).float(), rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("ci", range(7))
+@pytest.mark.parametrize("ci", range(9))
 @pytest.mark.parametrize("case", [CASES[i] for i in (0, 1, 3, 7, 8, 9)])
 def test_x3_tuner_candidates(dev, monkeypatch, ci, case):
     """Every launch configuration the per-shape tuner may pick for the bf16x3 kernels (block tile x

@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--tiles", default="0x0", help="comma list of BMTxBN overrides, 0x0 = auto")
     ap.add_argument("--splits", default="0", help="comma list of fwd/dgrad split-K caps, 0 = auto")
     ap.add_argument("--stages", default="0", help="comma list of buffer-kernel ring depths, 0 = auto")
+    ap.add_argument("--korder", default="1", help="comma list of buffer-kernel K-tile orders (0 tap-, 1 channel-major)")
     ap.add_argument("--graph", action="store_true", help="time launches replayed from a HIP graph")
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "f32"),
                     help="f32: the precision-faithful bf16x3 kernels (TFLOP/s are f32-equivalent, peak 833)")
@@ -85,19 +86,20 @@ def main():
     import itertools
     from mx_det import _lib
     ints = lambda v: [int(x) for x in v.split(",")]  # noqa: E731
-    for ld, v, wv, wt, stg, sp, tl in itertools.product(ints(args.loaders), ints(args.variants), ints(args.wgrad),
-                                                         ints(args.wtarget), ints(args.stages), ints(args.splits),
-                                                         args.tiles.split(",")):
+    for ko, ld, v, wv, wt, stg, sp, tl in itertools.product(ints(args.korder), ints(args.loaders), ints(args.variants),
+                                                             ints(args.wgrad), ints(args.wtarget), ints(args.stages),
+                                                             ints(args.splits), args.tiles.split(",")):
         bm, bn = [int(x) for x in tl.split("x")]
         _lib.call("mx_conv_set_tile", bm, bn)
         _lib.call("mx_conv_set_max_splits", sp)
         _lib.call("mx_conv_set_stages", stg)
+        _lib.call("mx_conv_set_korder", ko)
         _lib.call("mx_conv_set_loader", ld)
         _lib.call("mx_conv_set_variant", v)
         _lib.call("mx_conv_set_wgrad_variant", wv)
         _lib.call("mx_conv_set_wgrad_target", wt)
         print(f"== loader {ld} tile {tl} conv variant {v} wgrad variant {wv} wgrad target {wt} "
-              f"max splits {sp} stages {stg}", flush=True)
+              f"max splits {sp} stages {stg} korder {ko}", flush=True)
         run(args)
 
 
