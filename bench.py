@@ -252,6 +252,20 @@ def hbm_ops_roofline(model, opt, imgs, tg, reps=20):
                                 "dtype": str(feats[0].dtype).replace("torch.", ""), "avg_launch_us": round(us, 2),
                                 "algorithmic_mb": round(byts / 1e6, 2), "achieved": round(gbs, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        # backward (deterministic gather): every f32 level-map element written once + gout read once
+        fs = [f.clone().requires_grad_(True) for f in feats]
+        out = ops.multiscale_roi_align(fs, rois, scales, k_min)
+        g = torch.randn_like(out)
+        det = ops.roi_align_deterministic(C)
+        us = timed(lambda: torch.autograd.grad(out, fs, g, retain_graph=True))
+        maps = sum(f.numel() for f in feats) * 4
+        byts = maps + g.numel() * g.element_size()
+        gbs = byts / (us * 1e-6) / 1e9
+        res["roi_align_bwd"] = {"kernel": "roi_bwd_gather_kernel (+ roi_bwd_prep_kernel)" if det else
+                                "roi_align_bwd_kernel (atomics) + zero fill", "deterministic": det, "rois": K,
+                                "channels": C, "avg_call_us": round(us, 2), "level_map_mb": round(maps / 1e6, 2),
+                                "algorithmic_mb": round(byts / 1e6, 2), "achieved": round(gbs, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
     if "nms" in cap:
         boxes, scores, lvl, group, G, L, thr, max_seg = cap["nms"]
         n = boxes.shape[0]

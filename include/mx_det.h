@@ -97,23 +97,30 @@ int mx_batched_nms(const float* boxes, const float* scores, const int64_t* idxs,
  * (floor(4 + log2(sqrt(area)/224) + 1e-6) clamped to [k_min, k_max]) — replaces
  * RoIHeads.box_roi_pool reached from train_frcnn_baseline.py:171 / eval_all.py:111.
  *   feats[l]: NHWC [N, H[l], W[l], C] of dtype; rois[K,5] f32 (batch, x1,y1,x2,y2).
- *   out: [K, PH, PW, C] dtype.  Backward: grad_feats[l] NHWC f32, zero-initialised by the caller,
- *   accumulated with float atomics (order-dependent in the last bits).
+ *   out: [K, PH, PW, C] dtype.  Backward (torchvision _roi_align_backward,
+ *   roi_align_kernel.cpp roi_align_backward_kernel_impl): grad_feats[l] NHWC f32 over N images.
+ *     deterministic = 1: atomic-free gather -- every element of every grad map is WRITTEN (no
+ *       zero-fill needed) with one fixed summation order per element (RoI ascending, bin, corner):
+ *       bitwise reproducible run to run. Needs C % 4 == 0 with C <= 256, pooled bins <= 64, sampling <= 4, level maps
+ *       < 32768 px a side, and a workspace of mx_roi_align_bwd_workspace(K, PH, PW, sampling) bytes.
+ *     deterministic = 0: float atomics ACCUMULATE into caller-zeroed maps (order-dependent in
+ *       the last bits; no workspace).
  * ------------------------------------------------------------------------------------------- */
+size_t mx_roi_align_bwd_workspace(int64_t K, int PH, int PW, int sampling);
 int mx_roi_align_fwd(const void* feat, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, const float* rois,
                      int64_t K, float spatial_scale, int PH, int PW, int sampling, int aligned, void* out,
                      mx_stream_t stream);
 int mx_roi_align_bwd(const void* grad_out, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, const float* rois,
                      int64_t K, float spatial_scale, int PH, int PW, int sampling, int aligned, float* grad_feat,
-                     mx_stream_t stream);
+                     int deterministic, void* ws, size_t ws_bytes, mx_stream_t stream);
 int mx_multiscale_roi_align_fwd(const void* const* feats_host, const int64_t* H_host, const int64_t* W_host,
                                 const float* scales_host, int nlev, int k_min, int dtype, int64_t C,
                                 const float* rois, int64_t K, int PH, int PW, int sampling, void* out,
                                 int32_t* levels_out, mx_stream_t stream);
-int mx_multiscale_roi_align_bwd(const void* grad_out, int dtype, float* const* grad_feats_host,
+int mx_multiscale_roi_align_bwd(const void* grad_out, int dtype, float* const* grad_feats_host, int64_t N,
                                 const int64_t* H_host, const int64_t* W_host, const float* scales_host, int nlev,
                                 int64_t C, const float* rois, const int32_t* levels, int64_t K, int PH, int PW,
-                                int sampling, mx_stream_t stream);
+                                int sampling, int deterministic, void* ws, size_t ws_bytes, mx_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Anchors and box coder (torchvision AnchorGenerator / BoxCoder, anchor_utils.py, _utils.py).

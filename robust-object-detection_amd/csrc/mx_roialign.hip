@@ -5,7 +5,9 @@
 // when !aligned, bin = size/pooled, sample at start + p*bin + (i+.5)*bin/grid, bilinear with the
 // (<-1 or >H) skip and edge clamp, out = sum(((w1 f1 + w2 f2) + w3 f3) + w4 f4) / count.
 // Built -ffp-contract=off so each f32 op rounds as the C++ does: with f32 features the forward is
-// bit-identical to the CPU kernel (same op order per output element). Backward uses f32 atomics.
+// bit-identical to the CPU kernel (same op order per output element). Backward: a deterministic
+// gather (default; fixed summation order per element, bitwise reproducible, every level-map element
+// written once) or f32 atomics (deterministic = 0; the caller zero-fills the gradient maps).
 //
 // Serves RoIHeads.box_roi_pool = MultiScaleRoIAlign(['0','1','2','3'], 7, 2) (reached from
 // train_frcnn_baseline.py:171 / eval_all.py:111), whose LevelMapper is fused here:
@@ -53,24 +55,36 @@ __device__ __forceinline__ RoiGeo roi_geo(const float* r, float scale, int PH, i
   return g;
 }
 
-__device__ __forceinline__ Samp make_samp(const RoiGeo& g, int64_t H, int64_t W, int ph, int pw, int iy, int ix) {
-  Samp s;
+// One bilinear sample: its corner rows/cols (yl, yh) x (xl, xh) and weights; false if the sample
+// lies outside [-1, H] x [-1, W] (contributes nothing).
+__device__ __forceinline__ bool sample_corners(const RoiGeo& g, int64_t H, int64_t W, int ph, int pw, int iy, int ix,
+                                               int& yl, int& xl, int& yh, int& xh, float (&w)[4]) {
   float y = (g.sh + (float)ph * g.bh) + ((float)iy + .5f) * g.bh / (float)g.gh;
   float x = (g.sw + (float)pw * g.bw) + ((float)ix + .5f) * g.bw / (float)g.gw;
-  if (y < -1.0f || y > (float)H || x < -1.0f || x > (float)W) {
+  if (y < -1.0f || y > (float)H || x < -1.0f || x > (float)W) return false;
+  if (y <= 0) y = 0;
+  if (x <= 0) x = 0;
+  yl = (int)y;
+  xl = (int)x;
+  if (yl >= H - 1) { yh = yl = (int)H - 1; y = (float)yl; } else yh = yl + 1;
+  if (xl >= W - 1) { xh = xl = (int)W - 1; x = (float)xl; } else xh = xl + 1;
+  float ly = y - (float)yl, lx = x - (float)xl, hy = 1.f - ly, hx = 1.f - lx;
+  w[0] = hy * hx; w[1] = hy * lx; w[2] = ly * hx; w[3] = ly * lx;
+  return true;
+}
+
+__device__ __forceinline__ Samp make_samp(const RoiGeo& g, int64_t H, int64_t W, int ph, int pw, int iy, int ix) {
+  Samp s;
+  int yl, xl, yh, xh;
+  float w[4];
+  if (!sample_corners(g, H, W, ph, pw, iy, ix, yl, xl, yh, xh, w)) {
     s.p1 = -1; s.p2 = s.p3 = s.p4 = 0;
     s.w1 = s.w2 = s.w3 = s.w4 = 0.f;
     return s;
   }
-  if (y <= 0) y = 0;
-  if (x <= 0) x = 0;
-  int64_t yl = (int64_t)y, xl = (int64_t)x, yh, xh;
-  if (yl >= H - 1) { yh = yl = H - 1; y = (float)yl; } else yh = yl + 1;
-  if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else xh = xl + 1;
-  float ly = y - (float)yl, lx = x - (float)xl, hy = 1.f - ly, hx = 1.f - lx;
-  s.p1 = (int32_t)(yl * W + xl); s.p2 = (int32_t)(yl * W + xh);
-  s.p3 = (int32_t)(yh * W + xl); s.p4 = (int32_t)(yh * W + xh);
-  s.w1 = hy * hx; s.w2 = hy * lx; s.w3 = ly * hx; s.w4 = ly * lx;
+  s.p1 = (int32_t)((int64_t)yl * W + xl); s.p2 = (int32_t)((int64_t)yl * W + xh);
+  s.p3 = (int32_t)((int64_t)yh * W + xl); s.p4 = (int32_t)((int64_t)yh * W + xh);
+  s.w1 = w[0]; s.w2 = w[1]; s.w3 = w[2]; s.w4 = w[3];
   return s;
 }
 
@@ -216,12 +230,14 @@ __global__ void __launch_bounds__(256) roi_align_bwd_kernel(Levels L, int64_t C,
   }
 }
 
-// ---- bf16 forward, 8 channels per lane ----------------------------------------------------------
-// Same per-channel arithmetic (and order) as roi_align_fwd_kernel, 16-B loads: a group of C/8 lanes
-// covers one bin's channel row, 256 / (C/8) groups stride the bins.
+// ---- vector forward, 8 channels per lane (bf16: one 16-B load, f32: two) -------------------------
+// Same per-channel arithmetic (and order) as roi_align_fwd_kernel: a group of C/8 lanes covers one
+// bin's channel row, 256 / (C/8) groups stride the bins, and every lane keeps its 4 samples x 4
+// corners of loads independent (16-32 loads in flight per lane instead of one scalar at a time).
+template <typename T>
 __global__ void __launch_bounds__(256) roi_align_fwd_v8_kernel(Levels L, int64_t C, const float* __restrict__ rois, int PH,
                                                                int PW, int sampling, int aligned, int multiscale,
-                                                               uint16_t* __restrict__ out, int32_t* __restrict__ lv_out) {
+                                                               T* __restrict__ out, int32_t* __restrict__ lv_out) {
   __shared__ Samp tab[kMaxSamp];
   __shared__ RoiGeo sg;
   __shared__ int slv;
@@ -246,26 +262,261 @@ __global__ void __launch_bounds__(256) roi_align_fwd_v8_kernel(Levels L, int64_t
   }
   __syncthreads();
   const int C8 = (int)(C / 8);
-  const uint16_t* f = (const uint16_t*)L.f[lv] + g.b * H * W * C;
+  const T* f = (const T*)L.f[lv] + g.b * H * W * C;
   for (int e = threadIdx.x; e < nbins * C8; e += blockDim.x) {
     const int bin = e / C8, c0 = (e - bin * C8) * 8;
     float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int s = 0; s < per_bin; ++s) {
       const Samp p = tab[bin * per_bin + s];
       if (p.p1 < 0) continue;
-      const uint4 u1 = *(const uint4*)(f + (int64_t)p.p1 * C + c0), u2 = *(const uint4*)(f + (int64_t)p.p2 * C + c0);
-      const uint4 u3 = *(const uint4*)(f + (int64_t)p.p3 * C + c0), u4 = *(const uint4*)(f + (int64_t)p.p4 * C + c0);
-      const uint16_t *h1 = (const uint16_t*)&u1, *h2 = (const uint16_t*)&u2, *h3 = (const uint16_t*)&u3,
-                     *h4 = (const uint16_t*)&u4;
+      float f1[8], f2[8], f3[8], f4[8];
+      ld8(f + (int64_t)p.p1 * C + c0, f1);
+      ld8(f + (int64_t)p.p2 * C + c0, f2);
+      ld8(f + (int64_t)p.p3 * C + c0, f3);
+      ld8(f + (int64_t)p.p4 * C + c0, f4);
 #pragma unroll
-      for (int t = 0; t < 8; ++t)
-        v[t] += ((p.w1 * bf2f(h1[t]) + p.w2 * bf2f(h2[t])) + p.w3 * bf2f(h3[t])) + p.w4 * bf2f(h4[t]);
+      for (int t = 0; t < 8; ++t) v[t] += ((p.w1 * f1[t] + p.w2 * f2[t]) + p.w3 * f3[t]) + p.w4 * f4[t];
     }
-    uint4 o;
-    uint16_t* oh = (uint16_t*)&o;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) oh[t] = f2bf(v[t] / g.count);
-    *(uint4*)(out + (k * nbins + bin) * C + c0) = o;
+    for (int t = 0; t < 8; ++t) v[t] = v[t] / g.count;
+    st8(out + (k * nbins + bin) * C + c0, v);
+  }
+}
+
+// ---- deterministic backward (gather form, no atomics) ---------------------------------------------
+// grad_feat[n, y, x, :] = sum over the RoIs k of image n at this level, their bins and the bilinear
+// corners landing on (y, x) of gout[k, bin, :] / count * w. Pass 1 (one block per RoI) merges each
+// bin's corners per distinct pixel (summed weights, fixed sample/corner order) into
+// ent[k][bin][0..cnt) and records the RoI's pixel footprint. Pass 2 (one block per 8x8 pixel tile of
+// every level map and image) walks the RoIs overlapping its tile in ascending k; wave w owns 64/G
+// of the tile's pixels in an LDS f32 accumulator and adds their contributions in (k, bin, corner)
+// order, so every output element has one fixed summation order: bitwise reproducible. Every pixel
+// of every level map is written exactly once (untouched ones as 0): no zero-fill, no atomics.
+struct BwdEnt {
+  int32_t yx;  // y << 16 | x on the level map
+  float w;     // summed bilinear weight of this pixel within the bin
+};
+
+// Pass 1: one block per RoI, one thread per bin: the bin's per_bin samples x 4 corners as entries in
+// torchvision's loop order (iy, ix, corner 1..4; roi_align_kernel.cpp roi_align_backward_kernel_impl),
+// yx = -1 for samples outside the map, plus the bin's and the RoI's pixel bbox.
+__global__ void __launch_bounds__(64) roi_bwd_prep_kernel(Levels L, const float* __restrict__ rois,
+                                                          const int32_t* __restrict__ lv_in, int PH, int PW, int sampling,
+                                                          int aligned, int S4, BwdEnt* __restrict__ ent,
+                                                          int2* __restrict__ binbox, int4* __restrict__ box,
+                                                          int32_t* __restrict__ meta) {
+  __shared__ int sb[4];
+  const int64_t k = blockIdx.x;
+  const float* r = rois + 5 * k;
+  const int lv = lv_in ? lv_in[k] : 0;
+  const RoiGeo g = roi_geo(r, L.scale[lv], PH, PW, sampling, aligned);
+  const int64_t H = L.H[lv], W = L.W[lv];
+  const int per_bin = g.gh * g.gw, nbins = PH * PW;
+  if (threadIdx.x == 0) {
+    sb[0] = sb[2] = 0x7fffffff;
+    sb[1] = sb[3] = -1;
+  }
+  __syncthreads();
+  int y0 = 0x7fffffff, y1 = -1, x0 = 0x7fffffff, x1 = -1;
+  for (int bin = threadIdx.x; bin < nbins; bin += blockDim.x) {
+    BwdEnt* e = ent + (k * nbins + bin) * S4;
+    int by0 = 0x7fff, by1 = -1, bx0 = 0x7fff, bx1 = -1;
+    for (int sidx = 0; sidx < per_bin; ++sidx) {
+      int yl, xl, yh, xh;
+      float ww[4];
+      if (!sample_corners(g, H, W, bin / PW, bin % PW, sidx / g.gw, sidx % g.gw, yl, xl, yh, xh, ww)) {
+        for (int q = 0; q < 4; ++q) { e[4 * sidx + q].yx = -1; e[4 * sidx + q].w = 0.f; }
+        continue;
+      }
+      const int cy[4] = {yl, yl, yh, yh}, cx[4] = {xl, xh, xl, xh};
+      for (int q = 0; q < 4; ++q) {
+        e[4 * sidx + q].yx = (cy[q] << 16) | cx[q];
+        e[4 * sidx + q].w = ww[q];
+      }
+      by0 = min(by0, yl); by1 = max(by1, yh); bx0 = min(bx0, xl); bx1 = max(bx1, xh);
+    }
+    for (int j = 4 * per_bin; j < S4; ++j) { e[j].yx = -1; e[j].w = 0.f; }
+    binbox[k * nbins + bin] = make_int2((by0 & 0xffff) | (by1 << 16), (bx0 & 0xffff) | (bx1 << 16));
+    y0 = min(y0, by0); y1 = max(y1, by1); x0 = min(x0, bx0); x1 = max(x1, bx1);
+  }
+  atomicMin(&sb[0], y0); atomicMax(&sb[1], y1); atomicMin(&sb[2], x0); atomicMax(&sb[3], x1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    box[k] = make_int4(sb[0], sb[1], sb[2], sb[3]);
+    meta[k] = (int32_t)(g.b * 8 + lv);
+  }
+}
+
+struct TileGrid {
+  int64_t first[6];  // first tile id of each level (level-major, then image, then tile row, col)
+  int tw[5], th[5];
+  int n;
+};
+
+template <typename T>
+__device__ __forceinline__ float4 ld4f(const T* p) {
+  if constexpr (sizeof(T) == 2) {
+    const uint2 u = *(const uint2*)p;
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xffff0000u));
+  } else {
+    return *(const float4*)p;
+  }
+}
+
+// Pass 2: one block per 8x8 tile, 8 waves; wave w owns the tile's pixel row w (8 pixels, f32
+// accumulators in registers), lanes = channel quads (C <= 256). The RoIs overlapping the tile
+// are listed in ascending k (one ordered block compaction per 1024 RoIs); each wave then walks them
+// independently (no barriers): a ballot over the RoI's bins picks those whose pixel bbox meets the
+// wave's strip, 64/S4 (<= 4) such bins are loaded at once -- their corner slots one per lane and their
+// gout rows one quad per lane, the next group prefetched while the current one is applied -- and
+// the hit bits are walked in slot order with readlane: fixed order per output element.
+template <typename T>
+__global__ void __launch_bounds__(512, 2) roi_bwd_gather_kernel(Levels L, TileGrid TG, int64_t C, int64_t K, int nbins, int S4,
+                                                             float count, const BwdEnt* __restrict__ ent,
+                                                             const int2* __restrict__ binbox, const int4* __restrict__ box,
+                                                             const int32_t* __restrict__ meta, const T* __restrict__ gout) {
+  __shared__ int list[1024];
+  __shared__ int wcnt[2][8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t id = blockIdx.x;
+  int lv = 0;
+  while (lv + 1 < TG.n && id >= TG.first[lv + 1]) ++lv;
+  const int64_t rem = id - TG.first[lv];
+  const int per_img = TG.th[lv] * TG.tw[lv];
+  const int n = (int)(rem / per_img), t = (int)(rem % per_img);
+  const int ty0 = (t / TG.tw[lv]) * 8, tx0 = (t % TG.tw[lv]) * 8;
+  const int64_t H = L.H[lv], W = L.W[lv];
+  const int Q = (int)(C / 4);
+  const bool qa = lane < Q;  // this lane's channel quad exists
+  // this wave's 8 pixels (named registers: an indexed array would go to scratch)
+  float4 a0{}, a1{}, a2{}, a3{}, a4{}, a5{}, a6{}, a7{};
+  const float inv = 1.f / count;
+  const bool pow2 = inv * count == 1.f && (__float_as_uint(count) & 0x7fffffu) == 0;
+  const int32_t want = n * 8 + lv;
+  const int sy0 = ty0 + wave;  // this wave's strip: row sy0, cols tx0..tx0+7
+  const int NBC = min(4, 64 / S4);  // bins per load group
+  const int sub = lane / S4, sj = lane - sub * S4;
+  for (int64_t c0 = 0; c0 < K; c0 += 1024) {
+    bool hit[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int64_t kq = c0 + r * 512 + tid;
+      hit[r] = false;
+      if (kq < K && meta[kq] == want) {
+        const int4 b = box[kq];
+        hit[r] = b.x <= ty0 + 7 && b.y >= ty0 && b.z <= tx0 + 7 && b.w >= tx0;
+      }
+    }
+    uint64_t m[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      m[r] = __ballot(hit[r]);
+      if (lane == 0) wcnt[r][wave] = __popcll(m[r]);
+    }
+    __syncthreads();
+    int base = 0;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      int pre = 0, tot = 0;
+      for (int w = 0; w < 8; ++w) {
+        pre += w < wave ? wcnt[r][w] : 0;
+        tot += wcnt[r][w];
+      }
+      if (hit[r]) list[base + pre + __popcll(m[r] & ((1ull << lane) - 1))] = (int)(c0 + r * 512 + tid);
+      base += tot;
+    }
+    const int nl = base;
+    __syncthreads();
+    for (int li = 0; li < nl; ++li) {
+      const int64_t kk = list[li];
+      // bins of this RoI whose pixel bbox meets the strip (nbins <= 64 for the deterministic path)
+      bool bh = false;
+      if (lane < nbins) {
+        const int2 bb = binbox[kk * nbins + lane];
+        const int by0 = (int)(int16_t)(bb.x & 0xffff), by1 = bb.x >> 16;
+        const int bx0 = (int)(int16_t)(bb.y & 0xffff), bx1 = bb.y >> 16;
+        bh = by0 <= sy0 && by1 >= sy0 && bx0 <= tx0 + 7 && bx1 >= tx0;
+      }
+      uint64_t bm = __ballot(bh);
+      // load group: up to NBC (<= 4) bins of bm in order; lane (sub, sj) holds slot sj of bin sub,
+      // lane q holds channel quad q of each bin's gout row
+      int gb0 = -1, gb1 = -1, gb2 = -1, gb3 = -1;
+      BwdEnt e;
+      float4 go0, go1, go2, go3;
+#define MX_TAKE(gbv, s)                        \
+  if (s < NBC && bm) {                         \
+    gbv = __builtin_ctzll(bm);                 \
+    bm &= bm - 1;                              \
+  }
+#define MX_ROW(gbv) (gbv >= 0 && qa ? ld4f(gout + (kk * nbins + gbv) * C + 4 * lane) : make_float4(0.f, 0.f, 0.f, 0.f))
+#define MX_LOAD_GROUP()                                                                        \
+  {                                                                                            \
+    gb0 = gb1 = gb2 = gb3 = -1;                                                                \
+    MX_TAKE(gb0, 0) MX_TAKE(gb1, 1) MX_TAKE(gb2, 2) MX_TAKE(gb3, 3)                            \
+    const int mb = sub == 0 ? gb0 : sub == 1 ? gb1 : sub == 2 ? gb2 : sub == 3 ? gb3 : -1;   \
+    e.yx = -1;                                                                                 \
+    e.w = 0.f;                                                                                 \
+    if (sub < NBC && mb >= 0) e = ent[(kk * nbins + mb) * S4 + sj];                            \
+    go0 = MX_ROW(gb0); go1 = MX_ROW(gb1); go2 = MX_ROW(gb2); go3 = MX_ROW(gb3);                \
+  }
+      MX_LOAD_GROUP();
+      while (gb0 >= 0) {
+        const BwdEnt ce = e;
+        const float4 c0g = go0, c1g = go1, c2g = go2, c3g = go3;
+        if (bm) MX_LOAD_GROUP()  // prefetch the next group
+        else gb0 = -1;
+        const int y = (ce.yx >> 16) - sy0, x = (ce.yx & 0xffff) - tx0;
+        const bool inb = ce.yx >= 0 && y == 0 && (unsigned)x < 8u;
+        const int plv = inb ? x : -1;  // pixel within the wave's 1x8 strip
+        const uint64_t hm = __ballot(inb);
+        if (hm) {
+          // per pixel, its hits in slot order (bin-sub s ascending, then lane): the static loops keep
+          // every accumulator and gout quad in named registers
+          uint64_t pm[8];
+#pragma unroll
+          for (int p = 0; p < 8; ++p) pm[p] = __ballot(plv == p);
+          const uint64_t sl = S4 >= 64 ? ~0ull : ((1ull << S4) - 1);
+#define MX_RUN(sv, cgv)                                                            \
+  {                                                                                \
+    const float4 cg = cgv;                                                         \
+    const uint64_t sm = hm & (sl << (sv * S4));                                    \
+    if (sv < NBC && sm) {                                                          \
+      MX_PIX(0) MX_PIX(1) MX_PIX(2) MX_PIX(3) MX_PIX(4) MX_PIX(5) MX_PIX(6) MX_PIX(7)  \
+    }                                                                              \
+  }
+#define MX_PIX(pp)                                                                  \
+  {                                                                                 \
+    uint64_t m = sm & pm[pp];                                                       \
+    while (m) {                                                                     \
+      const int b = __builtin_ctzll(m);                                             \
+      m &= m - 1;                                                                   \
+      const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ce.w), b)); \
+      float vx = cg.x * w, vy = cg.y * w, vz = cg.z * w, vw = cg.w * w;             \
+      if (pow2) { vx *= inv; vy *= inv; vz *= inv; vw *= inv; }                     \
+      else { vx /= count; vy /= count; vz /= count; vw /= count; }                  \
+      a##pp.x += vx; a##pp.y += vy; a##pp.z += vz; a##pp.w += vw;                   \
+    }                                                                               \
+  }
+          MX_RUN(0, c0g) MX_RUN(1, c1g) MX_RUN(2, c2g) MX_RUN(3, c3g)
+#undef MX_PIX
+#undef MX_RUN
+        }
+      }
+#undef MX_LOAD_GROUP
+#undef MX_ROW
+#undef MX_TAKE
+    }
+    __syncthreads();  // list rebuilt for the next 1024 RoIs
+  }
+  float* gmap = L.g[lv] + (int64_t)n * H * W * C;
+  if (qa) {
+    const float4 av[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int y = sy0, x = tx0 + i;
+      if (y < H && x < W) *((float4*)(gmap + ((int64_t)y * W + x) * C) + lane) = av[i];
+    }
   }
 }
 
@@ -286,10 +537,13 @@ static int launch_fwd(const Levels& L, int dtype, int64_t C, const float* rois, 
   MX_CHECK_ARG(dtype == MX_F32 || dtype == MX_BF16, "roi_align: bad dtype %d", dtype);
   if (K == 0) return MX_OK;
   int threads = C >= 256 ? 256 : (int)(cdiv(C, 64) * 64);
-  if (dtype == MX_F32)
-    roi_align_fwd_kernel<float><<<(unsigned)K, threads, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms, (float*)out, lv);
+  if (C % 8 == 0 && dtype == MX_F32)
+    roi_align_fwd_v8_kernel<float><<<(unsigned)K, 256, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms, (float*)out, lv);
   else if (C % 8 == 0)
-    roi_align_fwd_v8_kernel<<<(unsigned)K, 256, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms, (uint16_t*)out, lv);
+    roi_align_fwd_v8_kernel<uint16_t><<<(unsigned)K, 256, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms,
+                                                                   (uint16_t*)out, lv);
+  else if (dtype == MX_F32)
+    roi_align_fwd_kernel<float><<<(unsigned)K, threads, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms, (float*)out, lv);
   else
     roi_align_fwd_kernel<uint16_t><<<(unsigned)K, threads, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms,
                                                                     (uint16_t*)out, lv);
@@ -297,11 +551,65 @@ static int launch_fwd(const Levels& L, int dtype, int64_t C, const float* rois, 
   return MX_OK;
 }
 
-static int launch_bwd(const Levels& L, int dtype, int64_t C, const float* rois, const int32_t* lv, int64_t K, int PH, int PW,
-                      int sampling, int aligned, const void* gout, hipStream_t s) {
+// deterministic-backward workspace: ent [K][nbins][4*sampling^2], cnt [K][nbins], box [K], meta [K]
+static size_t det_ws_bytes(int64_t K, int PH, int PW, int sampling) {
+  const int64_t nb = (int64_t)PH * PW, S4 = 4ll * sampling * sampling;
+  return align_up(sizeof(BwdEnt) * K * nb * S4) + align_up(sizeof(int2) * K * nb) + align_up(sizeof(int4) * K) +
+         align_up(sizeof(int32_t) * K);
+}
+
+// one channel quad per lane (C <= 256); 16 pixels x 4 channels of f32 accumulators per lane
+static bool det_supported(int64_t C) { return C >= 4 && C <= 256 && C % 4 == 0; }
+
+static int launch_bwd(const Levels& L, int64_t N, int dtype, int64_t C, const float* rois, const int32_t* lv, int64_t K,
+                      int PH, int PW, int sampling, int aligned, const void* gout, int deterministic, void* ws,
+                      size_t ws_bytes, hipStream_t s) {
   MX_CHECK_ARG(check_grid(PH, PW, sampling), "roi_align: unsupported pooled %dx%d sampling %d", PH, PW, sampling);
   MX_CHECK_ARG(sampling > 0, "roi_align: adaptive sampling (sampling_ratio<=0) not supported");
   MX_CHECK_ARG(dtype == MX_F32 || dtype == MX_BF16, "roi_align: bad dtype %d", dtype);
+  if (deterministic) {
+    MX_CHECK_ARG(det_supported(C), "roi_align_bwd deterministic: C=%lld must be a multiple of 4 in 4..256", (long long)C);
+    MX_CHECK_ARG(N >= 1 && N < (1 << 27), "roi_align_bwd deterministic: bad image count");
+    for (int i = 0; i < L.n; ++i)
+      MX_CHECK_ARG(L.H[i] < 32768 && L.W[i] < 32768, "roi_align_bwd deterministic: level map too large");
+    const size_t need = det_ws_bytes(K, PH, PW, sampling);
+    MX_CHECK_ARG(K == 0 || (ws && ws_bytes >= need), "roi_align_bwd deterministic: workspace of %zu bytes required", need);
+    const int nbins = PH * PW, S4 = 4 * sampling * sampling;
+    MX_CHECK_ARG(nbins <= 64 && S4 <= 64, "roi_align_bwd deterministic: pooled bins <= 64 and sampling <= 4");
+    char* w = (char*)ws;
+    BwdEnt* ent = (BwdEnt*)w;
+    w += align_up(sizeof(BwdEnt) * K * nbins * S4);
+    int2* cnt = (int2*)w;
+    w += align_up(sizeof(int2) * K * nbins);
+    int4* box = (int4*)w;
+    w += align_up(sizeof(int4) * K);
+    int32_t* meta = (int32_t*)w;
+    if (K > 0) {
+      roi_bwd_prep_kernel<<<(unsigned)K, 64, 0, s>>>(L, rois, lv, PH, PW, sampling, aligned, S4, ent, cnt, box, meta);
+      MX_LAUNCH_CHECK();
+    }
+    TileGrid tg{};
+    tg.n = L.n;
+    int64_t tot = 0;
+    for (int i = 0; i < L.n; ++i) {
+      tg.first[i] = tot;
+      tg.th[i] = (int)cdiv(L.H[i], 8);
+      tg.tw[i] = (int)cdiv(L.W[i], 8);
+      tot += N * tg.th[i] * tg.tw[i];
+    }
+    tg.first[L.n] = tot;
+    MX_CHECK_ARG(tot < (1ll << 31), "roi_align_bwd deterministic: grid too large");
+    if (tot == 0) return MX_OK;
+    const float count = (float)(sampling * sampling);
+    if (dtype == MX_F32)
+      roi_bwd_gather_kernel<float><<<(unsigned)tot, 512, 0, s>>>(L, tg, C, K, nbins, S4, count, ent, cnt, box, meta,
+                                                                 (const float*)gout);
+    else
+      roi_bwd_gather_kernel<uint16_t><<<(unsigned)tot, 512, 0, s>>>(L, tg, C, K, nbins, S4, count, ent, cnt, box, meta,
+                                                                    (const uint16_t*)gout);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+  }
   if (K == 0) return MX_OK;
   int threads = C >= 256 ? 256 : (int)(cdiv(C, 64) * 64);
   if (dtype == MX_F32)
@@ -311,6 +619,11 @@ static int launch_bwd(const Levels& L, int dtype, int64_t C, const float* rois, 
                                                                     (const uint16_t*)gout);
   MX_LAUNCH_CHECK();
   return MX_OK;
+}
+
+extern "C" size_t mx_roi_align_bwd_workspace(int64_t K, int PH, int PW, int sampling) {
+  if (K <= 0 || PH <= 0 || PW <= 0 || sampling <= 0) return 0;
+  return det_ws_bytes(K, PH, PW, sampling);
 }
 
 extern "C" int mx_roi_align_fwd(const void* feat, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, const float* rois,
@@ -325,12 +638,12 @@ extern "C" int mx_roi_align_fwd(const void* feat, int dtype, int64_t N, int64_t 
 
 extern "C" int mx_roi_align_bwd(const void* gout, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, const float* rois,
                                 int64_t K, float scale, int PH, int PW, int sampling, int aligned, float* grad_feat,
-                                mx_stream_t stream) {
-  (void)N;
+                                int deterministic, void* ws, size_t ws_bytes, mx_stream_t stream) {
   MX_CHECK_ARG(H * W < (1ll << 31), "roi_align: feature map too large");
   Levels L{};
   L.g[0] = grad_feat; L.H[0] = H; L.W[0] = W; L.scale[0] = scale; L.n = 1; L.k_min = 0;
-  return launch_bwd(L, dtype, C, rois, nullptr, K, PH, PW, sampling, aligned, gout, (hipStream_t)stream);
+  return launch_bwd(L, N, dtype, C, rois, nullptr, K, PH, PW, sampling, aligned, gout, deterministic, ws, ws_bytes,
+                    (hipStream_t)stream);
 }
 
 extern "C" int mx_multiscale_roi_align_fwd(const void* const* feats, const int64_t* Hs, const int64_t* Ws,
@@ -347,10 +660,10 @@ extern "C" int mx_multiscale_roi_align_fwd(const void* const* feats, const int64
   return launch_fwd(L, dtype, C, rois, K, PH, PW, sampling, 0, 1, out, levels_out, (hipStream_t)stream);
 }
 
-extern "C" int mx_multiscale_roi_align_bwd(const void* gout, int dtype, float* const* gfeats, const int64_t* Hs,
+extern "C" int mx_multiscale_roi_align_bwd(const void* gout, int dtype, float* const* gfeats, int64_t N, const int64_t* Hs,
                                            const int64_t* Ws, const float* scales, int nlev, int64_t C, const float* rois,
                                            const int32_t* levels, int64_t K, int PH, int PW, int sampling,
-                                           mx_stream_t stream) {
+                                           int deterministic, void* ws, size_t ws_bytes, mx_stream_t stream) {
   MX_CHECK_ARG(nlev >= 1 && nlev <= 5, "multiscale_roi_align: 1..5 levels");
   MX_CHECK_ARG(levels != nullptr, "multiscale_roi_align_bwd: levels from the forward are required");
   Levels L{};
@@ -358,5 +671,6 @@ extern "C" int mx_multiscale_roi_align_bwd(const void* gout, int dtype, float* c
     L.g[i] = gfeats[i]; L.H[i] = Hs[i]; L.W[i] = Ws[i]; L.scale[i] = scales[i];
   }
   L.n = nlev; L.k_min = 0;
-  return launch_bwd(L, dtype, C, rois, levels, K, PH, PW, sampling, 0, gout, (hipStream_t)stream);
+  return launch_bwd(L, N, dtype, C, rois, levels, K, PH, PW, sampling, 0, gout, deterministic, ws, ws_bytes,
+                    (hipStream_t)stream);
 }

@@ -171,6 +171,15 @@ def nms(boxes, scores, iou_threshold):
 
 
 # ---------------------------------------------------------------------------------------------
+def roi_align_deterministic(C, ph=7, pw=7, sampling=2):
+    """The RoIAlign backward runs the atomic-free gather (bitwise reproducible, writes every element
+    of the gradient maps) unless MX_ROI_DETERMINISTIC=0 or the shape is outside its supported set
+    (C % 4 == 0, C <= 256, ph * pw <= 64, 1 <= sampling <= 4)."""
+    import os
+    return (os.environ.get("MX_ROI_DETERMINISTIC", "1") != "0" and 4 <= C <= 256 and C % 4 == 0 and ph * pw <= 64
+            and 1 <= sampling <= 4)
+
+
 class _RoIAlign(torch.autograd.Function):
     @staticmethod
     def forward(ctx, feat, rois, scale, ph, pw, sampling, aligned):
@@ -193,10 +202,12 @@ class _RoIAlign(torch.autograd.Function):
         (r,) = ctx.saved_tensors
         N, H, W, C, scale, ph, pw, sampling, aligned, dt = ctx.cfg
         g = gout.contiguous()
-        gf = torch.zeros((N, H, W, C), dtype=torch.float32, device=g.device)
-        if r.shape[0]:
-            call("mx_roi_align_bwd", _p(g), _dtype_code(g), N, H, W, C, _p(r), r.shape[0], scale, ph, pw, sampling,
-                 aligned, _p(gf), _stream())
+        det = roi_align_deterministic(C, ph, pw, sampling)
+        K = r.shape[0]
+        gf = (torch.empty if det else torch.zeros)((N, H, W, C), dtype=torch.float32, device=g.device)
+        ws = _ws(_lib.load().mx_roi_align_bwd_workspace(K, ph, pw, sampling) if det else 0, g.device)
+        call("mx_roi_align_bwd", _p(g), _dtype_code(g), N, H, W, C, _p(r), K, scale, ph, pw, sampling,
+             aligned, _p(gf), int(det), _p(ws), ws.numel(), _stream())
         return gf.to(dt), None, None, None, None, None, None
 
 
@@ -238,15 +249,17 @@ class _MultiScaleRoIAlign(torch.autograd.Function):
         r, levels = ctx.saved_tensors
         shapes, scales, ph, pw, sampling, dt = ctx.cfg
         g = gout.contiguous()
-        gfs = [torch.zeros(s, dtype=torch.float32, device=g.device) for s in shapes]
+        C, K = shapes[0][3], r.shape[0]
+        det = roi_align_deterministic(C, ph, pw, sampling)
+        gfs = [(torch.empty if det else torch.zeros)(s, dtype=torch.float32, device=g.device) for s in shapes]
         n = len(gfs)
-        if r.shape[0]:
-            ptrs = (ctypes.c_void_p * n)(*[f.data_ptr() for f in gfs])
-            Hs = (ctypes.c_int64 * n)(*[s[1] for s in shapes])
-            Ws = (ctypes.c_int64 * n)(*[s[2] for s in shapes])
-            sc = (ctypes.c_float * n)(*scales)
-            call("mx_multiscale_roi_align_bwd", _p(g), _dtype_code(g), ptrs, Hs, Ws, sc, n, shapes[0][3], _p(r),
-                 _p(levels), r.shape[0], ph, pw, sampling, _stream())
+        ws = _ws(_lib.load().mx_roi_align_bwd_workspace(K, ph, pw, sampling) if det else 0, g.device)
+        ptrs = (ctypes.c_void_p * n)(*[f.data_ptr() for f in gfs])
+        Hs = (ctypes.c_int64 * n)(*[s[1] for s in shapes])
+        Ws = (ctypes.c_int64 * n)(*[s[2] for s in shapes])
+        sc = (ctypes.c_float * n)(*scales)
+        call("mx_multiscale_roi_align_bwd", _p(g), _dtype_code(g), ptrs, shapes[0][0], Hs, Ws, sc, n, C, _p(r),
+             _p(levels), K, ph, pw, sampling, int(det), _p(ws), ws.numel(), _stream())
         return (None, None, None, None, None, None) + tuple(x.to(dt) for x in gfs)
 
 

@@ -206,6 +206,53 @@ def test_roi_align_backward(dev):
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("C,gdt", [(256, torch.float32), (64, torch.float32), (32, torch.bfloat16), (12, torch.float32)])
+def test_multiscale_roi_align_backward_deterministic(dev, monkeypatch, C, gdt):
+    """Atomic-free gather backward: BIT-EXACT against the oracle (torchvision's CPU loop order: RoI,
+    bin, sample, corner, each contribution g * w / count added in turn), bitwise identical run to run,
+    equal to the atomic form up to summation order, and every level-map element written (the maps
+    come from torch.empty)."""
+    from mx_det import ops
+    rng = np.random.default_rng(C + 1)
+    N = 2
+    shapes = [(60, 101), (30, 51), (15, 26), (8, 13)]
+    scales = [0.25, 0.125, 0.0625, 0.03125]
+    feats = [torch.from_numpy(rng.standard_normal((N, h, w, C)).astype(np.float32)) for h, w in shapes]
+    boxes = np.concatenate([_rand_boxes(rng, 120, H=240, W=404, med=16), _rand_boxes(rng, 80, H=240, W=404, med=150)])
+    boxes[0] = [-30, -30, 430, 260]  # overhangs every edge
+    boxes[1] = [3, 3, 3.2, 3.1]      # sub-pixel
+    bi = rng.integers(0, N, len(boxes)).astype(np.float32)[:, None]
+    rois = np.concatenate([bi, boxes], 1).astype(np.float32)
+    lv = _level_mapper_np(boxes)
+    g = torch.from_numpy(rng.standard_normal((len(rois), 7, 7, C)).astype(np.float32)).to(gdt)
+    rt = torch.from_numpy(rois).to(dev)
+
+    def run(det):
+        monkeypatch.setenv("MX_ROI_DETERMINISTIC", "1" if det else "0")
+        ft = [f.to(dev).to(gdt).requires_grad_(True) for f in feats]
+        out = ops.multiscale_roi_align(ft, rt, scales, 2)
+        return torch.autograd.grad(out, ft, g.to(dev))
+    a, b, c = run(True), run(True), run(False)
+    gn = g.float().permute(0, 3, 1, 2).numpy()
+    for l in range(4):
+        assert torch.equal(a[l], b[l]), l
+        tol = 1e-5 if gdt == torch.float32 else 1e-2
+        torch.testing.assert_close(a[l].float(), c[l].float(), rtol=tol, atol=tol)
+        sel = np.where(lv == l)[0]
+        r = orc.roi_align_backward(gn[sel], rois[sel], scales[l], (N, C) + shapes[l], 2, False)
+        r = torch.from_numpy(r).to(gdt).float().numpy()  # the returned grad is in the feature dtype
+        assert np.array_equal(a[l].float().permute(0, 3, 1, 2).cpu().numpy(), r), l
+
+
+def test_roi_align_backward_no_rois_writes_zeros(dev):
+    """K = 0: the gather still writes every element of the (torch.empty) gradient map."""
+    from mx_det import ops
+    f = torch.randn(1, 20, 30, 64, device=dev).requires_grad_(True)
+    out = ops.roi_align(f, torch.zeros((0, 5), device=dev), 7, 0.25, 2, False)
+    (gf,) = torch.autograd.grad(out, f, torch.zeros_like(out))
+    assert gf.shape == f.shape and (gf == 0).all()
+
+
 def _level_mapper_np(boxes, k_min=2, k_max=5):
     # torchvision poolers.LevelMapper in f32 (CPU path)
     b = torch.from_numpy(boxes)
