@@ -210,7 +210,11 @@ class AnchorGenerator(nn.Module):
             for (gh, gw), size, ratios in zip(grid_sizes, self.sizes, self.aspect_ratios):
                 sh, sw = padded_hw[0] // gh, padded_hw[1] // gw  # torch integer division as torchvision
                 out.append(be.anchors_level(float(size[0]), list(ratios), gh, gw, sh, sw, device))
-            self._cache = {key: torch.cat(out)}
+            # every shape's anchors stay alive (a few MB each): a HIP graph captured for one input
+            # shape holds their device address, and replacing the cache on a shape change freed that
+            # memory under it (the replay read freed memory -- the round-1 "illegal address on replay"
+            # of the proposal-chain graph, tests/test_gpu_graphs.py)
+            self._cache[key] = torch.cat(out)
         return self._cache[key]
 
 

@@ -180,34 +180,49 @@ def roi_align_deterministic(C, ph=7, pw=7, sampling=2):
             and 1 <= sampling <= 4)
 
 
+def roi_align_fwd_nhwc(feat, rois, scale, ph, pw, sampling, aligned):
+    """mx_roi_align_fwd on NHWC features: rois [K,5] f32 -> [K, ph, pw, C] in the feature dtype."""
+    _dev(feat, rois)
+    _check(feat.dim() == 4, "roi_align input must be NHWC [N,H,W,C]")
+    _check(rois.dim() == 2 and rois.shape[1] == 5, f"rois must be [K,5], got {tuple(rois.shape)}")
+    f = feat.contiguous()
+    r = rois.float().contiguous()
+    N, H, W, C = f.shape
+    out = torch.empty((r.shape[0], ph, pw, C), dtype=f.dtype, device=f.device)
+    if r.shape[0]:
+        call("mx_roi_align_fwd", _p(f), _dtype_code(f), N, H, W, C, _p(r), r.shape[0], float(scale), ph, pw,
+             sampling, int(aligned), _p(out), _stream())
+    return out
+
+
+def roi_align_bwd_nhwc(gout, rois, N, H, W, C, scale, ph, pw, sampling, aligned):
+    """mx_roi_align_bwd: gout [K, ph, pw, C] -> f32 grad_feat [N, H, W, C] (deterministic gather when
+    supported, see roi_align_deterministic; else atomics into a zero-filled map)."""
+    g = gout.contiguous()
+    r = rois.float().contiguous()
+    K = r.shape[0]
+    det = roi_align_deterministic(C, ph, pw, sampling)
+    gf = (torch.empty if det else torch.zeros)((N, H, W, C), dtype=torch.float32, device=g.device)
+    ws = _ws(_lib.load().mx_roi_align_bwd_workspace(K, ph, pw, sampling) if det else 0, g.device)
+    call("mx_roi_align_bwd", _p(g), _dtype_code(g), N, H, W, C, _p(r), K, float(scale), ph, pw, sampling,
+         int(aligned), _p(gf), int(det), _p(ws), ws.numel(), _stream())
+    return gf
+
+
 class _RoIAlign(torch.autograd.Function):
     @staticmethod
     def forward(ctx, feat, rois, scale, ph, pw, sampling, aligned):
-        _dev(feat, rois)
-        _check(feat.dim() == 4, "roi_align input must be NHWC [N,H,W,C]")
-        _check(rois.dim() == 2 and rois.shape[1] == 5, f"rois must be [K,5], got {tuple(rois.shape)}")
-        f = feat.contiguous()
-        r = rois.float().contiguous()
-        N, H, W, C = f.shape
-        out = torch.empty((r.shape[0], ph, pw, C), dtype=f.dtype, device=f.device)
-        if r.shape[0]:
-            call("mx_roi_align_fwd", _p(f), _dtype_code(f), N, H, W, C, _p(r), r.shape[0], float(scale), ph, pw,
-                 sampling, int(aligned), _p(out), _stream())
-        ctx.save_for_backward(r)
-        ctx.cfg = (N, H, W, C, float(scale), ph, pw, sampling, int(aligned), f.dtype)
+        out = roi_align_fwd_nhwc(feat, rois, scale, ph, pw, sampling, aligned)
+        ctx.save_for_backward(rois.float().contiguous())
+        N, H, W, C = feat.shape
+        ctx.cfg = (N, H, W, C, float(scale), ph, pw, sampling, int(aligned), feat.dtype)
         return out
 
     @staticmethod
     def backward(ctx, gout):
         (r,) = ctx.saved_tensors
         N, H, W, C, scale, ph, pw, sampling, aligned, dt = ctx.cfg
-        g = gout.contiguous()
-        det = roi_align_deterministic(C, ph, pw, sampling)
-        K = r.shape[0]
-        gf = (torch.empty if det else torch.zeros)((N, H, W, C), dtype=torch.float32, device=g.device)
-        ws = _ws(_lib.load().mx_roi_align_bwd_workspace(K, ph, pw, sampling) if det else 0, g.device)
-        call("mx_roi_align_bwd", _p(g), _dtype_code(g), N, H, W, C, _p(r), K, scale, ph, pw, sampling,
-             aligned, _p(gf), int(det), _p(ws), ws.numel(), _stream())
+        gf = roi_align_bwd_nhwc(gout, r, N, H, W, C, scale, ph, pw, sampling, aligned)
         return gf.to(dt), None, None, None, None, None, None
 
 
