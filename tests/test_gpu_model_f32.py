@@ -44,15 +44,25 @@ def _keys(seed):
     return lambda shape, device: torch.rand(shape, generator=g).to(device)
 
 
-def test_f32_eval_detections_match_cpu_backend(dev):
+def _eval_pair(dev):
     from mx_det.data import synth_batch
     m, mc = _pair(dev, 0)
     m.eval()
     mc.eval()
     imgs, _ = synth_batch(20, 2, H=512, W=672)
     with torch.no_grad():
-        out = m(list(imgs.to(dev)))
         ref = mc(list(imgs))
+        out = m(list(imgs.to(dev)))
+    return out, ref
+
+
+def test_f32_eval_detections_match_cpu_backend(dev, monkeypatch):
+    """eval_all.py:111 model(images) with the RoI head fed the fp32 CPU model's proposals (see
+    _pin_proposals: the RPN's 0.7-IoU NMS over a random-init anchor-grid-like proposal set flips on
+    float noise): identical labels, boxes and scores within 1e-3."""
+    from mx_det import frcnn
+    monkeypatch.setattr(frcnn.RegionProposalNetwork, "filter_proposals_padded", _pin_proposals())
+    out, ref = _eval_pair(dev)
     for o, r in zip(out, ref):
         n = r["labels"].numel()
         assert n > 10, n
@@ -60,6 +70,23 @@ def test_f32_eval_detections_match_cpu_backend(dev):
         assert torch.equal(o["labels"].cpu(), r["labels"])
         torch.testing.assert_close(o["scores"].cpu(), r["scores"], rtol=1e-3, atol=1e-3)
         torch.testing.assert_close(o["boxes"].cpu(), r["boxes"], rtol=1e-3, atol=1e-3)
+
+
+def test_f32_eval_detections_unpinned(dev):
+    """The same call end to end with each backend running its own RPN: at least 97 % of the CPU
+    detections have a HIP detection with the same label, score and box within 1e-3 (a flipped
+    proposal-NMS decision moves the odd detection by a few pixels: measured 1 of 200 on one box)."""
+    out, ref = _eval_pair(dev)
+    for o, r in zip(out, ref):
+        n = r["labels"].numel()
+        assert n > 10 and abs(o["labels"].numel() - n) <= max(2, n // 50), (o["labels"].numel(), n)
+        ob, os_, ol = o["boxes"].cpu(), o["scores"].cpu(), o["labels"].cpu()
+        hit = 0
+        for b, s, lab in zip(r["boxes"], r["scores"], r["labels"]):
+            ok = (ol == lab) & ((os_ - s).abs() <= 1e-3 + 1e-3 * s.abs()) & \
+                 ((ob - b).abs() <= 1e-3 + 1e-3 * b.abs()).all(1)
+            hit += bool(ok.any())
+        assert hit >= 0.97 * n, (hit, n)
 
 
 def _tf32(t):
@@ -121,16 +148,18 @@ def test_f32_trunk_closer_than_tf32(dev, damp):
 def _pin_proposals():
     """Hand the fp32 CPU model's RPN proposals (padded boxes, scores, valid) to every later model's RoI
     head: the order of near-equal proposal scores is not defined at f32 level (adjacent top-2000
-    objectness gaps ~3e-4 of its spread), and the RoI sampler draws its keys by proposal slot."""
+    objectness gaps ~3e-4 of its spread), and the RoI sampler draws its keys by proposal slot.
+    The first call made on a CPU tensor is the one captured (the CPU models run first)."""
     from mx_det import frcnn
     orig = frcnn.RegionProposalNetwork.filter_proposals_padded
     cap = {}
 
     def fp(self, proposals, objectness, image_sizes, num_per_level, be):
-        out = orig(self, proposals, objectness, image_sizes, num_per_level, be)
+        if "p" not in cap and proposals.device.type == "cpu":
+            cap["p"] = orig(self, proposals, objectness, image_sizes, num_per_level, be)
+            return cap["p"]
         if "p" not in cap:
-            cap["p"] = out
-            return out
+            return orig(self, proposals, objectness, image_sizes, num_per_level, be)
         return tuple(t.to(proposals.device) for t in cap["p"])
     return fp
 
