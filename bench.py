@@ -134,17 +134,21 @@ def pmc_traffic(kind):
     return round(tot / 1e6, 2) if hit else None
 
 
-def conv_roofline(model, opt, imgs, tg, peak=X3_PEAK_TFLOPS):
-    """Live HIP-event timing of every conv kernel launch in one train step; the dominant kernel kind
-    (largest total time) is reported with its algorithmic FLOPs (2 * M * N * K per conv, f32-equivalent
-    for the bf16x3 path) against the peak of the arithmetic it runs (bf16 dense / 3 for bf16x3)."""
+def conv_roofline(model, opt, imgs, tg, peak=X3_PEAK_TFLOPS, step_fn=None):
+    """Live HIP-event timing of every conv kernel launch in one train step (or one call of step_fn);
+    the dominant kernel kind (largest total time) is reported with its algorithmic FLOPs (2 * M * N * K
+    per conv, f32-equivalent for the bf16x3 path) against the peak of the arithmetic it runs (bf16
+    dense / 3 for bf16x3)."""
     from mx_det import conv as mc
     t = mc.KernelTimer()
     mc.set_timer(t)
     graphs = os.environ.get("MX_GRAPHS")
     os.environ["MX_GRAPHS"] = "0"  # an eager step: every conv launch passes through the timer
     try:
-        train_step(model, opt, imgs, tg)
+        if step_fn is None:
+            train_step(model, opt, imgs, tg)
+        else:
+            step_fn()
     finally:
         mc.set_timer(None)
         if graphs is None:
@@ -319,6 +323,101 @@ def _time_precision(precision, args, world, rank, dev, imgs, tg):
     return model, ddp, opt, dt
 
 
+def eval_step(model, img, unet=None):
+    """One image of the reference's evaluation loop (eval_all.py:106-124, batch_size=1): model([image])
+    in eval mode, the detections copied to the host; with unet, the corrupted uint8 image is first
+    restored on the device (restore_testsets.py:53-79 fused in front of eval_restored.py:171-184)."""
+    with torch.no_grad():
+        if unet is not None:
+            img = unet.restore_u8(img[None])[0]
+        out = model([img])[0]
+        return out["boxes"].cpu(), out["scores"].cpu(), out["labels"].cpu()
+
+
+def _time_eval(precision, args, world, rank, dev, imgs, restored):
+    """Eval-mode per-image throughput: W warmup images, then exactly K images timed between
+    barrier + synchronize pairs (each rank evaluates its own shard, as engine.evaluate does)."""
+    from mx_det.unet import RestorationUNet
+    torch.manual_seed(42)
+    model = build_model(dev, precision=precision).eval()
+    unet = RestorationUNet(channels=(32, 64, 128, 256), precision=precision).to(dev).eval() if restored else None
+    n = imgs.shape[0]
+    for i in range(args.warmup):
+        eval_step(model, imgs[i % n], unet)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        eval_step(model, imgs[(args.warmup + i) % n], unet)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    return model, unet, dt
+
+
+def cpu_eval_baseline(gpu_model, gpu_unet, img, seconds_hint=30.0):
+    """The oracle CPU restatement (CpuBackend model + oracle/unet_ref.py U-Net) timed on one image of
+    the same eval workload, from the GPU models' weights."""
+    from oracle.cpu_backend import CpuBackend
+    cores = torch.get_num_threads()
+    m = build_model("cpu", backend=CpuBackend())
+    m.load_state_dict({k: v.detach().cpu() for k, v in gpu_model.state_dict().items()})
+    m.eval()
+    u8 = img.cpu()
+    ref_unet = None
+    if gpu_unet is not None:
+        from oracle.unet_ref import torch_reference_unet
+        ref_unet = torch_reference_unet({k: v.detach().cpu() for k, v in gpu_unet.state_dict().items()},
+                                        (32, 64, 128, 256))
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        with torch.no_grad():
+            x = u8
+            if ref_unet is not None:
+                from oracle.unet_ref import restore_cpu
+                x = torch.from_numpy(restore_cpu(ref_unet, u8.numpy()))
+            m([x])
+        n += 1
+        if time.perf_counter() - t0 > seconds_hint or n >= 2:
+            break
+    dt = time.perf_counter() - t0
+    what = "U-Net restore + " if ref_unet is not None else ""
+    return {"value": n / dt, "unit": "images/sec", "cores": cores, "kind": "port",
+            "sample": f"{n} image(s) 1333x800 ({what}eval forward) on {cores} CPU threads ({dt:.1f} s)"}
+
+
+def eval_main(args, world, rank, dev, imgs):
+    restored = args.mode == "eval_restored"
+    prec = "bf16" if args.precision == "bf16" else "f32"
+    model, unet, dt = _time_eval(prec, args, world, rank, dev, imgs, restored)
+    images = args.steps * world
+    what = "U-Net restore (fp32) + FRCNN eval" if restored else "FRCNN eval"
+    rec = {"metric": f"images/sec {what} @1333x800 bs=1 (per-image)", "value": round(images / dt, 3),
+           "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": DTYPE_TEXT[prec], "arithmetic": ARITH_TEXT[prec],
+           "data": "synthetic VisDrone-shaped uint8 1333x800, random-init weights; detections copied to host",
+           "config": {"workload": ("configs[3]: eval_restored.py:171-184 with restore_testsets.py:53-79 fused on "
+                                   "the device" if restored else "eval_all.py:97-143 per-image eval forward"),
+                      "global_batch": world, "per_gpu_batch": 1, "image": "1333x800",
+                      "parallelism": f"shard{world}", "rpn_post_nms_top_n_test": 1000}}
+    peak = {"f32": X3_PEAK_TFLOPS, "bf16": BF16_PEAK_TFLOPS}[prec]
+    if rank == 0 and not args.no_roofline:
+        rec["roofline"] = conv_roofline(model, None, None, None, peak,
+                                        step_fn=lambda: eval_step(model, imgs[0], unet))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_eval_baseline(model, unet, imgs[0])
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+
+
 DTYPE_TEXT = {"f32": "f32", "bf16": "bf16"}
 ARITH_TEXT = {"f32": "f32 activations/gradients/BN/RoIAlign; conv products as bf16x3 MFMA (hi*hi + hi*lo + lo*hi, "
                      "f32 accumulate, ~2^-16 rel. per product vs TF32 2^-11)",
@@ -331,6 +430,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--augment", action="store_true")
+    ap.add_argument("--mode", choices=("train", "eval", "eval_restored"), default="train",
+                    help="train (default): the headline train step; eval: per-image eval forward "
+                         "(eval_all.py); eval_restored: on-device U-Net restore + eval (eval_restored.py)")
     ap.add_argument("--precision", choices=("both", "f32", "bf16"), default="both",
                     help="both (default): the f32 headline, then the bf16 variant in the same JSON line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -357,6 +459,12 @@ def main():
 
     from mx_det.data import synth_batch
     imgs, tg = synth_batch(rank * N_IMAGES_PER_RANK, N_IMAGES_PER_RANK, device=dev)
+    if args.mode != "train":
+        eval_main(args, world, rank, dev, imgs)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     precs = ["f32", "bf16"] if args.precision == "both" else [args.precision]
     head = precs[0]
     model, ddp, opt, dt = _time_precision(head, args, world, rank, dev, imgs, tg)

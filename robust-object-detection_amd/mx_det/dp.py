@@ -8,11 +8,15 @@ scripts use (DistributedDataParallel(broadcast_buffers=False)):
   * identical start: parameters and buffers broadcast from rank 0;
   * per-GPU BatchNorm statistics (buffers are never synchronised afterwards);
   * gradients averaged over ranks before the optimizer step
-while the graphs stay on: after `loss.backward()` the trainable gradients are averaged by a few
-large flat all-reduces (one per ~`bucket_mb` of gradients, issued back to back on RCCL's stream,
-then scaled and scattered back with one multi-tensor copy each). The exchange is not overlapped
-with the backward (the trunk's gradients all appear when its graph finishes); over xGMI a ring
-all-reduce of the 172 MB of f32 gradients costs ~2·(N-1)/N·172 MB / bus bandwidth.
+while the graphs stay on. The exchange overlaps the backward: the RoI head's gradients are
+all-reduced as soon as its backward graph has replayed, and under this wrapper the trunk's backward
+is captured as a chain of per-segment graphs (frcnn._SegGraphs: FPN + RPN head, layer4, layer3,
+layer2) whose hand-off hook starts each segment's all-reduce (one flat bucket per segment, 5-60 MB)
+on RCCL's stream while the later segments' graphs run; `sync_gradients()` then only waits, scales
+and scatters back. Anything not started by a hook (eager trunk, other parameters) is reduced there
+in ~`bucket_mb` buckets. Over xGMI a ring all-reduce of the 172 MB of f32 gradients costs
+~2·(N-1)/N·172 MB / bus bandwidth; with the overlap only the last segment's (layer2, 5 MB) is
+exposed.
 """
 import torch
 import torch.distributed as dist
@@ -30,16 +34,29 @@ class DataParallel:
             for t in list(model.parameters()) + list(model.buffers()):
                 dist.broadcast(t.data, 0, group=group)
         self.params = [p for p in model.parameters() if p.requires_grad]
+        self._work = {}  # key -> (work, flat, grads) started from a graph hand-off hook
         # the RoI head's gradients are complete as soon as its backward graph has replayed, before
         # the trunk's (most of the step's backward): their all-reduce starts right then and overlaps
         # the trunk backward (hook fired by frcnn._Graphs; without it they join the normal buckets)
         rh = getattr(model, "roi_heads", None)
         early = {id(p) for p in rh.parameters() if p.requires_grad} if rh is not None else set()
         self.early = [p for p in self.params if id(p) in early]
-        self._early_work = None
         if self.early:
             rh.__dict__["_mx_grads_ready"] = self._early_reduce
-        rest = [p for p in self.params if id(p) not in early]
+        # trunk segments (frcnn._SegGraphs keys): started from the segmented backward graphs' hook
+        self.segments = {}
+        if hasattr(model, "backbone") and hasattr(model, "rpn"):
+            body = model.backbone.body
+            seg = {"fpn+rpn_head": list(model.backbone.fpn.parameters()) + list(model.rpn.head.parameters()),
+                   "layer4": list(body.layer4.parameters()), "layer3": list(body.layer3.parameters()),
+                   "layer2": list(body.layer2.parameters()),
+                   "stem+layer1": list(body.conv1.parameters()) + list(body.bn1.parameters()) +
+                   list(body.layer1.parameters())}
+            self.segments = {k: [p for p in v if p.requires_grad] for k, v in seg.items()}
+            self.segments = {k: v for k, v in self.segments.items() if v}
+            model.__dict__["_mx_seg_ready"] = self._segment_reduce
+        seen = early | {id(p) for v in self.segments.values() for p in v}
+        rest = [p for p in self.params if id(p) not in seen]
         # buckets in reverse registration order (the backward produces the later layers' first)
         self.buckets, cur, size = [], [], 0
         for p in reversed(rest):
@@ -50,6 +67,7 @@ class DataParallel:
                 cur, size = [], 0
         if cur:
             self.buckets.append(cur)
+        self.bucket_mb = bucket_mb
         for m in model.modules():  # graphs and side-stream wgrad stay enabled under this wrapper
             m.__dict__["_mx_dp"] = True
         _conv.set_data_parallel(True)
@@ -76,17 +94,31 @@ class DataParallel:
         return dist.all_reduce(flat, group=self.group, async_op=True), flat, grads
 
     def _early_reduce(self):
-        if self._early_work is None:
-            self._early_work = self._start(self.early)
+        if "roi_heads" not in self._work:
+            self._work["roi_heads"] = self._start(self.early)
+
+    def _segment_reduce(self, key, params):
+        """frcnn._SegGraphs hand-off: `params`' gradients are final for this backward."""
+        if key in self.segments and key not in self._work:
+            self._work[key] = self._start(self.segments[key])
 
     @torch.no_grad()
     def sync_gradients(self):
         """Average the trainable gradients over all ranks (call after backward, before step). A
-        parameter without a gradient on this rank contributes zeros (and gets the average)."""
+        parameter without a gradient on this rank contributes zeros (and gets the average).
+        Every rank issues the all-reduces in the same order: hook-started ones in backward order
+        (the same on every rank: the same graphs replay), then the rest."""
         pending = []
-        if self.early:
-            pending.append(self._early_work if self._early_work is not None else self._start(self.early))
-            self._early_work = None
+        groups = ([("roi_heads", self.early)] if self.early else []) + list(self.segments.items())
+        started = self._work
+        self._work = {}
+        for key, params in groups:
+            if key in started:
+                pending.append(started[key])
+            else:
+                # one flat per group whether or not a hook started it: every rank issues the same
+                # collectives (sizes and order) even when its trunk ran eagerly on this shape
+                pending.append(self._start(params))
         for b in self.buckets:
             pending.append(self._start(b))
         for work, flat, grads in pending:

@@ -95,19 +95,28 @@ class ResNet50Body(nn.Module):
         layers += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
-    def forward(self, x, be):
+    LAYERS = ("layer1", "layer2", "layer3", "layer4")
+
+    def stem(self, x, be):
         x = be.conv_bn(x, self.conv1, self.bn1, ACT_RELU)
-        x = be.maxpool(x, 3, 2, 1)
+        return be.maxpool(x, 3, 2, 1)
+
+    def run_layer(self, name, x, be):
+        blocks = list(getattr(self, name))
+        feed = None
+        for j, blk in enumerate(blocks):
+            # a block's output feeds only the next block of its layer (conv1 + identity); the
+            # layer output also feeds the next layer's downsample and the FPN -> no hand-off
+            own = j + 1 < len(blocks)
+            r = blk(x, be, feed=feed, own_out=own)
+            x, feed = r if own else (r, None)
+        return x
+
+    def forward(self, x, be):
+        x = self.stem(x, be)
         out = OrderedDict()
-        for i, name in enumerate(("layer1", "layer2", "layer3", "layer4")):
-            blocks = list(getattr(self, name))
-            feed = None
-            for j, blk in enumerate(blocks):
-                # a block's output feeds only the next block of its layer (conv1 + identity); the
-                # layer output also feeds the next layer's downsample and the FPN -> no hand-off
-                own = j + 1 < len(blocks)
-                r = blk(x, be, feed=feed, own_out=own)
-                x, feed = r if own else (r, None)
+        for i, name in enumerate(self.LAYERS):
+            x = self.run_layer(name, x, be)
             out[str(i)] = x
         return out
 
@@ -859,8 +868,145 @@ class _GraphFn(torch.autograd.Function):
 
 
 def _capture_trunk(model, be, x):
+    if model.__dict__.get("_mx_seg_ready") is not None:  # data-parallel: per-segment gradient hand-off
+        return _SegGraphs(model, be, x)
     trunk = _Trunk(model, be)
     return _Graphs(trunk, trunk.parameters(), model, x)
+
+
+class _SegGraphs:
+    """The trunk (backbone + FPN + RPN head) as ONE forward graph and a chain of backward graphs, one
+    per segment in backward order: FPN + RPN head, layer4, layer3, layer2, stem + layer1. The forward
+    detaches each layer output into a leaf that both the next layer and the FPN consume; each
+    backward graph back-propagates one segment from its output leaf's gradient (written by the graphs
+    replayed before it), so when a segment's graph has been issued its parameters' gradients are
+    final and `model._mx_seg_ready(key, params, grads)` can start their all-reduce on RCCL's stream
+    while the remaining segments' backward graphs run (mx_det.dp.DataParallel; SURVEY.md §8e: bucketed
+    all-reduce overlapped with the backward). Same kernels as the one-graph trunk; the only change is
+    that the gradient reaching a layer output is summed over its consumers (FPN lateral, next layer)
+    in a different order. Buffers and captures follow _Graphs (shared private pool, replays in capture
+    order)."""
+
+    SEGS = ("fpn+rpn_head", "layer4", "layer3", "layer2", "stem+layer1")
+
+    def __init__(self, model, be, x):
+        self.model, self.be = model, be
+        body = model.backbone.body
+        self.seg_params = {"stem+layer1": list(body.conv1.parameters()) + list(body.bn1.parameters()) +
+                           list(body.layer1.parameters()),
+                           "layer2": list(body.layer2.parameters()), "layer3": list(body.layer3.parameters()),
+                           "layer4": list(body.layer4.parameters()),
+                           "fpn+rpn_head": list(model.backbone.fpn.parameters()) + list(model.rpn.head.parameters())}
+        self.seg_params = {k: [p for p in v if p.requires_grad] for k, v in self.seg_params.items()}
+        # leaf k (C2..C5) needs a gradient iff some segment upstream of it trains
+        up = ["stem+layer1", "layer2", "layer3", "layer4"]
+        self.need = [any(self.seg_params[u] for u in up[:k + 1]) for k in range(4)]
+        self.params = [p for k in self.SEGS for p in self.seg_params[k]]
+        saved = {k: v.clone() for k, v in model.state_dict().items()
+                 if k.endswith(("running_mean", "running_var", "num_batches_tracked"))}
+        grads = [p.grad for p in self.params]
+        self.static_x = x.detach().clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                outs, leaves, cs = self._fwd(self.static_x)
+                self._bwd_all(outs, [torch.ones_like(o) for o in outs], leaves, cs)
+                del outs, leaves, cs
+                for p in self.params:
+                    p.grad = None
+        torch.cuda.current_stream().wait_stream(side)
+        pool = torch.cuda.graph_pool_handle()
+        self.fwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.fwd, pool=pool):
+            outs, self.leaves, self.cs = self._fwd(self.static_x)
+        self.static_gout = [torch.zeros_like(o) for o in outs]
+        self.bwd = []  # (segment key, graph)
+        for key, roots, groots in self._bwd_plan(outs, self.static_gout, self.leaves, self.cs):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                torch.autograd.backward(roots, groots())
+            self.bwd.append((key, g))
+        self.static_out = tuple(o.detach() for o in outs)
+        self.static_grads = {k: [p.grad for p in v] for k, v in self.seg_params.items()}
+        # the boundary-leaf gradients pass between the backward graphs: keep them referenced
+        self.keep = [l.grad for l in self.leaves] + [o for o in outs]
+        self.leaves, self.cs = None, None
+        for p, g in zip(self.params, grads):
+            p.grad = g
+        with torch.no_grad():
+            sd = model.state_dict()
+            for k, v in saved.items():
+                sd[k].copy_(v)
+        self.anchor = torch.zeros((), device=x.device, requires_grad=True)
+        self.on_ready = None
+
+    def _fwd(self, x):
+        body, be = self.model.backbone.body, self.be
+        c = body.run_layer("layer1", body.stem(x, be), be)
+        leaves, cs = [], [c]
+        for k, name in enumerate(("layer2", "layer3", "layer4")):
+            leaf = c.detach().requires_grad_(self.need[k])
+            leaves.append(leaf)
+            c = body.run_layer(name, leaf, be)
+            cs.append(c)
+        leaves.append(c.detach().requires_grad_(self.need[3]))
+        feats = self.model.backbone.fpn(OrderedDict((str(i), l) for i, l in enumerate(leaves)), be)
+        logits, deltas = self.model.rpn.head(list(feats.values()), be)
+        return tuple(feats.values()) + tuple(logits) + tuple(deltas), leaves, cs
+
+    def _bwd_plan(self, outs, gouts, leaves, cs):
+        """[(segment key, roots, () -> root gradients)] in backward order; a layer segment runs only
+        when its output leaf carries a gradient (read lazily: the leaf's .grad exists once the
+        segments before it have run)."""
+        plan = [("fpn+rpn_head", outs, lambda: gouts)]
+        for k, key in zip((3, 2, 1, 0), ("layer4", "layer3", "layer2", "stem+layer1")):
+            if self.need[k]:
+                plan.append((key, [cs[k]], (lambda lf: (lambda: [lf.grad]))(leaves[k])))
+        return plan
+
+    def _bwd_all(self, outs, gouts, leaves, cs):
+        for _, roots, groots in self._bwd_plan(outs, gouts, leaves, cs):
+            torch.autograd.backward(roots, groots())
+
+    def __call__(self, x):
+        return _SegGraphFn.apply(x, self.anchor, self)
+
+
+class _SegGraphFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, tg):
+        tg.static_x.copy_(x)
+        tg.fwd.replay()
+        ctx.tg = tg
+        return tuple(o.detach() for o in tg.static_out)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        tg = ctx.tg
+        for s, g in zip(tg.static_gout, gouts):
+            if g is None:
+                s.zero_()
+            else:
+                s.copy_(g)
+        for key, _ in tg.bwd:  # see _GraphFn.backward
+            for p, g in zip(tg.seg_params[key], tg.static_grads[key]):
+                if g is not None and p.grad is g:
+                    p.grad = g.clone()
+        hook = tg.model.__dict__.get("_mx_seg_ready")
+        for key, graph in tg.bwd:
+            graph.replay()
+            ps, gs = tg.seg_params[key], tg.static_grads[key]
+            for p, g in zip(ps, gs):
+                if g is None:
+                    continue
+                if p.grad is None:
+                    p.grad = g
+                else:
+                    p.grad.add_(g)
+            if hook is not None and ps:
+                hook(key, ps)
+        return None, None, None
 
 
 class _Head(nn.Module):
