@@ -418,6 +418,60 @@ def eval_main(args, world, rank, dev, imgs):
         print(json.dumps(rec), flush=True)
 
 
+def unet_train_main(args, world, rank, dev):
+    """train_restoration.py:199-205 step (batch 8 of 256x256 patches: device corruption, U-Net forward,
+    L1 + 0.3 (1 - SSIM), backward, AdamW), patches/sec."""
+    from mx_det.restoration import CombinedLoss, RestorationBatcher
+    from mx_det.unet import RestorationUNet
+    prec = "bf16" if args.precision == "bf16" else "f32"
+    torch.manual_seed(42)
+    m = RestorationUNet(channels=(32, 64, 128, 256), precision=prec).to(dev).train()
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    crit, batcher = CombinedLoss(0.3), RestorationBatcher(dev)
+    from mx_det.data import synth_image
+    import numpy as np
+    src = torch.from_numpy(np.stack([synth_image(rank * 16 + i, 256, 256) for i in range(16)]))
+
+    def step(i):
+        clean = src[(8 * i) % 16:(8 * i) % 16 + 8]
+        cor, tgt = batcher(clean)
+        loss = crit(m(cor), tgt)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return float(loss.item())
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    rec = {"metric": "patches/sec U-Net restoration train 256x256 bs=8/GPU", "value": round(8 * args.steps * world / dt, 3),
+           "unit": "patches/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": DTYPE_TEXT[prec], "arithmetic": ARITH_TEXT[prec],
+           "data": "synthetic VisDrone-shaped uint8 patches, on-device corruption, random-init weights",
+           "config": {"workload": "train_restoration.py:199-205 (AdamW, L1 + 0.3 (1 - SSIM))", "global_batch": 8 * world,
+                      "per_gpu_batch": 8, "patch": "256x256", "channels": [32, 64, 128, 256],
+                      "parallelism": f"replicas{world}"}}
+    if rank == 0 and not args.no_roofline:
+        peak = {"f32": X3_PEAK_TFLOPS, "bf16": BF16_PEAK_TFLOPS}[prec]
+        rec["roofline"] = conv_roofline(m, None, None, None, peak, step_fn=lambda: step(0))
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+
+
 DTYPE_TEXT = {"f32": "f32", "bf16": "bf16"}
 ARITH_TEXT = {"f32": "f32 activations/gradients/BN/RoIAlign; conv products as bf16x3 MFMA (hi*hi + hi*lo + lo*hi, "
                      "f32 accumulate, ~2^-16 rel. per product vs TF32 2^-11)",
@@ -430,7 +484,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--augment", action="store_true")
-    ap.add_argument("--mode", choices=("train", "eval", "eval_restored"), default="train",
+    ap.add_argument("--mode", choices=("train", "eval", "eval_restored", "unet_train"), default="train",
                     help="train (default): the headline train step; eval: per-image eval forward "
                          "(eval_all.py); eval_restored: on-device U-Net restore + eval (eval_restored.py)")
     ap.add_argument("--precision", choices=("both", "f32", "bf16"), default="both",
@@ -460,7 +514,10 @@ def main():
     from mx_det.data import synth_batch
     imgs, tg = synth_batch(rank * N_IMAGES_PER_RANK, N_IMAGES_PER_RANK, device=dev)
     if args.mode != "train":
-        eval_main(args, world, rank, dev, imgs)
+        if args.mode == "unet_train":
+            unet_train_main(args, world, rank, dev)
+        else:
+            eval_main(args, world, rank, dev, imgs)
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()

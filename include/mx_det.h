@@ -398,6 +398,10 @@ int mx_reflect_pad_u8(const uint8_t* src, int64_t B, int64_t H, int64_t W, int64
                       uint8_t* dst, mx_stream_t stream);
 int mx_up_concat(const void* up, const void* skip, int dtype, int64_t N, int64_t H, int64_t W, int64_t Cu, int64_t Cs,
                  void* out, mx_stream_t stream);
+/* Backward of mx_up_concat (U-Net training, train_restoration.py:199-205): gcat [N,2H,2W,Cu+Cs] ->
+ * gup [N,H,W,4*Cu] and gskip [N,2H,2W,Cs] (NULL: skipped). */
+int mx_up_concat_bwd(const void* gcat, int dtype, int64_t N, int64_t H, int64_t W, int64_t Cu, int64_t Cs, void* gup,
+                     void* gskip, mx_stream_t stream);
 int mx_restore_finish(const uint8_t* img_padded, int64_t B, int64_t Hp, int64_t Wp, const float* residual, int64_t H,
                       int64_t W, uint8_t* out, mx_stream_t stream);
 

@@ -50,6 +50,31 @@ __global__ void up_concat_kernel(const T* __restrict__ up, const T* __restrict__
   for (int i = 0; i < V; ++i) ((uint4*)(out + p * Co + c0))[i] = ((const uint4*)src)[i];
 }
 
+// Backward of up_concat (U-Net training, train_restoration.py:199-205): gcat [N,2H,2W,Cu+Cs] ->
+// gup [N,H,W,4*Cu] (the same (i, j, co) channel order: the gradient of the 1x1 conv's output) and
+// gskip [N,2H,2W,Cs]. Every element of gcat is read once and written to exactly one place (8 channels
+// per thread, 16/32-B vectors).
+template <typename T>
+__global__ void up_concat_bwd_kernel(const T* __restrict__ g, int64_t N, int64_t H, int64_t W, int64_t Cu, int64_t Cs,
+                                     T* __restrict__ gup, T* __restrict__ gskip) {
+  const int64_t Co = Cu + Cs, C8 = Co / 8;
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * 2 * H * 2 * W * C8) return;
+  int64_t c0 = (e % C8) * 8, p = e / C8;
+  int64_t x = p % (2 * W), y = (p / (2 * W)) % (2 * H), n = p / (4 * H * W);
+  T* dst;
+  if (c0 < Cu) {
+    int64_t q = (y & 1) * 2 + (x & 1);
+    dst = gup + ((n * H + (y >> 1)) * W + (x >> 1)) * 4 * Cu + q * Cu + c0;
+  } else {
+    if (gskip == nullptr) return;
+    dst = gskip + p * Cs + (c0 - Cu);
+  }
+  constexpr int V = sizeof(T) / 2;
+#pragma unroll
+  for (int i = 0; i < V; ++i) ((uint4*)dst)[i] = ((const uint4*)(g + p * Co + c0))[i];
+}
+
 __global__ void restore_finish_kernel(const uint8_t* __restrict__ img, int64_t B, int64_t Hp, int64_t Wp, const float* __restrict__ res,
                                       int64_t H, int64_t W, uint8_t* __restrict__ out) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -89,6 +114,23 @@ extern "C" int mx_up_concat(const void* up, const void* skip, int dtype, int64_t
   int64_t n = N * 4 * H * W * ((Cu + Cs) / 8);
   if (n == 0) return MX_OK;
   MX_DT_DISPATCH(dtype, up_concat_launch, up, skip, N, H, W, Cu, Cs, out, n, (hipStream_t)stream);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+template <typename T>
+static void up_concat_bwd_launch(const void* g, int64_t N, int64_t H, int64_t W, int64_t Cu, int64_t Cs, void* gup,
+                                 void* gskip, int64_t n, hipStream_t s) {
+  up_concat_bwd_kernel<T><<<(unsigned)cdiv(n, 256), 256, 0, s>>>((const T*)g, N, H, W, Cu, Cs, (T*)gup, (T*)gskip);
+}
+
+extern "C" int mx_up_concat_bwd(const void* gcat, int dtype, int64_t N, int64_t H, int64_t W, int64_t Cu, int64_t Cs,
+                                void* gup, void* gskip, mx_stream_t stream) {
+  MX_CHECK_ARG(Cu % 8 == 0 && Cs % 8 == 0, "up_concat_bwd: channel counts must be multiples of 8");
+  MX_CHECK_ARG(gup != nullptr, "up_concat_bwd: gup is required");
+  int64_t n = N * 4 * H * W * ((Cu + Cs) / 8);
+  if (n == 0) return MX_OK;
+  MX_DT_DISPATCH(dtype, up_concat_bwd_launch, gcat, N, H, W, Cu, Cs, gup, gskip, n, (hipStream_t)stream);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

@@ -94,6 +94,7 @@ _SIGS = {
     "mx_upsample_nearest_bwd": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mx_reflect_pad_u8": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mx_up_concat": (c_int, [c_vp, c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "mx_up_concat_bwd": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "mx_restore_finish": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mx_bn_finalize": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_vp]),

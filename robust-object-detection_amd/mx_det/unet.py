@@ -1,4 +1,5 @@
-"""Restoration U-Net (scripts/restoration_net.py) on the libmx_det HIP kernels, forward (eval) path.
+"""Restoration U-Net (scripts/restoration_net.py) on the libmx_det HIP kernels: eval forward and
+training (train_restoration.py:199-205).
 
 Same module tree and state_dict keys as the reference (down1.conv.block.{0,1,3,4}.*, up4.up.*,
 out_conv.*; 118 entries incl. BN buffers), so experiments/restoration/best.pth loads unchanged.
@@ -7,6 +8,11 @@ reference runs the U-Net in fp32, restore_testsets.py:64-68) or bf16 ("bf16"):
   ConvBlock  = 2 x [conv3x3 with eval-BN folded into weights+bias, LeakyReLU(0.2) fused in the epilogue]
   MaxPool2d(2), ConvTranspose2d(2, s2) as a 1x1 MFMA conv to 4*Cout channels + fused pixel-shuffle/concat,
   out_conv 1x1 (f32 out) + clamp(x + residual, 0, 1).
+Training (module in train mode, grad enabled): the same kernels as the detector's trunk --
+  ConvBlock  = 2 x ConvBNAct (batch-statistics BN + LeakyReLU(0.2) fused, running stats updated),
+  MaxPool2d(2) with argmax backward, ConvTranspose2d(2, s2) = ConvAct 1x1 GEMM to (i, j, co) channels
+  whose weight view keeps autograd to up.weight / up.bias, up_concat with its HIP backward,
+  out_conv ConvAct (f32 out); weights of all 3x3 / 1x1 convs repacked in one launch per step.
 restore_u8() is restore_testsets.py:53-79 on device: reflect-pad to /16, /255, U-Net, *255, clip,
 truncate, crop — uint8 in, uint8 out, no host round trip.
 """
@@ -38,6 +44,33 @@ def _wk(w, cin, x):
     return mc.weight_krsc(w, cin)
 
 
+def _training(mod):
+    return mod.training and torch.is_grad_enabled()
+
+
+class _UpConcat(torch.autograd.Function):
+    """up [N,H,W,4*Cu] (ConvTranspose2d as a 1x1 conv, channel = (i, j, co)) + skip -> [N,2H,2W,Cu+Cs]."""
+
+    @staticmethod
+    def forward(ctx, u, skip, cu):
+        N, H, W, _ = u.shape
+        skip = skip.contiguous()
+        cs = skip.shape[3]
+        cat = torch.empty((N, 2 * H, 2 * W, cu + cs), dtype=u.dtype, device=u.device)
+        call("mx_up_concat", _p(u.contiguous()), _p(skip), mc.dcode(u), N, H, W, cu, cs, _p(cat), _s())
+        ctx.cfg = (N, H, W, cu, cs)
+        return cat
+
+    @staticmethod
+    def backward(ctx, g):
+        N, H, W, cu, cs = ctx.cfg
+        g = g.contiguous()
+        gu = torch.empty((N, H, W, 4 * cu), dtype=g.dtype, device=g.device)
+        gs = torch.empty((N, 2 * H, 2 * W, cs), dtype=g.dtype, device=g.device) if ctx.needs_input_grad[1] else None
+        call("mx_up_concat_bwd", _p(g), mc.dcode(g), N, H, W, cu, cs, _p(gu), _p(gs), _s())
+        return gu, gs, None
+
+
 class ConvBlock(nn.Module):
     def __init__(self, in_ch, out_ch):
         super().__init__()
@@ -46,6 +79,10 @@ class ConvBlock(nn.Module):
             nn.Conv2d(out_ch, out_ch, 3, padding=1, bias=False), nn.BatchNorm2d(out_ch), nn.LeakyReLU(0.2, inplace=True))
 
     def forward(self, x):
+        if _training(self):  # batch-statistics BN, fused LeakyReLU, autograd through the HIP kernels
+            for ci, bi in ((0, 1), (3, 4)):
+                x = mc.conv_bn(x, self.block[ci], self.block[bi], mc.ACT_LEAKY)
+            return x
         for ci, bi in ((0, 1), (3, 4)):
             c, b = self.block[ci], self.block[bi]
             w, bias = mc.fold_bn(c, b)
@@ -68,6 +105,9 @@ class DownBlock(nn.Module):
 
     def forward(self, x):
         feat = self.conv(x)
+        if _training(self):
+            from .backend import _MaxPool
+            return _MaxPool.apply(feat, 2, 2, 0), feat
         return _maxpool2(feat), feat
 
 
@@ -79,6 +119,17 @@ class UpBlock(nn.Module):
 
     def forward(self, x, skip):
         N, H, W, C = x.shape
+        if _training(self):
+            wt = self.up.weight                                   # [Cin, Cout, 2, 2]
+            Cout = wt.shape[1]
+            w1 = wt.permute(2, 3, 1, 0).reshape(4 * Cout, C, 1, 1)   # output channel = (i, j, co)
+            u = mc.ConvAct.apply(x, w1, self.up.bias.repeat(4), (1, 1), (0, 0), mc.ACT_NONE, None)
+            if (2 * H, 2 * W) == (skip.shape[1], skip.shape[2]):
+                return self.conv(_UpConcat.apply(u, skip, Cout))
+            up = u.view(N, H, W, 2, 2, Cout).permute(0, 1, 3, 2, 4, 5).reshape(N, 2 * H, 2 * W, Cout)
+            up = F.interpolate(up.permute(0, 3, 1, 2), size=tuple(skip.shape[1:3]), mode="bilinear",
+                               align_corners=False).permute(0, 2, 3, 1)
+            return self.conv(torch.cat([up, skip], dim=3).contiguous())
         wt = self.up.weight.detach()                     # [Cin, Cout, 2, 2]
         Cout = wt.shape[1]
         w1 = wt.permute(2, 3, 1, 0).reshape(4 * Cout, C, 1, 1)  # output channel = (i, j, co)
@@ -125,13 +176,34 @@ class RestorationUNet(nn.Module):
         b = self.bottleneck(d4)
         u = self.up1(self.up2(self.up3(self.up4(b, s4), s3), s2), s1)
         oc = self.out_conv
+        if _training(self):
+            return mc.ConvAct.apply(u, oc.weight, oc.bias, (1, 1), (0, 0), mc.ACT_NONE, torch.float32)
         return mc.conv_fwd(u, _wk(oc.weight.detach(), u.shape[3], u), (1, 1), (0, 0), bias=oc.bias.detach().float(),
                            out_dtype=torch.float32)
 
-    @torch.no_grad()
+    def _prepare(self):
+        """Training: every 3x3 / 1x1 conv weight repacked (hi/lo planes in f32 mode) in one launch."""
+        pk = self.__dict__.get("_mx_packer")
+        if pk is None:
+            pk = self.__dict__["_mx_packer"] = mc.WeightPacker()
+            for m in self.modules():
+                if isinstance(m, nn.Conv2d):
+                    pk.register(m.weight, m.stride, m.padding, True, split=self.precision == "f32")
+        mc.set_packer(pk)
+        pk.refresh()
+
     def forward(self, x):
-        """Reference contract: x [N,3,H,W] f32 in [0,1] -> clamp(x + residual, 0, 1) [N,3,H,W] f32."""
-        x8 = F.pad(x.permute(0, 2, 3, 1), (0, 5)).to(self.act_dtype).contiguous()
+        """Reference contract: x [N,3,H,W] f32 in [0,1] -> clamp(x + residual, 0, 1) [N,3,H,W] f32.
+        In train mode with grad enabled the output carries autograd through the HIP kernels."""
+        if not _training(self):
+            with torch.no_grad():
+                x8 = F.pad(x.permute(0, 2, 3, 1), (0, 5)).to(self.act_dtype).contiguous()
+                r = self.residual_nhwc(x8)
+                return torch.clamp(x + r.permute(0, 3, 1, 2), 0.0, 1.0)
+        if not x.is_cuda:
+            raise RuntimeError("RestorationUNet training runs on the HIP device (no CPU path)")
+        self._prepare()
+        x8 = F.pad(x.detach().permute(0, 2, 3, 1), (0, 5)).to(self.act_dtype).contiguous()
         r = self.residual_nhwc(x8)
         return torch.clamp(x + r.permute(0, 3, 1, 2), 0.0, 1.0)
 

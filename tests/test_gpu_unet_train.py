@@ -1,0 +1,145 @@
+"""U-Net training on the HIP kernels (reference train_restoration.py:199-205: restored = model(corrupted);
+loss = CombinedLoss(restored, clean); loss.backward()) against the CPU restatement of the reference
+module (oracle/unet_ref.py, plain torch fp32, train-mode BatchNorm) with the same weights and batch.
+Precision "f32" (bf16x3 conv products): output max abs 1e-4, loss 1e-4 relative, BN running statistics
+1e-4. Gradients: measured against the same module in float64 (the exact answer), every parameter's
+gradient is closer to it than the reference's own arithmetic is (the CPU module with TF32-rounded conv
+operands: cudnn's default on its Ampere GPU), >= 5x closer on average -- the batch-statistics BN
+backward over few samples (64 per channel at the 4x4 bottleneck) magnifies any per-product rounding
+(measured 1e-3 .. 6e-3 relative vs the fp32 CPU module), so an absolute bound would test BN
+conditioning, not the kernels. Sizes: 64x64 (the up path's exact x2
+scatter + its HIP backward) and 72x72 (9 -> 4 at the bottleneck: the bilinear fix-up of
+restoration_net.py:53-55). Plus the drop-in script end to end on a tiny synthetic image folder."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CH = (8, 16, 32, 64)
+
+
+def _pair(dev, seed=0):
+    from mx_det.unet import RestorationUNet
+    from oracle.unet_ref import torch_reference_unet
+    torch.manual_seed(seed)
+    m = RestorationUNet(channels=CH, precision="f32")
+    with torch.no_grad():  # non-trivial BN affine and ConvTranspose biases
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.weight.uniform_(0.5, 1.5)
+                mod.bias.uniform_(-0.2, 0.2)
+            if isinstance(mod, torch.nn.ConvTranspose2d):
+                mod.bias.uniform_(-0.1, 0.1)
+    ref = torch_reference_unet({k: v.clone() for k, v in m.state_dict().items()}, CH).train()
+    return m.to(dev).train(), ref
+
+
+def _tf32(t):
+    i = t.contiguous().view(torch.int32).to(torch.int64)
+    r = ((i + 0xFFF + ((i >> 13) & 1)) >> 13) << 13
+    return (((r + 2 ** 31) % 2 ** 32) - 2 ** 31).to(torch.int32).view(torch.float32)
+
+
+def _st(t):  # TF32-rounded value, gradient straight through
+    return t + (_tf32(t.detach()) - t).detach()
+
+
+def _tf32_module(ref):
+    """The CPU module with every conv / conv-transpose operand rounded to TF32 (forward), the
+    reference's own arithmetic on its Ampere GPU."""
+    import copy
+    import torch.nn.functional as F
+    m = copy.deepcopy(ref)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Conv2d):
+            mod.forward = (lambda c: lambda x: F.conv2d(_st(x), _st(c.weight), c.bias, c.stride, c.padding))(mod)
+        elif isinstance(mod, torch.nn.ConvTranspose2d):
+            mod.forward = (lambda c: lambda x: F.conv_transpose2d(_st(x), _st(c.weight), c.bias, c.stride))(mod)
+    return m
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("hw", [64, 72])
+def test_unet_train_step_matches_cpu(dev, hw):
+    from mx_det.restoration import CombinedLoss
+    m, ref = _pair(dev)
+    g = torch.Generator().manual_seed(1)
+    clean = torch.rand(4, 3, hw, hw, generator=g)
+    corrupted = (clean + 0.1 * torch.randn(4, 3, hw, hw, generator=g)).clamp(0, 1)
+    crit = CombinedLoss(0.3)
+    import copy
+    r64, rt = copy.deepcopy(ref).double(), _tf32_module(ref)
+    (crit(r64(corrupted.double()), clean.double())).backward()
+    (crit(rt(corrupted), clean)).backward()
+    out_r = ref(corrupted)
+    loss_r = crit(out_r, clean)
+    loss_r.backward()
+    out = m(corrupted.to(dev))
+    loss = crit(out, clean.to(dev))
+    loss.backward()
+    assert (out.detach().cpu() - out_r.detach()).abs().max().item() < 1e-4
+    assert abs(float(loss) - float(loss_r)) <= 1e-4 * abs(float(loss_r)), (float(loss), float(loss_r))
+    p64, pt = dict(r64.named_parameters()), dict(rt.named_parameters())
+    eh, et, bad = [], [], []
+    for n, p in m.named_parameters():
+        a, b = _rel(p.grad, p64[n].grad), _rel(pt[n].grad, p64[n].grad)
+        eh.append(a)
+        et.append(b)
+        if not (a < b and a < 2e-2):
+            bad.append((n, a, b))
+    assert not bad, bad
+    assert 5 * sum(eh) < sum(et), (sum(eh) / len(eh), sum(et) / len(et))
+    br = dict(ref.named_buffers())
+    for n, b in m.named_buffers():
+        if n.endswith(("running_mean", "running_var")):
+            assert (b.cpu() - br[n]).abs().max().item() < 1e-4, n
+        elif n.endswith("num_batches_tracked"):
+            assert int(b) == int(br[n]) == 1, n
+
+
+def test_unet_train_steps_decrease_loss(dev):
+    """A few AdamW steps (the reference's optimizer) on one batch: the HIP training loop learns."""
+    from mx_det.restoration import CombinedLoss
+    m, _ = _pair(dev, 3)
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(2)
+    clean = torch.rand(8, 3, 64, 64, generator=g).to(dev)
+    corrupted = (clean + 0.1 * torch.randn(8, 3, 64, 64, generator=g).to(dev)).clamp(0, 1)
+    crit = CombinedLoss(0.3)
+    losses = []
+    for _ in range(8):
+        loss = crit(m(corrupted), clean)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    assert losses[-1] < 0.8 * losses[0], losses
+
+
+def test_train_restoration_script(dev, tmp_path, monkeypatch):
+    from PIL import Image
+
+    from mx_det.data import synth_image
+    from scripts import train_restoration as tr
+    for split, n in (("train", 16), ("val", 8)):
+        d = tmp_path / split
+        d.mkdir()
+        for i in range(n):
+            Image.fromarray(synth_image(i, 280, 300)).save(d / f"{i:04d}.jpg", quality=95)
+    monkeypatch.setattr(tr, "PATCH_SIZE", 64)
+    best = tr.main(tmp_path / "train", tmp_path / "val", tmp_path / "out", epochs=5)
+    hist = [json.loads(line) for line in open(tmp_path / "out/history.jsonl")]
+    assert [h["epoch"] for h in hist] == [1, 2, 3, 4, 5]
+    assert set(hist[0]) == {"epoch", "train_loss", "lr", "val_psnr", "val_ssim", "elapsed_sec"}
+    assert hist[0]["val_psnr"] is None and hist[4]["val_psnr"] is not None and np.isfinite(best)
+    ck = torch.load(tmp_path / "out/best.pth", weights_only=True)
+    assert set(ck) == {"model", "epoch", "psnr", "ssim"} and ck["epoch"] == 5
+    from mx_det.unet import RestorationUNet
+    RestorationUNet(channels=(32, 64, 128, 256)).load_state_dict(ck["model"])
