@@ -20,7 +20,7 @@ import torch.nn as nn
 
 from . import ops
 
-NOISE, BLUR, LOWRES = 1, 2, 3  # ops.corrupt_u8 codes (augmentations.py apply_noise / motion_blur / lowres)
+NOISE, BLUR, LOWRES = ops.CORRUPT_NOISE, ops.CORRUPT_BLUR, ops.CORRUPT_LOWRES  # augmentations.py ops
 
 
 def _gaussian_kernel(size=11, sigma=1.5):

@@ -30,8 +30,13 @@ for s in $STEPS; do
         python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/prof.log" 2>&1 \
         || { echo "prof failed rc=$?"; tail -30 "$OUT/prof.log"; exit 1; }
       for f in $(find "$OUT/prof" -name '*_stats.csv'); do cp "$f" "$OUT/"; done
+      python3 tools/prof_steps.py "$OUT/prof" --steps 10 --out "$OUT/step_kernels.csv" > "$OUT/step_kernels.log" 2>&1 \
+        || { echo "prof_steps failed"; tail -5 "$OUT/step_kernels.log"; }
       rm -rf "$OUT/prof"
       tail -1 "$OUT/prof.log" ;;
+    pmc)
+      timeout -k 10 500 bash tools/pmc_traffic.sh > "$OUT/pmc.log" 2>&1 || { echo "pmc failed"; tail -20 "$OUT/pmc.log"; exit 1; }
+      cp gpurun_out/pmc_traffic/traffic.json "$OUT/traffic.json"; tail -3 "$OUT/pmc.log" ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
