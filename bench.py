@@ -472,6 +472,74 @@ def unet_train_main(args, world, rank, dev):
         print(json.dumps(rec), flush=True)
 
 
+def jpeg_main(args, world, rank, dev):
+    """Test-set / loader image decode (coco_detection_dataset.py:23, restore_testsets.py:99): JPEG bytes
+    of 1333x800 VisDrone-shaped images (q95 4:2:0, as build_corrupted_testsets writes them) -> uint8
+    HWC RGB in HBM. Per image: host entropy decode (1 thread) + copy + device IDCT / upsample / colour.
+    The device kernels are also timed alone with HIP events (roofline: HBM bytes = coefficients read
+    2 B/coef + planes written and read + RGB written)."""
+    import io
+    import numpy as np
+    from PIL import Image
+    from mx_det import jpeg
+    from mx_det.data import synth_image
+    blobs = []
+    for i in range(8):
+        b = io.BytesIO()
+        Image.fromarray(synth_image(rank * 8 + i, 800, 1333)).save(b, format="JPEG", quality=95)
+        blobs.append(b.getvalue())
+    for i in range(args.warmup):
+        jpeg.decode(blobs[i % 8], dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        jpeg.decode(blobs[i % 8], dev)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # device stage alone
+    import ctypes
+    from mx_det import _lib
+    info, coefs = jpeg.decode_coefs(blobs[0])
+    cd = torch.from_numpy(coefs).to(dev)
+    ws = torch.empty(_lib.load().mx_jpeg_workspace(ctypes.byref(info)), dtype=torch.uint8, device=dev)
+    out = torch.empty((info.height, info.width, 3), dtype=torch.uint8, device=dev)
+    run = lambda: _lib.call("mx_jpeg_reconstruct", cd.data_ptr(), ctypes.byref(info), ws.data_ptr(), ws.numel(),  # noqa: E731
+                            out.data_ptr(), 0, _lib.stream())
+    run()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(50):
+        run()
+    b.record()
+    torch.cuda.synchronize()
+    us = a.elapsed_time(b) / 50 * 1e3
+    byts = coefs.size * 2 + 2 * ws.numel() + out.numel()
+    th = time.perf_counter()
+    for i in range(16):
+        jpeg.decode_coefs(blobs[i % 8])
+    host_ms = (time.perf_counter() - th) / 16 * 1e3
+    rec = {"metric": "images/sec JPEG decode 1333x800 q95 4:2:0 -> uint8 RGB in HBM", "value": round(args.steps / dt, 3),
+           "unit": "images/sec", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u8/int16", "data": "synthetic VisDrone-shaped images encoded by PIL",
+           "config": {"workload": "coco_detection_dataset.py:23 / restore_testsets.py:99 image decode",
+                      "image": "1333x800", "host_entropy_ms": round(host_ms, 3)},
+           "roofline": {"bound": "hbm", "achieved": round(byts / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(byts / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "kernel": "jpeg_idct_kernel + jpeg_colour_kernel", "avg_launch_us": round(us, 2),
+                        "algorithmic_mb": round(byts / 1e6, 3)}}
+    if not args.no_cpu_baseline:
+        tc = time.perf_counter()
+        n = 0
+        while time.perf_counter() - tc < 3.0:
+            np.asarray(Image.open(io.BytesIO(blobs[n % 8])).convert("RGB"))
+            n += 1
+        rec["cpu_baseline"] = {"value": n / (time.perf_counter() - tc), "unit": "images/sec", "cores": 1,
+                               "kind": "reference", "sample": f"{n} PIL (libjpeg-turbo) decodes, 1 thread"}
+    print(json.dumps(rec), flush=True)
+
+
 DTYPE_TEXT = {"f32": "f32", "bf16": "bf16"}
 ARITH_TEXT = {"f32": "f32 activations/gradients/BN/RoIAlign; conv products as bf16x3 MFMA (hi*hi + hi*lo + lo*hi, "
                      "f32 accumulate, ~2^-16 rel. per product vs TF32 2^-11)",
@@ -484,7 +552,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--augment", action="store_true")
-    ap.add_argument("--mode", choices=("train", "eval", "eval_restored", "unet_train"), default="train",
+    ap.add_argument("--mode", choices=("train", "eval", "eval_restored", "unet_train", "jpeg"), default="train",
                     help="train (default): the headline train step; eval: per-image eval forward "
                          "(eval_all.py); eval_restored: on-device U-Net restore + eval (eval_restored.py)")
     ap.add_argument("--precision", choices=("both", "f32", "bf16"), default="both",
@@ -516,6 +584,8 @@ def main():
     if args.mode != "train":
         if args.mode == "unet_train":
             unet_train_main(args, world, rank, dev)
+        elif args.mode == "jpeg":
+            jpeg_main(args, world, rank, dev)
         else:
             eval_main(args, world, rank, dev, imgs)
         if world > 1:

@@ -266,6 +266,8 @@ int mx_conv_set_stages(int stages);
 /* K-tile order of the buffer-descriptor conv kernels: 0 tap-major, 1 (default) channel-major (all taps
    of a 32-channel chunk before the next chunk: cross-tap re-reads of the gathered rows hit L2). */
 int mx_conv_set_korder(int order);
+/* Timing experiments only: 1 = the bf16x3 buffer kernels skip their epilogue (outputs undefined). */
+int mx_conv_set_debug(int v);
 int mx_conv_set_wgrad_target(int64_t blocks);
 
 /* ---------------------------------------------------------------------------------------------
@@ -404,6 +406,40 @@ int mx_up_concat_bwd(const void* gcat, int dtype, int64_t N, int64_t H, int64_t 
                      void* gskip, mx_stream_t stream);
 int mx_restore_finish(const uint8_t* img_padded, int64_t B, int64_t Hp, int64_t Wp, const float* residual, int64_t H,
                       int64_t W, uint8_t* out, mx_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Baseline JPEG decode, hybrid (replaces the PIL / cv2.imread JPEG decode of
+ * coco_detection_dataset.py:23 (Image.open(...).convert("RGB")), restore_testsets.py:99 and
+ * build_corrupted_testsets.py:139, all libjpeg(-turbo) ISLOW + fancy upsampling):
+ *   mx_jpeg_parse         host: markers of a baseline (SOF0/SOF1) Huffman JPEG -> mx_jpeg_info
+ *                         (MX_EUNSUPPORTED for progressive / arithmetic / lossless / CMYK / 4:4:0).
+ *   mx_jpeg_decode_coefs  host: entropy decoding (sequential bitstream; restart markers honoured)
+ *                         into quantised coefficients, natural order, int16 [comp][by][bx][64].
+ *   mx_jpeg_reconstruct   device: dequantisation + jpeg_idct_islow (jidctint.c integer IDCT) per
+ *                         8x8 block into component planes (ws, mx_jpeg_workspace() bytes), then
+ *                         h2v1 / h2v2 fancy upsampling (jdsample.c) and the YCbCr -> RGB tables of
+ *                         jdcolor.c into out[height][width][3] uint8 (RGB, or BGR with bgr = 1 like
+ *                         cv2.imread). Bit-exact with libjpeg-turbo's default decode.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t width, height, ncomp;       /* ncomp 1 (grey) or 3 (YCbCr) */
+  int32_t h[3], v[3], tq[3];          /* sampling factors, quantisation table per component */
+  int32_t hmax, vmax, mcux, mcuy;     /* MCUs across / down */
+  int32_t bw[3], bh[3];               /* blocks per row / block rows of each component (MCU padded) */
+  int32_t dw[3], dh[3];               /* downsampled_width / height (jdmaster.c) */
+  int64_t coef_off[3], coef_total;    /* int16 offsets of each component's blocks; total int16s */
+  int32_t restart_interval;
+  int32_t scan_off;                   /* byte offset of the entropy-coded data */
+  uint16_t qt[4][64];                 /* quantisation tables, natural order */
+  uint8_t cid[3], td[3], ta[3];       /* component ids, DC / AC Huffman table of each component */
+  uint8_t hbits[8][17], hval[8][256]; /* Huffman tables: 0-3 DC, 4-7 AC (BITS, HUFFVAL) */
+  uint8_t hdef[8];
+} mx_jpeg_info;
+int mx_jpeg_parse(const uint8_t* data, int64_t n, mx_jpeg_info* info);
+int mx_jpeg_decode_coefs(const uint8_t* data, int64_t n, const mx_jpeg_info* info, int16_t* coefs_host);
+size_t mx_jpeg_workspace(const mx_jpeg_info* info);
+int mx_jpeg_reconstruct(const int16_t* coefs, const mx_jpeg_info* info, void* ws, size_t ws_bytes, uint8_t* out,
+                        int bgr, mx_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -600,3 +600,196 @@ void orc_motion_blur_kernel(int k, double angle_deg, float* out /* k*k */) {
   for (int i = 0; i < k * k; ++i) out[i] = out[i] / den;
   free(src);
 }
+
+/* ---------------------------------------------------------------------------------------------
+ * JPEG pixel reconstruction from quantised coefficients, restated from libjpeg-turbo (the decoder
+ * behind PIL / cv2.imread) in its own loop structure:
+ *   jidctint.c jpeg_idct_islow (6b algorithm: CONST_BITS 13, PASS1_BITS 2, JLONG intermediates, the
+ *   post-IDCT range-limit table of jdmaster.c prepare_range_limit_table),
+ *   jdsample.c h2v1_fancy_upsample / h2v2_fancy_upsample (context rows replicated at the image
+ *   edges, jdmainct.c) and the plain replicating upsamplers when downsampled_width <= 2,
+ *   jdcolor.c build_ycc_rgb_table / ycc_rgb_convert.
+ * TEST INFRASTRUCTURE: the checker of mx_jpeg_reconstruct, itself checked against PIL's decode.
+ * ------------------------------------------------------------------------------------------- */
+static unsigned char rl_table[256 * 4 + 256 + 128];  /* sample_range_limit block */
+static const unsigned char* sample_range_limit;
+static void prep_range_limit(void) {
+  if (sample_range_limit) return;
+  unsigned char* t = rl_table + 256;
+  memset(t - 256, 0, 256);
+  for (int i = 0; i <= 255; ++i) t[i] = (unsigned char)i;
+  unsigned char* p = t + 128;
+  for (int i = 128; i < 512; ++i) p[i] = 255;
+  memset(p + 512, 0, 512 - 128);
+  memcpy(p + 1024 - 128, t, 128);
+  sample_range_limit = t;
+}
+
+#define DESCALE(x, n) (((x) + ((int64_t)1 << ((n) - 1))) >> (n))
+
+static void islow(const int16_t* coef, const uint16_t* q, unsigned char* out, int64_t stride) {
+  int ws[64];
+  const unsigned char* range_limit = sample_range_limit + 128;
+  for (int col = 0; col < 8; ++col) {
+    const int16_t* in = coef + col;
+    const uint16_t* qp = q + col;
+    int64_t z1, z2, z3, z4, z5, tmp0, tmp1, tmp2, tmp3, tmp10, tmp11, tmp12, tmp13;
+    z2 = (int64_t)in[16] * qp[16];
+    z3 = (int64_t)in[48] * qp[48];
+    z1 = (z2 + z3) * 4433;
+    tmp2 = z1 + z3 * -15137;
+    tmp3 = z1 + z2 * 6270;
+    z2 = (int64_t)in[0] * qp[0];
+    z3 = (int64_t)in[32] * qp[32];
+    tmp0 = (z2 + z3) * 8192;
+    tmp1 = (z2 - z3) * 8192;
+    tmp10 = tmp0 + tmp3; tmp13 = tmp0 - tmp3; tmp11 = tmp1 + tmp2; tmp12 = tmp1 - tmp2;
+    tmp0 = (int64_t)in[56] * qp[56];
+    tmp1 = (int64_t)in[40] * qp[40];
+    tmp2 = (int64_t)in[24] * qp[24];
+    tmp3 = (int64_t)in[8] * qp[8];
+    z1 = tmp0 + tmp3; z2 = tmp1 + tmp2; z3 = tmp0 + tmp2; z4 = tmp1 + tmp3;
+    z5 = (z3 + z4) * 9633;
+    tmp0 *= 2446; tmp1 *= 16819; tmp2 *= 25172; tmp3 *= 12299;
+    z1 *= -7373; z2 *= -20995; z3 *= -16069; z4 *= -3196;
+    z3 += z5; z4 += z5;
+    tmp0 += z1 + z3; tmp1 += z2 + z4; tmp2 += z2 + z3; tmp3 += z1 + z4;
+    ws[col] = (int)DESCALE(tmp10 + tmp3, 11);
+    ws[56 + col] = (int)DESCALE(tmp10 - tmp3, 11);
+    ws[8 + col] = (int)DESCALE(tmp11 + tmp2, 11);
+    ws[48 + col] = (int)DESCALE(tmp11 - tmp2, 11);
+    ws[16 + col] = (int)DESCALE(tmp12 + tmp1, 11);
+    ws[40 + col] = (int)DESCALE(tmp12 - tmp1, 11);
+    ws[24 + col] = (int)DESCALE(tmp13 + tmp0, 11);
+    ws[32 + col] = (int)DESCALE(tmp13 - tmp0, 11);
+  }
+  for (int row = 0; row < 8; ++row) {
+    const int* w = ws + row * 8;
+    unsigned char* o = out + row * stride;
+    int64_t z1, z2, z3, z4, z5, tmp0, tmp1, tmp2, tmp3, tmp10, tmp11, tmp12, tmp13;
+    z2 = w[2]; z3 = w[6];
+    z1 = (z2 + z3) * 4433;
+    tmp2 = z1 + z3 * -15137;
+    tmp3 = z1 + z2 * 6270;
+    tmp0 = ((int64_t)w[0] + w[4]) * 8192;
+    tmp1 = ((int64_t)w[0] - w[4]) * 8192;
+    tmp10 = tmp0 + tmp3; tmp13 = tmp0 - tmp3; tmp11 = tmp1 + tmp2; tmp12 = tmp1 - tmp2;
+    tmp0 = w[7]; tmp1 = w[5]; tmp2 = w[3]; tmp3 = w[1];
+    z1 = tmp0 + tmp3; z2 = tmp1 + tmp2; z3 = tmp0 + tmp2; z4 = tmp1 + tmp3;
+    z5 = (z3 + z4) * 9633;
+    tmp0 *= 2446; tmp1 *= 16819; tmp2 *= 25172; tmp3 *= 12299;
+    z1 *= -7373; z2 *= -20995; z3 *= -16069; z4 *= -3196;
+    z3 += z5; z4 += z5;
+    tmp0 += z1 + z3; tmp1 += z2 + z4; tmp2 += z2 + z3; tmp3 += z1 + z4;
+    o[0] = range_limit[(int)DESCALE(tmp10 + tmp3, 18) & 1023];
+    o[7] = range_limit[(int)DESCALE(tmp10 - tmp3, 18) & 1023];
+    o[1] = range_limit[(int)DESCALE(tmp11 + tmp2, 18) & 1023];
+    o[6] = range_limit[(int)DESCALE(tmp11 - tmp2, 18) & 1023];
+    o[2] = range_limit[(int)DESCALE(tmp12 + tmp1, 18) & 1023];
+    o[5] = range_limit[(int)DESCALE(tmp12 - tmp1, 18) & 1023];
+    o[3] = range_limit[(int)DESCALE(tmp13 + tmp0, 18) & 1023];
+    o[4] = range_limit[(int)DESCALE(tmp13 - tmp0, 18) & 1023];
+  }
+}
+
+/* one upsampled chroma row (output width 2*dw or dw) from sample rows `in0` (nearer) / `in1` */
+static void up_h2v1(const unsigned char* in, int dw, unsigned char* o) {
+  if (dw <= 2) { for (int c = 0; c < dw; ++c) o[2 * c] = o[2 * c + 1] = in[c]; return; }
+  int v = in[0];
+  o[0] = (unsigned char)v;
+  o[1] = (unsigned char)((v * 3 + in[1] + 2) >> 2);
+  for (int c = 1; c < dw - 1; ++c) {
+    v = in[c] * 3;
+    o[2 * c] = (unsigned char)((v + in[c - 1] + 1) >> 2);
+    o[2 * c + 1] = (unsigned char)((v + in[c + 1] + 2) >> 2);
+  }
+  v = in[dw - 1];
+  o[2 * dw - 2] = (unsigned char)((v * 3 + in[dw - 2] + 1) >> 2);
+  o[2 * dw - 1] = (unsigned char)v;
+}
+
+static void up_h2v2_row(const unsigned char* in0, const unsigned char* in1, int dw, unsigned char* o) {
+  if (dw <= 2) { for (int c = 0; c < dw; ++c) o[2 * c] = o[2 * c + 1] = in0[c]; return; }
+  int this_ = in0[0] * 3 + in1[0], next = in0[1] * 3 + in1[1], last;
+  o[0] = (unsigned char)((this_ * 4 + 8) >> 4);
+  o[1] = (unsigned char)((this_ * 3 + next + 7) >> 4);
+  last = this_; this_ = next;
+  int k = 2;
+  for (int c = 2; c < dw; ++c) {
+    next = in0[c] * 3 + in1[c];
+    o[k++] = (unsigned char)((this_ * 3 + last + 8) >> 4);
+    o[k++] = (unsigned char)((this_ * 3 + next + 7) >> 4);
+    last = this_; this_ = next;
+  }
+  o[k++] = (unsigned char)((this_ * 3 + last + 8) >> 4);
+  o[k++] = (unsigned char)((this_ * 4 + 7) >> 4);
+}
+
+int orc_jpeg_reconstruct(const int16_t* coefs, const mx_jpeg_info* info, unsigned char* out, int bgr) {
+  prep_range_limit();
+  const int W = info->width, H = info->height, nc = info->ncomp;
+  unsigned char* plane[3] = {0, 0, 0};
+  for (int c = 0; c < nc; ++c) {
+    const int64_t stride = (int64_t)info->bw[c] * 8;
+    plane[c] = (unsigned char*)malloc((size_t)stride * info->bh[c] * 8);
+    if (!plane[c]) return -1;
+    for (int by = 0; by < info->bh[c]; ++by)
+      for (int bx = 0; bx < info->bw[c]; ++bx)
+        islow(coefs + info->coef_off[c] + ((int64_t)by * info->bw[c] + bx) * 64, info->qt[info->tq[c]],
+              plane[c] + (int64_t)by * 8 * stride + bx * 8, stride);
+  }
+  /* colour tables (jdcolor.c) */
+  int crr[256], cbb[256], crg[256], cbg[256];
+  for (int i = 0; i < 256; ++i) {
+    const int x = i - 128;
+    crr[i] = (91881 * x + 32768) >> 16;
+    cbb[i] = (116130 * x + 32768) >> 16;
+    crg[i] = -46802 * x;
+    cbg[i] = -22554 * x + 32768;
+  }
+  const unsigned char* lim = sample_range_limit;
+  unsigned char* up[3] = {0, 0, 0};
+  for (int c = 1; c < nc; ++c) up[c] = (unsigned char*)malloc((size_t)2 * info->dw[c] + 16);
+  for (int y = 0; y < H; ++y) {
+    const unsigned char* Y = plane[0] + (int64_t)y * info->bw[0] * 8;
+    const unsigned char* cb = 0;
+    const unsigned char* cr = 0;
+    for (int c = 1; c < nc; ++c) {
+      const int hs = info->hmax / info->h[c], vs = info->vmax / info->v[c];
+      const int64_t st = (int64_t)info->bw[c] * 8;
+      const unsigned char* src;
+      if (hs == 1 && vs == 1) {
+        src = plane[c] + (int64_t)y * st;
+      } else if (vs == 1) {
+        up_h2v1(plane[c] + (int64_t)y * st, info->dw[c], up[c]);
+        src = up[c];
+      } else {
+        const int r0 = y >> 1;
+        int r1 = (y & 1) ? r0 + 1 : r0 - 1;
+        if (r1 < 0) r1 = 0;
+        if (r1 > info->dh[c] - 1) r1 = info->dh[c] - 1;
+        if (info->dw[c] <= 2) r1 = r0;
+        up_h2v2_row(plane[c] + (int64_t)r0 * st, plane[c] + (int64_t)r1 * st, info->dw[c], up[c]);
+        src = up[c];
+      }
+      if (c == 1) cb = src; else cr = src;
+    }
+    for (int x = 0; x < W; ++x) {
+      unsigned char* o = out + ((int64_t)y * W + x) * 3;
+      const int yy = Y[x];
+      int R, G, B;
+      if (nc == 1) {
+        R = G = B = yy;
+      } else {
+        R = lim[yy + crr[cr[x]]];
+        G = lim[yy + ((cbg[cb[x]] + crg[cr[x]]) >> 16)];
+        B = lim[yy + cbb[cb[x]]];
+      }
+      o[0] = (unsigned char)(bgr ? B : R);
+      o[1] = (unsigned char)G;
+      o[2] = (unsigned char)(bgr ? R : B);
+    }
+  }
+  for (int c = 0; c < 3; ++c) { free(plane[c]); free(up[c]); }
+  return 0;
+}

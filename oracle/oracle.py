@@ -208,3 +208,16 @@ def resize_area_fast2_u8(img):
     out = np.empty((H // 2, W // 2, C), np.uint8)
     lib().orc_resize_area_fast2_u8(_p(img, U8), i64(H), i64(W), i64(C), _p(out, U8), i64(H // 2), i64(W // 2))
     return out
+
+
+def jpeg_reconstruct(coefs, info, bgr=False):
+    """libjpeg-turbo pixel reconstruction (islow IDCT, fancy upsampling, ycc->rgb) of the quantised
+    coefficients `coefs` (int16, mx_jpeg_decode_coefs layout) described by `info` (an mx_jpeg_info
+    ctypes structure) -> uint8 [H, W, 3]."""
+    coefs = np.ascontiguousarray(coefs, np.int16)
+    out = np.empty((info.height, info.width, 3), np.uint8)
+    rc = lib().orc_jpeg_reconstruct(coefs.ctypes.data_as(ctypes.c_void_p), ctypes.byref(info),
+                                    out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(int(bool(bgr))))
+    if rc != 0:
+        raise MemoryError("orc_jpeg_reconstruct")
+    return out

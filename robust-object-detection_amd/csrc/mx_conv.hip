@@ -64,6 +64,7 @@ struct ConvP {
   // block gathers between two visits of the same cache line shrink from BMT full pixel rows to the
   // tap window of one chunk, so the re-reads across taps stay in L2
   int korder;
+  int dbg_skip_epi;  // timing experiments only (mx_conv_set_debug): skip the bf16x3 buffer kernel's epilogue
   // dgrad feeding a train-mode BatchNorm backward (mx_conv2d_dgrad_bnb): per 64-row block column
   // sums of g = bf16(dx) * act'(y) and g * (z - mean) * invstd -> bnb_part [2][mblocks64][Ncol]
   const void* bnb_y;
@@ -985,8 +986,8 @@ __device__ __forceinline__ int64_t wgrad_dst(const WgP& p, int64_t k, int col) {
 
 // Block epilogue: the split's partial tile to the slab (plain stores), or, unsplit, the final dw.
 __device__ __forceinline__ void wgrad_store(const WgP& p, f32x4 (&acc)[4][4], int64_t k0, int64_t c0, int wm, int wn,
-                                            int lane) {
-  float* slab = p.slab ? p.slab + (int64_t)blockIdx.y * p.K * p.Ncol : nullptr;
+                                            int lane, int64_t split = -1) {
+  float* slab = p.slab ? p.slab + (split < 0 ? (int64_t)blockIdx.y : split) * p.K * p.Ncol : nullptr;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1708,13 +1709,17 @@ __global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
     const char* Ag = A + (g >> 1) * AH;
     const char* Bh = A + 2 * AH;
     const char* Bl = Bh + BP;
-    bf16x8 ah[TI], al[TI], bh[TJ], bl[TJ];
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
+    constexpr int TJB = TJ > 4 ? 1 : TJ;  // B fragments held at once (wide wave tiles: one column at a time)
+    bf16x8 ah[TI], al[TI], bh[TJB], bl[TJB];
+    auto loadb = [&](int j, int slot) {
       const int row = wn * WN + j * 16 + (lane & 15);
       const int off = row * RB + ((g ^ tile_swz<4>(row)) << 4);
-      bh[j] = *(const bf16x8*)(Bh + off);
-      bl[j] = *(const bf16x8*)(Bl + off);
+      bh[slot] = *(const bf16x8*)(Bh + off);
+      bl[slot] = *(const bf16x8*)(Bl + off);
+    };
+    if constexpr (TJB == TJ) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) loadb(j, j);
     }
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
@@ -1727,14 +1732,36 @@ __global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
       ah[i] = __builtin_bit_cast(bf16x8, h);
       al[i] = __builtin_bit_cast(bf16x8, l);
     }
+    if constexpr (TJB == TJ) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    } else {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        loadb(j, 0);
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[0], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (p.dbg_skip_epi) {  // keep every accumulator live, store nothing
+    float sum = 0.f;
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-      }
+      for (int j = 0; j < TJ; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sum == 1.2345e-30f) ((float*)p.out)[0] = sum;
+    return;
   }
   __syncthreads();
   conv_epilogue<BN, WR, BMT, float, WR>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
@@ -1752,10 +1779,14 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int64_t ntn = (p.Ncol + 127) / 128;
-  const int64_t tile = blockIdx.x;
+  // flat grid, XCD-aware: the blocks an XCD runs are consecutive work items, i.e. all (k, col) tiles of
+  // the same pixel splits, so the dy / x rows they share stay in that XCD's L2
+  const int64_t ntiles = ((p.K + 127) / 128) * ntn;
+  const int64_t work = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int64_t split = work / ntiles, tile = work % ntiles;
   const int64_t mt = tile / ntn, nt = tile % ntn;
   const int64_t k0 = mt * 128, c0 = nt * 128;
-  const int64_t pbeg = (int64_t)blockIdx.y * p.kchunk;
+  const int64_t pbeg = split * p.kchunk;
   const int64_t pend = min<int64_t>(p.P, pbeg + p.kchunk);
   if (pbeg >= pend) return;
   const float* __restrict__ dy = (const float*)p.dy;
@@ -1874,7 +1905,7 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
     if (it + 1 < nk) store(buf ^ 1);
     __syncthreads();
   }
-  wgrad_store(p, acc, k0, c0, wm, wn, lane);
+  wgrad_store(p, acc, k0, c0, wm, wn, lane, split);
 #endif
 }
 
@@ -2149,6 +2180,11 @@ static int g_buf_stages = 0;  // mx_conv_set_stages: LDS ring depth of the 64x12
 extern "C" int mx_conv_set_stages(int n) {
   MX_CHECK_ARG(n == 0 || n == 3 || n == 4 || n == 6, "mx_conv_set_stages: 0 (auto), 3, 4 or 6 (x3 kernels: 3 = alternative ring)");
   g_buf_stages = n;
+  return MX_OK;
+}
+static int g_conv_debug = 0;  // mx_conv_set_debug: 1 = skip the bf16x3 buffer kernels' epilogue (timing only)
+extern "C" int mx_conv_set_debug(int v) {
+  g_conv_debug = v;
   return MX_OK;
 }
 static int g_conv_korder = 1;  // mx_conv_set_korder: K-tile order of the buffer kernels (ConvP::korder)
@@ -2784,7 +2820,8 @@ static Geo make_geo_x3(int64_t M, int64_t Ncol, int64_t Kdim) {
   // 2 blocks per CU: below two full rounds of 128-row tiles, 64-row tiles (twice the blocks)
   // 128 x 128 at 2 blocks per CU; below two full rounds, 64-row tiles. (256 x 128 tiles -- 8 waves,
   // one block per CU, 25 % fewer LDS-DMA pieces per MFMA -- measured 15 % slower on the P2 3x3; a
-  // tuner candidate only.)
+  // tuner candidate only. 256 x 256 with 8 waves of 64 x 128 -- 8 pieces per 96 MFMAs -- measured
+  // no faster than 128 x 128 on the P2 3x3 (615 vs 592 us fwd) and slower everywhere else: removed.)
   g.bmt = 128;
   g.tiles = cdiv(M, 128) * cdiv(Ncol, g.bn);
   if (g.tiles < 2 * cus) {
@@ -2793,8 +2830,7 @@ static Geo make_geo_x3(int64_t M, int64_t Ncol, int64_t Kdim) {
   }
   if (g_force_bmt) {
     g.bmt = g_force_bmt;
-    g.bn = std::min(g_force_bn, 128);
-    if (g.bmt == 256) g.bn = 128;
+    g.bn = g.bmt == 256 ? 128 : std::min(g_force_bn, 128);
     g.narrow = g.bn == 64;
     g.tiles = cdiv(M, g.bmt) * cdiv(Ncol, g.bn);
   }
@@ -2852,6 +2888,7 @@ static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, h
     // ring depth x blocks per CU; mx_conv_set_stages(3) picks the alternative of each tile shape
     const bool alt = g_buf_stages == 3;
     p.korder = g_conv_korder;
+    p.dbg_skip_epi = g_conv_debug;
     if (g.bmt == 256) {
       alt ? launch_x3_buf<128, MODE, 2, 1, 256, 4>(p, blocks, st) : launch_x3_buf<128, MODE, 3, 1, 256, 4>(p, blocks, st);
     } else if (g.bmt == 64) {
@@ -3010,9 +3047,8 @@ extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const
                  need);
     p.slab = (float*)ws;
   }
-  MX_CHECK_ARG(g.tiles < (1ll << 31) && g.splits < 65536, "conv wgrad x3: grid too large");
-  dim3 grid((unsigned)g.tiles, (unsigned)g.splits);
-  conv_wgrad_x3_kernel<<<grid, NT, 2 * 4 * 32 * 256, st>>>(p);
+  MX_CHECK_ARG(g.tiles * g.splits < (1ll << 31), "conv wgrad x3: grid too large");
+  conv_wgrad_x3_kernel<<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);
   MX_LAUNCH_CHECK();
   if (g.splits > 1) {
     MX_CHECK_ARG(Kout < 65536, "conv wgrad x3: too many output channels for the split reduce");

@@ -26,6 +26,19 @@ class ConvShape(ctypes.Structure):
                 ("pad_h", ctypes.c_int32), ("pad_w", ctypes.c_int32)]
 
 
+class JpegInfo(ctypes.Structure):
+    """mx_jpeg_info (include/mx_det.h)."""
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("ncomp", ctypes.c_int32),
+                ("h", ctypes.c_int32 * 3), ("v", ctypes.c_int32 * 3), ("tq", ctypes.c_int32 * 3),
+                ("hmax", ctypes.c_int32), ("vmax", ctypes.c_int32), ("mcux", ctypes.c_int32), ("mcuy", ctypes.c_int32),
+                ("bw", ctypes.c_int32 * 3), ("bh", ctypes.c_int32 * 3), ("dw", ctypes.c_int32 * 3),
+                ("dh", ctypes.c_int32 * 3), ("coef_off", c_i64 * 3), ("coef_total", c_i64),
+                ("restart_interval", ctypes.c_int32), ("scan_off", ctypes.c_int32),
+                ("qt", (ctypes.c_uint16 * 64) * 4), ("cid", ctypes.c_uint8 * 3), ("td", ctypes.c_uint8 * 3),
+                ("ta", ctypes.c_uint8 * 3), ("hbits", (ctypes.c_uint8 * 17) * 8), ("hval", (ctypes.c_uint8 * 256) * 8),
+                ("hdef", ctypes.c_uint8 * 8)]
+
+
 _SIGS = {
     "mx_version": (c_int, []),
     "mx_last_error": (ctypes.c_char_p, []),
@@ -68,6 +81,11 @@ _SIGS = {
     "mx_conv_set_max_splits": (c_int, [c_int]),
     "mx_conv_set_stages": (c_int, [c_int]),
     "mx_conv_set_korder": (c_int, [c_int]),
+    "mx_conv_set_debug": (c_int, [c_int]),
+    "mx_jpeg_parse": (c_int, [c_vp, c_i64, c_vp]),
+    "mx_jpeg_decode_coefs": (c_int, [c_vp, c_i64, c_vp, c_vp]),
+    "mx_jpeg_workspace": (c_sz, [c_vp]),
+    "mx_jpeg_reconstruct": (c_int, [c_vp, c_vp, c_vp, c_sz, c_vp, c_int, c_vp]),
     "mx_conv_set_wgrad_variant": (c_int, [c_int]),
     "mx_conv_get_wgrad_variant": (c_int, []),
     "mx_conv_set_wgrad_target": (c_int, [c_i64]),

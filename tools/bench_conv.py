@@ -77,6 +77,7 @@ def main():
     ap.add_argument("--splits", default="0", help="comma list of fwd/dgrad split-K caps, 0 = auto")
     ap.add_argument("--stages", default="0", help="comma list of buffer-kernel ring depths, 0 = auto")
     ap.add_argument("--korder", default="1", help="comma list of buffer-kernel K-tile orders (0 tap-, 1 channel-major)")
+    ap.add_argument("--debug", default="0", help="comma list of mx_conv_set_debug values (1: no epilogue)")
     ap.add_argument("--graph", action="store_true", help="time launches replayed from a HIP graph")
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "f32"),
                     help="f32: the precision-faithful bf16x3 kernels (TFLOP/s are f32-equivalent, peak 833)")
@@ -86,7 +87,7 @@ def main():
     import itertools
     from mx_det import _lib
     ints = lambda v: [int(x) for x in v.split(",")]  # noqa: E731
-    for ko, ld, v, wv, wt, stg, sp, tl in itertools.product(ints(args.korder), ints(args.loaders), ints(args.variants),
+    for dbg, ko, ld, v, wv, wt, stg, sp, tl in itertools.product(ints(args.debug), ints(args.korder), ints(args.loaders), ints(args.variants),
                                                              ints(args.wgrad), ints(args.wtarget), ints(args.stages),
                                                              ints(args.splits), args.tiles.split(",")):
         bm, bn = [int(x) for x in tl.split("x")]
@@ -94,12 +95,13 @@ def main():
         _lib.call("mx_conv_set_max_splits", sp)
         _lib.call("mx_conv_set_stages", stg)
         _lib.call("mx_conv_set_korder", ko)
+        _lib.call("mx_conv_set_debug", dbg)
         _lib.call("mx_conv_set_loader", ld)
         _lib.call("mx_conv_set_variant", v)
         _lib.call("mx_conv_set_wgrad_variant", wv)
         _lib.call("mx_conv_set_wgrad_target", wt)
         print(f"== loader {ld} tile {tl} conv variant {v} wgrad variant {wv} wgrad target {wt} "
-              f"max splits {sp} stages {stg} korder {ko}", flush=True)
+              f"max splits {sp} stages {stg} korder {ko} debug {dbg}", flush=True)
         run(args)
 
 

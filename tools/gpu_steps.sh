@@ -18,7 +18,7 @@ for s in "$@"; do
       timeout -k 10 600 python -u -m pytest "${s#t:}" -x -v --timeout 300 --timeout-method thread > "$OUT/t$n.log" 2>&1 \
         || { echo "tests $s failed"; tail -40 "$OUT/t$n.log"; exit 1; }
       tail -2 "$OUT/t$n.log" ;;
-    eval|eval_restored|unet_train)
+    eval|eval_restored|unet_train|jpeg)
       timeout -k 10 400 python -u bench.py --mode $s --steps 20 --warmup 3 > "$OUT/$s.log" 2>&1 \
         || { echo "$s failed"; tail -30 "$OUT/$s.log"; exit 1; }
       tail -1 "$OUT/$s.log" ;;

@@ -10,6 +10,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "robust-object-detection_amd")]
 
+os.environ.setdefault("MX_GRAPHS", "0")  # eager: every conv launch passes through the timer
+
 import torch  # noqa: E402
 
 import bench  # noqa: E402
