@@ -256,12 +256,15 @@ def hbm_ops_roofline(model, opt, imgs, tg, reps=20):
                                 "dtype": str(feats[0].dtype).replace("torch.", ""), "avg_launch_us": round(us, 2),
                                 "algorithmic_mb": round(byts / 1e6, 2), "achieved": round(gbs, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
-        # backward (deterministic gather): every f32 level-map element written once + gout read once
+        # backward (deterministic gather): every f32 level-map element written once + gout read once;
+        # the op's own call (the autograd node's body), timed without autograd bookkeeping
         fs = [f.clone().requires_grad_(True) for f in feats]
         out = ops.multiscale_roi_align(fs, rois, scales, k_min)
         g = torch.randn_like(out)
         det = ops.roi_align_deterministic(C)
-        us = timed(lambda: torch.autograd.grad(out, fs, g, retain_graph=True))
+        r_saved, lv_saved = out.grad_fn.saved_tensors
+        shapes = [tuple(f.shape) for f in feats]
+        us = timed(lambda: ops.multiscale_roi_align_backward(g, r_saved, lv_saved, shapes, list(scales)))
         maps = sum(f.numel() for f in feats) * 4
         byts = maps + g.numel() * g.element_size()
         gbs = byts / (us * 1e-6) / 1e9

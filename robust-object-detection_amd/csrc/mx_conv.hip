@@ -1298,10 +1298,13 @@ __global__ void __launch_bounds__(NT, 3) conv_wgrad_buf_kernel(WgP p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int64_t ntn = (p.Ncol + 127) / 128;
-  const int64_t tile = blockIdx.x;
+  // flat XCD-aware grid (as conv_wgrad_x3_kernel): one XCD runs all tiles of the same pixel splits
+  const int64_t ntiles = ((p.K + 127) / 128) * ntn;
+  const int64_t work = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int64_t split = work / ntiles, tile = work % ntiles;
   const int64_t mt = tile / ntn, nt = tile % ntn;
   const int64_t k0 = mt * 128, c0 = nt * 128;
-  const int64_t pbeg = (int64_t)blockIdx.y * p.kchunk;
+  const int64_t pbeg = split * p.kchunk;
   const int64_t pend = min<int64_t>(p.P, pbeg + p.kchunk);
   if (pbeg >= pend) return;
   const int lr = lane >> 4;
@@ -1402,7 +1405,7 @@ __global__ void __launch_bounds__(NT, 3) conv_wgrad_buf_kernel(WgP p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
   }
-  wgrad_store(p, acc, k0, c0, wm, wn, lane);
+  wgrad_store(p, acc, k0, c0, wm, wn, lane, split);
 #endif
 }
 
@@ -2783,7 +2786,7 @@ extern "C" int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, co
   if (v == 3 && !(p.P * p.K * 2 < (1ll << 31) && s->N * s->H * s->W * s->C * 2 < (1ll << 31) &&
                  (p.OH * p.OW >= 32 || (p.OH == 1 && p.OW == 1))))
     v = 0;
-  if (v == 3) conv_wgrad_buf_kernel<<<grid, NT, 3 * 2 * 32 * 256, st>>>(p);
+  if (v == 3) conv_wgrad_buf_kernel<<<(unsigned)(g.tiles * g.splits), NT, 3 * 2 * 32 * 256, st>>>(p);
   else if (v == 2) conv_wgrad_glds_kernel<<<grid, NT, 2 * 2 * BKG * 256, st>>>(p);
   else if (v == 1) conv_wgrad_kernel<64><<<grid, NT, 0, st>>>(p);
   else conv_wgrad_kernel<32><<<grid, NT, 0, st>>>(p);

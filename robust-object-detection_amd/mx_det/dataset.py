@@ -23,7 +23,11 @@ def uint8_transform(img):
 
 
 class COCODetectionDataset(Dataset):
-    def __init__(self, img_dir: str, ann_file: str, transforms=None):
+    """raw=True: __getitem__ returns the file's bytes (uint8 numpy) instead of a decoded image, for the
+    device JPEG decoder (mx_det.jpeg via engine.DeviceJpegLoader); transforms are not applied."""
+
+    def __init__(self, img_dir: str, ann_file: str, transforms=None, raw=False):
+        self.raw = raw
         COCO, _ = get_coco_api()
         self.img_dir = Path(img_dir)
         self.coco = COCO(ann_file)
@@ -52,6 +56,8 @@ class COCODetectionDataset(Dataset):
     def __getitem__(self, idx: int):
         img_id = self.ids[idx]
         info = self.coco.loadImgs(img_id)[0]
+        if self.raw:
+            return np.fromfile(self.img_dir / info["file_name"], dtype=np.uint8), self._target(img_id)
         img = Image.open(self.img_dir / info["file_name"]).convert("RGB")
         target = self._target(img_id)
         if self.transforms is not None:

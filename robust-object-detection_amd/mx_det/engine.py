@@ -258,13 +258,42 @@ def eval_frcnn_variant(model, img_dir, ann_file, dev, restorer=None):
     uint8 image before detection (the fused restored-eval path of eval_restored.py)."""
     from .dataset import COCODetectionDataset, collate_fn, uint8_transform
     world, rank, _ = dist_info()
-    ds = COCODetectionDataset(img_dir, ann_file, transforms=uint8_transform)
+    device_jpeg = os.environ.get("MX_DEVICE_JPEG", "1") != "0"
+    ds = COCODetectionDataset(img_dir, ann_file, transforms=uint8_transform, raw=device_jpeg)
     sampler = ShardSampler(len(ds), world, rank) if world > 1 else None
     loader = DataLoader(ds, batch_size=1, shuffle=False, sampler=sampler, num_workers=0, collate_fn=collate_fn,
-                        pin_memory=True)
+                        pin_memory=not device_jpeg)
+    if device_jpeg:
+        loader = DeviceJpegLoader(loader, dev)
     if restorer is not None:
         loader = _RestoredLoader(loader, restorer, dev)
     return evaluate(model, loader, ann_file, dev, per_class=True)
+
+
+class DeviceJpegLoader:
+    """(file bytes, target) batches -> (uint8 HWC device images, target): the hybrid JPEG decoder
+    (mx_det.jpeg, bit-identical to PIL's libjpeg-turbo decode). Files it does not handle (progressive,
+    CMYK, 4:4:0) are decoded by PIL on the host, as the reference does for every file."""
+
+    def __init__(self, loader, dev):
+        self.loader, self.dev = loader, dev
+
+    def _one(self, b):
+        from . import jpeg
+        try:
+            return jpeg.decode(b, self.dev)
+        except jpeg.JpegUnsupported:
+            import io
+            from PIL import Image
+            img = np.asarray(Image.open(io.BytesIO(b.tobytes())).convert("RGB"))
+            return torch.from_numpy(img.copy()).to(self.dev)
+
+    def __iter__(self):
+        for images, targets in self.loader:
+            yield [self._one(b) for b in images], targets
+
+    def __len__(self):
+        return len(self.loader)
 
 
 class _RestoredLoader:

@@ -263,19 +263,26 @@ class _MultiScaleRoIAlign(torch.autograd.Function):
     def backward(ctx, gout):
         r, levels = ctx.saved_tensors
         shapes, scales, ph, pw, sampling, dt = ctx.cfg
-        g = gout.contiguous()
-        C, K = shapes[0][3], r.shape[0]
-        det = roi_align_deterministic(C, ph, pw, sampling)
-        gfs = [(torch.empty if det else torch.zeros)(s, dtype=torch.float32, device=g.device) for s in shapes]
-        n = len(gfs)
-        ws = _ws(_lib.load().mx_roi_align_bwd_workspace(K, ph, pw, sampling) if det else 0, g.device)
-        ptrs = (ctypes.c_void_p * n)(*[f.data_ptr() for f in gfs])
-        Hs = (ctypes.c_int64 * n)(*[s[1] for s in shapes])
-        Ws = (ctypes.c_int64 * n)(*[s[2] for s in shapes])
-        sc = (ctypes.c_float * n)(*scales)
-        call("mx_multiscale_roi_align_bwd", _p(g), _dtype_code(g), ptrs, shapes[0][0], Hs, Ws, sc, n, C, _p(r),
-             _p(levels), K, ph, pw, sampling, int(det), _p(ws), ws.numel(), _stream())
+        gfs = multiscale_roi_align_backward(gout, r, levels, shapes, scales, ph, pw, sampling)
         return (None, None, None, None, None, None) + tuple(x.to(dt) for x in gfs)
+
+
+def multiscale_roi_align_backward(gout, rois, levels, shapes, scales, ph=7, pw=7, sampling=2):
+    """torchvision _roi_align_backward over the pyramid: grad_out [K,ph,pw,C] -> f32 NHWC gradients of
+    the level maps `shapes` (deterministic gather when the shape allows it, else atomics)."""
+    g = gout.contiguous()
+    C, K = shapes[0][3], rois.shape[0]
+    det = roi_align_deterministic(C, ph, pw, sampling)
+    gfs = [(torch.empty if det else torch.zeros)(s, dtype=torch.float32, device=g.device) for s in shapes]
+    n = len(gfs)
+    ws = _ws(_lib.load().mx_roi_align_bwd_workspace(K, ph, pw, sampling) if det else 0, g.device)
+    ptrs = (ctypes.c_void_p * n)(*[f.data_ptr() for f in gfs])
+    Hs = (ctypes.c_int64 * n)(*[s[1] for s in shapes])
+    Ws = (ctypes.c_int64 * n)(*[s[2] for s in shapes])
+    sc = (ctypes.c_float * n)(*scales)
+    call("mx_multiscale_roi_align_bwd", _p(g), _dtype_code(g), ptrs, shapes[0][0], Hs, Ws, sc, n, C, _p(rois),
+         _p(levels), K, ph, pw, sampling, int(det), _p(ws), ws.numel(), _stream())
+    return gfs
 
 
 def multiscale_roi_align(feats, rois, scales, k_min, output_size=(7, 7), sampling_ratio=2):

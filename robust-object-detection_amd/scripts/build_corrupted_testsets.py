@@ -8,16 +8,19 @@ same order: YOLO first, then COCO, variants and images in the reference's glob o
 np.random stream seeded with 42 hands every Test_Noise image the reference's noise field. The pixel
 work runs on the device (mx_det.augment: noise add/clip/truncate, cv2.filter2D motion blur, INTER_AREA
 down + INTER_LINEAR up; bit-exact against the reference's apply_noise golden and the OpenCV
-restatements in oracle/). Decode / JPEG encode stay on the host (PIL / libjpeg; cv2.imwrite's default
-quality 95). Images are corrupted in their BGR view, as cv2.imread hands them to the reference.
+restatements in oracle/). Each source JPEG is decoded on the device (mx_det.jpeg: host entropy decode,
+device IDCT / upsampling / colour, bit-identical to cv2.imread's libjpeg-turbo decode, in BGR like
+cv2.imread; PIL decodes the formats it does not handle), corrupted there, and copied back once for the
+JPEG encode (PIL / libjpeg-turbo, cv2.imwrite's default quality 95).
 """
 import shutil
 from pathlib import Path
 
 import numpy as np
+import torch
 from PIL import Image
 
-from mx_det import augment
+from mx_det import augment, jpeg, ops
 
 YOLO_SRC = Path("data/processed/visdrone_yolo6")
 COCO_SRC = Path("data/processed/visdrone_coco6")
@@ -40,25 +43,47 @@ def ensure_dir(p):
 
 
 def corrupt(img_bgr, variant):
-    """One variant of build_corrupted_testsets.py:140-150 on a BGR uint8 image (device ops)."""
-    if variant == "Test_Noise":
-        return augment.apply_noise(img_bgr, NOISE_SIGMA)
+    """One variant of build_corrupted_testsets.py:140-150 on a BGR uint8 image, a device tensor
+    [H, W, 3] (returned on the device) or a numpy array (returned as numpy)."""
+    if not torch.is_tensor(img_bgr):
+        if variant == "Test_Noise":
+            return augment.apply_noise(img_bgr, NOISE_SIGMA)
+        if variant == "Test_Blur":
+            return augment.apply_motion_blur(img_bgr, BLUR_KERNEL, BLUR_ANGLE_DEG)
+        if variant == "Test_LowRes":
+            return augment.apply_lowres(img_bgr, DOWNSCALE_FACTOR)
+        return img_bgr
+    x = img_bgr[None]
+    if variant == "Test_Noise":  # the reference's numpy stream, added / clipped / truncated on the device
+        noise = np.random.normal(0, NOISE_SIGMA, tuple(img_bgr.shape)).astype(np.float32)
+        return ops.corrupt_u8(x, [ops.CORRUPT_NOISE], noise=torch.from_numpy(noise).to(x.device))[0]
     if variant == "Test_Blur":
-        return augment.apply_motion_blur(img_bgr, BLUR_KERNEL, BLUR_ANGLE_DEG)
+        taps = augment.kernel_taps(augment.motion_blur_kernel(BLUR_KERNEL, BLUR_ANGLE_DEG))
+        return ops.filter2d_u8(x, taps)[0]
     if variant == "Test_LowRes":
-        return augment.apply_lowres(img_bgr, DOWNSCALE_FACTOR)
+        return ops.corrupt_u8(x, [ops.CORRUPT_LOWRES], factor=float(DOWNSCALE_FACTOR))[0]
     return img_bgr
 
 
 def _read_bgr(path):
+    """cv2.imread(path) on the device: BGR uint8 [H, W, 3]; None for unreadable files (skipped, like
+    cv2.imread's None)."""
+    dev = torch.device("cuda", torch.cuda.current_device())
     try:
-        with Image.open(path) as im:
-            return np.ascontiguousarray(np.asarray(im.convert("RGB"))[..., ::-1])
+        data = Path(path).read_bytes()
+        try:
+            return jpeg.decode(data, dev, bgr=True)
+        except (jpeg.JpegUnsupported, ValueError):
+            with Image.open(path) as im:
+                rgb = np.ascontiguousarray(np.asarray(im.convert("RGB"))[..., ::-1])
+            return torch.from_numpy(rgb).to(dev)
     except OSError:
-        return None  # cv2.imread returns None for unreadable files: skipped
+        return None
 
 
 def _write_bgr(path, img_bgr):
+    if torch.is_tensor(img_bgr):
+        img_bgr = img_bgr.cpu().numpy()
     Image.fromarray(np.ascontiguousarray(img_bgr[..., ::-1])).save(path, quality=95)
 
 

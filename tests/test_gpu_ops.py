@@ -519,6 +519,44 @@ def test_sampler_draw_via_level_topk(dev):
     assert not torch.equal(pm2[1], pm[1])  # 128 of 700 positives redrawn
 
 
+def test_sampler_picks_equal_topk_on_same_keys_and_are_uniform(dev):
+    """The level_topk draw picks exactly the candidates torch.topk(largest=False) picks on the same
+    injected keys (the k smallest keys: randperm[:k] semantics), and over 400 fresh draws every
+    candidate is picked with frequency k / #candidates (+-5 sigma), non-candidates never: no bias
+    from filler-key ties or index order."""
+    from mx_det.backend import HipBackend
+    from mx_det.frcnn import BalancedPositiveNegativeSampler
+    torch.manual_seed(4)
+    L = 2100
+    lab = torch.full((2, L), -1, dtype=torch.int64)
+    lab[0, :700] = 1
+    lab[0, 700:1900] = 0
+    lab[1, torch.randperm(L)[:300]] = 1
+    lab[1, torch.randperm(L)[:900]] = 0
+    lab = lab.to(dev)
+    s = BalancedPositiveNegativeSampler(512, 0.25)
+    g = torch.Generator().manual_seed(11)
+    keys = torch.rand(lab.shape, generator=g).to(dev)
+    s.rand = lambda shape, device: keys
+    pm, nm = s(lab, HipBackend())
+    pt, nt = s(lab, None)
+    assert torch.equal(pm, pt) and torch.equal(nm, nt)
+    s.rand = None
+    cnt = torch.zeros(lab.shape, device=dev)
+    n = 400
+    for _ in range(n):
+        p, _ = s(lab, HipBackend())
+        cnt += p
+    pos = lab >= 1
+    for r in range(2):
+        c = int(pos[r].sum())
+        k = min(128, c)
+        f = cnt[r][pos[r]] / n
+        sd = (k / c * (1 - k / c) / n) ** 0.5
+        assert (f - k / c).abs().max().item() < 5 * sd + 1e-6, (r, f.min().item(), f.max().item(), k / c)
+        assert cnt[r][~pos[r]].sum().item() == 0
+
+
 @pytest.mark.parametrize("k,angle", [(9, 0), (9, 45), (9, 90), (7, 30), (11, 135), (5, -20)])
 def test_motion_blur_any_angle(dev, k, angle):
     """apply_motion_blur at any kernel size / angle (augmentations.py:21-38): the device filter2D on

@@ -37,7 +37,7 @@ def test_build_corrupted_testsets(dev, tmp_path, monkeypatch):
     orig = b._write_bgr
 
     def spy(path, img):  # keep the pre-encode pixels
-        written[str(path)] = img.copy()
+        written[str(path)] = img.cpu().numpy() if hasattr(img, "cpu") else img.copy()
         orig(path, img)
     monkeypatch.setattr(b, "_write_bgr", spy)
     b.main(tmp_path / "src/yolo6", tmp_path / "src/coco6", tmp_path / "out")
