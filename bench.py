@@ -105,9 +105,10 @@ TRAFFIC_FILE = os.environ.get("MX_TRAFFIC_FILE", os.path.join(ROOT, "profiles", 
 # kernels of one op: outer list = the op's sequential kernels (summed), inner = alternative template
 # instances of one kernel (launch-weighted mean)
 KIND_KERNELS = {"x3_wgrad": [["mx::conv_wgrad_x3_kernel"], ["mx::wgrad_reduce_kernel"]],
-                "x3_fwd128": [["mx::conv_x3_kernel<128, 0", "mx::conv_x3_kernel<64, 0"]],
-                "x3_fwd64": [["mx::conv_x3_kernel<64, 0"]],
-                "x3_dgrad": [["mx::conv_x3_kernel<128, 1", "mx::conv_x3_kernel<64, 1"]],
+                "x3_fwd128": [["mx::conv_x3_buf_kernel<128, 0", "mx::conv_x3_kernel<128, 0"]],
+                "x3_fwd64": [["mx::conv_x3_buf_kernel<64, 0", "mx::conv_x3_kernel<64, 0"]],
+                "x3_dgrad": [["mx::conv_x3_buf_kernel<128, 1", "mx::conv_x3_buf_kernel<64, 1",
+                              "mx::conv_x3_kernel<128, 1", "mx::conv_x3_kernel<64, 1"]],
                 "wgrad": [["mx::conv_wgrad_buf_kernel"], ["mx::wgrad_reduce_kernel"]],
                 "fwd128": [["mx::conv_igemm_buf_kernel<128, 0", "mx::conv_igemm_buf_kernel<256, 0"]],
                 "dgrad": [["mx::conv_igemm_buf_kernel<128, 1", "mx::conv_igemm_buf_kernel<256, 1",
