@@ -704,6 +704,40 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_pipe_kernel(ConvP p) {
 // epilogue as the pipe kernel.
 static constexpr uint32_t kOOB = 0x80000000u;
 
+// Wave-uniform K position (tap row cr, tap column cq, channel chunk cc) of the buffer kernels' next
+// K-tile, advanced in value form: both K-tile orders computed branch-free and selected. A branchy
+// update (`if (++cq == S) ...` / `else if ((cc += BKT) == IC) ...`) let the compiler merge the two
+// branches' stores into one store through a selected address, which kept the counters in scratch
+// memory (a scratch load plus a vmcnt drain per K-tile, i.e. a wait for the ring's own LDS-DMA) and
+// made the B operand's soffset look divergent (a readfirstlane waterfall loop around every load).
+struct KPos {
+  int cc, cr, cq;
+  __device__ __forceinline__ void init(int korder, int kb, int R, int S, int IC, int bkt) {
+    const int RS = R * S;
+    const int ctap = korder ? kb % RS : kb * bkt / IC;
+    cc = korder ? kb / RS * bkt : kb * bkt - ctap * IC;
+    cr = ctap / S;
+    cq = ctap - cr * S;
+  }
+  __device__ __forceinline__ void advance(int korder, int R, int S, int IC, int bkt) {
+    // korder 1 (channel-major): q, then r, then the channel chunk
+    const int q1 = cq + 1;
+    const int wq = q1 == S ? 1 : 0;
+    const int r1 = cr + wq;
+    const int wr = (wq && r1 == R) ? 1 : 0;
+    const int a_cq = wq ? 0 : q1, a_cr = wr ? 0 : r1, a_cc = cc + (wr ? bkt : 0);
+    // korder 0 (tap-major): the channel chunk, then q, then r
+    const int c1 = cc + bkt;
+    const int wc = c1 == IC ? 1 : 0;
+    const int q0 = cq + wc;
+    const int wq0 = (wc && q0 == S) ? 1 : 0;
+    const int b_cc = wc ? 0 : c1, b_cq = wq0 ? 0 : q0, b_cr = cr + wq0;
+    cc = korder ? a_cc : b_cc;
+    cr = korder ? a_cr : b_cr;
+    cq = korder ? a_cq : b_cq;
+  }
+};
+
 template <int BN, int MODE, int STAGES, int OCC, int BMT = BM>
 __global__ void __launch_bounds__(NT, OCC) conv_igemm_buf_kernel(ConvP p) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
@@ -765,21 +799,17 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_buf_kernel(ConvP p) {
   const int64_t kbeg = (int64_t)split * p.kt_per_split;
   const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
   // wave-uniform K position of the next tile to issue: tap (r, q), channel c (p.korder: K-tile order)
-  int cc, cr, cq;
-  {
-    const int RS = R * S, kb = (int)kbeg;
-    const int ctap = p.korder ? kb % RS : kb * BKT / IC;
-    cc = p.korder ? kb / RS * BKT : kb * BKT - ctap * IC;
-    cr = ctap / S;
-    cq = ctap - cr * S;
-  }
+  const int korder = __builtin_amdgcn_readfirstlane(p.korder);
+  KPos kp;
+  kp.init(korder, (int)kbeg, R, S, IC, BKT);
   auto issue = [&](int buf) {
     char* A = smem + buf * STAGE;
     char* B = A + A_BYTES;
+    const int cr = kp.cr, cq = kp.cq, cc = kp.cc;
     const int rr = MODE == 0 ? cr : R - 1 - cr, qq = MODE == 0 ? cq : S - 1 - cq;
     const uint32_t a_soff = (uint32_t)(((rr * IW + qq) * IC + cc) * 2);
     const int tap = cr * S + cq;
-    const uint32_t b_soff = (uint32_t)((tap * IC + cc) * 2);
+    const uint32_t b_soff = (uint32_t)__builtin_amdgcn_readfirstlane((int)((tap * IC + cc) * 2));
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       // the whole offset in voffset (the origin may be negative; the tap offset brings it in range)
@@ -790,15 +820,7 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_buf_kernel(ConvP p) {
     for (int i = 0; i < BI; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (LDS_AS void*)(B + (wave * (BN / 4) + i * RPI) * RB), 16, b_voff[i],
                                                b_soff, 0, 0);
-    if (p.korder) {
-      if (++cq == S) {
-        cq = 0;
-        if (++cr == R) { cr = 0; cc += BKT; }
-      }
-    } else if ((cc += BKT) == IC) {
-      cc = 0;
-      if (++cq == S) { cq = 0; ++cr; }
-    }
+    kp.advance(korder, R, S, IC, BKT);
   };
   f32x4 acc[TI][TJ];
 #pragma unroll
@@ -1655,21 +1677,17 @@ __global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
   const int64_t kbeg = (int64_t)split * p.kt_per_split;
   const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
   // wave-uniform K position of the next tile to issue: tap (cr, cq), channel cc
-  int cc, cr, cq;
-  {
-    const int RS = R * S, kb = (int)kbeg;
-    const int ctap = p.korder ? kb % RS : kb * 32 / IC;
-    cc = p.korder ? kb / RS * 32 : kb * 32 - ctap * IC;
-    cr = ctap / S;
-    cq = ctap - cr * S;
-  }
+  const int korder = __builtin_amdgcn_readfirstlane(p.korder);
+  KPos kp;
+  kp.init(korder, (int)kbeg, R, S, IC, 32);
   auto issue = [&](int buf) {
     char* A = smem + buf * STAGE;
     char* B = A + 2 * AH;
+    const int cr = kp.cr, cq = kp.cq, cc = kp.cc;
     const int rr = MODE == 0 ? cr : R - 1 - cr, qq = MODE == 0 ? cq : S - 1 - cq;
     const uint32_t a_soff = (uint32_t)(((rr * IW + qq) * IC + cc) * 4);
     const int tap = cr * S + cq;
-    const uint32_t b_soff = (uint32_t)((tap * IC + cc) * 2);
+    const uint32_t b_soff = (uint32_t)__builtin_amdgcn_readfirstlane((int)((tap * IC + cc) * 2));
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const bool ok = (a_mask[i] >> tap) & 1ull;
@@ -1684,15 +1702,7 @@ __global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(bhrsrc, (LDS_AS void*)dst, 16, b_voff[i], b_soff, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(blrsrc, (LDS_AS void*)(dst + BP), 16, b_voff[i], b_soff, 0, 0);
     }
-    if (p.korder) {
-      if (++cq == S) {
-        cq = 0;
-        if (++cr == R) { cr = 0; cc += 32; }
-      }
-    } else if ((cc += 32) == IC) {
-      cc = 0;
-      if (++cq == S) { cq = 0; ++cr; }
-    }
+    kp.advance(korder, R, S, IC, 32);
   };
   f32x4 acc[TI][TJ];
 #pragma unroll
@@ -1801,50 +1811,54 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
   const int cc = col_ok ? (int)(col - (int64_t)tap * p.C) : 0;
   const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
   const bool k_ok = (k0 + ch * 8) < p.K;
-  const int OW = (int)p.OW, OH = (int)p.OH, H = (int)p.H, W = (int)p.W;
-  int px_n[2], px_oh[2], px_ow[2];
-  int64_t px_i[2];
+  const int OW = (int)p.OW, OH = (int)p.OH, H = (int)p.H, W = (int)p.W, C = (int)p.C;
+  // operands read through buffer descriptors with 32-bit byte offsets (mx_conv2d_wgrad_x3 checks
+  // that both fit): an invalid row (past the split, a padding tap, a column / channel past the
+  // matrix) gets an out-of-range offset and the hardware returns zeros -- no 64-bit address math,
+  // no divergent branches around the loads
+  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, (int)(p.P * p.K * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)(p.N * p.H * p.W * p.C * 4), 0x00020000);
+  // per-tile pixel step PXT = dn images + dh rows + dw columns of the output grid (wave-uniform)
+  const int dw = PXT % OW, dh = (PXT / OW) % OH, dn = PXT / (OW * OH);
+  const int ihb = -p.pad_h + r, iwb = -p.pad_w + s;
+  int px_n[2], px_oh[2], px_ow[2], px_i[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    px_i[i] = pbeg + (tid >> 4) + 16 * i;
-    const int64_t t = px_i[i] / OW;
-    px_ow[i] = (int)(px_i[i] - t * OW);
+    const int64_t pi = pbeg + (tid >> 4) + 16 * i;
+    px_i[i] = (int)pi;
+    const int64_t t = pi / OW;
+    px_ow[i] = (int)(pi - t * OW);
     px_oh[i] = (int)(t % OH);
     px_n[i] = (int)(t / OH);
   }
+  const int pend32 = (int)pend;
+  const uint32_t dy_col = (uint32_t)(k0 + ch * 8) * 4u;
   float4 rd[2][2], rx[2][2];
   auto load = [&]() {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int64_t px = px_i[i];
-      rd[i][0] = rd[i][1] = rx[i][0] = rx[i][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (px < pend) {
-        if (k_ok) {
-          const float* sp = dy + px * p.K + k0 + ch * 8;
-          rd[i][0] = *(const float4*)sp;
-          rd[i][1] = *(const float4*)(sp + 4);
-        }
-        if (col_ok) {
-          const int ih = px_oh[i] * p.st_h - p.pad_h + r, iw = px_ow[i] * p.st_w - p.pad_w + s;
-          if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
-            const float* sp = x + (((int64_t)px_n[i] * H + ih) * W + iw) * p.C + cc;
-            rx[i][0] = *(const float4*)sp;
-            rx[i][1] = *(const float4*)(sp + 4);
-          }
-        }
-      }
+      const bool pok = px_i[i] < pend32;
+      const uint32_t od = (pok && k_ok) ? __umul24((uint32_t)px_i[i], (uint32_t)(p.K * 4)) + dy_col : kOOB;
+      const int ih = __mul24(px_oh[i], p.st_h) + ihb, iw = __mul24(px_ow[i], p.st_w) + iwb;
+      const bool xok = pok && col_ok && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const uint32_t ox = xok ? (uint32_t)__mul24(__mul24(px_n[i], H) + ih, W) + (uint32_t)iw : 0u;
+      const uint32_t oxb = xok ? __umul24(ox, (uint32_t)(C * 4)) + (uint32_t)cc * 4u : kOOB;
+      rd[i][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(dyr, od, 0, 0));
+      rd[i][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(dyr, od + 16u, 0, 0));
+      rx[i][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, oxb, 0, 0));
+      rx[i][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, oxb + 16u, 0, 0));
+      // advance PXT pixels: branch-free carries (ow < OW, oh < OH stay invariant)
       px_i[i] += PXT;
-      px_ow[i] += PXT;
-      if (px_ow[i] >= OW) {  // small maps wrap several rows per tile
-        const int q = px_ow[i] / OW;
-        px_ow[i] -= q * OW;
-        px_oh[i] += q;
-        if (px_oh[i] >= OH) {
-          const int q2 = px_oh[i] / OH;
-          px_oh[i] -= q2 * OH;
-          px_n[i] += q2;
-        }
-      }
+      int ow = px_ow[i] + dw;
+      const int c1 = ow >= OW ? 1 : 0;
+      ow -= c1 * OW;
+      int oh = px_oh[i] + dh + c1;
+      const int c2 = oh >= OH ? 1 : 0;
+      oh -= c2 * OH;
+      px_ow[i] = ow;
+      px_oh[i] = oh;
+      px_n[i] += dn + c2;
     }
   };
   auto store = [&](int buf) {
@@ -3051,6 +3065,9 @@ extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const
     p.slab = (float*)ws;
   }
   MX_CHECK_ARG(g.tiles * g.splits < (1ll << 31), "conv wgrad x3: grid too large");
+  MX_CHECK_ARG(p.P * p.K * 4 < (1ll << 31) && p.N * p.H * p.W * p.C * 4 < (1ll << 31) && p.P + 64 < (1ll << 23) &&
+                   p.N * p.H * p.W < (1ll << 23) && p.K * 4 < (1ll << 24) && p.C * 4 < (1ll << 24),
+               "conv wgrad x3: dy / x must each stay below 2 GiB and 8M pixels (32-bit / 24-bit offset math)");
   conv_wgrad_x3_kernel<<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);
   MX_LAUNCH_CHECK();
   if (g.splits > 1) {
