@@ -550,15 +550,45 @@ ARITH_TEXT = {"f32": "f32 activations/gradients/BN/RoIAlign; conv products as bf
               "bf16": "bf16 activations and conv operands, f32 accumulate"}
 
 
+# VisDrone-DET frame sizes (H, W) as the reference's loader yields them; GeneralizedRCNNTransform
+# resizes each to min 800 / max 1333 (padded 768x1344 or 800x1088 batches)
+VISDRONE_FRAMES = [(1080, 1920), (1080, 1920), (1500, 2000), (1500, 2000), (765, 1360), (1080, 1920),
+                   (540, 960), (1050, 1400)]
+
+
+def visdrone_main(args, world, rank, dev):
+    """The configs[1] train step on the data path the reference actually runs: uint8 frames of VisDrone's
+    native sizes, each resized on the device (mx_resize_normalize_pad: normalize + bilinear +
+    zero-padded batch in one launch, boxes rescaled), two padded batch shapes alternating."""
+    from mx_det.data import synth_image, synth_target
+    imgs, tg = [], []
+    for k, (H, W) in enumerate(VISDRONE_FRAMES):
+        imgs.append(torch.from_numpy(synth_image(rank * 64 + k, H, W)).to(dev))
+        tg.append({kk: v.to(dev) for kk, v in synth_target(rank * 64 + k, H, W).items()})
+    prec = "f32" if args.precision == "both" else args.precision
+    model, ddp, opt, dt = _time_precision(prec, args, world, rank, dev, imgs, tg)
+    rec = {"metric": "images/sec FRCNN-R50-FPN train, VisDrone frame sizes (resize on device) bs=2/GPU",
+           "value": round(2 * args.steps * world / dt, 3), "unit": "images/sec", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": DTYPE_TEXT[prec],
+           "data": "synthetic uint8 frames at VisDrone sizes " + ", ".join(f"{w}x{h}" for h, w in VISDRONE_FRAMES),
+           "config": {"workload": "configs[1] train step, native-size frames", "global_batch": 2 * world,
+                      "per_gpu_batch": 2, "parallelism": f"dp{world}"}}
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--augment", action="store_true")
-    ap.add_argument("--mode", choices=("train", "eval", "eval_restored", "unet_train", "jpeg"), default="train",
+    ap.add_argument("--mode", choices=("train", "eval", "eval_restored", "unet_train", "jpeg", "visdrone"),
+                    default="train",
                     help="train (default): the headline train step; eval: per-image eval forward "
-                         "(eval_all.py); eval_restored: on-device U-Net restore + eval (eval_restored.py)")
+                         "(eval_all.py); eval_restored: on-device U-Net restore + eval (eval_restored.py); "
+                         "visdrone: the train step on uint8 frames of VisDrone's native sizes (resize on device)")
     ap.add_argument("--precision", choices=("both", "f32", "bf16"), default="both",
                     help="both (default): the f32 headline, then the bf16 variant in the same JSON line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -590,6 +620,8 @@ def main():
             unet_train_main(args, world, rank, dev)
         elif args.mode == "jpeg":
             jpeg_main(args, world, rank, dev)
+        elif args.mode == "visdrone":
+            visdrone_main(args, world, rank, dev)
         else:
             eval_main(args, world, rank, dev, imgs)
         if world > 1:

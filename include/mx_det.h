@@ -158,6 +158,18 @@ int mx_normalize_pad(const uint8_t* img, int64_t B, int64_t H, int64_t W, const 
                      const float* std3_host, int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out,
                      mx_stream_t stream);
 
+/* GeneralizedRCNNTransform for images that need a resize (torchvision 0.20.1 transform.py
+ * _resize_image_and_masks -> F.interpolate(scale_factor, bilinear, align_corners=False,
+ * recompute_scale_factor=True), reached via the model call at train_frcnn_baseline.py:171 and
+ * eval_all.py:111 on VisDrone frames of any size), fused with ToDtype(scale=True), normalize and
+ * batch_images' zero padding: B u8 HWC images imgs[b] [Hs[b], Ws[b], 3] (device pointers; sizes host
+ * arrays) -> NHWC [B, Hp, Wp, Cp] dtype; image b fills its [nhs[b], nws[b]] corner (nh = floor(H*s),
+ * computed by the caller as torch does), the rest is zero. Bilinear weights as torch's CUDA kernel:
+ * scale = (float)H / nh, src = scale * (dst + 0.5) - 0.5 (clamped at 0). */
+int mx_resize_normalize_pad(const uint8_t* const* imgs, const int64_t* Hs, const int64_t* Ws, const int64_t* nhs,
+                            const int64_t* nws, int64_t B, const float* mean3_host, const float* std3_host,
+                            int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out, mx_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Convolution (implicit GEMM on MFMA, bf16 in / f32 accumulate), NHWC x KRSC.
  * Replaces the cuDNN convs of ResNet-50 / FPN / RPN head / box head (torchvision model reached at

@@ -168,6 +168,12 @@ class CpuBackend:
     def anchors_level(self, size, ratios, gh, gw, sh, sw, device):
         return torch.from_numpy(orc.anchors_level(size, ratios, gh, gw, sh, sw))
 
+    def resize_normalize_pad_u8(self, images_u8, out_sizes, padded_hw):
+        out = torch.zeros((len(images_u8), padded_hw[0], padded_hw[1], 3))
+        for i, (im, (nh, nw)) in enumerate(zip(images_u8, out_sizes)):
+            out[i, :nh, :nw] = torch.from_numpy(orc.resize_normalize(im.cpu().numpy(), nh, nw))
+        return out
+
     def normalize_pad_u8(self, images_u8, padded_hw):
         x = images_u8.float().mul_(1.0 / 255)
         mean = torch.tensor((0.485, 0.456, 0.406))

@@ -793,3 +793,37 @@ int orc_jpeg_reconstruct(const int16_t* coefs, const mx_jpeg_info* info, unsigne
   for (int c = 0; c < 3; ++c) { free(plane[c]); free(up[c]); }
   return 0;
 }
+
+/* GeneralizedRCNNTransform resize (torchvision 0.20.1 transform.py _resize_image_and_masks ->
+ * F.interpolate(scale_factor=s, mode="bilinear", align_corners=False, recompute_scale_factor=True)),
+ * on the ToDtype(scale=True) + normalize output, restating torch's CUDA upsample_bilinear2d_out_frame
+ * (aten/src/ATen/native/cuda/UpSampleBilinear2d.cu; area_pixel_compute_scale / _source_index in
+ * UpSample.h) in float, one rounding per op: scale = (float)in / out; src = scale * (dst + 0.5) - 0.5,
+ * clamped at 0; i0 = (int)src; i1 = i0 + (i0 < in - 1); l1 = src - i0; l0 = 1 - l1;
+ * v = h0 * (w0 * v00 + w1 * v01) + h1 * (w0 * v10 + w1 * v11). img u8 [H][W][3] -> out f32 [nh][nw][3]. */
+static inline float rz_src(float scale, int64_t dst) {
+  float s = scale * ((float)dst + 0.5f) - 0.5f;
+  return s < 0.f ? 0.f : s;
+}
+void orc_resize_normalize(const uint8_t* img, int64_t H, int64_t W, int64_t nh, int64_t nw, const float* mean,
+                          const float* stdv, float* out) {
+  const float sh = (float)H / (float)nh, sw = (float)W / (float)nw;
+  const float inv = (float)(1.0 / 255.0);
+  for (int64_t y = 0; y < nh; ++y) {
+    const float hr = rz_src(sh, y);
+    const int64_t h0 = (int64_t)hr, h1 = h0 + (h0 < H - 1 ? 1 : 0);
+    const float hl1 = hr - (float)h0, hl0 = 1.f - hl1;
+    for (int64_t x = 0; x < nw; ++x) {
+      const float wr = rz_src(sw, x);
+      const int64_t w0 = (int64_t)wr, w1 = w0 + (w0 < W - 1 ? 1 : 0);
+      const float wl1 = wr - (float)w0, wl0 = 1.f - wl1;
+      for (int c = 0; c < 3; ++c) {
+        const float a = ((float)img[(h0 * W + w0) * 3 + c] * inv - mean[c]) / stdv[c];
+        const float b = ((float)img[(h0 * W + w1) * 3 + c] * inv - mean[c]) / stdv[c];
+        const float d0 = ((float)img[(h1 * W + w0) * 3 + c] * inv - mean[c]) / stdv[c];
+        const float d1 = ((float)img[(h1 * W + w1) * 3 + c] * inv - mean[c]) / stdv[c];
+        out[(y * nw + x) * 3 + c] = hl0 * (wl0 * a + wl1 * b) + hl1 * (wl0 * d0 + wl1 * d1);
+      }
+    }
+  }
+}

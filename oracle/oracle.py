@@ -165,6 +165,18 @@ def resize_linear_u8(img, dh, dw):
     return out
 
 
+def resize_normalize(img, nh, nw, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)):
+    """GeneralizedRCNNTransform normalize + bilinear resize (torch CUDA upsample_bilinear2d arithmetic,
+    mx_oracle.c orc_resize_normalize): u8 HWC [H,W,3] -> f32 [nh,nw,3]."""
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W, _ = img.shape
+    out = np.empty((nh, nw, 3), np.float32)
+    m = np.asarray(mean, np.float32)
+    s = np.asarray(std, np.float32)
+    lib().orc_resize_normalize(_p(img, U8), i64(H), i64(W), i64(nh), i64(nw), _p(m, F32), _p(s, F32), _p(out, F32))
+    return out
+
+
 def reflect_pad_u8(img, ph, pw):
     img = np.ascontiguousarray(img, np.uint8)
     H, W, C = img.shape

@@ -228,6 +228,62 @@ __global__ void normalize_pad_kernel(const uint8_t* __restrict__ img, int64_t B,
   for (int64_t c = 0; c < Cp; ++c) io<T>::st(o + c, c < 3 ? v[c] : 0.f);
 }
 
+
+// GeneralizedRCNNTransform for images that need a resize (torchvision 0.20.1 transform.py
+// _resize_image_and_masks: F.interpolate(scale_factor=s, mode="bilinear", align_corners=False,
+// recompute_scale_factor=True)), fused with ToDtype(scale=True), normalize and batch_images' zero
+// padding. The interpolation restates torch's upsample_bilinear2d_out_frame (CUDA: the reference
+// trains on the GPU) in float: scale = (float)in / out, src = scale * (dst + 0.5) - 0.5 clamped at 0,
+// i0 = (int)src, i1 = i0 + (i0 < in - 1), l1 = src - i0, l0 = 1 - l1,
+// v = h0 * (w0 * v00 + w1 * v01) + h1 * (w0 * v10 + w1 * v11) over the normalised source values.
+// Built -ffp-contract=off: every product and sum rounds once, in this order.
+struct RzImg {
+  const uint8_t* src;  // [H][W][3]
+  int H, W, nh, nw;
+  float sh, sw;        // (float)H / nh, (float)W / nw
+};
+static constexpr int RZ_MAX = 16;
+struct RzBatch {
+  RzImg im[RZ_MAX];
+};
+
+__device__ __forceinline__ float rz_src(float scale, int dst) {
+  const float s = scale * ((float)dst + 0.5f) - 0.5f;
+  return s < 0.f ? 0.f : s;
+}
+
+template <typename T>
+__global__ void resize_normalize_pad_kernel(RzBatch bt, int64_t B, float3 mean, float3 stdv, int64_t Hp, int64_t Wp,
+                                            int64_t Cp, T* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * Hp * Wp) return;
+  const int x = (int)(i % Wp), y = (int)((i / Wp) % Hp), b = (int)(i / (Wp * Hp));
+  const RzImg& m = bt.im[b];
+  float v[3] = {0.f, 0.f, 0.f};
+  if (y < m.nh && x < m.nw) {
+    const float hr = rz_src(m.sh, y), wr = rz_src(m.sw, x);
+    const int h0 = (int)hr, w0 = (int)wr;
+    const int h1 = h0 + (h0 < m.H - 1 ? 1 : 0), w1 = w0 + (w0 < m.W - 1 ? 1 : 0);
+    const float hl1 = hr - (float)h0, wl1 = wr - (float)w0;
+    const float hl0 = 1.f - hl1, wl0 = 1.f - wl1;
+    const uint8_t* p00 = m.src + ((int64_t)h0 * m.W + w0) * 3;
+    const uint8_t* p01 = m.src + ((int64_t)h0 * m.W + w1) * 3;
+    const uint8_t* p10 = m.src + ((int64_t)h1 * m.W + w0) * 3;
+    const uint8_t* p11 = m.src + ((int64_t)h1 * m.W + w1) * 3;
+    const float inv = (float)(1.0 / 255.0);
+    const float mu[3] = {mean.x, mean.y, mean.z}, sd[3] = {stdv.x, stdv.y, stdv.z};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float a = ((float)p00[c] * inv - mu[c]) / sd[c];
+      const float bb = ((float)p01[c] * inv - mu[c]) / sd[c];
+      const float cc = ((float)p10[c] * inv - mu[c]) / sd[c];
+      const float d = ((float)p11[c] * inv - mu[c]) / sd[c];
+      v[c] = hl0 * (wl0 * a + wl1 * bb) + hl1 * (wl0 * cc + wl1 * d);
+    }
+  }
+  T* o = out + i * Cp;
+  for (int64_t c = 0; c < Cp; ++c) io<T>::st(o + c, c < 3 ? v[c] : 0.f);
+}
 }  // namespace mx
 
 using namespace mx;
@@ -346,6 +402,45 @@ extern "C" int mx_normalize_pad(const uint8_t* img, int64_t B, int64_t H, int64_
     normalize_pad_kernel<uint16_t><<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(img, B, H, W, m, sd, Hp, Wp,
                                                                                              Cp, (uint16_t*)out);
   MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" int mx_resize_normalize_pad(const uint8_t* const* imgs, const int64_t* Hs, const int64_t* Ws,
+                                       const int64_t* nhs, const int64_t* nws, int64_t B, const float* mean,
+                                       const float* stdv, int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out,
+                                       mx_stream_t stream) {
+  MX_CHECK_ARG(B >= 0 && Cp >= 3 && Hp >= 0 && Wp >= 0, "mx_resize_normalize_pad: bad batch / padded shape");
+  MX_CHECK_ARG(dtype == MX_F32 || dtype == MX_BF16, "mx_resize_normalize_pad: bad dtype %d", dtype);
+  const float3 m = make_float3(mean[0], mean[1], mean[2]), sd = make_float3(stdv[0], stdv[1], stdv[2]);
+  for (int64_t b0 = 0; b0 < B; b0 += RZ_MAX) {
+    const int64_t nb = std::min<int64_t>(RZ_MAX, B - b0);
+    RzBatch bt{};
+    for (int64_t j = 0; j < nb; ++j) {
+      const int64_t b = b0 + j;
+      MX_CHECK_ARG(imgs[b] != nullptr && Hs[b] >= 1 && Ws[b] >= 1 && nhs[b] >= 1 && nws[b] >= 1,
+                   "mx_resize_normalize_pad: image %lld: bad source / output size", (long long)b);
+      MX_CHECK_ARG(nhs[b] <= Hp && nws[b] <= Wp, "mx_resize_normalize_pad: image %lld larger than the padded batch",
+                   (long long)b);
+      MX_CHECK_ARG(Hs[b] < (1 << 24) && Ws[b] < (1 << 24) && nhs[b] < (1 << 24) && nws[b] < (1 << 24),
+                   "mx_resize_normalize_pad: image too large");
+      RzImg& r = bt.im[j];
+      r.src = imgs[b];
+      r.H = (int)Hs[b]; r.W = (int)Ws[b]; r.nh = (int)nhs[b]; r.nw = (int)nws[b];
+      r.sh = (float)r.H / (float)r.nh;  // area_pixel_compute_scale: static_cast<float>(in) / out
+      r.sw = (float)r.W / (float)r.nw;
+    }
+    const int64_t n = nb * Hp * Wp;
+    if (n == 0) continue;
+    const size_t es = dtype == MX_F32 ? 4 : 2;
+    char* o = (char*)out + (size_t)b0 * Hp * Wp * Cp * es;
+    if (dtype == MX_F32)
+      resize_normalize_pad_kernel<float><<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(bt, nb, m, sd, Hp, Wp, Cp,
+                                                                                                   (float*)o);
+    else
+      resize_normalize_pad_kernel<uint16_t><<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(bt, nb, m, sd, Hp, Wp,
+                                                                                                      Cp, (uint16_t*)o);
+    MX_LAUNCH_CHECK();
+  }
   return MX_OK;
 }
 

@@ -67,6 +67,8 @@ _SIGS = {
     "mx_corrupt_u8": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_f, c_u64, c_vp, c_d, c_vp, c_vp, c_vp]),
     "mx_filter2d_u8": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp]),
     "mx_normalize_pad": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp]),
+    "mx_resize_normalize_pad": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_int,
+                                        c_vp, c_vp]),
     "mx_conv_mblocks": (c_i64, [ctypes.POINTER(ConvShape)]),
     "mx_conv2d_fwd": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "mx_conv2d_dgrad": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp]),

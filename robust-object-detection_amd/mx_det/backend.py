@@ -169,6 +169,10 @@ class HipBackend:
     def normalize_pad_u8(self, images_u8, padded_hw):
         return ops.normalize_pad(images_u8, padded_hw, channels=self.stem_channels, dtype=self.act_dtype)
 
+    def resize_normalize_pad_u8(self, images_u8, out_sizes, padded_hw):
+        return ops.resize_normalize_pad(images_u8, out_sizes, padded_hw, channels=self.stem_channels,
+                                        dtype=self.act_dtype)
+
 
 _default = {}
 

@@ -630,6 +630,22 @@ class GeneralizedRCNNTransform(nn.Module):
             if self._scale(H, W) == 1.0:
                 sizes = [(H, W)] * B
                 return ImageList(be.normalize_pad_u8(images, self._padded(sizes)), sizes), targets
+        u8 = isinstance(images, torch.Tensor) and images.dtype == torch.uint8 and images.dim() == 4 or \
+            isinstance(images, (list, tuple)) and len(images) and images[0].dtype == torch.uint8 and \
+            all(im.dim() == 3 and im.shape[2] == 3 for im in images)
+        if u8 and hasattr(be, "resize_normalize_pad_u8") and images[0].is_cuda == (getattr(be, "name", "") == "hip"):
+            # uint8 HWC frames of any size (VisDrone): one fused resize + normalize + pad launch
+            sizes, orig = [], []
+            for im in images:
+                h, w = int(im.shape[0]), int(im.shape[1])
+                s = self._scale(h, w)
+                # F.interpolate(recompute_scale_factor=True): out = floor(in * s) in double precision
+                sizes.append((h, w) if s == 1.0 else (int(math.floor(h * s)), int(math.floor(w * s))))
+                orig.append((h, w))
+            batch = be.resize_normalize_pad_u8(list(images), sizes, self._padded(sizes))
+            if targets is not None:
+                targets = [self._resize_boxes(dict(t), o, n) for t, o, n in zip(targets, orig, sizes)]
+            return ImageList(batch, sizes), targets
         if len(images) and images[0].dtype == torch.uint8:  # HWC uint8 -> ToDtype(float32, scale=True)
             images = [im.permute(2, 0, 1).float().mul_(1.0 / 255) for im in images]
         dev = images[0].device
@@ -645,14 +661,7 @@ class GeneralizedRCNNTransform(nn.Module):
                                    recompute_scale_factor=True, align_corners=False)[0]
             nh, nw = im.shape[-2:]
             if targets is not None:
-                t = dict(targets[i])
-                if (nh, nw) != (h, w):
-                    rh = torch.tensor(nh, dtype=torch.float32) / torch.tensor(h, dtype=torch.float32)
-                    rw = torch.tensor(nw, dtype=torch.float32) / torch.tensor(w, dtype=torch.float32)
-                    b = t["boxes"]
-                    t["boxes"] = torch.stack((b[:, 0] * rw.to(b.device), b[:, 1] * rh.to(b.device),
-                                              b[:, 2] * rw.to(b.device), b[:, 3] * rh.to(b.device)), 1)
-                new_targets.append(t)
+                new_targets.append(self._resize_boxes(dict(targets[i]), (h, w), (nh, nw)))
             out.append(im)
             sizes.append((int(nh), int(nw)))
         Hp, Wp = self._padded(sizes)
@@ -660,6 +669,18 @@ class GeneralizedRCNNTransform(nn.Module):
         for i, im in enumerate(out):
             batch[i, : im.shape[1], : im.shape[2], :3] = im.permute(1, 2, 0).to(be.act_dtype)
         return ImageList(batch, sizes), (new_targets if targets is not None else None)
+
+    @staticmethod
+    def _resize_boxes(t, orig, new):
+        """torchvision transform.py resize_boxes: ratios as float32 tensors new / orig per axis."""
+        (h, w), (nh, nw) = orig, new
+        if (nh, nw) != (h, w):
+            rh = torch.tensor(nh, dtype=torch.float32) / torch.tensor(h, dtype=torch.float32)
+            rw = torch.tensor(nw, dtype=torch.float32) / torch.tensor(w, dtype=torch.float32)
+            b = t["boxes"]
+            t["boxes"] = torch.stack((b[:, 0] * rw.to(b.device), b[:, 1] * rh.to(b.device),
+                                      b[:, 2] * rw.to(b.device), b[:, 3] * rh.to(b.device)), 1)
+        return t
 
     def postprocess(self, result, image_sizes, original_sizes):
         for i, (pred, s, o) in enumerate(zip(result, image_sizes, original_sizes)):

@@ -367,6 +367,31 @@ def normalize_pad(images, padded_hw, channels=3, dtype=torch.float32, mean=IMAGE
     return out
 
 
+def resize_normalize_pad(images, out_sizes, padded_hw, channels=3, dtype=torch.float32, mean=IMAGE_MEAN,
+                         std=IMAGE_STD):
+    """GeneralizedRCNNTransform with a resize (torchvision transform.py _resize_image_and_masks: bilinear,
+    align_corners=False, recompute_scale_factor=True) fused with ToDtype(scale=True), normalize and the
+    zero-padded batch: uint8 HWC device images of any sizes -> NHWC [B,Hp,Wp,channels]; image b fills
+    its out_sizes[b] = (nh, nw) corner."""
+    B = len(images)
+    _check(B == len(out_sizes), "resize_normalize_pad: one output size per image")
+    xs = [im.contiguous() for im in images]
+    for x in xs:
+        _dev(x)
+        _check(x.dtype == torch.uint8 and x.dim() == 3 and x.shape[2] == 3, "images must be uint8 [H,W,3]")
+    Hp, Wp = padded_hw
+    dev = xs[0].device if B else torch.device("cuda")
+    out = torch.empty((B, Hp, Wp, channels), dtype=dtype, device=dev)
+    if B:
+        arr = lambda t, v: (t * B)(*v)  # noqa: E731
+        call("mx_resize_normalize_pad", arr(ctypes.c_void_p, [x.data_ptr() for x in xs]),
+             arr(ctypes.c_int64, [x.shape[0] for x in xs]), arr(ctypes.c_int64, [x.shape[1] for x in xs]),
+             arr(ctypes.c_int64, [int(s[0]) for s in out_sizes]), arr(ctypes.c_int64, [int(s[1]) for s in out_sizes]),
+             B, (ctypes.c_float * 3)(*mean), (ctypes.c_float * 3)(*std), Hp, Wp, channels, _dtype_code(out), _p(out),
+             _stream())
+    return out
+
+
 # ---------------------------------------------------------------------------------------------
 class _RPNLoss(torch.autograd.Function):
     """RegionProposalNetwork.compute_loss fused (mx_rpn_loss_fwd / _bwd): two launches instead of the
