@@ -127,13 +127,15 @@ static constexpr int SROWS = 64;
 
 // WR = wave-rows of the block (2: 4 waves in 2x2, 4: 8 waves in 4x2; HALVES == WR then stages one
 // wave-row per pass).
-template <int BN, int HALVES = 1, int BMT = BM, typename TA = uint16_t, int WR = 2>
-__device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT / (16 * WR)][BN / 32], char* smem,
-                                              int64_t m0, int64_t n0, int64_t mt, int wm, int wn, int lane, int tid,
-                                              int split) {
-  constexpr int WN = BN / 2, TJ = WN / 16, WM = BMT / WR, TI = WM / 16, NT = 128 * WR;
+// WC = wave-columns (2: wave tiles of BN/2 columns; 1: each wave spans all BN columns).
+template <int BN, int HALVES = 1, int BMT = BM, typename TA = uint16_t, int WR = 2, int WC = 2>
+__device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT / (16 * WR)][BN / (16 * WC)],
+                                              char* smem, int64_t m0, int64_t n0, int64_t mt, int wm, int wn,
+                                              int lane, int tid, int split) {
+  constexpr int WN = BN / WC, TJ = WN / 16, WM = BMT / WR, TI = WM / 16, NT = 64 * WR * WC;
   constexpr int PR = BMT / HALVES;  // rows staged per pass
-  static_assert(WR == 2 || (HALVES == WR && WM == SROWS), "8-wave tiles: one 64-row wave-row per pass");
+  static_assert(HALVES == 1 ? WR == 2 : (HALVES == WR && (WM == SROWS || (SROWS % WM == 0 && WR * WM >= SROWS))),
+                "multi-pass staging: one wave-row of 64, 32 or 16 rows per pass");
   (void)mt;
   if (p.slab) {  // split-K partial: f32 tile to the slab, epilogue deferred to the reduce kernel
     constexpr int LD = BN + 4;
@@ -188,19 +190,22 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
     }
     __syncthreads();
     const int64_t srow = m0 / SROWS;
+    constexpr int WPS = WM >= SROWS ? 1 : SROWS / WM;  // wave-rows per 64-row statistics row
     for (int c = tid; c < BN; c += NT) {
       int64_t col = n0 + c;
       if (col >= p.Ncol) continue;
-      if (WM == SROWS) {  // each wave-row is one statistics row
-        for (int w = 0; w < WR; ++w)
-          if (m0 + w * WM < p.M) {
-            p.stats[(srow + w) * p.Ncol + col] = red[(w * 2) * BN + c];
-            p.stats[(p.mblocks + srow + w) * p.Ncol + col] = red[(w * 2 + 1) * BN + c];
+#pragma unroll
+      for (int g = 0; g < WR / WPS; ++g)
+        if (m0 + g * SROWS < p.M) {
+          float sg = red[(g * WPS * 2) * BN + c], qg = red[(g * WPS * 2 + 1) * BN + c];
+#pragma unroll
+          for (int w = g * WPS + 1; w < (g + 1) * WPS; ++w) {
+            sg += red[(w * 2) * BN + c];
+            qg += red[(w * 2 + 1) * BN + c];
           }
-      } else {  // BMT == 64: both wave-rows form one statistics row
-        p.stats[srow * p.Ncol + col] = red[c] + red[2 * BN + c];
-        p.stats[(p.mblocks + srow) * p.Ncol + col] = red[BN + c] + red[3 * BN + c];
-      }
+          p.stats[(srow + g) * p.Ncol + col] = sg;
+          p.stats[(p.mblocks + srow + g) * p.Ncol + col] = qg;
+        }
     }
     __syncthreads();
   }
@@ -1615,19 +1620,22 @@ __device__ __forceinline__ int x3_swz(int row) {
 // conv_igemm_buf_kernel); the pre-split weight planes land the same way. A fragments are split into
 // hi / lo in registers at read time (6 VALU per pair, ~2 per MFMA, hidden in the MFMA issue gaps),
 // so no register staging or ds_write sits on the critical path and STAGES-1 K-tiles stay in flight.
-template <int BN, int MODE, int STAGES, int OCC, int BMT, int WR = 2>
-__global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
+// WC = 1 (wide wave tiles: WR waves stacked along M, each spanning all BN columns): every A row is
+// split by exactly one wave (WC = 2 splits each row in both wave-columns), half the split VALU per
+// MFMA, at twice the B fragment reads per wave.
+template <int BN, int MODE, int STAGES, int OCC, int BMT, int WR = 2, int WC = 2>
+__global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p) {
 #if defined(__HIP_DEVICE_COMPILE__)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int RB = 64, RPI = 16;  // bytes per LDS row; rows landed per wave instruction
-  constexpr int NW = 2 * WR;  // waves: WR rows x 2 columns of wave tiles
+  constexpr int NW = WC * WR;  // waves: WR rows x WC columns of wave tiles
   constexpr int AR = BMT / NW, AI = AR / RPI, BR = BN / NW, BI = BR / RPI;
   constexpr int LOADS = 2 * AI + 2 * BI;  // vmem instructions per K-tile per wave
   constexpr int AH = BMT * RB, BP = BN * RB, STAGE = 2 * AH + 2 * BP;
-  constexpr int WN = BN / 2, TJ = WN / 16, WM = BMT / WR, TI = WM / 16;
+  constexpr int WN = BN / WC, TJ = WN / 16, WM = BMT / WR, TI = WM / 16;
   static_assert(AI >= 1 && BI >= 1 && STAGES >= 2, "tile shape");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WC, wn = wave % WC;
   const int64_t ntiles_n = (p.Ncol + BN - 1) / BN;
   const int64_t gid = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
   const int split = (int)(gid % p.splits);
@@ -1680,6 +1688,9 @@ __global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
   const int korder = __builtin_amdgcn_readfirstlane(p.korder);
   KPos kp;
   kp.init(korder, (int)kbeg, R, S, IC, 32);
+  // timing-only diagnostics (mx_conv_set_debug bits): 1 no epilogue, 2 no hi/lo split (raw bits),
+  // 4 no B LDS-DMA, 8 no A LDS-DMA -- wrong results, prices each part of the main loop
+  const int dbg = __builtin_amdgcn_readfirstlane(p.dbg_skip_epi);
   auto issue = [&](int buf) {
     char* A = smem + buf * STAGE;
     char* B = A + 2 * AH;
@@ -1688,6 +1699,7 @@ __global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
     const uint32_t a_soff = (uint32_t)(((rr * IW + qq) * IC + cc) * 4);
     const int tap = cr * S + cq;
     const uint32_t b_soff = (uint32_t)__builtin_amdgcn_readfirstlane((int)((tap * IC + cc) * 2));
+    if (!(dbg & 8)) {
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const bool ok = (a_mask[i] >> tap) & 1ull;
@@ -1696,11 +1708,14 @@ __global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (LDS_AS void*)dst, 16, ok ? v : kOOB, 0, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (LDS_AS void*)(dst + AH), 16, ok ? v + 64u : kOOB, 0, 0, 0);
     }
+    }
+    if (!(dbg & 4)) {
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       char* dst = B + (wave * BR + i * RPI) * RB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(bhrsrc, (LDS_AS void*)dst, 16, b_voff[i], b_soff, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(blrsrc, (LDS_AS void*)(dst + BP), 16, b_voff[i], b_soff, 0, 0);
+    }
     }
     kp.advance(korder, R, S, IC, 32);
   };
@@ -1722,7 +1737,7 @@ __global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
     const char* Ag = A + (g >> 1) * AH;
     const char* Bh = A + 2 * AH;
     const char* Bl = Bh + BP;
-    constexpr int TJB = TJ > 4 ? 1 : TJ;  // B fragments held at once (wide wave tiles: one column at a time)
+    constexpr int TJB = (TJ > 4 && WC == 2) ? 1 : TJ;  // B fragments held at once
     bf16x8 ah[TI], al[TI], bh[TJB], bl[TJB];
     auto loadb = [&](int j, int slot) {
       const int row = wn * WN + j * 16 + (lane & 15);
@@ -1741,7 +1756,12 @@ __global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
       const float4 u = *(const float4*)(Ag + row * RB + ((q0 ^ f) << 4));
       const float4 w = *(const float4*)(Ag + row * RB + (((q0 + 1) ^ f) << 4));
       uint4 h, l;
-      split8(u, w, h, l);
+      if (dbg & 2) {
+        h = __builtin_bit_cast(uint4, u);
+        l = __builtin_bit_cast(uint4, w);
+      } else {
+        split8(u, w, h, l);
+      }
       ah[i] = __builtin_bit_cast(bf16x8, h);
       al[i] = __builtin_bit_cast(bf16x8, l);
     }
@@ -1767,7 +1787,7 @@ __global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
       }
     }
   }
-  if (p.dbg_skip_epi) {  // keep every accumulator live, store nothing
+  if (dbg & 1) {  // keep every accumulator live, store nothing
     float sum = 0.f;
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -1777,7 +1797,7 @@ __global__ void __launch_bounds__(128 * WR, OCC) conv_x3_buf_kernel(ConvP p) {
     return;
   }
   __syncthreads();
-  conv_epilogue<BN, WR, BMT, float, WR>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
+  conv_epilogue<BN, WR, BMT, float, WR, WC>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
 #endif
 }
 
@@ -2195,11 +2215,12 @@ extern "C" int mx_conv_set_tile(int bmt, int bn) {
 
 static int g_buf_stages = 0;  // mx_conv_set_stages: LDS ring depth of the 64x128 / 128x128 buffer kernels
 extern "C" int mx_conv_set_stages(int n) {
-  MX_CHECK_ARG(n == 0 || n == 3 || n == 4 || n == 6, "mx_conv_set_stages: 0 (auto), 3, 4 or 6 (x3 kernels: 3 = alternative ring)");
+  MX_CHECK_ARG(n == 0 || n == 3 || n == 4 || n == 6,
+               "mx_conv_set_stages: 0 (auto), 3, 4 or 6 (x3 kernels: 3 alternative ring, 4 2x2 wave tiles)");
   g_buf_stages = n;
   return MX_OK;
 }
-static int g_conv_debug = 0;  // mx_conv_set_debug: 1 = skip the bf16x3 buffer kernels' epilogue (timing only)
+static int g_conv_debug = 0;  // mx_conv_set_debug: bf16x3 buffer kernel timing-only bits (see the kernel)
 extern "C" int mx_conv_set_debug(int v) {
   g_conv_debug = v;
   return MX_OK;
@@ -2868,11 +2889,11 @@ static void launch_x3(const ConvP& p, int64_t blocks, hipStream_t st) {
   conv_x3_kernel<BN, MODE, BMT><<<(unsigned)blocks, NT, std::max(ring, epi), st>>>(p);
 }
 
-template <int BN, int MODE, int STAGES, int OCC, int BMT, int WR = 2>
+template <int BN, int MODE, int STAGES, int OCC, int BMT, int WR = 2, int WC = 2>
 static void launch_x3_buf(const ConvP& p, int64_t blocks, hipStream_t st) {
   const size_t ring = (size_t)STAGES * 2 * (BMT + BN) * 64;
   const size_t epi = (size_t)(BMT / WR) * (BN + 4) * 4;
-  conv_x3_buf_kernel<BN, MODE, STAGES, OCC, BMT, WR><<<(unsigned)blocks, 128 * WR, std::max(ring, epi), st>>>(p);
+  conv_x3_buf_kernel<BN, MODE, STAGES, OCC, BMT, WR, WC><<<(unsigned)blocks, 64 * WR * WC, std::max(ring, epi), st>>>(p);
 }
 
 template <int MODE>
@@ -2904,15 +2925,22 @@ static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, h
   if (buf) {
     // ring depth x blocks per CU; mx_conv_set_stages(3) picks the alternative of each tile shape
     const bool alt = g_buf_stages == 3;
+    // 128 x 128 / 64 x 128 tiles as 4 wide wave tiles (32 x 128 / 16 x 128: each A row split by one
+    // wave) unless mx_conv_set_stages(4) asks for the 2 x 2 layout of 64 x 64 / 32 x 64 wave tiles
+    const bool wide = g_buf_stages == 0, wide64 = wide;
     p.korder = g_conv_korder;
     p.dbg_skip_epi = g_conv_debug;
+    if (g_conv_loader == 2) p.src_elems = 0;  // timing-only diagnostics (mx_conv_set_loader)
+    if (g_conv_loader == 3) p.wt_elems = 0;
     if (g.bmt == 256) {
       alt ? launch_x3_buf<128, MODE, 2, 1, 256, 4>(p, blocks, st) : launch_x3_buf<128, MODE, 3, 1, 256, 4>(p, blocks, st);
     } else if (g.bmt == 64) {
       if (g.bn == 64) alt ? launch_x3_buf<64, MODE, 4, 2, 64>(p, blocks, st) : launch_x3_buf<64, MODE, 3, 3, 64>(p, blocks, st);
+      else if (wide64) launch_x3_buf<128, MODE, 3, 2, 64, 4, 1>(p, blocks, st);
       else alt ? launch_x3_buf<128, MODE, 2, 3, 64>(p, blocks, st) : launch_x3_buf<128, MODE, 3, 2, 64>(p, blocks, st);
     } else {
       if (g.bn == 64) alt ? launch_x3_buf<64, MODE, 2, 3, 128>(p, blocks, st) : launch_x3_buf<64, MODE, 3, 2, 128>(p, blocks, st);
+      else if (wide) launch_x3_buf<128, MODE, 2, 2, 128, 4, 1>(p, blocks, st);
       else alt ? launch_x3_buf<128, MODE, 3, 1, 128>(p, blocks, st) : launch_x3_buf<128, MODE, 2, 2, 128>(p, blocks, st);
     }
   } else if (g.bmt == 64) {
