@@ -134,8 +134,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
                                               int lane, int tid, int split) {
   constexpr int WN = BN / WC, TJ = WN / 16, WM = BMT / WR, TI = WM / 16, NT = 64 * WR * WC;
   constexpr int PR = BMT / HALVES;  // rows staged per pass
-  static_assert(HALVES == 1 ? WR == 2 : (HALVES == WR && (WM == SROWS || (SROWS % WM == 0 && WR * WM >= SROWS))),
-                "multi-pass staging: one wave-row of 64, 32 or 16 rows per pass");
+  static_assert(HALVES == 1 || HALVES == WR, "staging: the whole tile at once, or one wave-row per pass");
+  static_assert(WM == SROWS || (SROWS % WM == 0 && WR * WM >= SROWS), "wave-rows of 64, 32 or 16 rows");
   (void)mt;
   if (p.slab) {  // split-K partial: f32 tile to the slab, epilogue deferred to the reduce kernel
     constexpr int LD = BN + 4;
@@ -1797,7 +1797,9 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
     return;
   }
   __syncthreads();
-  conv_epilogue<BN, WR, BMT, float, WR, WC>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
+  // wide tiles stage the whole f32 tile at once (one barrier, every wave storing); 8-wave 2x2 tiles
+  // stage one wave-row per pass (their whole tile would not fit beside a second block)
+  conv_epilogue<BN, (WC == 1 ? 1 : WR), BMT, float, WR, WC>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
 #endif
 }
 
@@ -2892,7 +2894,7 @@ static void launch_x3(const ConvP& p, int64_t blocks, hipStream_t st) {
 template <int BN, int MODE, int STAGES, int OCC, int BMT, int WR = 2, int WC = 2>
 static void launch_x3_buf(const ConvP& p, int64_t blocks, hipStream_t st) {
   const size_t ring = (size_t)STAGES * 2 * (BMT + BN) * 64;
-  const size_t epi = (size_t)(BMT / WR) * (BN + 4) * 4;
+  const size_t epi = (size_t)(WC == 1 ? BMT : BMT / WR) * (BN + 4) * 4;
   conv_x3_buf_kernel<BN, MODE, STAGES, OCC, BMT, WR, WC><<<(unsigned)blocks, 64 * WR * WC, std::max(ring, epi), st>>>(p);
 }
 
