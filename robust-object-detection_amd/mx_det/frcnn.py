@@ -15,6 +15,7 @@ RoIHeads with MultiScaleRoIAlign(['0'..'3'], 7, 2), FastRCNNConvFCHead (4 conv+B
 BoxCoder weights (1,1,1,1) / (10,10,5,5), Matcher / BalancedPositiveNegativeSampler settings.
 """
 import math
+import os
 from collections import OrderedDict
 
 import torch
@@ -187,16 +188,59 @@ class RPNHead(nn.Module):
                 if m.bias is not None:
                     nn.init.constant_(m.bias, 0)
 
+    @staticmethod
+    def canvas_layout(hws):
+        """Top-left corners of the levels hws[0..] on one zero canvas: the first at (0, 0), the rest in
+        rows below it, every level framed by at least one zero row / column (the 3x3 convs' padding)."""
+        H0, W0 = hws[0]
+        pos, y, x, rowh, Wc = [(0, 0)], H0 + 1, 0, 0, W0
+        for h, w in hws[1:]:
+            if x > 0 and x + w > W0:
+                y, x, rowh = y + rowh + 1, 0, 0
+            pos.append((y, x))
+            Wc = max(Wc, x + w)
+            x, rowh = x + w + 1, max(rowh, h)
+        return pos, y + rowh, Wc
+
+    def _run(self, t, be, w, b, mask=None):
+        for ci, c in enumerate(self.conv):
+            t = c(t, be)
+            if mask is not None and ci + 1 < len(self.conv):
+                t = t * mask  # zero frame between levels: the next 3x3 conv reads it as padding
+        return be.conv(t, w, b, (1, 1), (0, 0), ACT_NONE, out_dtype=torch.float32)  # [N,H,W,A*5]
+
     def forward(self, feats, be):
+        """torchvision RPNHead.forward per level. The small levels (all but the first, P3..P6) run as ONE
+        conv chain over a zero canvas that holds each level framed by zero rows / columns: a 3x3 conv
+        with padding 1 then sees exactly each level's own neighbourhood, and the ReLU outputs on the
+        frame are zeroed before the next 3x3 conv -- the same arithmetic per output element as per-level
+        convs, in 2 launches per conv instead of 5 (the P4..P6 maps are too small to fill the GPU alone).
+        The shared weights' gradients then sum the canvas pixels in one wgrad (frame pixels add exact
+        zeros). MX_RPN_CANVAS=0 runs every level separately."""
         A = self.cls_logits.weight.shape[0]
         w = torch.cat([self.cls_logits.weight, self.bbox_pred.weight])
         b = torch.cat([self.cls_logits.bias, self.bbox_pred.bias])
+        L = len(feats)
+        outs = [None] * L
+        canvas = L >= 3 and os.environ.get("MX_RPN_CANVAS", "1") != "0"
+        for i in ([0] if canvas else range(L)):
+            outs[i] = self._run(feats[i], be, w, b)
+        if canvas:
+            small = list(range(1, L))
+            hws = [tuple(feats[i].shape[1:3]) for i in small]
+            pos, Hc, Wc = self.canvas_layout(hws)
+            f0 = feats[small[0]]
+            N, C = f0.shape[0], f0.shape[3]
+            cv = f0.new_zeros((N, Hc, Wc, C))
+            mask = f0.new_zeros((1, Hc, Wc, 1))
+            for i, (h, wd), (y, x) in zip(small, hws, pos):
+                cv[:, y:y + h, x:x + wd] = feats[i]
+                mask[:, y:y + h, x:x + wd] = 1
+            o = self._run(cv, be, w, b, mask)
+            for i, (h, wd), (y, x) in zip(small, hws, pos):
+                outs[i] = o[:, y:y + h, x:x + wd]
         logits, deltas = [], []
-        for f in feats:
-            t = f
-            for c in self.conv:
-                t = c(t, be)
-            o = be.conv(t, w, b, (1, 1), (0, 0), ACT_NONE, out_dtype=torch.float32)  # [N,H,W,A*5]
+        for o in outs:
             N = o.shape[0]
             logits.append(o[..., :A].reshape(N, -1))          # (h, w, a) order = torchvision permute
             deltas.append(o[..., A:].reshape(N, -1, 4))

@@ -67,3 +67,49 @@ def test_degenerate_boxes_rejected():
     img = [torch.rand(3, 64, 64)]
     with pytest.raises(ValueError):
         m(img, [{"boxes": torch.tensor([[10., 10., 5., 20.]]), "labels": torch.tensor([1])}])
+
+
+def _rpn_head_run(be, feats, canvas, monkeypatch, seed=0):
+    from mx_det import frcnn
+    monkeypatch.setenv("MX_RPN_CANVAS", "1" if canvas else "0")
+    torch.manual_seed(seed)
+    head = frcnn.RPNHead(256, 3)
+    for p in head.parameters():
+        torch.nn.init.normal_(p, std=0.05)
+    head = head.to(feats[0].device)
+    fs = [f.clone().requires_grad_(True) for f in feats]
+    logits, deltas = head(fs, be)
+    loss = sum((lg * (i + 1)).sin().sum() + dl.cos().sum() for i, (lg, dl) in enumerate(zip(logits, deltas)))
+    loss.backward()
+    return ([t.detach() for t in logits + deltas], [f.grad for f in fs],
+            {k: p.grad for k, p in head.named_parameters()})
+
+
+def test_rpn_head_canvas_equals_per_level(monkeypatch):
+    """RPNHead's small levels run as one conv chain over a zero-framed canvas (frcnn.RPNHead.forward):
+    logits / deltas, feature gradients and the shared weights' gradients equal the per-level chains
+    (torchvision's loop), here on the CPU restatement backend."""
+    torch.manual_seed(1)
+    hw = [(40, 52), (20, 26), (10, 13), (5, 7), (3, 4)]
+    feats = [torch.randn(2, h, w, 256) for h, w in hw]
+    a = _rpn_head_run(CpuBackend(), feats, True, monkeypatch)
+    b = _rpn_head_run(CpuBackend(), feats, False, monkeypatch)
+    for x, y in zip(a[0] + a[1], b[0] + b[1]):
+        assert x.shape == y.shape
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-4)
+    for k in a[2]:
+        torch.testing.assert_close(a[2][k], b[2][k], rtol=1e-4, atol=1e-3)
+
+
+def test_rpn_canvas_layout_frames_levels():
+    from mx_det import frcnn
+    hws = [(100, 168), (50, 84), (25, 42), (13, 21)]
+    pos, Hc, Wc = frcnn.RPNHead.canvas_layout(hws)
+    occ = torch.zeros(Hc + 2, Wc + 2, dtype=torch.int32)
+    for (h, w), (y, x) in zip(hws, pos):
+        assert y + h <= Hc and x + w <= Wc
+        occ[y:y + h + 2, x:x + w + 2] += 1  # the level plus a one-pixel frame on every side
+    inner = torch.zeros_like(occ)
+    for (h, w), (y, x) in zip(hws, pos):
+        inner[y + 1:y + h + 1, x + 1:x + w + 1] += 1
+    assert int((inner * (occ - 1)).sum()) == 0  # no level pixel lies in another level's frame
