@@ -2116,15 +2116,16 @@ __device__ __forceinline__ void pack_wt_tile(const PackP& p, int64_t t, uint16_t
   }
 }
 
-// tiles: [planes][nwk] wk tiles, then [planes][nwt] wt tiles (planes = 2 when split)
+// tiles: nwk wk tiles, then nwt wt tiles; a split job's block writes both planes of its tile, the
+// second staging re-reading the f32 region it has just read (L2-hot) instead of another block
+// fetching it from HBM again
 __device__ __forceinline__ void pack_tile(const PackP& p, int64_t t) {
   __shared__ uint16_t T[PACK_LDS];
   const int np = p.split ? 2 : 1;
-  if (t < np * p.nwk) {
-    pack_wk_tile(p, t % p.nwk, T, (int)(t / p.nwk));
-  } else {
-    t -= np * p.nwk;
-    pack_wt_tile(p, t % p.nwt, T, (int)(t / p.nwt));
+  for (int plane = 0; plane < np; ++plane) {
+    if (plane) __syncthreads();  // the previous plane's writes have read T
+    if (t < p.nwk) pack_wk_tile(p, t, T, plane);
+    else pack_wt_tile(p, t - p.nwk, T, plane);
   }
 }
 
@@ -2554,7 +2555,7 @@ extern "C" int mx_conv_pack_weight(const mx_conv_shape* s, const float* w, int64
   // wk covers Kout rows only; wt also covers the zero-padded output channels up to s->K
   MX_CHECK_ARG(pack_plan(p) == MX_OK, "conv pack: at most 196 taps");
   p.split = split ? 1 : 0;
-  const int64_t tiles = (p.nwk + p.nwt) * (split ? 2 : 1);
+  const int64_t tiles = p.nwk + p.nwt;
   MX_CHECK_ARG(tiles < (1ll << 31), "conv pack: too many tiles");
   pack_weight_kernel<<<(unsigned)tiles, 256, 0, (hipStream_t)stream>>>(p);
   MX_LAUNCH_CHECK();
@@ -2582,7 +2583,7 @@ static int make_pack(const mx_pack_desc& d, PackP& p, int64_t& tiles) {
     p.st_h = p.st_w = 1;
   }
   MX_CHECK_ARG(pack_plan(p) == MX_OK, "conv pack: at most 196 taps");
-  tiles = (p.nwk + p.nwt) * (p.split ? 2 : 1);
+  tiles = p.nwk + p.nwt;
   return MX_OK;
 }
 
