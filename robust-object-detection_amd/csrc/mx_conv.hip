@@ -1948,6 +1948,157 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
 #endif
 }
 
+// bf16x3 wgrad, wide block tile: 128 output channels x 256 (r,s,c) columns, 8 waves (2 x 4 wave tiles
+// of 64 x 64, the same MFMA inner loop). Per 32-pixel K-step a block stores 32 x (128 + 256) split
+// elements for 384 MFMAs: 0.75x the LDS stores and split VALU per MFMA of the 128 x 128 tile (whose
+// LDS store path prices ~25 % of the P2 wgrad), and dy is re-read for every 256 columns instead of
+// every 128. LDS: dy hi / lo [32][128] and x hi / lo as two [32][128] halves each, 256-B rows with the
+// swz_w swizzle -- 6 sub-planes of 8 KiB per stage, double-buffered (96 KiB, one block per CU).
+__global__ void __launch_bounds__(512, 1) conv_wgrad_x3w_kernel(WgP p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int PXT = 32, OPB = PXT * 256, STAGE = 6 * OPB;  // dy hi, dy lo, x hi 0/1, x lo 0/1
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int64_t ntn = (p.Ncol + 255) / 256;
+  const int64_t ntiles = ((p.K + 127) / 128) * ntn;
+  const int64_t work = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int64_t split = work / ntiles, tile = work % ntiles;
+  const int64_t mt = tile / ntn, nt = tile % ntn;
+  const int64_t k0 = mt * 128, c0 = nt * 256;
+  const int64_t pbeg = split * p.kchunk;
+  const int64_t pend = min<int64_t>(p.P, pbeg + p.kchunk);
+  if (pbeg >= pend) return;
+  const float* __restrict__ dy = (const float*)p.dy;
+  const float* __restrict__ x = (const float*)p.x;
+  // dy: one 8-channel chunk of one pixel row per thread; x: one 8-column chunk of two pixel rows
+  const int chd = tid & 15, rowd = tid >> 4;
+  const int chx = tid & 31, rowx = tid >> 5;
+  const bool k_ok = (k0 + chd * 8) < p.K;
+  const int64_t col = c0 + chx * 8;
+  const bool col_ok = col < p.Ncol;
+  const int tap = col_ok ? (int)(col / p.C) : 0;
+  const int cc = col_ok ? (int)(col - (int64_t)tap * p.C) : 0;
+  const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
+  const int OW = (int)p.OW, OH = (int)p.OH, H = (int)p.H, W = (int)p.W, C = (int)p.C;
+  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, (int)(p.P * p.K * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)(p.N * p.H * p.W * p.C * 4), 0x00020000);
+  const int dw = PXT % OW, dh = (PXT / OW) % OH, dn = PXT / (OW * OH);
+  const int ihb = -p.pad_h + r, iwb = -p.pad_w + s;
+  int pxd = (int)(pbeg + rowd);
+  int px_n[2], px_oh[2], px_ow[2], px_i[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int64_t pi = pbeg + rowx + 16 * i;
+    px_i[i] = (int)pi;
+    const int64_t t = pi / OW;
+    px_ow[i] = (int)(pi - t * OW);
+    px_oh[i] = (int)(t % OH);
+    px_n[i] = (int)(t / OH);
+  }
+  const int pend32 = (int)pend;
+  const uint32_t dy_col = (uint32_t)(k0 + chd * 8) * 4u;
+  float4 rd[2], rx[2][2];
+  auto load = [&]() {
+    {
+      const uint32_t od = (pxd < pend32 && k_ok) ? __umul24((uint32_t)pxd, (uint32_t)(p.K * 4)) + dy_col : kOOB;
+      rd[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(dyr, od, 0, 0));
+      rd[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(dyr, od + 16u, 0, 0));
+      pxd += PXT;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool pok = px_i[i] < pend32;
+      const int ih = __mul24(px_oh[i], p.st_h) + ihb, iw = __mul24(px_ow[i], p.st_w) + iwb;
+      const bool xok = pok && col_ok && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const uint32_t ox = xok ? (uint32_t)__mul24(__mul24(px_n[i], H) + ih, W) + (uint32_t)iw : 0u;
+      const uint32_t oxb = xok ? __umul24(ox, (uint32_t)(C * 4)) + (uint32_t)cc * 4u : kOOB;
+      rx[i][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, oxb, 0, 0));
+      rx[i][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, oxb + 16u, 0, 0));
+      px_i[i] += PXT;
+      int ow = px_ow[i] + dw;
+      const int c1 = ow >= OW ? 1 : 0;
+      ow -= c1 * OW;
+      int oh = px_oh[i] + dh + c1;
+      const int c2 = oh >= OH ? 1 : 0;
+      oh -= c2 * OH;
+      px_ow[i] = ow;
+      px_oh[i] = oh;
+      px_n[i] += dn + c2;
+    }
+  };
+  // x column chunk chx of 32: half chx >> 4 (sub-plane), chunk chx & 15 within the 256-B row
+  const int xh = chx >> 4, xc = chx & 15;
+  auto store = [&](int buf) {
+    char* D = smem + buf * STAGE;
+    uint4 h, l;
+    {
+      const int off = rowd * 256 + (swz_w(rowd, chd) << 4);
+      split8(rd[0], rd[1], h, l);
+      *(uint4*)(D + off) = h;
+      *(uint4*)(D + OPB + off) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = rowx + 16 * i;
+      const int off = row * 256 + (swz_w(row, xc) << 4);
+      split8(rx[i][0], rx[i][1], h, l);
+      *(uint4*)(D + (2 + xh) * OPB + off) = h;
+      *(uint4*)(D + (4 + xh) * OPB + off) = l;
+    }
+  };
+  auto tr_read = [&](const char* T, int prow0, int colbase) -> s16x4 {
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int row = prow0 + 8 * g + q;
+    const int colx = colbase + 4 * pp;
+    const int chunk = colx >> 3, within = (colx & 7) * 2;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(T + row * 256 + (swz_w(row, chunk) << 4) + within));
+  };
+  auto frag = [&](const char* T, int colbase) -> bf16x8 {
+    const s16x4 lo = tr_read(T, 0, colbase), hi = tr_read(T, 4, colbase);
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nk = (pend - pbeg + PXT - 1) / PXT;
+  load();
+  store(0);
+  __syncthreads();
+  const int xplane = wn >> 1, xcol = (wn & 1) * 64;
+  for (int64_t it = 0; it < nk; ++it) {
+    const int buf = (int)(it & 1);
+    if (it + 1 < nk) load();
+    const char* D = smem + buf * STAGE;
+    bf16x8 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ah[i] = frag(D, wm * 64 + i * 16);
+      al[i] = frag(D + OPB, wm * 64 + i * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bh[j] = frag(D + (2 + xplane) * OPB, xcol + j * 16);
+      bl[j] = frag(D + (4 + xplane) * OPB, xcol + j * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+    if (it + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+  wgrad_store(p, acc, k0, c0, wm, wn, lane, split);
+#endif
+}
+
 __global__ void transpose_w_kernel(const uint16_t* __restrict__ w, int64_t K, int64_t RS, int64_t C, uint16_t* __restrict__ wt) {
   // w[K][RS][C] -> wt[C][RS][K]
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2476,7 +2627,8 @@ extern "C" int mx_conv_get_variant(void) { return g_conv_variant; }
 // 3 (default) buffer descriptors (conv_wgrad_buf_kernel; maps under 32 output pixels take 0)
 static int g_wgrad_variant = 3;
 extern "C" int mx_conv_set_wgrad_variant(int v) {
-  MX_CHECK_ARG(v >= 0 && v <= 3, "mx_conv_set_wgrad_variant: 0 px32, 1 px64, 2 direct-to-LDS, 3 buffer descriptors");
+  MX_CHECK_ARG(v >= 0 && v <= 4, "mx_conv_set_wgrad_variant: 0 px32, 1 px64, 2 direct-to-LDS, 3 buffer descriptors, "
+                                "4 = 3 for bf16 / the 128 x 256 wide block for bf16x3");
   g_wgrad_variant = v;
   return MX_OK;
 }
@@ -2746,7 +2898,7 @@ static WGeo wgrad_geo(const mx_conv_shape* s) {
   WGeo g;
   const int64_t P = s->N * s->Ho * s->Wo, Ncol = s->R * s->S * s->C;
   g.tiles = cdiv(s->K, 128) * cdiv(Ncol, 128);
-  const int v = g_wgrad_variant;
+  const int v = g_wgrad_variant == 4 ? 3 : g_wgrad_variant;
   g.pxt = v == 2 ? BKG : (v == 1 ? 64 : BKW);
   // resident blocks per CU: px32 / buffer 3 (142 VGPRs), px64 / direct-to-LDS 2
   const int64_t slots = g_wgrad_target ? g_wgrad_target : (int64_t)num_cus() * ((v == 0 || v == 3) ? 3 : 2);
@@ -2818,7 +2970,7 @@ extern "C" int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, co
   }
   MX_CHECK_ARG(g.tiles < (1ll << 31) && g.splits < 65536, "conv wgrad: grid too large");
   dim3 grid((unsigned)g.tiles, (unsigned)g.splits);
-  int v = g_wgrad_variant;
+  int v = g_wgrad_variant == 4 ? 3 : g_wgrad_variant;
   // the buffer kernel walks each lane's pixels by (n, oh, ow) increments: maps of fewer than 32
   // output pixels (FC6 as a 7x7 conv on the RoI tile) would wrap many times per tile -> register kernel
   if (v == 3 && !(p.P * p.K * 2 < (1ll << 31) && s->N * s->H * s->W * s->C * 2 < (1ll << 31) &&
@@ -2967,12 +3119,16 @@ static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, h
   return MX_OK;
 }
 
+// wgrad x3 block shape: 0 = 128 x 128 (4 waves, 2 blocks per CU), 1 = 128 x 256 (8 waves, one block
+// per CU; mx_conv_set_wgrad_variant(4) -- a tuner candidate)
+static int wgrad_x3_wide() { return g_wgrad_variant == 4; }
 static WGeo wgrad_geo_x3(const mx_conv_shape* s) {
   WGeo g;
   const int64_t P = s->N * s->Ho * s->Wo, Ncol = s->R * s->S * s->C;
-  g.tiles = cdiv(s->K, 128) * cdiv(Ncol, 128);
+  const bool wide = wgrad_x3_wide();
+  g.tiles = cdiv(s->K, 128) * cdiv(Ncol, wide ? 256 : 128);
   g.pxt = 32;
-  const int64_t slots = g_wgrad_target ? g_wgrad_target : (int64_t)num_cus() * 2;
+  const int64_t slots = g_wgrad_target ? g_wgrad_target : (int64_t)num_cus() * (wide ? 1 : 2);
   int64_t splits = std::max<int64_t>(1, slots / g.tiles);
   const int64_t max_splits = std::max<int64_t>(1, P / (g.pxt * 4));
   splits = std::min(splits, max_splits);
@@ -3099,7 +3255,10 @@ extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const
   MX_CHECK_ARG(p.P * p.K * 4 < (1ll << 31) && p.N * p.H * p.W * p.C * 4 < (1ll << 31) && p.P + 64 < (1ll << 23) &&
                    p.N * p.H * p.W < (1ll << 23) && p.K * 4 < (1ll << 24) && p.C * 4 < (1ll << 24),
                "conv wgrad x3: dy / x must each stay below 2 GiB and 8M pixels (32-bit / 24-bit offset math)");
-  conv_wgrad_x3_kernel<<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);
+  if (wgrad_x3_wide())
+    conv_wgrad_x3w_kernel<<<(unsigned)(g.tiles * g.splits), 512, 2 * 6 * 32 * 256, st>>>(p);
+  else
+    conv_wgrad_x3_kernel<<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);
   MX_LAUNCH_CHECK();
   if (g.splits > 1) {
     MX_CHECK_ARG(Kout < 65536, "conv wgrad x3: too many output channels for the split reduce");
