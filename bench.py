@@ -104,7 +104,7 @@ def cpu_baseline(gpu_model, seconds_hint=30.0):
 TRAFFIC_FILE = os.environ.get("MX_TRAFFIC_FILE", os.path.join(ROOT, "profiles", "r02_traffic.json"))
 # kernels of one op: outer list = the op's sequential kernels (summed), inner = alternative template
 # instances of one kernel (launch-weighted mean)
-KIND_KERNELS = {"x3_wgrad": [["mx::conv_wgrad_x3_kernel"], ["mx::wgrad_reduce_kernel"]],
+KIND_KERNELS = {"x3_wgrad": [["mx::conv_wgrad_x3_kernel", "mx::conv_wgrad_x3w_kernel"], ["mx::wgrad_reduce_kernel"]],
                 "x3_fwd128": [["mx::conv_x3_buf_kernel<128, 0", "mx::conv_x3_kernel<128, 0"]],
                 "x3_fwd64": [["mx::conv_x3_buf_kernel<64, 0", "mx::conv_x3_kernel<64, 0"]],
                 "x3_dgrad": [["mx::conv_x3_buf_kernel<128, 1", "mx::conv_x3_buf_kernel<64, 1",
@@ -160,21 +160,26 @@ def conv_roofline(model, opt, imgs, tg, peak=X3_PEAK_TFLOPS, step_fn=None):
     dom = max(s, key=lambda k: s[k]["ms"])
     d = s[dom]
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+    traf = pmc_traffic(dom)
     allf = sum(v["flops"] for v in s.values())
     allms = sum(v["ms"] for v in s.values())
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom),
+            "frac": round(achieved / peak, 4), "traffic": traf,
             "traffic_unit": "MB per launch (HBM, rocprofv3 PMC, " + os.path.relpath(TRAFFIC_FILE, ROOT) + ")",
             "kernel": {"fwd128": "conv_igemm_buf_kernel<128|256,0,*> (+ conv_splitk_reduce_kernel)",
                        "fwd64": "conv_igemm_buf_kernel<64,0,*> (+ conv_splitk_reduce_kernel)",
                        "dgrad": "conv_igemm_buf_kernel<*,1,*> (+ conv_splitk_reduce_kernel)",
                        "wgrad": "conv_wgrad_buf_kernel (+ wgrad_reduce_kernel)",
-                       "x3_fwd128": "conv_x3_kernel<*,0,*> (+ conv_splitk_reduce_kernel<*,float>)",
-                       "x3_fwd64": "conv_x3_kernel<64,0,*> (+ conv_splitk_reduce_kernel<*,float>)",
-                       "x3_dgrad": "conv_x3_kernel<*,1,*> (+ conv_splitk_reduce_kernel<*,float>)",
-                       "x3_wgrad": "conv_wgrad_x3_kernel (+ wgrad_reduce_kernel)"}[dom],
+                       "x3_fwd128": "conv_x3_buf_kernel<*,0,*> (+ conv_splitk_reduce_kernel<*,float>)",
+                       "x3_fwd64": "conv_x3_buf_kernel<64,0,*> (+ conv_splitk_reduce_kernel<*,float>)",
+                       "x3_dgrad": "conv_x3_buf_kernel<*,1,*> (+ conv_splitk_reduce_kernel<*,float>)",
+                       "x3_wgrad": "conv_wgrad_x3_kernel / conv_wgrad_x3w_kernel (+ wgrad_reduce_kernel)"}[dom],
             "launches_per_step": d["launches"], "avg_launch_us": round(1000 * d["ms"] / d["launches"], 2),
             "gflop_per_launch": round(d["flops"] / d["launches"] / 1e9, 3),
+            # operands read once + output written once, mean over the kind's launches; traffic / this
+            # is the re-read factor (L2 misses beyond the algorithmic minimum)
+            "algorithmic_mb_per_launch": round(d["bytes"] / d["launches"] / 1e6, 2),
+            "traffic_ratio": (round(traf / (d["bytes"] / d["launches"] / 1e6), 2) if traf else None),
             "conv_stack": {"tflops": round(allf / (allms * 1e-3) / 1e12, 2), "gflop_per_step": round(allf / 1e9, 1),
                            "ms_per_step": round(allms, 2),
                            "by_kind": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),

@@ -54,20 +54,22 @@ class KernelTimer:
         e.record()
         return e
 
-    def stop(self, kind, flops, e0, tag=""):
+    def stop(self, kind, flops, e0, tag="", byts=0.0):
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        self.rec.append((kind, float(flops), e0, e1, tag))
+        self.rec.append((kind, float(flops), e0, e1, tag, float(byts)))
 
     def summary(self, by_tag=False):
-        """{kind: {launches, flops, ms}}; by_tag: keyed by (kind, shape tag) instead."""
+        """{kind: {launches, flops, ms, bytes}}; by_tag: keyed by (kind, shape tag) instead. bytes =
+        algorithmic HBM bytes of the convs (operands read once, output written once)."""
         torch.cuda.synchronize()
         out = {}
-        for kind, fl, a, b, tag in self.rec:
-            d = out.setdefault((kind, tag) if by_tag else kind, {"launches": 0, "flops": 0.0, "ms": 0.0})
+        for kind, fl, a, b, tag, by in self.rec:
+            d = out.setdefault((kind, tag) if by_tag else kind, {"launches": 0, "flops": 0.0, "ms": 0.0, "bytes": 0.0})
             d["launches"] += 1
             d["flops"] += fl
             d["ms"] += a.elapsed_time(b)
+            d["bytes"] += by
         return out
 
 
@@ -234,7 +236,8 @@ def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dty
     _tuned(key, _FD_CANDS_X3 if x3 else _FD_CANDS, _apply_fd, run, _FD_DEFAULT)
     if _timer:
         kind = ("x3_" if x3 else "") + ("fwd128" if K > 64 else "fwd64")
-        _timer.stop(kind, 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * C, t0, _tag(sh.N, sh.H, sh.W, C, K, R, S, stride))
+        _timer.stop(kind, 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * C, t0, _tag(sh.N, sh.H, sh.W, C, K, R, S, stride),
+                    x.numel() * x.element_size() + wk.numel() * 2 + y.numel() * y.element_size())
     return (y, st) if stats else y
 
 
@@ -418,7 +421,8 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
         bnb.part = part
     if _timer:
         _timer.stop(("x3_" if x3 else "") + "dgrad", 2.0 * N * Ho * Wo * K * R * S * C, t0,
-                    _tag(N, H, W, C, K, R, S, stride))
+                    _tag(N, H, W, C, K, R, S, stride),
+                    dy.numel() * dy.element_size() + wt.numel() * 2 + dx.numel() * dx.element_size())
     return dx
 
 
@@ -531,7 +535,8 @@ def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False):
         _pending.append((ev, (dyc, x, ws)))
     if _timer:
         _timer.stop(("x3_" if x3 else "") + "wgrad", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * x.shape[3], t0,
-                    _tag(sh.N, sh.H, sh.W, x.shape[3], K, R, S, stride))
+                    _tag(sh.N, sh.H, sh.W, x.shape[3], K, R, S, stride),
+                    dyc.numel() * dyc.element_size() + x.numel() * x.element_size() + dw.numel() * 4)
     return dw
 
 
