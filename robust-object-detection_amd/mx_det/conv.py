@@ -435,6 +435,11 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
 # from its AccumulateGrad hook on the main stream, so multi-rank runs keep wgrad in order.
 _side = {}
 _pending = []
+# The side-stream wgrad's dw reaches AccumulateGrad from the side stream; the backward's end-of-pass
+# callback (_join_side) makes the main stream wait for it, so torch's "AccumulateGrad node's stream does
+# not match" warning (printed once per process, then the engine's own stream wait) is expected here.
+if hasattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch"):
+    torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
 _dp = False
 
 
