@@ -2369,8 +2369,9 @@ extern "C" int mx_conv_set_tile(int bmt, int bn) {
 
 static int g_buf_stages = 0;  // mx_conv_set_stages: LDS ring depth of the 64x128 / 128x128 buffer kernels
 extern "C" int mx_conv_set_stages(int n) {
-  MX_CHECK_ARG(n == 0 || n == 3 || n == 4 || n == 6,
-               "mx_conv_set_stages: 0 (auto), 3, 4 or 6 (x3 kernels: 3 alternative ring, 4 2x2 wave tiles)");
+  MX_CHECK_ARG(n == 0 || n == 3 || n == 4 || n == 5 || n == 6,
+               "mx_conv_set_stages: 0 (auto), 3, 4, 5 or 6 (x3 kernels: 3 alternative ring, 4 2x2 wave tiles, "
+               "5 alternative ring with wide wave tiles)");
   g_buf_stages = n;
   return MX_OK;
 }
@@ -3083,6 +3084,7 @@ static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, h
     // 128 x 128 / 64 x 128 tiles as 4 wide wave tiles (32 x 128 / 16 x 128: each A row split by one
     // wave) unless mx_conv_set_stages(4) asks for the 2 x 2 layout of 64 x 64 / 32 x 64 wave tiles
     const bool wide = g_buf_stages == 0, wide64 = wide;
+    const bool altw = g_buf_stages == 5;  // the alternative ring depth with wide wave tiles
     p.korder = g_conv_korder;
     p.dbg_skip_epi = g_conv_debug;
     if (g_conv_loader == 2) p.src_elems = 0;  // timing-only diagnostics (mx_conv_set_loader)
@@ -3091,10 +3093,12 @@ static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, h
       alt ? launch_x3_buf<128, MODE, 2, 1, 256, 4>(p, blocks, st) : launch_x3_buf<128, MODE, 3, 1, 256, 4>(p, blocks, st);
     } else if (g.bmt == 64) {
       if (g.bn == 64) alt ? launch_x3_buf<64, MODE, 4, 2, 64>(p, blocks, st) : launch_x3_buf<64, MODE, 3, 3, 64>(p, blocks, st);
+      else if (altw) launch_x3_buf<128, MODE, 2, 3, 64, 4, 1>(p, blocks, st);
       else if (wide64) launch_x3_buf<128, MODE, 3, 2, 64, 4, 1>(p, blocks, st);
       else alt ? launch_x3_buf<128, MODE, 2, 3, 64>(p, blocks, st) : launch_x3_buf<128, MODE, 3, 2, 64>(p, blocks, st);
     } else {
       if (g.bn == 64) alt ? launch_x3_buf<64, MODE, 2, 3, 128>(p, blocks, st) : launch_x3_buf<64, MODE, 3, 2, 128>(p, blocks, st);
+      else if (altw) launch_x3_buf<128, MODE, 3, 1, 128, 4, 1>(p, blocks, st);
       else if (wide) launch_x3_buf<128, MODE, 2, 2, 128, 4, 1>(p, blocks, st);
       else alt ? launch_x3_buf<128, MODE, 3, 1, 128>(p, blocks, st) : launch_x3_buf<128, MODE, 2, 2, 128>(p, blocks, st);
     }
