@@ -3092,8 +3092,10 @@ static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, h
     if (g.bmt == 256) {
       alt ? launch_x3_buf<128, MODE, 2, 1, 256, 4>(p, blocks, st) : launch_x3_buf<128, MODE, 3, 1, 256, 4>(p, blocks, st);
     } else if (g.bmt == 64) {
-      if (g.bn == 64) alt ? launch_x3_buf<64, MODE, 4, 2, 64>(p, blocks, st) : launch_x3_buf<64, MODE, 3, 3, 64>(p, blocks, st);
-      else if (altw) launch_x3_buf<128, MODE, 2, 3, 64, 4, 1>(p, blocks, st);
+      if (g.bn == 64) {
+        if (altw) launch_x3_buf<64, MODE, 3, 3, 64, 4, 1>(p, blocks, st);  // 4 wide wave tiles of 16 x 64
+        else alt ? launch_x3_buf<64, MODE, 4, 2, 64>(p, blocks, st) : launch_x3_buf<64, MODE, 3, 3, 64>(p, blocks, st);
+      } else if (altw) launch_x3_buf<128, MODE, 2, 3, 64, 4, 1>(p, blocks, st);
       else if (wide64) launch_x3_buf<128, MODE, 3, 2, 64, 4, 1>(p, blocks, st);
       else alt ? launch_x3_buf<128, MODE, 2, 3, 64>(p, blocks, st) : launch_x3_buf<128, MODE, 3, 2, 64>(p, blocks, st);
     } else {

@@ -121,9 +121,9 @@ _WG_CANDS = ((3, 0), (3, 512), (3, 1024), (3, 384), (2, 0), (0, 0))  # (wgrad ke
 # 256x128 at 2 stages, ...; wgrad block target)
 _FD_CANDS_X3 = ((0, 0, 0, 0), (0, 0, 1, 0), (0, 0, 2, 0), (64, 128, 0, 0), (128, 128, 1, 0), (64, 64, 0, 0),
                 (64, 128, 1, 0), (256, 128, 0, 0), (0, 0, 0, 3), (0, 0, 0, 4), (128, 128, 0, 0),
-                (0, 0, 0, 5))
+                (0, 0, 0, 5), (64, 64, 0, 5))
 if __import__("os").environ.get("MX_X3_ALTW", "1") == "0":  # A/B switch for the newest candidate
-    _FD_CANDS_X3 = tuple(c for c in _FD_CANDS_X3 if c != (0, 0, 0, 5))
+    _FD_CANDS_X3 = tuple(c for c in _FD_CANDS_X3 if c[3] != 5)
 _WG_CANDS_X3 = ((3, 0), (3, 256), (3, 768), (3, 1024), (4, 0), (4, 512))
 _tune_cache = {}
 

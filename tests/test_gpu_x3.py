@@ -256,7 +256,7 @@ def test_x3_act_bias_bwd_f32(dev, M, K, act):
     torch.testing.assert_close(db.cpu(), ref.double().sum(0).float(), rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("ci", range(12))  # every entry of conv._FD_CANDS_X3
+@pytest.mark.parametrize("ci", range(13))  # every entry of conv._FD_CANDS_X3
 @pytest.mark.parametrize("case", [CASES[i] for i in (0, 1, 3, 7, 8, 9)])
 def test_x3_tuner_candidates(dev, monkeypatch, ci, case):
     """Every launch configuration the per-shape tuner may pick for the bf16x3 kernels (block tile x
