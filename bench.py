@@ -598,6 +598,7 @@ def main():
                     help="both (default): the f32 headline, then the bf16 variant in the same JSON line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-augment-variant", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -674,6 +675,20 @@ def main():
             var["roofline"] = conv_roofline(ddp, opt, imgs[0:2], tg[0:2], peak[p])
         rec[p + "_variant"] = var
         del m2
+    if not args.augment and not args.no_augment_variant:
+        # configs[2]'s augmented step (train_frcnn_augmented.py:159-177: RandomCorruption(p=0.5) on the
+        # device in front of the same step), headline precision, timed the same way
+        del ddp, opt
+        torch.cuda.empty_cache()
+        args.augment = True
+        try:
+            m3, ddp, opt, dt3 = _time_precision(head, args, world, rank, dev, imgs, tg)
+        finally:
+            args.augment = False
+        rec["augment_variant"] = {"workload": "configs[2] step: 50% on-GPU noise/blur/lowres (RandomCorruption) + "
+                                              "the same train step", "dtype": DTYPE_TEXT[head],
+                                  "value": round(images / dt3, 3), "ms_per_step": round(1000 * dt3 / args.steps, 3)}
+        del m3
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(cpu_model)
     if rank == 0:

@@ -105,6 +105,9 @@ int mx_batched_nms(const float* boxes, const float* scores, const int64_t* idxs,
  *       < 32768 px a side, and a workspace of mx_roi_align_bwd_workspace(K, PH, PW, sampling) bytes.
  *     deterministic = 0: float atomics ACCUMULATE into caller-zeroed maps (order-dependent in
  *       the last bits; no workspace).
+ *   sampling <= 0: torchvision's adaptive grid (the roi_align default sampling_ratio=-1): per RoI,
+ *     ceil(roi_h / PH) x ceil(roi_w / PW) samples per bin. Forward bit-exact like the fixed grid;
+ *     backward with deterministic = 0 only (atomics, as torchvision's CUDA kernel).
  * ------------------------------------------------------------------------------------------- */
 size_t mx_roi_align_bwd_workspace(int64_t K, int PH, int PW, int sampling);
 int mx_roi_align_fwd(const void* feat, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, const float* rois,
@@ -169,6 +172,13 @@ int mx_normalize_pad(const uint8_t* img, int64_t B, int64_t H, int64_t W, const 
 int mx_resize_normalize_pad(const uint8_t* const* imgs, const int64_t* Hs, const int64_t* Ws, const int64_t* nhs,
                             const int64_t* nws, int64_t B, const float* mean3_host, const float* std3_host,
                             int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out, mx_stream_t stream);
+/* The same for the reference loader's own image tensors: ToDtype(float32, scale=True) output, f32 CHW
+ * [3, Hs[b], Ws[b]] contiguous (train_frcnn_baseline.py:50-54 build_transforms, fed to the model at :171).
+ * A float image equal to u8 * (float)(1/255) gives the bit-identical batch of mx_resize_normalize_pad;
+ * no resize (nh = H, nw = W) reproduces normalize + pad exactly. */
+int mx_resize_normalize_pad_f32(const float* const* imgs_chw, const int64_t* Hs, const int64_t* Ws, const int64_t* nhs,
+                                const int64_t* nws, int64_t B, const float* mean3_host, const float* std3_host,
+                                int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out, mx_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Convolution (implicit GEMM on MFMA, bf16 in / f32 accumulate), NHWC x KRSC.
@@ -420,11 +430,35 @@ int mx_restore_finish(const uint8_t* img_padded, int64_t B, int64_t Hp, int64_t 
                       int64_t W, uint8_t* out, mx_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * U-Net training loss L1 + weight * (1 - SSIM) (train_restoration.py:142-178: ssim() with an 11x11
+ * Gaussian window, sigma 1.5, zero 'same' padding, C1 = 0.01^2, C2 = 0.03^2; CombinedLoss). Images
+ * pred / target NHWC f32 [N,H,W,C] (the NCHW tensors of the reference in channels-last memory).
+ *   mx_ssim_l1_fwd: out3[0] = mean SSIM, out3[1] = mean |pred - target|, out3[2] = out3[1] +
+ *                   weight * (1 - out3[0]) (device floats). dmaps (nullable, 3 * N*H*W*C f32) receives
+ *                   the per-pixel derivatives of the SSIM map the backward needs. Deterministic
+ *                   (fixed-order f64 reduction); window sums in f64. Workspace mx_ssim_workspace().
+ *   mx_ssim_l1_bwd: grad = gout[0] * (cs * d(sum SSIM)/d pred + cl * sign(pred - target)); for the
+ *                   combined loss cs = -weight / numel, cl = 1 / numel; for mean SSIM cs = 1/numel, cl = 0.
+ *   window odd <= 15, sigma > 0.
+ * ------------------------------------------------------------------------------------------- */
+size_t mx_ssim_workspace(int64_t N, int64_t H, int64_t W, int64_t C);
+int mx_ssim_l1_fwd(const float* pred, const float* target, int64_t N, int64_t H, int64_t W, int64_t C, int window,
+                   float sigma, float c1, float c2, float weight, float* out3, float* dmaps, void* ws, size_t ws_bytes,
+                   mx_stream_t stream);
+int mx_ssim_l1_bwd(const float* pred, const float* target, const float* dmaps, int64_t N, int64_t H, int64_t W,
+                   int64_t C, int window, float sigma, const float* gout, float cs, float cl, float* grad,
+                   mx_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Baseline JPEG decode, hybrid (replaces the PIL / cv2.imread JPEG decode of
  * coco_detection_dataset.py:23 (Image.open(...).convert("RGB")), restore_testsets.py:99 and
  * build_corrupted_testsets.py:139, all libjpeg(-turbo) ISLOW + fancy upsampling):
  *   mx_jpeg_parse         host: markers of a baseline (SOF0/SOF1) Huffman JPEG -> mx_jpeg_info
- *                         (MX_EUNSUPPORTED for progressive / arithmetic / lossless / CMYK / 4:4:0).
+ *                         (MX_EUNSUPPORTED for progressive / arithmetic / lossless / CMYK / 4:4:0,
+ *                         RGB-coded frames (libjpeg default_decompress_parms: no JFIF and Adobe
+ *                         transform 0, or component ids 'R','G','B') and frames over 2^28 pixels;
+ *                         MX_EINVAL for malformed headers: over-subscribed Huffman counts, undefined
+ *                         quantisation tables, short segments).
  *   mx_jpeg_decode_coefs  host: entropy decoding (sequential bitstream; restart markers honoured)
  *                         into quantised coefficients, natural order, int16 [comp][by][bx][64].
  *   mx_jpeg_reconstruct   device: dequantisation + jpeg_idct_islow (jidctint.c integer IDCT) per

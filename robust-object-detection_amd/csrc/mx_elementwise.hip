@@ -238,7 +238,7 @@ __global__ void normalize_pad_kernel(const uint8_t* __restrict__ img, int64_t B,
 // v = h0 * (w0 * v00 + w1 * v01) + h1 * (w0 * v10 + w1 * v11) over the normalised source values.
 // Built -ffp-contract=off: every product and sum rounds once, in this order.
 struct RzImg {
-  const uint8_t* src;  // [H][W][3]
+  const void* src;     // u8 [H][W][3] (HWC) or f32 [3][H][W] (CHW, the ToDtype(float32, scale=True) output)
   int H, W, nh, nw;
   float sh, sw;        // (float)H / nh, (float)W / nw
 };
@@ -252,7 +252,19 @@ __device__ __forceinline__ float rz_src(float scale, int dst) {
   return s < 0.f ? 0.f : s;
 }
 
-template <typename T>
+// source pixel (h, w), channel c, as the f32 value ToDtype(float32, scale=True) yields: u8 * (float)(1/255)
+// for uint8 HWC frames, the stored value for float CHW tensors (already that product when the reference
+// loader made them) -- so both inputs give bit-identical batches.
+template <bool F32CHW>
+__device__ __forceinline__ float rz_px(const RzImg& m, int h, int w, int c) {
+  if constexpr (F32CHW) {
+    return ((const float*)m.src)[((int64_t)c * m.H + h) * m.W + w];
+  } else {
+    return (float)((const uint8_t*)m.src)[((int64_t)h * m.W + w) * 3 + c] * (float)(1.0 / 255.0);
+  }
+}
+
+template <typename T, bool F32CHW>
 __global__ void resize_normalize_pad_kernel(RzBatch bt, int64_t B, float3 mean, float3 stdv, int64_t Hp, int64_t Wp,
                                             int64_t Cp, T* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -266,18 +278,13 @@ __global__ void resize_normalize_pad_kernel(RzBatch bt, int64_t B, float3 mean, 
     const int h1 = h0 + (h0 < m.H - 1 ? 1 : 0), w1 = w0 + (w0 < m.W - 1 ? 1 : 0);
     const float hl1 = hr - (float)h0, wl1 = wr - (float)w0;
     const float hl0 = 1.f - hl1, wl0 = 1.f - wl1;
-    const uint8_t* p00 = m.src + ((int64_t)h0 * m.W + w0) * 3;
-    const uint8_t* p01 = m.src + ((int64_t)h0 * m.W + w1) * 3;
-    const uint8_t* p10 = m.src + ((int64_t)h1 * m.W + w0) * 3;
-    const uint8_t* p11 = m.src + ((int64_t)h1 * m.W + w1) * 3;
-    const float inv = (float)(1.0 / 255.0);
     const float mu[3] = {mean.x, mean.y, mean.z}, sd[3] = {stdv.x, stdv.y, stdv.z};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const float a = ((float)p00[c] * inv - mu[c]) / sd[c];
-      const float bb = ((float)p01[c] * inv - mu[c]) / sd[c];
-      const float cc = ((float)p10[c] * inv - mu[c]) / sd[c];
-      const float d = ((float)p11[c] * inv - mu[c]) / sd[c];
+      const float a = (rz_px<F32CHW>(m, h0, w0, c) - mu[c]) / sd[c];
+      const float bb = (rz_px<F32CHW>(m, h0, w1, c) - mu[c]) / sd[c];
+      const float cc = (rz_px<F32CHW>(m, h1, w0, c) - mu[c]) / sd[c];
+      const float d = (rz_px<F32CHW>(m, h1, w1, c) - mu[c]) / sd[c];
       v[c] = hl0 * (wl0 * a + wl1 * bb) + hl1 * (wl0 * cc + wl1 * d);
     }
   }
@@ -405,10 +412,9 @@ extern "C" int mx_normalize_pad(const uint8_t* img, int64_t B, int64_t H, int64_
   return MX_OK;
 }
 
-extern "C" int mx_resize_normalize_pad(const uint8_t* const* imgs, const int64_t* Hs, const int64_t* Ws,
-                                       const int64_t* nhs, const int64_t* nws, int64_t B, const float* mean,
-                                       const float* stdv, int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out,
-                                       mx_stream_t stream) {
+static int resize_normalize_pad(const void* const* imgs, bool f32chw, const int64_t* Hs, const int64_t* Ws,
+                                const int64_t* nhs, const int64_t* nws, int64_t B, const float* mean, const float* stdv,
+                                int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out, hipStream_t stream) {
   MX_CHECK_ARG(B >= 0 && Cp >= 3 && Hp >= 0 && Wp >= 0, "mx_resize_normalize_pad: bad batch / padded shape");
   MX_CHECK_ARG(dtype == MX_F32 || dtype == MX_BF16, "mx_resize_normalize_pad: bad dtype %d", dtype);
   const float3 m = make_float3(mean[0], mean[1], mean[2]), sd = make_float3(stdv[0], stdv[1], stdv[2]);
@@ -433,15 +439,34 @@ extern "C" int mx_resize_normalize_pad(const uint8_t* const* imgs, const int64_t
     if (n == 0) continue;
     const size_t es = dtype == MX_F32 ? 4 : 2;
     char* o = (char*)out + (size_t)b0 * Hp * Wp * Cp * es;
-    if (dtype == MX_F32)
-      resize_normalize_pad_kernel<float><<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(bt, nb, m, sd, Hp, Wp, Cp,
-                                                                                                   (float*)o);
+    const unsigned g = (unsigned)cdiv(n, 256);
+    if (dtype == MX_F32 && f32chw)
+      resize_normalize_pad_kernel<float, true><<<g, 256, 0, stream>>>(bt, nb, m, sd, Hp, Wp, Cp, (float*)o);
+    else if (dtype == MX_F32)
+      resize_normalize_pad_kernel<float, false><<<g, 256, 0, stream>>>(bt, nb, m, sd, Hp, Wp, Cp, (float*)o);
+    else if (f32chw)
+      resize_normalize_pad_kernel<uint16_t, true><<<g, 256, 0, stream>>>(bt, nb, m, sd, Hp, Wp, Cp, (uint16_t*)o);
     else
-      resize_normalize_pad_kernel<uint16_t><<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(bt, nb, m, sd, Hp, Wp,
-                                                                                                      Cp, (uint16_t*)o);
+      resize_normalize_pad_kernel<uint16_t, false><<<g, 256, 0, stream>>>(bt, nb, m, sd, Hp, Wp, Cp, (uint16_t*)o);
     MX_LAUNCH_CHECK();
   }
   return MX_OK;
+}
+
+extern "C" int mx_resize_normalize_pad(const uint8_t* const* imgs, const int64_t* Hs, const int64_t* Ws,
+                                       const int64_t* nhs, const int64_t* nws, int64_t B, const float* mean,
+                                       const float* stdv, int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out,
+                                       mx_stream_t stream) {
+  return resize_normalize_pad((const void* const*)imgs, false, Hs, Ws, nhs, nws, B, mean, stdv, Hp, Wp, Cp, dtype, out,
+                              (hipStream_t)stream);
+}
+
+extern "C" int mx_resize_normalize_pad_f32(const float* const* imgs_chw, const int64_t* Hs, const int64_t* Ws,
+                                           const int64_t* nhs, const int64_t* nws, int64_t B, const float* mean,
+                                           const float* stdv, int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out,
+                                           mx_stream_t stream) {
+  return resize_normalize_pad((const void* const*)imgs_chw, true, Hs, Ws, nhs, nws, B, mean, stdv, Hp, Wp, Cp, dtype,
+                              out, (hipStream_t)stream);
 }
 
 // Empty kernel that marks a point in a rocprofv3 kernel trace (bench.py brackets its timed steps with

@@ -46,6 +46,8 @@ bool build_huff(const uint8_t* bits, const uint8_t* vals, Huff* h) {
   memcpy(h->val, vals, total);
   memset(h->look_len, 0, sizeof(h->look_len));
   for (int l = 1; l <= 16; ++l) {
+    // over-subscription check BEFORE any table write: every code of this length must fit in l bits
+    if (code + bits[l] > (1 << l)) return false;
     h->valoff[l] = k - code;  // value index = code + valoff[l]
     for (int i = 0; i < bits[l]; ++i, ++k, ++code) {
       if (l <= 9) {
@@ -57,12 +59,26 @@ bool build_huff(const uint8_t* bits, const uint8_t* vals, Huff* h) {
       }
     }
     h->maxcode[l] = bits[l] ? code - 1 : -1;
-    if (code > (1 << l)) return false;  // over-subscribed
     code <<= 1;
   }
   h->maxcode[17] = 0x7fffffff;
   return true;
 }
+
+// T.81 C.2 code assignment: false when the counts over-subscribe some code length (a table no
+// encoder can produce; libjpeg rejects it as JERR_BAD_HUFF_TABLE)
+bool huff_counts_ok(const uint8_t* bits) {
+  int code = 0;
+  for (int l = 1; l <= 16; ++l) {
+    code += bits[l];
+    if (code > (1 << l)) return false;
+    code <<= 1;
+  }
+  return true;
+}
+
+// JPEG_MAX pixel count accepted on the hybrid path (larger frames decode on the host)
+constexpr int64_t kMaxPixels = (int64_t)1 << 28;
 
 struct Bits {
   const uint8_t* p;
@@ -133,9 +149,14 @@ extern "C" int mx_jpeg_parse(const uint8_t* d, int64_t n, mx_jpeg_info* info) {
   memset(info, 0, sizeof(*info));
   if (d[0] != 0xFF || d[1] != 0xD8) return fail(MX_EINVAL, "jpeg: no SOI marker");
   int64_t i = 2;
-  bool sof = false;
+  bool sof = false, jfif = false, adobe = false;
+  int adobe_transform = -1;
+  bool qdef[4] = {false, false, false, false};
   while (i + 4 <= n) {
-    if (d[i] != 0xFF) return fail(MX_EINVAL, "jpeg: marker expected");
+    if (d[i] != 0xFF) {  // extraneous bytes before a marker: skipped, as libjpeg's next_marker does
+      ++i;
+      continue;
+    }
     int m = d[i + 1];
     if (m == 0xFF) { ++i; continue; }  // fill byte
     i += 2;
@@ -152,6 +173,8 @@ extern "C" int mx_jpeg_parse(const uint8_t* d, int64_t n, mx_jpeg_info* info) {
       info->ncomp = s[5];
       if (info->height == 0 || info->width == 0) return fail(MX_EUNSUPPORTED, "jpeg: DNL-defined height");
       if (info->ncomp != 1 && info->ncomp != 3) return fail(MX_EUNSUPPORTED, "jpeg: 1 or 3 components only");
+      if ((int64_t)info->height * info->width > kMaxPixels)
+        return fail(MX_EUNSUPPORTED, "jpeg: frame larger than 2^28 pixels (decoded on the host)");
       if (sl < 6 + 3 * info->ncomp) return fail(MX_EINVAL, "jpeg: short SOF");
       for (int c = 0; c < info->ncomp; ++c) {
         info->cid[c] = s[6 + 3 * c];
@@ -177,7 +200,8 @@ extern "C" int mx_jpeg_parse(const uint8_t* d, int64_t n, mx_jpeg_info* info) {
           info->hbits[t][l] = s[o + l];
           tot += s[o + l];
         }
-        if (tot > 256 || o + 17 + tot > sl) return fail(MX_EINVAL, "jpeg: bad DHT counts");
+        if (tot > 256 || o + 17 + tot > sl || !huff_counts_ok(info->hbits[t]))
+          return fail(MX_EINVAL, "jpeg: bad DHT counts");
         memcpy(info->hval[t], s + o + 17, tot);
         info->hdef[t] = 1;
         o += 17 + tot;
@@ -189,13 +213,22 @@ extern "C" int mx_jpeg_parse(const uint8_t* d, int64_t n, mx_jpeg_info* info) {
         if (tq > 3 || pq > 1 || o + 1 + 64 * (pq + 1) > sl) return fail(MX_EINVAL, "jpeg: bad DQT");
         for (int k = 0; k < 64; ++k)
           info->qt[tq][kNatural[k]] = pq ? (uint16_t)((s[o + 1 + 2 * k] << 8) | s[o + 2 + 2 * k]) : s[o + 1 + k];
+        qdef[tq] = true;
         o += 1 + 64 * (pq + 1);
+      }
+    } else if (m == 0xE0) {  // APP0: a JFIF marker implies YCbCr (jdmarker.c examine_app0)
+      if (sl >= 5 && memcmp(s, "JFIF\0", 5) == 0) jfif = true;
+    } else if (m == 0xEE) {  // APP14: Adobe colour transform flag (jdmarker.c examine_app14)
+      if (sl >= 12 && memcmp(s, "Adobe", 5) == 0) {
+        adobe = true;
+        adobe_transform = s[11];
       }
     } else if (m == 0xDD) {  // DRI
       if (sl < 2) return fail(MX_EINVAL, "jpeg: bad DRI");
       info->restart_interval = (s[0] << 8) | s[1];
     } else if (m == 0xDA) {  // SOS: the (single, interleaved) scan starts after this header
       if (!sof) return fail(MX_EINVAL, "jpeg: SOS before SOF");
+      if (sl < 1) return fail(MX_EINVAL, "jpeg: short SOS");
       const int ns = s[0];
       if (ns != info->ncomp || sl < 1 + 2 * ns + 3)
         return fail(MX_EUNSUPPORTED, "jpeg: only single-scan (all components interleaved) images are supported");
@@ -207,6 +240,20 @@ extern "C" int mx_jpeg_parse(const uint8_t* d, int64_t n, mx_jpeg_info* info) {
         info->ta[c] = s[2 + 2 * k] & 15;
         if (info->td[c] > 3 || info->ta[c] > 3 || !info->hdef[info->td[c]] || !info->hdef[4 + info->ta[c]])
           return fail(MX_EINVAL, "jpeg: scan references an undefined Huffman table");
+      }
+      for (int c = 0; c < info->ncomp; ++c)
+        if (!qdef[info->tq[c]]) return fail(MX_EINVAL, "jpeg: component references an undefined quantisation table");
+      if (info->ncomp == 3) {
+        // libjpeg default_decompress_parms: the colour space of a 3-component frame is YCbCr unless an
+        // Adobe marker says transform 0 or (no JFIF / Adobe marker) the component IDs are 'R','G','B';
+        // RGB-coded frames have no colour transform and are decoded on the host
+        bool rgb = false;
+        if (!jfif && adobe) {
+          rgb = adobe_transform == 0;
+        } else if (!jfif && !adobe) {
+          rgb = info->cid[0] == 82 && info->cid[1] == 71 && info->cid[2] == 66;
+        }
+        if (rgb) return fail(MX_EUNSUPPORTED, "jpeg: RGB-coded frame (no YCbCr transform)");
       }
       const int ss = s[1 + 2 * ns], se = s[2 + 2 * ns], ahl = s[3 + 2 * ns];
       if (ss != 0 || se != 63 || ahl != 0) return fail(MX_EUNSUPPORTED, "jpeg: not a sequential scan");

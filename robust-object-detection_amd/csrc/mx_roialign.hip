@@ -520,6 +520,70 @@ __global__ void __launch_bounds__(512, 2) roi_bwd_gather_kernel(Levels L, TileGr
   }
 }
 
+// ---- adaptive sampling grid (sampling_ratio <= 0: ceil(roi_h / PH) x ceil(roi_w / PW) per RoI) -------
+// torchvision.ops.roi_align's default. The grid of a large RoI can hold thousands of samples per bin,
+// so the bilinear setup is recomputed per sample instead of tabled in LDS; the per-channel
+// accumulation order (iy, ix; corners 1..4) is torchvision's. One block per RoI, threads over
+// (bin, channel), consecutive lanes on consecutive channels.
+template <typename T>
+__global__ void __launch_bounds__(256) roi_align_fwd_adaptive_kernel(Levels L, int64_t C, const float* __restrict__ rois,
+                                                                     int PH, int PW, int aligned, int multiscale,
+                                                                     T* __restrict__ out, int32_t* __restrict__ lv_out) {
+  const int64_t k = blockIdx.x;
+  const float* r = rois + 5 * k;
+  const int lv = multiscale ? level_of(r, L.k_min, L.n) : 0;
+  if (lv_out && threadIdx.x == 0) lv_out[k] = lv;
+  const RoiGeo g = roi_geo(r, L.scale[lv], PH, PW, 0, aligned);
+  const int64_t H = L.H[lv], W = L.W[lv];
+  const T* f = (const T*)L.f[lv] + g.b * H * W * C;
+  const int64_t nbins = (int64_t)PH * PW;
+  for (int64_t e = threadIdx.x; e < nbins * C; e += blockDim.x) {
+    const int bin = (int)(e / C);
+    const int64_t c = e - (int64_t)bin * C;
+    float v = 0.f;
+    for (int iy = 0; iy < g.gh; ++iy)
+      for (int ix = 0; ix < g.gw; ++ix) {
+        int yl, xl, yh, xh;
+        float w[4];
+        if (!sample_corners(g, H, W, bin / PW, bin % PW, iy, ix, yl, xl, yh, xh, w)) continue;
+        const float f1 = io<T>::ld(f + ((int64_t)yl * W + xl) * C + c), f2 = io<T>::ld(f + ((int64_t)yl * W + xh) * C + c);
+        const float f3 = io<T>::ld(f + ((int64_t)yh * W + xl) * C + c), f4 = io<T>::ld(f + ((int64_t)yh * W + xh) * C + c);
+        v += ((w[0] * f1 + w[1] * f2) + w[2] * f3) + w[3] * f4;
+      }
+    io<T>::st(out + (k * nbins + bin) * C + c, v / g.count);
+  }
+}
+
+// backward with the adaptive grid: f32 atomics into zero-filled maps (torchvision's CUDA backward
+// scheme; g_i = gout * w_i / count per corner)
+template <typename T>
+__global__ void __launch_bounds__(256) roi_align_bwd_adaptive_kernel(Levels L, int64_t C, const float* __restrict__ rois,
+                                                                     const int32_t* __restrict__ lv_in, int PH, int PW,
+                                                                     int aligned, const T* __restrict__ gout) {
+  const int64_t k = blockIdx.x;
+  const float* r = rois + 5 * k;
+  const int lv = lv_in ? lv_in[k] : 0;
+  const RoiGeo g = roi_geo(r, L.scale[lv], PH, PW, 0, aligned);
+  const int64_t H = L.H[lv], W = L.W[lv];
+  float* gf = L.g[lv] + g.b * H * W * C;
+  const int64_t nbins = (int64_t)PH * PW;
+  for (int64_t e = threadIdx.x; e < nbins * C; e += blockDim.x) {
+    const int bin = (int)(e / C);
+    const int64_t c = e - (int64_t)bin * C;
+    const float go = io<T>::ld(gout + (k * nbins + bin) * C + c);
+    for (int iy = 0; iy < g.gh; ++iy)
+      for (int ix = 0; ix < g.gw; ++ix) {
+        int yl, xl, yh, xh;
+        float w[4];
+        if (!sample_corners(g, H, W, bin / PW, bin % PW, iy, ix, yl, xl, yh, xh, w)) continue;
+        atomicAdd(gf + ((int64_t)yl * W + xl) * C + c, go * w[0] / g.count);
+        atomicAdd(gf + ((int64_t)yl * W + xh) * C + c, go * w[1] / g.count);
+        atomicAdd(gf + ((int64_t)yh * W + xl) * C + c, go * w[2] / g.count);
+        atomicAdd(gf + ((int64_t)yh * W + xh) * C + c, go * w[3] / g.count);
+      }
+  }
+}
+
 static int check_grid(int PH, int PW, int sampling) {
   if (PH <= 0 || PW <= 0) return 0;
   if (sampling > 0 && PH * PW * sampling * sampling > kMaxSamp) return 0;
@@ -533,9 +597,17 @@ using namespace mx;
 static int launch_fwd(const Levels& L, int dtype, int64_t C, const float* rois, int64_t K, int PH, int PW, int sampling,
                       int aligned, int ms, void* out, int32_t* lv, hipStream_t s) {
   MX_CHECK_ARG(check_grid(PH, PW, sampling), "roi_align: unsupported pooled %dx%d sampling %d", PH, PW, sampling);
-  MX_CHECK_ARG(sampling > 0, "roi_align: adaptive sampling (sampling_ratio<=0) not supported");
   MX_CHECK_ARG(dtype == MX_F32 || dtype == MX_BF16, "roi_align: bad dtype %d", dtype);
   if (K == 0) return MX_OK;
+  if (sampling <= 0) {
+    if (dtype == MX_F32)
+      roi_align_fwd_adaptive_kernel<float><<<(unsigned)K, 256, 0, s>>>(L, C, rois, PH, PW, aligned, ms, (float*)out, lv);
+    else
+      roi_align_fwd_adaptive_kernel<uint16_t><<<(unsigned)K, 256, 0, s>>>(L, C, rois, PH, PW, aligned, ms,
+                                                                          (uint16_t*)out, lv);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+  }
   int threads = C >= 256 ? 256 : (int)(cdiv(C, 64) * 64);
   if (C % 8 == 0 && dtype == MX_F32)
     roi_align_fwd_v8_kernel<float><<<(unsigned)K, 256, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms, (float*)out, lv);
@@ -565,8 +637,18 @@ static int launch_bwd(const Levels& L, int64_t N, int dtype, int64_t C, const fl
                       int PH, int PW, int sampling, int aligned, const void* gout, int deterministic, void* ws,
                       size_t ws_bytes, hipStream_t s) {
   MX_CHECK_ARG(check_grid(PH, PW, sampling), "roi_align: unsupported pooled %dx%d sampling %d", PH, PW, sampling);
-  MX_CHECK_ARG(sampling > 0, "roi_align: adaptive sampling (sampling_ratio<=0) not supported");
   MX_CHECK_ARG(dtype == MX_F32 || dtype == MX_BF16, "roi_align: bad dtype %d", dtype);
+  if (sampling <= 0) {  // adaptive grid: atomics only (the caller zero-fills the maps)
+    MX_CHECK_ARG(!deterministic, "roi_align_bwd: the deterministic gather needs a fixed sampling_ratio in 1..4");
+    if (K == 0) return MX_OK;
+    if (dtype == MX_F32)
+      roi_align_bwd_adaptive_kernel<float><<<(unsigned)K, 256, 0, s>>>(L, C, rois, lv, PH, PW, aligned, (const float*)gout);
+    else
+      roi_align_bwd_adaptive_kernel<uint16_t><<<(unsigned)K, 256, 0, s>>>(L, C, rois, lv, PH, PW, aligned,
+                                                                          (const uint16_t*)gout);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+  }
   if (deterministic) {
     MX_CHECK_ARG(det_supported(C), "roi_align_bwd deterministic: C=%lld must be a multiple of 4 in 4..256", (long long)C);
     MX_CHECK_ARG(N >= 1 && N < (1 << 27), "roi_align_bwd deterministic: bad image count");

@@ -69,6 +69,8 @@ _SIGS = {
     "mx_normalize_pad": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp]),
     "mx_resize_normalize_pad": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_int,
                                         c_vp, c_vp]),
+    "mx_resize_normalize_pad_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_int,
+                                        c_vp, c_vp]),
     "mx_conv_mblocks": (c_i64, [ctypes.POINTER(ConvShape)]),
     "mx_conv2d_fwd": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "mx_conv2d_dgrad": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp]),
@@ -116,6 +118,10 @@ _SIGS = {
     "mx_up_concat": (c_int, [c_vp, c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mx_up_concat_bwd": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "mx_restore_finish": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "mx_ssim_workspace": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
+    "mx_ssim_l1_fwd": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_f, c_f, c_f, c_f, c_vp, c_vp, c_vp,
+                               c_sz, c_vp]),
+    "mx_ssim_l1_bwd": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_int, c_f, c_vp, c_f, c_f, c_vp, c_vp]),
     "mx_bn_finalize": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_vp]),
     "mx_bn_finalize_workspace": (ctypes.c_size_t, [c_i64, c_i64]),

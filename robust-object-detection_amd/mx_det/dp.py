@@ -13,7 +13,15 @@ all-reduced as soon as its backward graph has replayed, and under this wrapper t
 is captured as a chain of per-segment graphs (frcnn._SegGraphs: FPN + RPN head, layer4, layer3,
 layer2) whose hand-off hook starts each segment's all-reduce (one flat bucket per segment, 5-60 MB)
 on RCCL's stream while the later segments' graphs run; `sync_gradients()` then only waits, scales
-and scatters back. Anything not started by a hook (eager trunk, other parameters) is reduced there
+and scatters back.
+
+Rank consistency: RCCL pairs collectives by issue order, and whether a unit replays a graph (and so
+fires a hook) is decided per rank from local shapes (e.g. a rank whose sampled RoI count differs runs
+its RoI head eagerly). The hooks therefore only mark a group ready; collectives are always issued in
+one canonical order [roi_heads, fpn+rpn_head, layer4, layer3, layer2, stem+layer1, buckets]. A hook
+for a later group first issues every earlier group not yet started (their gradients are final: the
+backward produces them before the later group's), so each rank issues the same sizes in the same
+order whichever of its units replayed graphs. Anything not started by a hook (eager trunk, other parameters) is reduced there
 in ~`bucket_mb` buckets. Over xGMI a ring all-reduce of the 172 MB of f32 gradients costs
 ~2·(N-1)/N·172 MB / bus bandwidth; with the overlap only the last segment's (layer2, 5 MB) is
 exposed.
@@ -57,6 +65,9 @@ class DataParallel:
             model.__dict__["_mx_seg_ready"] = self._segment_reduce
         seen = early | {id(p) for v in self.segments.values() for p in v}
         rest = [p for p in self.params if id(p) not in seen]
+        # the canonical issue order of the hook-startable groups (backward order)
+        self.groups = ([("roi_heads", self.early)] if self.early else []) + list(self.segments.items())
+        self.issued, self.last_issued = [], []  # keys in issue order: this step's, the last synced step's
         # buckets in reverse registration order (the backward produces the later layers' first)
         self.buckets, cur, size = [], [], 0
         for p in reversed(rest):
@@ -93,35 +104,42 @@ class DataParallel:
         flat = _flatten_dense_tensors(grads)
         return dist.all_reduce(flat, group=self.group, async_op=True), flat, grads
 
+    def _issue_through(self, key):
+        """Start, in canonical order, every group up to and including `key` not yet started."""
+        if key not in dict(self.groups):
+            return
+        for k, params in self.groups:
+            if k not in self._work:
+                self._work[k] = self._start(params)
+                self.issued.append(k)
+            if k == key:
+                return
+
     def _early_reduce(self):
-        if "roi_heads" not in self._work:
-            self._work["roi_heads"] = self._start(self.early)
+        """frcnn._Graphs hand-off of the RoI head (first in canonical order)."""
+        self._issue_through("roi_heads")
 
     def _segment_reduce(self, key, params):
-        """frcnn._SegGraphs hand-off: `params`' gradients are final for this backward."""
-        if key in self.segments and key not in self._work:
-            self._work[key] = self._start(self.segments[key])
+        """frcnn._SegGraphs hand-off: `params`' gradients are final for this backward, and so are those
+        of every group before `key` in canonical order."""
+        self._issue_through(key)
 
     @torch.no_grad()
     def sync_gradients(self):
         """Average the trainable gradients over all ranks (call after backward, before step). A
         parameter without a gradient on this rank contributes zeros (and gets the average).
-        Every rank issues the all-reduces in the same order: hook-started ones in backward order
-        (the same on every rank: the same graphs replay), then the rest."""
-        pending = []
-        groups = ([("roi_heads", self.early)] if self.early else []) + list(self.segments.items())
+        Every rank issues the all-reduces in the same canonical order (module docstring), whichever
+        of them its hooks started."""
+        if self.groups:
+            self._issue_through(self.groups[-1][0])  # whatever no hook started, in canonical order
         started = self._work
         self._work = {}
-        for key, params in groups:
-            if key in started:
-                pending.append(started[key])
-            else:
-                # one flat per group whether or not a hook started it: every rank issues the same
-                # collectives (sizes and order) even when its trunk ran eagerly on this shape
-                pending.append(self._start(params))
+        pending = [started[k] for k, _ in self.groups]
         for b in self.buckets:
             pending.append(self._start(b))
+            self.issued.append("bucket")
         for work, flat, grads in pending:
             work.wait()
             flat.mul_(1.0 / self.world)
             torch._foreach_copy_(grads, _unflatten_dense_tensors(flat, grads))
+        self.last_issued, self.issued = self.issued, []

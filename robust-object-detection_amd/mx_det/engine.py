@@ -282,7 +282,9 @@ class DeviceJpegLoader:
         from . import jpeg
         try:
             return jpeg.decode(b, self.dev)
-        except jpeg.JpegUnsupported:
+        except (jpeg.JpegUnsupported, ValueError):
+            # unsupported coding, or a stream the strict parser rejects but libjpeg decodes with a
+            # warning: decode on the host exactly as the reference does (PIL raises if it cannot)
             import io
             from PIL import Image
             img = np.asarray(Image.open(io.BytesIO(b.tobytes())).convert("RGB"))

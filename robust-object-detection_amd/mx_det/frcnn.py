@@ -654,7 +654,9 @@ class ImageList:
 
 class GeneralizedRCNNTransform(nn.Module):
     """normalize -> resize (min 800 / max 1333, bilinear) -> zero-pad to /32, NHWC output with the stem's
-    8 channels. uint8 [B,H,W,3] device batches that need no resize take the fused HIP kernel."""
+    8 channels. On the HIP backend every device input takes a fused kernel: uint8 [B,H,W,3] batches
+    that need no resize mx_normalize_pad, uint8 HWC frames of any size and the reference loader's
+    float32 CHW tensors mx_resize_normalize_pad(_f32). The torch ops below serve the CPU backend."""
 
     def __init__(self, min_size=800, max_size=1333, image_mean=(0.485, 0.456, 0.406),
                  image_std=(0.229, 0.224, 0.225), size_divisible=32):
@@ -691,6 +693,23 @@ class GeneralizedRCNNTransform(nn.Module):
                 h, w = int(im.shape[0]), int(im.shape[1])
                 s = self._scale(h, w)
                 # F.interpolate(recompute_scale_factor=True): out = floor(in * s) in double precision
+                sizes.append((h, w) if s == 1.0 else (int(math.floor(h * s)), int(math.floor(w * s))))
+                orig.append((h, w))
+            batch = be.resize_normalize_pad_u8(list(images), sizes, self._padded(sizes))
+            if targets is not None:
+                targets = [self._resize_boxes(dict(t), o, n) for t, o, n in zip(targets, orig, sizes)]
+            return ImageList(batch, sizes), targets
+        f32chw = isinstance(images, (list, tuple)) and len(images) and all(
+            isinstance(im, torch.Tensor) and im.dtype == torch.float32 and im.dim() == 3 and im.shape[0] == 3
+            for im in images)
+        if f32chw and hasattr(be, "resize_normalize_pad_u8") and getattr(be, "name", "") == "hip" and \
+                all(im.is_cuda for im in images):
+            # the reference loader's ToDtype(float32, scale=True) CHW tensors (train_frcnn_baseline.py:50-54):
+            # the same fused resize + normalize + pad launch as uint8 frames (bit-identical batch)
+            sizes, orig = [], []
+            for im in images:
+                h, w = int(im.shape[1]), int(im.shape[2])
+                s = self._scale(h, w)
                 sizes.append((h, w) if s == 1.0 else (int(math.floor(h * s)), int(math.floor(w * s))))
                 orig.append((h, w))
             batch = be.resize_normalize_pad_u8(list(images), sizes, self._padded(sizes))

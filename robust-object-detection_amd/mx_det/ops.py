@@ -371,21 +371,27 @@ def resize_normalize_pad(images, out_sizes, padded_hw, channels=3, dtype=torch.f
                          std=IMAGE_STD):
     """GeneralizedRCNNTransform with a resize (torchvision transform.py _resize_image_and_masks: bilinear,
     align_corners=False, recompute_scale_factor=True) fused with ToDtype(scale=True), normalize and the
-    zero-padded batch: uint8 HWC device images of any sizes -> NHWC [B,Hp,Wp,channels]; image b fills
-    its out_sizes[b] = (nh, nw) corner."""
+    zero-padded batch: uint8 HWC device images (or the reference loader's float32 CHW [3,H,W] tensors in
+    [0, 1]) of any sizes -> NHWC [B,Hp,Wp,channels]; image b fills its out_sizes[b] = (nh, nw) corner."""
     B = len(images)
     _check(B == len(out_sizes), "resize_normalize_pad: one output size per image")
     xs = [im.contiguous() for im in images]
+    f32 = B > 0 and xs[0].dtype == torch.float32
     for x in xs:
         _dev(x)
-        _check(x.dtype == torch.uint8 and x.dim() == 3 and x.shape[2] == 3, "images must be uint8 [H,W,3]")
+        if f32:  # the reference loader's ToDtype(float32, scale=True) output: f32 CHW [3, H, W]
+            _check(x.dtype == torch.float32 and x.dim() == 3 and x.shape[0] == 3, "images must be float32 [3,H,W]")
+        else:
+            _check(x.dtype == torch.uint8 and x.dim() == 3 and x.shape[2] == 3, "images must be uint8 [H,W,3]")
+    hw = [(x.shape[1], x.shape[2]) if f32 else (x.shape[0], x.shape[1]) for x in xs]
     Hp, Wp = padded_hw
     dev = xs[0].device if B else torch.device("cuda")
     out = torch.empty((B, Hp, Wp, channels), dtype=dtype, device=dev)
     if B:
         arr = lambda t, v: (t * B)(*v)  # noqa: E731
-        call("mx_resize_normalize_pad", arr(ctypes.c_void_p, [x.data_ptr() for x in xs]),
-             arr(ctypes.c_int64, [x.shape[0] for x in xs]), arr(ctypes.c_int64, [x.shape[1] for x in xs]),
+        call("mx_resize_normalize_pad_f32" if f32 else "mx_resize_normalize_pad",
+             arr(ctypes.c_void_p, [x.data_ptr() for x in xs]),
+             arr(ctypes.c_int64, [h for h, _ in hw]), arr(ctypes.c_int64, [w for _, w in hw]),
              arr(ctypes.c_int64, [int(s[0]) for s in out_sizes]), arr(ctypes.c_int64, [int(s[1]) for s in out_sizes]),
              B, (ctypes.c_float * 3)(*mean), (ctypes.c_float * 3)(*std), Hp, Wp, channels, _dtype_code(out), _p(out),
              _stream())
@@ -475,3 +481,60 @@ def roi_loss(class_logits, box_regression, labels, regression_targets, beta=1.0 
     """(loss_classifier, loss_box_reg) of torchvision's fastrcnn_loss for the sampled RoIs."""
     _dev(class_logits, box_regression)
     return _RoILoss.apply(class_logits, box_regression, labels, regression_targets, beta)
+
+
+SSIM_C1, SSIM_C2 = 0.01 ** 2, 0.03 ** 2  # train_restoration.py ssim() stabilisers (K1 = 0.01, K2 = 0.03, L = 1)
+
+
+class _SSIML1(torch.autograd.Function):
+    """Fused SSIM / L1 + w(1 - SSIM) loss (mx_ssim_l1_fwd / _bwd) on NCHW f32 images; the kernels read
+    NHWC memory, so channels-last tensors (the HIP U-Net's output) pass without a copy. combined=True
+    returns the L1 + weight * (1 - SSIM) loss, else the mean SSIM. Gradient w.r.t. `pred` only."""
+
+    @staticmethod
+    def forward(ctx, pred, target, weight, window, sigma, combined):
+        x = pred.detach().permute(0, 2, 3, 1).float().contiguous()
+        y = target.detach().permute(0, 2, 3, 1).float().contiguous()
+        N, H, W, C = x.shape
+        out = torch.empty(3, dtype=torch.float32, device=x.device)
+        maps = torch.empty((3,) + tuple(x.shape), dtype=torch.float32, device=x.device) if pred.requires_grad else None
+        ws = torch.empty(_lib.load().mx_ssim_workspace(N, H, W, C), dtype=torch.uint8, device=x.device)
+        call("mx_ssim_l1_fwd", _p(x), _p(y), N, H, W, C, int(window), float(sigma), SSIM_C1, SSIM_C2, float(weight),
+             _p(out), _p(maps), _p(ws), ws.numel(), _stream())
+        ctx.save_for_backward(x, y, maps)
+        ctx.cfg = (float(weight), int(window), float(sigma), bool(combined))
+        return out[2] if combined else out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y, maps = ctx.saved_tensors
+        weight, window, sigma, combined = ctx.cfg
+        N, H, W, C = x.shape
+        n = x.numel()
+        cs, cl = (-weight / n, 1.0 / n) if combined else (1.0 / n, 0.0)
+        gx = torch.empty_like(x)
+        g = g.detach().float().reshape(1).contiguous()
+        call("mx_ssim_l1_bwd", _p(x), _p(y), _p(maps), N, H, W, C, window, sigma, _p(g), cs, cl, _p(gx), _stream())
+        return gx.permute(0, 3, 1, 2), None, None, None, None, None
+
+
+def _ssim_args(pred, target, window):
+    _dev(pred, target)
+    _check(pred.dim() == 4 and pred.shape == target.shape, "ssim: pred and target must be [N, C, H, W] of one shape")
+    _check(pred.dtype == torch.float32 and target.dtype == torch.float32, "ssim: float32 images")
+    _check(not target.requires_grad, "ssim: no gradient w.r.t. target (the reference's clean image)")
+    _check(window % 2 == 1 and 1 <= window <= 15, "ssim: odd window size <= 15")
+
+
+def ssim(pred, target, window_size=11, sigma=1.5):
+    """Mean SSIM of [N,C,H,W] images in [0, 1]: Gaussian window (σ 1.5), zero 'same' padding, no
+    clipping -- the train_restoration.py:142-164 definition; differentiable in `pred`."""
+    _ssim_args(pred, target, window_size)
+    return _SSIML1.apply(pred, target, 0.0, window_size, sigma, False)
+
+
+def ssim_l1_loss(pred, target, ssim_weight=0.3, window_size=11, sigma=1.5):
+    """mean|pred - target| + ssim_weight * (1 - SSIM(pred, target)) in one forward and one backward launch
+    pair (train_restoration.py:167-178 CombinedLoss)."""
+    _ssim_args(pred, target, window_size)
+    return _SSIML1.apply(pred, target, ssim_weight, window_size, sigma, True)

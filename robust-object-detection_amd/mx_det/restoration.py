@@ -1,16 +1,18 @@
 """U-Net restoration training (reference scripts/train_restoration.py) on the HIP U-Net.
 
 Drop-in pieces with the reference's names and semantics:
-  ssim(pred, target, window_size=11)      train_restoration.py:116-135 (11x11 Gaussian sigma 1.5, C1/C2)
-  CombinedLoss(ssim_weight=0.3)           :138-150  L1 + 0.3 * (1 - SSIM)
-  compute_psnr(pred, target)              :153-158
+  ssim(pred, target, window_size=11)      train_restoration.py:142-164 (11x11 Gaussian sigma 1.5, C1/C2)
+  CombinedLoss(ssim_weight=0.3)           :167-178  L1 + 0.3 * (1 - SSIM)
+  compute_psnr(pred, target)              :185-190
   RestorationDataset(img_dir, patch, is_train)  :54-111 -- (corrupted, clean) f32 CHW patches; here the
       host only decodes, crops and flips (uint8) and the corruption of a whole batch runs on the device
       (ops.corrupt_u8: noise / motion blur / low-res, one random choice per patch) via RestorationBatcher
   train_epoch / validate                  :199-215 / :161-175
-The loss's five depthwise 11x11 window sums run as torch depthwise convs on 3 channels (< 0.3 % of
-the U-Net's FLOPs per step); the U-Net forward/backward is the HIP path (mx_det.unet).
+The loss runs as the fused HIP SSIM kernels (mx_ssim.hip: window sums, SSIM map, its derivative maps
+and the L1 term in one forward launch + a finish block; one backward launch); the U-Net
+forward/backward is the HIP path (mx_det.unet).
 """
+import math
 import random
 from pathlib import Path
 
@@ -23,53 +25,31 @@ from . import ops
 NOISE, BLUR, LOWRES = ops.CORRUPT_NOISE, ops.CORRUPT_BLUR, ops.CORRUPT_LOWRES  # augmentations.py ops
 
 
-def _gaussian_kernel(size=11, sigma=1.5):
-    coords = torch.arange(size, dtype=torch.float32) - size // 2
-    g = torch.exp(-(coords ** 2) / (2 * sigma ** 2))
-    g = torch.outer(g, g)
-    return (g / g.sum()).unsqueeze(0).unsqueeze(0)
-
-
-_kern = {}
-
-
 def ssim(pred, target, window_size=11):
-    """Mean SSIM of NCHW images in [0, 1] (the reference's zero-padded 'same' window, no clipping)."""
-    C1, C2 = 0.01 ** 2, 0.03 ** 2
-    ch = pred.size(1)
-    key = (window_size, ch, pred.device, pred.dtype)
-    k = _kern.get(key)
-    if k is None:
-        k = _kern[key] = _gaussian_kernel(window_size).to(pred.device, pred.dtype).expand(ch, 1, -1, -1).contiguous()
-    pad = window_size // 2
-    conv = nn.functional.conv2d
-    mu1, mu2 = conv(pred, k, padding=pad, groups=ch), conv(target, k, padding=pad, groups=ch)
-    mu1_sq, mu2_sq, mu12 = mu1 ** 2, mu2 ** 2, mu1 * mu2
-    s1 = conv(pred ** 2, k, padding=pad, groups=ch) - mu1_sq
-    s2 = conv(target ** 2, k, padding=pad, groups=ch) - mu2_sq
-    s12 = conv(pred * target, k, padding=pad, groups=ch) - mu12
-    m = ((2 * mu12 + C1) * (2 * s12 + C2)) / ((mu1_sq + mu2_sq + C1) * (s1 + s2 + C2))
-    return m.mean()
+    """Mean SSIM of NCHW f32 images in [0, 1] (train_restoration.py:142-164 semantics: Gaussian window
+    σ 1.5, zero-padded 'same' window sums, C1 = 0.01², C2 = 0.03², no clipping), computed by the fused
+    device kernel mx_ssim_l1_fwd; differentiable in `pred`."""
+    return ops.ssim(pred, target, window_size)
 
 
 class CombinedLoss(nn.Module):
-    """L1 + ssim_weight * (1 - SSIM)."""
+    """The reference's restoration loss, mean absolute error + ssim_weight · (1 − SSIM)
+    (train_restoration.py:167-178), as one fused forward launch and one fused backward launch."""
 
     def __init__(self, ssim_weight=0.3):
         super().__init__()
-        self.l1 = nn.L1Loss()
         self.ssim_weight = ssim_weight
 
     def forward(self, pred, target):
-        return self.l1(pred, target) + self.ssim_weight * (1.0 - ssim(pred, target))
+        return ops.ssim_l1_loss(pred, target, self.ssim_weight)
 
 
 @torch.no_grad()
 def compute_psnr(pred, target):
-    mse = nn.functional.mse_loss(pred, target)
-    if mse == 0:
-        return 100.0
-    return float(10 * torch.log10(1.0 / mse))
+    """Peak signal-to-noise ratio in dB for images in [0, 1] (train_restoration.py:185-190); identical
+    images report 100 dB as the reference does."""
+    err = float(torch.mean(torch.square(pred.float() - target.float())))
+    return 100.0 if err == 0.0 else -10.0 * math.log10(err)
 
 
 def _read_rgb(path):

@@ -61,7 +61,6 @@ def _nms_fake(dets, scores, iou_threshold):
 @torch.library.impl(_lib, "roi_align", "CUDA")
 def _roi_align_cuda(input, rois, spatial_scale, pooled_height, pooled_width, sampling_ratio, aligned):
     _check(input.dim() == 4, "input must be NCHW [N, C, H, W]")
-    _check(sampling_ratio > 0, "mx_det::roi_align: adaptive sampling (sampling_ratio <= 0) is not supported")
     out = ops.roi_align_fwd_nhwc(input.permute(0, 2, 3, 1), rois, spatial_scale, int(pooled_height),
                                  int(pooled_width), int(sampling_ratio), bool(aligned))
     return out.permute(0, 3, 1, 2).contiguous()
@@ -76,7 +75,6 @@ def _roi_align_fake(input, rois, spatial_scale, pooled_height, pooled_width, sam
 def _roi_align_backward_cuda(grad, rois, spatial_scale, pooled_height, pooled_width, batch_size, channels, height,
                              width, sampling_ratio, aligned):
     _check(grad.dim() == 4, "grad must be [K, C, pooled_height, pooled_width]")
-    _check(sampling_ratio > 0, "mx_det::_roi_align_backward: adaptive sampling is not supported")
     gf = ops.roi_align_bwd_nhwc(grad.permute(0, 2, 3, 1), rois, int(batch_size), int(height), int(width),
                                 int(channels), spatial_scale, int(pooled_height), int(pooled_width),
                                 int(sampling_ratio), bool(aligned))
@@ -111,9 +109,26 @@ def nms(boxes, scores, iou_threshold):
     return torch.ops.mx_det.nms(boxes, scores, float(iou_threshold))
 
 
+def _rois(boxes, like):
+    """torchvision.ops._utils.convert_boxes_to_roi_format: Tensor[K, 5] as is, or a list of per-image
+    Tensor[L_i, 4] -> Tensor[sum L_i, 5] with the image index in column 0."""
+    if isinstance(boxes, torch.Tensor):
+        _check(boxes.dim() == 2 and boxes.shape[1] == 5, "boxes must be Tensor[K, 5] or a list of Tensor[L, 4]")
+        return boxes
+    _check(isinstance(boxes, (list, tuple)) and all(isinstance(b, torch.Tensor) and b.dim() == 2 and b.shape[1] == 4
+                                                     for b in boxes), "boxes must be Tensor[K, 5] or a list of Tensor[L, 4]")
+    if not boxes:
+        return like.new_empty((0, 5))
+    cat = torch.cat(list(boxes), 0)
+    idx = torch.cat([torch.full_like(b[:, :1], i) for i, b in enumerate(boxes)], 0)
+    return torch.cat([idx, cat], 1)
+
+
 def roi_align(input, boxes, output_size, spatial_scale=1.0, sampling_ratio=-1, aligned=False):
-    """torchvision.ops.roi_align (NCHW input, boxes Tensor[K, 5]) through the registered op."""
+    """torchvision.ops.roi_align (NCHW input; boxes Tensor[K, 5] or list of Tensor[L, 4]) through the
+    registered op; sampling_ratio <= 0 is torchvision's adaptive grid (its default)."""
     if isinstance(output_size, int):
         output_size = (output_size, output_size)
+    boxes = _rois(boxes, input)
     return torch.ops.mx_det.roi_align(input, boxes, float(spatial_scale), int(output_size[0]), int(output_size[1]),
                                       int(sampling_ratio), bool(aligned))

@@ -92,3 +92,38 @@ def test_ddp_gradients_equal_mean_of_rank_gradients():
         assert out[r][0] < 1e-5, out[r][0]
     shards = sorted(i for r in range(world) for i in out[r][1])
     assert shards == list(range(7))
+
+
+def test_dp_issue_order_is_canonical_whatever_the_hooks():
+    """mx_det.dp.DataParallel issues its collectives in one canonical order on every rank, whichever
+    units fired a graph hand-off hook on this rank (a rank with an eager RoI head and a
+    graphed trunk used to issue fpn+rpn_head..layer2 before roi_heads)."""
+    from mx_det.dp import DataParallel
+    keys = ["roi_heads", "fpn+rpn_head", "layer4", "layer3", "layer2"]
+    canonical = keys + ["bucket"]
+
+    def make():
+        dp = DataParallel.__new__(DataParallel)
+        dp.groups = [(k, [k]) for k in keys]
+        dp.buckets = [["rest"]]
+        dp._work, dp.issued, dp.last_issued, dp.world = {}, [], [], 1
+        dp._start = lambda params: (_Done(), torch.zeros(1), [torch.zeros(1)])
+        return dp
+
+    class _Done:
+        def wait(self):
+            pass
+
+    scenarios = {
+        "all graphs": lambda dp: (dp._early_reduce(), [dp._segment_reduce(k, None) for k in keys[1:]]),
+        "eager head, graphed trunk": lambda dp: [dp._segment_reduce(k, None) for k in keys[1:]],
+        "graphed head, eager trunk": lambda dp: dp._early_reduce(),
+        "all eager": lambda dp: None,
+        "head hook late": lambda dp: (dp._segment_reduce("layer4", None), dp._early_reduce(),
+                                      dp._segment_reduce("layer2", None)),
+    }
+    for name, fire in scenarios.items():
+        dp = make()
+        fire(dp)
+        dp.sync_gradients()
+        assert dp.last_issued == canonical, (name, dp.last_issued)

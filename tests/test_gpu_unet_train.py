@@ -74,12 +74,13 @@ def test_unet_train_step_matches_cpu(dev, hw):
     clean = torch.rand(4, 3, hw, hw, generator=g)
     corrupted = (clean + 0.1 * torch.randn(4, 3, hw, hw, generator=g)).clamp(0, 1)
     crit = CombinedLoss(0.3)
+    from oracle.ssim_ref import combined_loss as crit_cpu  # the reference formula on torch CPU
     import copy
     r64, rt = copy.deepcopy(ref).double(), _tf32_module(ref)
-    (crit(r64(corrupted.double()), clean.double())).backward()
-    (crit(rt(corrupted), clean)).backward()
+    (crit_cpu(r64(corrupted.double()), clean.double())).backward()
+    (crit_cpu(rt(corrupted), clean)).backward()
     out_r = ref(corrupted)
-    loss_r = crit(out_r, clean)
+    loss_r = crit_cpu(out_r, clean)
     loss_r.backward()
     out = m(corrupted.to(dev))
     loss = crit(out, clean.to(dev))

@@ -100,3 +100,111 @@ def test_device_decode_matches_libjpeg(dev, i):
     ref = _pil(data)
     assert np.array_equal(jpeg.decode(data, dev).cpu().numpy(), ref)
     assert np.array_equal(jpeg.decode(data, dev, bgr=True).cpu().numpy(), ref[..., ::-1])
+
+
+# ------------------------------------------------------------------ malformed / unusual streams (ADVICE r2)
+def _segs(data):
+    """[(marker, offset of 0xFF, segment end)] of the header segments up to and including SOS."""
+    out, i = [], 2
+    while i + 4 <= len(data):
+        m = data[i + 1]
+        ln = (data[i + 2] << 8) | data[i + 3]
+        out.append((m, i, i + 2 + ln))
+        if m == 0xDA:
+            break
+        i += 2 + ln
+    return out
+
+
+def _base():
+    b = io.BytesIO()
+    Image.fromarray(_image(48, 64, 3)).save(b, format="JPEG", quality=90)
+    return bytearray(b.getvalue())
+
+
+def test_oversubscribed_dht_rejected_before_table_writes():
+    from mx_det import jpeg
+    d = _base()
+    m, o, e = next(s for s in _segs(d) if s[0] == 0xC4)
+    bits = o + 5  # first table's 16 counts start after FF C4, length, Tc/Th
+    k = next(l for l in range(16) if d[bits + l] >= 3 and l > 0)
+    d[bits + 0] += 3          # three more 1-bit codes (only two exist)...
+    d[bits + k] -= 3          # ...same total, so only the code-space check can catch it
+    with pytest.raises(ValueError):
+        jpeg.parse(bytes(d))
+    # the entropy decoder's own table builder refuses it too (a caller handing it a crafted info)
+    good = _base()
+    info = jpeg.parse(bytes(good))
+    for t in range(8):
+        info.hbits[t][1] = 255
+    with pytest.raises(ValueError):
+        jpeg.decode_coefs(bytes(good), info)
+
+
+def test_short_sos_and_undefined_quant_table_rejected():
+    from mx_det import jpeg
+    d = _base()
+    m, o, e = next(s for s in _segs(d) if s[0] == 0xDA)
+    bad = bytes(d[:o + 2]) + b"\x00\x02" + bytes(d[o + 4:])
+    with pytest.raises((ValueError, jpeg.JpegUnsupported)):
+        jpeg.parse(bad)
+    d = _base()
+    m, o, e = next(s for s in _segs(d) if s[0] in (0xC0, 0xC1))
+    d[o + 4 + 6 + 2] = 3  # component 0 -> quant table 3, never defined
+    with pytest.raises(ValueError):
+        jpeg.parse(bytes(d))
+
+
+def test_huge_header_goes_to_host_and_truncated_stream_does_not_crash():
+    from mx_det import jpeg
+    d = _base()
+    m, o, e = next(s for s in _segs(d) if s[0] in (0xC0, 0xC1))
+    d[o + 5:o + 9] = b"\xff\xff\xff\xff"  # 65535 x 65535
+    with pytest.raises(jpeg.JpegUnsupported):
+        jpeg.parse(bytes(d))
+    d = bytes(_base())
+    for cut in (len(d) // 2, len(d) - 40, _segs(d)[-1][2] + 3):
+        try:
+            jpeg.decode_coefs(d[:cut])
+        except ValueError:
+            pass
+
+
+def _without_jfif(d):
+    m, o, e = next(s for s in _segs(d) if s[0] == 0xE0)
+    return d[:o] + d[e:]
+
+
+def test_rgb_coded_frames_go_to_host():
+    """libjpeg default_decompress_parms: no JFIF + Adobe transform 0, or no marker + component IDs
+    'R','G','B' -> RGB (no colour transform). Those are left to PIL; JFIF + Adobe stays YCbCr."""
+    from mx_det import jpeg
+    adobe0 = b"\xff\xee\x00\x0eAdobe\x00\x64\x00\x00\x00\x00\x00"
+    d = bytes(_base())
+    nj = _without_jfif(d)
+    with pytest.raises(jpeg.JpegUnsupported):
+        jpeg.parse(nj[:2] + adobe0 + nj[2:])
+    rgb = bytearray(nj)
+    m, o, e = next(s for s in _segs(rgb) if s[0] in (0xC0, 0xC1))
+    for c, cid in enumerate((82, 71, 66)):
+        rgb[o + 4 + 6 + 3 * c] = cid
+    m, o, e = next(s for s in _segs(rgb) if s[0] == 0xDA)
+    for c, cid in enumerate((82, 71, 66)):
+        rgb[o + 5 + 2 * c] = cid
+    with pytest.raises(jpeg.JpegUnsupported):
+        jpeg.parse(bytes(rgb))
+    # JFIF present: YCbCr whatever the Adobe flag says -> decoded here, equal to libjpeg
+    both = d[:2] + adobe0 + d[2:]
+    from oracle import oracle as orc
+    info, coefs = jpeg.decode_coefs(both)
+    assert np.array_equal(orc.jpeg_reconstruct(coefs, info), _pil(both))
+
+
+def test_extraneous_bytes_before_marker_skipped_like_libjpeg():
+    from mx_det import jpeg
+    from oracle import oracle as orc
+    d = bytes(_base())
+    m, o, e = next(s for s in _segs(d) if s[0] == 0xDB)
+    junk = d[:o] + b"\x00\x12\x34" + d[o:]
+    info, coefs = jpeg.decode_coefs(junk)
+    assert np.array_equal(orc.jpeg_reconstruct(coefs, info), _pil(d))

@@ -105,3 +105,33 @@ def test_opcheck(dev):
     s = torch.rand(50, device=dev)
     torch.library.opcheck(torch.ops.mx_det.nms.default, (b, s, 0.5), test_utils=("test_schema",))
     assert ops is not None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("aligned", [False, True])
+def test_roi_align_adaptive_sampling_and_list_boxes(dev, aligned):
+    """torchvision.ops.roi_align's defaults: sampling_ratio=-1 (per-RoI ceil(roi_h/ph) x ceil(roi_w/pw)
+    grid) and boxes as a list of per-image Tensor[L, 4]. Forward bit-exact vs the oracle's adaptive
+    grid; backward (atomics, as torchvision's CUDA kernel) within 1e-5 of it."""
+    from oracle import oracle as orc
+    ops = _ops()
+    rng = np.random.default_rng(31 + aligned)
+    N, C, H, W, scale = 2, 32, 36, 44, 0.25
+    feat = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    per = [_boxes(rng, n, H / scale, W / scale, med) for n, med in ((40, 30), (25, 90))]
+    per[1][0] = [-20, -30, 170, 150]  # partly outside, large grid (ceil(~45/7) = 7 samples a side)
+    rois = np.concatenate([np.concatenate([np.full((len(b), 1), i, np.float32), b], 1) for i, b in enumerate(per)])
+    x = torch.from_numpy(feat).to(dev).requires_grad_(True)
+    y = ops.roi_align(x, [torch.from_numpy(b).to(dev) for b in per], (5, 6), scale, -1, aligned)
+    ref = orc.roi_align(feat, rois, scale, (5, 6), -1, aligned)
+    assert np.array_equal(y.detach().cpu().numpy(), ref)
+    y0 = ops.roi_align(x, torch.from_numpy(rois).to(dev), (5, 6), scale, 0, aligned)  # 0 is adaptive too
+    assert torch.equal(y0, y)
+    g = rng.standard_normal(y.shape).astype(np.float32)
+    y.backward(torch.from_numpy(g).to(dev))
+    gr = orc.roi_align_backward(g, rois, scale, (N, C, H, W), -1, aligned)
+    err = np.abs(x.grad.cpu().numpy() - gr).max() / np.abs(gr).max()
+    assert err < 1e-5, err
+    with pytest.raises(RuntimeError):
+        ops.roi_align(x, torch.zeros(3, 4, device=dev), 7, scale, 2, aligned)
+    assert ops.roi_align(x, [], 7, scale, -1, aligned).shape == (0, C, 7, 7)

@@ -140,3 +140,62 @@ def test_model_transform_resizes_on_device(dev):
         rw = torch.tensor(nw, dtype=torch.float32) / torch.tensor(hw[1], dtype=torch.float32)
         exp = boxes[b].cpu() * torch.stack([rw, rh, rw, rh])
         assert torch.equal(tg2[b]["boxes"].cpu(), exp)
+
+
+def _todtype(img_u8):
+    """torchvision.transforms.v2 ToImage + ToDtype(float32, scale=True) (train_frcnn_baseline.py:50-54):
+    CHW float = u8 * (1/255) in float32."""
+    return torch.from_numpy(img_u8).permute(2, 0, 1).contiguous().float().mul_(1.0 / 255)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_float_chw_input_equals_uint8_path(dev, dtype):
+    """The reference loader's float CHW tensors take the same fused kernel (mx_resize_normalize_pad_f32)
+    and give the bit-identical batch of the uint8 path, with and without a resize; and they stay
+    within the existing torch F.interpolate tolerance."""
+    from mx_det import ops
+    rng = np.random.default_rng(11)
+    sizes = [SIZES[0], SIZES[1], SIZES[2], (800, 1333), SIZES[9]]
+    imgs = [_img(rng, *hw) for hw in sizes]
+    outs = [_out_size(*hw) for hw in sizes]
+    Hp = int(math.ceil(max(o[0] for o in outs) / 32) * 32)
+    Wp = int(math.ceil(max(o[1] for o in outs) / 32) * 32)
+    u8 = ops.resize_normalize_pad([torch.from_numpy(i).to(dev) for i in imgs], outs, (Hp, Wp), channels=8,
+                                  dtype=dtype)
+    f32 = ops.resize_normalize_pad([_todtype(i).to(dev) for i in imgs], outs, (Hp, Wp), channels=8, dtype=dtype)
+    assert torch.equal(u8, f32)
+    if dtype == torch.float32:
+        for b, img in enumerate(imgs[:3]):
+            nh, nw = outs[b]
+            ref = _torch_ref(img)
+            d = np.abs(f32[b, :nh, :nw, :3].cpu().numpy() - ref)
+            assert d.max() <= 2e-4 and (d > 2e-6).mean() <= 0.005
+
+
+@pytest.mark.gpu
+def test_model_transform_float_input_on_device(dev):
+    """GeneralizedRCNNTransform on the reference's own input contract (list of float [3,H,W] CUDA
+    tensors) never reaches the torch fallback: same batch, sizes and boxes as the uint8 frames."""
+    from mx_det import frcnn
+    from mx_det.backend import HipBackend
+    be = HipBackend("f32")
+    tr = frcnn.GeneralizedRCNNTransform()
+    rng = np.random.default_rng(4)
+    sizes = [SIZES[0], (800, 1333)]
+    raw = [_img(rng, *hw) for hw in sizes]
+    boxes = [torch.tensor([[10.0, 20.0, 300.0, 400.0]], device=dev) for _ in sizes]
+    mk = lambda: [{"boxes": b.clone(), "labels": torch.ones(1, dtype=torch.int64, device=dev)} for b in boxes]  # noqa: E731
+    calls = []
+    orig = frcnn.F.interpolate
+    frcnn.F.interpolate = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    try:
+        il_f, tg_f = tr([_todtype(i).to(dev) for i in raw], mk(), be)
+    finally:
+        frcnn.F.interpolate = orig
+    assert not calls, "float input fell back to torch F.interpolate"
+    il_u, tg_u = tr([torch.from_numpy(i).to(dev) for i in raw], mk(), be)
+    assert il_f.image_sizes == il_u.image_sizes
+    assert torch.equal(il_f.tensors, il_u.tensors)
+    for a, b in zip(tg_f, tg_u):
+        assert torch.equal(a["boxes"], b["boxes"])
