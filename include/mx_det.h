@@ -434,7 +434,7 @@ int mx_restore_finish(const uint8_t* img_padded, int64_t B, int64_t Hp, int64_t 
  * Gaussian window, sigma 1.5, zero 'same' padding, C1 = 0.01^2, C2 = 0.03^2; CombinedLoss). Images
  * pred / target NHWC f32 [N,H,W,C] (the NCHW tensors of the reference in channels-last memory).
  *   mx_ssim_l1_fwd: out3[0] = mean SSIM, out3[1] = mean |pred - target|, out3[2] = out3[1] +
- *                   weight * (1 - out3[0]) (device floats). dmaps (nullable, 3 * N*H*W*C f32) receives
+ *                   weight * (1 - out3[0]) (device floats). dmaps (nullable, 3 * N*H*W*C f64) receives
  *                   the per-pixel derivatives of the SSIM map the backward needs. Deterministic
  *                   (fixed-order f64 reduction); window sums in f64. Workspace mx_ssim_workspace().
  *   mx_ssim_l1_bwd: grad = gout[0] * (cs * d(sum SSIM)/d pred + cl * sign(pred - target)); for the
@@ -443,9 +443,9 @@ int mx_restore_finish(const uint8_t* img_padded, int64_t B, int64_t Hp, int64_t 
  * ------------------------------------------------------------------------------------------- */
 size_t mx_ssim_workspace(int64_t N, int64_t H, int64_t W, int64_t C);
 int mx_ssim_l1_fwd(const float* pred, const float* target, int64_t N, int64_t H, int64_t W, int64_t C, int window,
-                   float sigma, float c1, float c2, float weight, float* out3, float* dmaps, void* ws, size_t ws_bytes,
+                   float sigma, float c1, float c2, float weight, float* out3, double* dmaps, void* ws, size_t ws_bytes,
                    mx_stream_t stream);
-int mx_ssim_l1_bwd(const float* pred, const float* target, const float* dmaps, int64_t N, int64_t H, int64_t W,
+int mx_ssim_l1_bwd(const float* pred, const float* target, const double* dmaps, int64_t N, int64_t H, int64_t W,
                    int64_t C, int window, float sigma, const float* gout, float cs, float cl, float* grad,
                    mx_stream_t stream);
 

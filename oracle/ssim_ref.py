@@ -11,12 +11,13 @@ import torch.nn.functional as F
 
 
 def window_2d(size=11, sigma=1.5, dtype=torch.float32):
-    """The reference builds the 1-D profile in float32 (exp of −d²/2σ²), takes its outer product and
-    divides by the total (train_restoration.py:135-139)."""
-    d = torch.arange(size, dtype=torch.float32) - size // 2
+    """The reference builds the 1-D profile (exp of −d²/2σ²), takes its outer product and divides by
+    the total (train_restoration.py:135-139) -- in float32 there; here in `dtype` throughout, so the
+    float64 evaluation is the formula's exact reading."""
+    d = torch.arange(size, dtype=dtype) - size // 2
     prof = torch.exp(-(d * d) / (2 * sigma * sigma))
     w = prof[:, None] * prof[None, :]
-    return (w / w.sum()).to(dtype)
+    return w / w.sum()
 
 
 def _wmean(t, w):

@@ -567,6 +567,37 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
+// LDS-DMA (buffer_load_dwordx4 ... lds, 16 B per lane) issued from inline asm. Through the builtin
+// the compiler tracks the load as an LDS write it cannot place, so SIInsertWaitcnts puts an
+// s_waitcnt vmcnt(0) in front of the first later ds_read that may alias it: in the ring kernels that
+// is the current tile's fragment read, right after the next tiles' DMA was issued -- every K-tile
+// then waited for its successors' loads and the STAGES-deep ring never had more than one tile in
+// flight during the MFMAs. Hidden from the compiler, the loads are ordered only by the kernels'
+// own counted wait_vmcnt<> + barrier (the ring's protocol): ds_reads of tile t never alias the
+// slots being filled. `lds` (M0) and the descriptor are wave-uniform SGPRs; M0 -> LDS-DMA needs one
+// wait state.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 dma_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xffffu));
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(LDS_AS const void*)p);
+}
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // M0 is reserved: the kernels using this set it only here
+__device__ __forceinline__ void lds_dma16(i32x4 rsrc, uint32_t lds, uint32_t voff, uint32_t soff) {
+  const int l = __builtin_amdgcn_readfirstlane((int)lds), so = __builtin_amdgcn_readfirstlane((int)soff);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :: "s"(l), "v"(voff), "s"(rsrc), "s"(so) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 __device__ __forceinline__ void block_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -796,10 +827,9 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_buf_kernel(ConvP p) {
     const int64_t n = n0 + wave * (BN / 4) + i * RPI + lrow;
     b_voff[i] = n < p.Ncol ? (uint32_t)((n * p.Kdim + lch * 8) * 2) : kOOB;
   }
-  const __amdgpu_buffer_rsrc_t arsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.src, (short)0, (int)(p.src_elems * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t brsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.wt, (short)0, (int)(p.wt_elems * 2), 0x00020000);
+  const i32x4 arsrc = dma_rsrc(p.src, (uint32_t)(p.src_elems * 2));
+  const i32x4 brsrc = dma_rsrc(p.wt, (uint32_t)(p.wt_elems * 2));
+  const uint32_t lds0 = lds_addr(smem);
   const int64_t nk = p.Kdim / BKT;
   const int64_t kbeg = (int64_t)split * p.kt_per_split;
   const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
@@ -808,8 +838,8 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_buf_kernel(ConvP p) {
   KPos kp;
   kp.init(korder, (int)kbeg, R, S, IC, BKT);
   auto issue = [&](int buf) {
-    char* A = smem + buf * STAGE;
-    char* B = A + A_BYTES;
+    const uint32_t A = lds0 + buf * STAGE;
+    const uint32_t B = A + A_BYTES;
     const int cr = kp.cr, cq = kp.cq, cc = kp.cc;
     const int rr = MODE == 0 ? cr : R - 1 - cr, qq = MODE == 0 ? cq : S - 1 - cq;
     const uint32_t a_soff = (uint32_t)(((rr * IW + qq) * IC + cc) * 2);
@@ -819,12 +849,10 @@ __global__ void __launch_bounds__(NT, OCC) conv_igemm_buf_kernel(ConvP p) {
     for (int i = 0; i < AI; ++i) {
       // the whole offset in voffset (the origin may be negative; the tap offset brings it in range)
       const uint32_t v = ((a_mask[i] >> tap) & 1ull) ? a_voff[i] + a_soff : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (LDS_AS void*)(A + (wave * AR + i * RPI) * RB), 16, v, 0, 0, 0);
+      lds_dma16(arsrc, A + (wave * AR + i * RPI) * RB, v, 0u);
     }
 #pragma unroll
-    for (int i = 0; i < BI; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (LDS_AS void*)(B + (wave * (BN / 4) + i * RPI) * RB), 16, b_voff[i],
-                                               b_soff, 0, 0);
+    for (int i = 0; i < BI; ++i) lds_dma16(brsrc, B + (wave * (BN / 4) + i * RPI) * RB, b_voff[i], b_soff);
     kp.advance(korder, R, S, IC, BKT);
   };
   f32x4 acc[TI][TJ];
@@ -1364,21 +1392,21 @@ __global__ void __launch_bounds__(NT, 3) conv_wgrad_buf_kernel(WgP p) {
     b_r[i] = tap / p.S;
     b_s[i] = tap - b_r[i] * p.S;
   }
-  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, (short)0, (int)(pend * p.K * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t brsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)(p.N * p.H * p.W * p.C * 2), 0x00020000);
+  const i32x4 arsrc = dma_rsrc(p.dy, (uint32_t)(pend * p.K * 2));
+  const i32x4 brsrc = dma_rsrc(p.x, (uint32_t)(p.N * p.H * p.W * p.C * 2));
+  const uint32_t lds0 = lds_addr(smem);
   const uint32_t a_step = (uint32_t)(PXT * K * 2);
   auto issue = [&](int buf) {
-    char* A = smem + buf * STAGE;
-    char* B = A + OPB;
+    const uint32_t A = lds0 + buf * STAGE;
+    const uint32_t B = A + OPB;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = wave * 8 + i * 4;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (LDS_AS void*)(A + row * 256), 16, a_off[i], 0, 0, 0);
+      lds_dma16(arsrc, A + row * 256, a_off[i], 0u);
       const int ih = boh[i] * p.st_h - p.pad_h + b_r[i], iw = bow[i] * p.st_w - p.pad_w + b_s[i];
       const bool ok = b_col[i] && bpx[i] < pend && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
       const uint32_t bo = ok ? (uint32_t)((((bn_[i] * H + ih) * W + iw) * C + b_c[i]) * 2) : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (LDS_AS void*)(B + row * 256), 16, bo, 0, 0, 0);
+      lds_dma16(brsrc, B + row * 256, bo, 0u);
       // advance this lane's rows by one tile
       a_off[i] = a_off[i] == kOOB ? kOOB : a_off[i] + a_step;
       bpx[i] += PXT;
@@ -1675,12 +1703,10 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
     const int64_t n = n0 + wave * BR + i * RPI + lrow;
     b_voff[i] = n < p.Ncol ? (uint32_t)((n * p.Kdim + qb * 8) * 2) : kOOB;
   }
-  const __amdgpu_buffer_rsrc_t arsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.src, (short)0, (int)(p.src_elems * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t bhrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.wt, (short)0, (int)(p.wt_elems * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t blrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.wt + p.wt_plane), (short)0, (int)(p.wt_elems * 2), 0x00020000);
+  const i32x4 arsrc = dma_rsrc(p.src, (uint32_t)(p.src_elems * 4));
+  const i32x4 bhrsrc = dma_rsrc(p.wt, (uint32_t)(p.wt_elems * 2));
+  const i32x4 blrsrc = dma_rsrc(p.wt + p.wt_plane, (uint32_t)(p.wt_elems * 2));
+  const uint32_t lds0 = lds_addr(smem);
   const int64_t nk = p.Kdim / 32;
   const int64_t kbeg = (int64_t)split * p.kt_per_split;
   const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
@@ -1692,8 +1718,8 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
   // 4 no B LDS-DMA, 8 no A LDS-DMA -- wrong results, prices each part of the main loop
   const int dbg = __builtin_amdgcn_readfirstlane(p.dbg_skip_epi);
   auto issue = [&](int buf) {
-    char* A = smem + buf * STAGE;
-    char* B = A + 2 * AH;
+    const uint32_t A = lds0 + buf * STAGE;
+    const uint32_t B = A + 2 * AH;
     const int cr = kp.cr, cq = kp.cq, cc = kp.cc;
     const int rr = MODE == 0 ? cr : R - 1 - cr, qq = MODE == 0 ? cq : S - 1 - cq;
     const uint32_t a_soff = (uint32_t)(((rr * IW + qq) * IC + cc) * 4);
@@ -1704,17 +1730,17 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
     for (int i = 0; i < AI; ++i) {
       const bool ok = (a_mask[i] >> tap) & 1ull;
       const uint32_t v = a_voff[i] + a_soff;
-      char* dst = A + (wave * AR + i * RPI) * RB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (LDS_AS void*)dst, 16, ok ? v : kOOB, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (LDS_AS void*)(dst + AH), 16, ok ? v + 64u : kOOB, 0, 0, 0);
+      const uint32_t dst = A + (wave * AR + i * RPI) * RB;
+      lds_dma16(arsrc, dst, ok ? v : kOOB, 0u);
+      lds_dma16(arsrc, dst + AH, ok ? v + 64u : kOOB, 0u);
     }
     }
     if (!(dbg & 4)) {
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
-      char* dst = B + (wave * BR + i * RPI) * RB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(bhrsrc, (LDS_AS void*)dst, 16, b_voff[i], b_soff, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(blrsrc, (LDS_AS void*)(dst + BP), 16, b_voff[i], b_soff, 0, 0);
+      const uint32_t dst = B + (wave * BR + i * RPI) * RB;
+      lds_dma16(bhrsrc, dst, b_voff[i], b_soff);
+      lds_dma16(blrsrc, dst + BP, b_voff[i], b_soff);
     }
     }
     kp.advance(korder, R, S, IC, 32);

@@ -9,8 +9,9 @@
 //     deterministic, no atomics);
 //   backward: the three derivative maps are window-summed again (the window is symmetric, zero padding
 //     = the forward's) and combined per pixel: dx = g·(c_s·(W⊛a + 2x·W⊛b + y·W⊛c) + c_l·sign(x−y)).
-// Window sums and the SSIM algebra run in f64 on the f32 inputs, so the loss and gradient track the
-// f64 evaluation of the reference formula (the reference's own f32 depthwise convs lose ~1e-4 relative
+// Window sums, the SSIM algebra and the derivative maps are f64 on the f32 inputs (the three gradient
+// terms cancel heavily where the SSIM map is flat, so f32 maps would cost ~1e-5 of the gradient), so
+// the loss and gradient track the f64 evaluation of the reference formula (the reference's own f32 depthwise convs lose ~1e-4 relative
 // in the variance terms E[x²] − μ² on flat regions).
 #include "mx_common.h"
 
@@ -22,19 +23,19 @@ constexpr int kMaxR = 7;  // window sizes up to 15
 constexpr int kRows = kTile + 2 * kMaxR;
 
 struct Taps {
-  float g[16];
+  double g[16];
   int r;  // window radius (size = 2r + 1)
 };
 
 __global__ __launch_bounds__(256) void ssim_fwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
                                                        int H, int W, int C, int ntw, Taps t, double c1, double c2,
-                                                       float* __restrict__ ma, float* __restrict__ mb,
-                                                       float* __restrict__ mc, double* __restrict__ part) {
+                                                       double* __restrict__ ma, double* __restrict__ mb,
+                                                       double* __restrict__ mc, double* __restrict__ part) {
   __shared__ float xs[kRows][kRows + 1], ys[kRows][kRows + 1];
   __shared__ double hs[5][kRows][kTile];
   __shared__ double red[2][4];
   __shared__ double g[16];
-  if (threadIdx.x < 16) g[threadIdx.x] = (double)t.g[threadIdx.x];
+  if (threadIdx.x < 16) g[threadIdx.x] = t.g[threadIdx.x];
   const int r = t.r, n2 = kTile + 2 * r;
   const int plane = blockIdx.y, n = plane / C, c = plane - n * C;
   const int h0 = (blockIdx.x / ntw) * kTile, w0 = (blockIdx.x % ntw) * kTile;
@@ -95,9 +96,9 @@ __global__ __launch_bounds__(256) void ssim_fwd_kernel(const float* __restrict__
     if (ma) {
       const double dA1 = A2 / D, dA2 = A1 / D, dB1 = -S / B1, dB2 = -S / B2;
       const int64_t o = base + ((int64_t)h * W + w) * C;
-      ma[o] = (float)(2 * mu2 * dA1 - 2 * mu2 * dA2 + 2 * mu1 * dB1 - 2 * mu1 * dB2);  // dS/dmu1
-      mb[o] = (float)dB2;                                                             // dS/dE[x^2]
-      mc[o] = (float)(2 * dA2);                                                       // dS/dE[xy]
+      ma[o] = 2 * mu2 * dA1 - 2 * mu2 * dA2 + 2 * mu1 * dB1 - 2 * mu1 * dB2;  // dS/dmu1
+      mb[o] = dB2;                                                             // dS/dE[x^2]
+      mc[o] = 2 * dA2;                                                         // dS/dE[xy]
     }
   }
   // block sum in a fixed order: wave shuffles, then the four wave partials in order
@@ -150,14 +151,14 @@ __global__ __launch_bounds__(1024) void ssim_finish_kernel(const double* __restr
 }
 
 __global__ __launch_bounds__(256) void ssim_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
-                                                       const float* __restrict__ ma, const float* __restrict__ mb,
-                                                       const float* __restrict__ mc, int H, int W, int C, int ntw,
+                                                       const double* __restrict__ ma, const double* __restrict__ mb,
+                                                       const double* __restrict__ mc, int H, int W, int C, int ntw,
                                                        Taps t, const float* __restrict__ gout, float cs, float cl,
                                                        float* __restrict__ gx) {
-  __shared__ float as[3][kRows][kRows + 1];
+  __shared__ double as[3][kRows][kRows + 1];
   __shared__ double hs[3][kRows][kTile];
   __shared__ double g[16];
-  if (threadIdx.x < 16) g[threadIdx.x] = (double)t.g[threadIdx.x];
+  if (threadIdx.x < 16) g[threadIdx.x] = t.g[threadIdx.x];
   const int r = t.r, n2 = kTile + 2 * r;
   const int plane = blockIdx.y, n = plane / C, c = plane - n * C;
   const int h0 = (blockIdx.x / ntw) * kTile, w0 = (blockIdx.x % ntw) * kTile;
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(256) void ssim_bwd_kernel(const float* __restrict__
   for (int i = threadIdx.x; i < n2 * n2; i += 256) {
     const int rr = i / n2, cc = i - rr * n2;
     const int h = h0 - r + rr, w = w0 - r + cc;
-    float a = 0.f, b = 0.f, d = 0.f;
+    double a = 0, b = 0, d = 0;
     if (h >= 0 && h < H && w >= 0 && w < W) {
       const int64_t o = base + ((int64_t)h * W + w) * C;
       a = ma[o];
@@ -210,19 +211,23 @@ __global__ __launch_bounds__(256) void ssim_bwd_kernel(const float* __restrict__
   }
 }
 
-// torch: coords = arange(size) - size // 2 (f32); g = exp(-coords^2 / (2 sigma^2)); outer(g, g) / sum.
-// The 2-D window is separable: w2[i][j] = (g[i] / sum g)(g[j] / sum g).
+// The reference window (train_restoration.py:135-139): coords = arange(size) - size // 2,
+// g = exp(-coords^2 / (2 sigma^2)), w2 = outer(g, g) / sum -- separable: w2[i][j] = (g[i] / sum g) (g[j] /
+// sum g). Evaluated in f64 (the f64 reading of the formula; the reference builds it in f32, whose
+// per-element rounding of the 2-D window (~6e-8) is below every tolerance except the cancelling
+// mean-SSIM gradient's).
 bool make_taps(int window, float sigma, Taps* t) {
   if (window < 1 || window > 2 * kMaxR + 1 || (window & 1) == 0 || !(sigma > 0.f)) return false;
   t->r = window / 2;
   double s = 0;
   double gg[16];
+  const double sg = (double)sigma;
   for (int k = 0; k < window; ++k) {
-    const float cf = (float)(k - window / 2);
-    gg[k] = (double)expf(-(cf * cf) / (2.f * sigma * sigma));
+    const double c = (double)(k - window / 2);
+    gg[k] = exp(-(c * c) / (2.0 * sg * sg));
     s += gg[k];
   }
-  for (int k = 0; k < 16; ++k) t->g[k] = k < window ? (float)(gg[k] / s) : 0.f;
+  for (int k = 0; k < 16; ++k) t->g[k] = k < window ? gg[k] / s : 0.0;
   return true;
 }
 
@@ -237,7 +242,7 @@ extern "C" size_t mx_ssim_workspace(int64_t N, int64_t H, int64_t W, int64_t C) 
 }
 
 extern "C" int mx_ssim_l1_fwd(const float* pred, const float* target, int64_t N, int64_t H, int64_t W, int64_t C,
-                              int window, float sigma, float c1, float c2, float weight, float* out3, float* dmaps,
+                              int window, float sigma, float c1, float c2, float weight, float* out3, double* dmaps,
                               void* ws, size_t ws_bytes, mx_stream_t stream) {
   Taps t;
   MX_CHECK_ARG(make_taps(window, sigma, &t), "ssim: window must be odd and <= 15, sigma > 0");
@@ -247,9 +252,9 @@ extern "C" int mx_ssim_l1_fwd(const float* pred, const float* target, int64_t N,
   const int64_t planes = N * C, npx = N * H * W * C;
   MX_CHECK_ARG(planes < 65536, "ssim: at most 65535 channel planes per call");
   hipStream_t s = (hipStream_t)stream;
-  float* ma = dmaps;
-  float* mb = dmaps ? dmaps + npx : nullptr;
-  float* mc = dmaps ? dmaps + 2 * npx : nullptr;
+  double* ma = dmaps;
+  double* mb = dmaps ? dmaps + npx : nullptr;
+  double* mc = dmaps ? dmaps + 2 * npx : nullptr;
   ssim_fwd_kernel<<<dim3(ntw * nth, (unsigned)planes), 256, 0, s>>>(pred, target, (int)H, (int)W, (int)C, ntw, t,
                                                                      (double)c1, (double)c2, ma, mb, mc, (double*)ws);
   MX_LAUNCH_CHECK();
@@ -258,7 +263,7 @@ extern "C" int mx_ssim_l1_fwd(const float* pred, const float* target, int64_t N,
   return MX_OK;
 }
 
-extern "C" int mx_ssim_l1_bwd(const float* pred, const float* target, const float* dmaps, int64_t N, int64_t H,
+extern "C" int mx_ssim_l1_bwd(const float* pred, const float* target, const double* dmaps, int64_t N, int64_t H,
                               int64_t W, int64_t C, int window, float sigma, const float* gout, float cs, float cl,
                               float* grad, mx_stream_t stream) {
   Taps t;

@@ -497,7 +497,7 @@ class _SSIML1(torch.autograd.Function):
         y = target.detach().permute(0, 2, 3, 1).float().contiguous()
         N, H, W, C = x.shape
         out = torch.empty(3, dtype=torch.float32, device=x.device)
-        maps = torch.empty((3,) + tuple(x.shape), dtype=torch.float32, device=x.device) if pred.requires_grad else None
+        maps = torch.empty((3,) + tuple(x.shape), dtype=torch.float64, device=x.device) if pred.requires_grad else None
         ws = torch.empty(_lib.load().mx_ssim_workspace(N, H, W, C), dtype=torch.uint8, device=x.device)
         call("mx_ssim_l1_fwd", _p(x), _p(y), N, H, W, C, int(window), float(sigma), SSIM_C1, SSIM_C2, float(weight),
              _p(out), _p(maps), _p(ws), ws.numel(), _stream())
