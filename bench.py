@@ -639,9 +639,6 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
 
     from mx_det.data import synth_batch
-    if os.environ.get("MX_CONV_DEBUG"):  # timing experiments only (mx_conv_set_debug bits)
-        from mx_det import _lib
-        _lib.call("mx_conv_set_debug", int(os.environ["MX_CONV_DEBUG"]))
     imgs, tg = synth_batch(rank * N_IMAGES_PER_RANK, N_IMAGES_PER_RANK, device=dev)
     if args.mode != "train":
         if args.mode == "unet_train":

@@ -1714,9 +1714,10 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
   const int korder = __builtin_amdgcn_readfirstlane(p.korder);
   KPos kp;
   kp.init(korder, (int)kbeg, R, S, IC, 32);
-  // timing-only diagnostics (mx_conv_set_debug bits): 1 no epilogue, 2 no hi/lo split (raw bits),
-  // 4 no B LDS-DMA, 8 no A LDS-DMA -- wrong results, prices each part of the main loop
-  const int dbg = __builtin_amdgcn_readfirstlane(p.dbg_skip_epi);
+  // timing-only diagnostics (round 2, mx_conv_set_debug bits 1 no epilogue, 2 no hi/lo split, 4 no B
+  // LDS-DMA, 8 no A LDS-DMA) are compiled out: their run-time tests cost branches and register moves
+  // in every K-tile
+  constexpr int dbg = 0;
   auto issue = [&](int buf) {
     const uint32_t A = lds0 + buf * STAGE;
     const uint32_t B = A + 2 * AH;
@@ -2125,6 +2126,177 @@ __global__ void __launch_bounds__(512, 1) conv_wgrad_x3w_kernel(WgP p) {
 #endif
 }
 
+// bf16x3 wgrad, 256 x 256 block tile at one wave per SIMD (4 waves, 2 x 2 wave tiles of 128 x 128,
+// accumulators in the AGPR half of the 512-entry register file). PMC of the 128 x 128 kernel on the
+// P2 3x3 wgrad: 4.4 VALU per MFMA and 36 % of wave cycles stalled on instruction issue -- the split
+// (2 VALU per MFMA) and the other per-K-tile work are paid per 48 MFMAs a wave. Here a wave runs 192
+// MFMAs per 32-pixel K-tile for the same per-thread staging work pattern, so the split and the LDS
+// stores cost 1 VALU / 0.08 stores per MFMA and the K-tile's issue fits beside its MFMA time; the
+// global loads of the next K-tile are issued before the MFMAs and consumed after them (3072 MFMA
+// cycles to cover them). LDS per stage: dy hi / lo and x hi / lo, each [32 px][256] as two [32][128]
+// sub-planes of 256-B rows (swz_w swizzle), double-buffered: 128 KiB, one block per CU.
+__device__ __forceinline__ void wgrad_store8(const WgP& p, f32x4 (&acc)[8][8], int64_t k0, int64_t c0, int wm, int wn,
+                                             int lane, int64_t split) {
+  float* slab = p.slab ? p.slab + split * p.K * p.Ncol : nullptr;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int64_t k = k0 + wm * 128 + i * 16 + (lane >> 4) * 4 + rr;
+        const int64_t cl = c0 + wn * 128 + j * 16 + (lane & 15);
+        if (k >= p.K || cl >= p.Ncol) continue;
+        if (slab) {
+          slab[k * p.Ncol + cl] = acc[i][j][rr];
+        } else {
+          const int64_t o = wgrad_dst(p, k, (int)cl);
+          if (o >= 0) p.dw[o] = acc[i][j][rr];
+        }
+      }
+}
+
+__global__ void __launch_bounds__(256, 1) conv_wgrad_x3ww_kernel(WgP p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int PXT = 32, SUB = PXT * 256, STAGE = 8 * SUB;  // sub-planes: dy hi 0/1, dy lo 0/1, x hi 0/1, x lo 0/1
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t ntn = (p.Ncol + 255) / 256;
+  const int64_t ntiles = ((p.K + 255) / 256) * ntn;
+  const int64_t work = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int64_t split = work / ntiles, tile = work % ntiles;
+  const int64_t mt = tile / ntn, nt = tile % ntn;
+  const int64_t k0 = mt * 256, c0 = nt * 256;
+  const int64_t pbeg = split * p.kchunk;
+  const int64_t pend = min<int64_t>(p.P, pbeg + p.kchunk);
+  if (pbeg >= pend) return;
+  const float* __restrict__ dy = (const float*)p.dy;
+  const float* __restrict__ x = (const float*)p.x;
+  // this thread's fixed 8-wide chunk (0..31) of the dy k columns and of the x (r,s,c) columns; its
+  // pixel rows of every K-tile: row0 + 8 i, i < 4
+  const int ch = tid & 31, row0 = tid >> 5;
+  const bool k_ok = (k0 + ch * 8) < p.K;
+  const int64_t col = c0 + ch * 8;
+  const bool col_ok = col < p.Ncol;
+  const int tap = col_ok ? (int)(col / p.C) : 0;
+  const int cc = col_ok ? (int)(col - (int64_t)tap * p.C) : 0;
+  const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
+  const int OW = (int)p.OW, OH = (int)p.OH, H = (int)p.H, W = (int)p.W, C = (int)p.C;
+  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, (int)(p.P * p.K * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)(p.N * p.H * p.W * p.C * 4), 0x00020000);
+  const int dw = PXT % OW, dh = (PXT / OW) % OH, dn = PXT / (OW * OH);
+  const int ihb = -p.pad_h + r, iwb = -p.pad_w + s;
+  int px_n[4], px_oh[4], px_ow[4], px_i[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t pi = pbeg + row0 + 8 * i;
+    px_i[i] = (int)pi;
+    const int64_t t = pi / OW;
+    px_ow[i] = (int)(pi - t * OW);
+    px_oh[i] = (int)(t % OH);
+    px_n[i] = (int)(t / OH);
+  }
+  const int pend32 = (int)pend;
+  const uint32_t dy_col = (uint32_t)(k0 + ch * 8) * 4u;
+  float4 rd[4][2], rx[4][2];
+  auto load = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool pok = px_i[i] < pend32;
+      const uint32_t od = (pok && k_ok) ? __umul24((uint32_t)px_i[i], (uint32_t)(p.K * 4)) + dy_col : kOOB;
+      const int ih = __mul24(px_oh[i], p.st_h) + ihb, iw = __mul24(px_ow[i], p.st_w) + iwb;
+      const bool xok = pok && col_ok && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const uint32_t ox = xok ? (uint32_t)__mul24(__mul24(px_n[i], H) + ih, W) + (uint32_t)iw : 0u;
+      const uint32_t oxb = xok ? __umul24(ox, (uint32_t)(C * 4)) + (uint32_t)cc * 4u : kOOB;
+      rd[i][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(dyr, od, 0, 0));
+      rd[i][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(dyr, od + 16u, 0, 0));
+      rx[i][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, oxb, 0, 0));
+      rx[i][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, oxb + 16u, 0, 0));
+      px_i[i] += PXT;
+      int ow = px_ow[i] + dw;
+      const int c1 = ow >= OW ? 1 : 0;
+      ow -= c1 * OW;
+      int oh = px_oh[i] + dh + c1;
+      const int c2 = oh >= OH ? 1 : 0;
+      oh -= c2 * OH;
+      px_ow[i] = ow;
+      px_oh[i] = oh;
+      px_n[i] += dn + c2;
+    }
+  };
+  const int sub = ch >> 4, c16 = ch & 15;
+  auto store = [&](int buf) {
+    char* D = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = row0 + 8 * i;
+      const int off = row * 256 + (swz_w(row, c16) << 4);
+      uint4 h, l;
+      split8(rd[i][0], rd[i][1], h, l);
+      *(uint4*)(D + (0 + sub) * SUB + off) = h;
+      *(uint4*)(D + (2 + sub) * SUB + off) = l;
+      split8(rx[i][0], rx[i][1], h, l);
+      *(uint4*)(D + (4 + sub) * SUB + off) = h;
+      *(uint4*)(D + (6 + sub) * SUB + off) = l;
+    }
+  };
+  auto tr_read = [&](const char* T, int prow0, int colbase) -> s16x4 {
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int row = prow0 + 8 * g + q;
+    const int colx = colbase + 4 * pp;
+    const int chunk = colx >> 3, within = (colx & 7) * 2;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(T + row * 256 + (swz_w(row, chunk) << 4) + within));
+  };
+  auto frag = [&](const char* T, int colbase) -> bf16x8 {
+    const s16x4 lo = tr_read(T, 0, colbase), hi = tr_read(T, 4, colbase);
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nk = (pend - pbeg + PXT - 1) / PXT;
+  load();
+  store(0);
+  __syncthreads();
+  for (int64_t it = 0; it < nk; ++it) {
+    const int buf = (int)(it & 1);
+    if (it + 1 < nk) load();
+    const char* D = smem + buf * STAGE;
+    // this wave's k rows wm*128.. (dy sub-plane wm) and columns wn*128.. (x sub-plane wn)
+    const char* Ah = D + (0 + wm) * SUB;
+    const char* Al = D + (2 + wm) * SUB;
+    const char* Bh = D + (4 + wn) * SUB;
+    const char* Bl = D + (6 + wn) * SUB;
+    bf16x8 ah[8], al[8], bh[8], bl[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      ah[i] = frag(Ah, i * 16);
+      al[i] = frag(Al, i * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bh[j] = frag(Bh, j * 16);
+      bl[j] = frag(Bl, j * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+    if (it + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+  wgrad_store8(p, acc, k0, c0, wm, wn, lane, split);
+#endif
+}
+
 __global__ void transpose_w_kernel(const uint16_t* __restrict__ w, int64_t K, int64_t RS, int64_t C, uint16_t* __restrict__ wt) {
   // w[K][RS][C] -> wt[C][RS][K]
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2403,6 +2575,7 @@ extern "C" int mx_conv_set_stages(int n) {
 }
 static int g_conv_debug = 0;  // mx_conv_set_debug: bf16x3 buffer kernel timing-only bits (see the kernel)
 extern "C" int mx_conv_set_debug(int v) {
+  MX_CHECK_ARG(v == 0, "mx_conv_set_debug: the timing-only kernel bits are compiled out (0 only)");
   g_conv_debug = v;
   return MX_OK;
 }
@@ -2654,7 +2827,7 @@ extern "C" int mx_conv_get_variant(void) { return g_conv_variant; }
 // 3 (default) buffer descriptors (conv_wgrad_buf_kernel; maps under 32 output pixels take 0)
 static int g_wgrad_variant = 3;
 extern "C" int mx_conv_set_wgrad_variant(int v) {
-  MX_CHECK_ARG(v >= 0 && v <= 4, "mx_conv_set_wgrad_variant: 0 px32, 1 px64, 2 direct-to-LDS, 3 buffer descriptors, "
+  MX_CHECK_ARG(v >= 0 && v <= 5, "mx_conv_set_wgrad_variant: 0 px32, 1 px64, 2 direct-to-LDS, 3 buffer descriptors, "
                                 "4 = 3 for bf16 / the 128 x 256 wide block for bf16x3");
   g_wgrad_variant = v;
   return MX_OK;
@@ -2925,7 +3098,7 @@ static WGeo wgrad_geo(const mx_conv_shape* s) {
   WGeo g;
   const int64_t P = s->N * s->Ho * s->Wo, Ncol = s->R * s->S * s->C;
   g.tiles = cdiv(s->K, 128) * cdiv(Ncol, 128);
-  const int v = g_wgrad_variant == 4 ? 3 : g_wgrad_variant;
+  const int v = g_wgrad_variant >= 4 ? 3 : g_wgrad_variant;
   g.pxt = v == 2 ? BKG : (v == 1 ? 64 : BKW);
   // resident blocks per CU: px32 / buffer 3 (142 VGPRs), px64 / direct-to-LDS 2
   const int64_t slots = g_wgrad_target ? g_wgrad_target : (int64_t)num_cus() * ((v == 0 || v == 3) ? 3 : 2);
@@ -2997,7 +3170,7 @@ extern "C" int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, co
   }
   MX_CHECK_ARG(g.tiles < (1ll << 31) && g.splits < 65536, "conv wgrad: grid too large");
   dim3 grid((unsigned)g.tiles, (unsigned)g.splits);
-  int v = g_wgrad_variant == 4 ? 3 : g_wgrad_variant;
+  int v = g_wgrad_variant >= 4 ? 3 : g_wgrad_variant;
   // the buffer kernel walks each lane's pixels by (n, oh, ow) increments: maps of fewer than 32
   // output pixels (FC6 as a 7x7 conv on the RoI tile) would wrap many times per tile -> register kernel
   if (v == 3 && !(p.P * p.K * 2 < (1ll << 31) && s->N * s->H * s->W * s->C * 2 < (1ll << 31) &&
@@ -3154,13 +3327,15 @@ static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, h
 // wgrad x3 block shape: 0 = 128 x 128 (4 waves, 2 blocks per CU), 1 = 128 x 256 (8 waves, one block
 // per CU; mx_conv_set_wgrad_variant(4) -- a tuner candidate)
 static int wgrad_x3_wide() { return g_wgrad_variant == 4; }
+// 5: 256 x 256 tile, one wave per SIMD (conv_wgrad_x3ww_kernel; a tuner candidate)
+static int wgrad_x3_ww() { return g_wgrad_variant == 5; }
 static WGeo wgrad_geo_x3(const mx_conv_shape* s) {
   WGeo g;
   const int64_t P = s->N * s->Ho * s->Wo, Ncol = s->R * s->S * s->C;
-  const bool wide = wgrad_x3_wide();
-  g.tiles = cdiv(s->K, 128) * cdiv(Ncol, wide ? 256 : 128);
+  const bool wide = wgrad_x3_wide(), ww = wgrad_x3_ww();
+  g.tiles = ww ? cdiv(s->K, 256) * cdiv(Ncol, 256) : cdiv(s->K, 128) * cdiv(Ncol, wide ? 256 : 128);
   g.pxt = 32;
-  const int64_t slots = g_wgrad_target ? g_wgrad_target : (int64_t)num_cus() * (wide ? 1 : 2);
+  const int64_t slots = g_wgrad_target ? g_wgrad_target : (int64_t)num_cus() * ((wide || ww) ? 1 : 2);
   int64_t splits = std::max<int64_t>(1, slots / g.tiles);
   const int64_t max_splits = std::max<int64_t>(1, P / (g.pxt * 4));
   splits = std::min(splits, max_splits);
@@ -3287,7 +3462,9 @@ extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const
   MX_CHECK_ARG(p.P * p.K * 4 < (1ll << 31) && p.N * p.H * p.W * p.C * 4 < (1ll << 31) && p.P + 64 < (1ll << 23) &&
                    p.N * p.H * p.W < (1ll << 23) && p.K * 4 < (1ll << 24) && p.C * 4 < (1ll << 24),
                "conv wgrad x3: dy / x must each stay below 2 GiB and 8M pixels (32-bit / 24-bit offset math)");
-  if (wgrad_x3_wide())
+  if (wgrad_x3_ww())
+    conv_wgrad_x3ww_kernel<<<(unsigned)(g.tiles * g.splits), 256, 2 * 8 * 32 * 256, st>>>(p);
+  else if (wgrad_x3_wide())
     conv_wgrad_x3w_kernel<<<(unsigned)(g.tiles * g.splits), 512, 2 * 6 * 32 * 256, st>>>(p);
   else
     conv_wgrad_x3_kernel<<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);

@@ -274,6 +274,95 @@ __global__ void __launch_bounds__(256) nms_scan_lds_kernel(const uint64_t* __res
   }
 }
 
+// Single-wave scan (segments of up to 64*SCAN_WAVE_W boxes): one 64-lane workgroup per segment and
+// no workgroup barriers. Lane w keeps the removed bits of word w in a register; per 64-row block the
+// rows' words blk..W-1 are double-buffered in LDS (lane t loads row t's words into registers for the
+// next block while this block is resolved; odd LDS row stride), the in-tile chain is walked wave-uniformly over the survivors (as in
+// nms_scan_lds_kernel), and lane w ORs the kept rows' word w from LDS, four independent reads at a
+// time. Same greedy result; ~1 us per 64-row block instead of ~4 with three barriers per block.
+static constexpr int SCAN_WAVE_W = 32;
+__global__ void __launch_bounds__(64) nms_scan_wave_kernel(const uint64_t* __restrict__ mask,
+                                                           const int32_t* __restrict__ seg_start,
+                                                           const int32_t* __restrict__ nseg_p,
+                                                           const int32_t* __restrict__ svals, int Wm,
+                                                           int32_t* __restrict__ flags, int32_t* __restrict__ nkeep) {
+  extern __shared__ uint64_t sm[];  // [2][64][Wm + 1]
+  const int lane = threadIdx.x;
+  const int nseg = *nseg_p;
+  for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    const int64_t s0 = seg_start[seg], len = seg_start[seg + 1] - s0;
+    const int W = (int)((len + 63) / 64);
+    if (W > Wm || W > SCAN_WAVE_W) {
+      if (lane == 0) atomicExch(nkeep, (int32_t)0x80000000);
+      continue;
+    }
+    uint64_t rem = 0;  // removed bits of word `lane`
+    uint64_t pre[SCAN_WAVE_W];
+    const int RS = Wm + 1;  // LDS row stride in words (odd: row-strided lane access is 2-way banked)
+    // block b: lane t loads its row's words b..W-1 (row-contiguous 8-B loads)
+    auto fetch = [&](int b) {
+      const int64_t rb = s0 + (int64_t)b * 64;
+      const int c = (int)min<int64_t>(64, len - (int64_t)b * 64), nw = W - b;
+      const uint64_t* src = mask + (rb + lane) * Wm + b;
+#pragma unroll
+      for (int i = 0; i < SCAN_WAVE_W; ++i)
+        if (i < nw && lane < c) pre[i] = src[i];
+    };
+    auto stash = [&](int b) {
+      uint64_t* rows = sm + (b & 1) * 64 * RS + lane * RS + b;
+      const int c = (int)min<int64_t>(64, len - (int64_t)b * 64), nw = W - b;
+#pragma unroll
+      for (int i = 0; i < SCAN_WAVE_W; ++i)
+        if (i < nw && lane < c) rows[i] = pre[i];
+    };
+    fetch(0);
+    stash(0);
+    int kept_total = 0;
+    for (int blk = 0; blk < W; ++blk) {
+      if (blk + 1 < W) fetch(blk + 1);  // in flight while this block is resolved
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this block's LDS rows are written
+      const uint64_t* rows = sm + (blk & 1) * 64 * RS;
+      const int64_t rbase = s0 + (int64_t)blk * 64;
+      const int cnt = (int)min<int64_t>(64, len - (int64_t)blk * 64);
+      const uint64_t diag = lane < cnt ? rows[lane * RS + blk] : 0ull;
+      const uint64_t rm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(rem >> 32), blk) << 32) |
+                          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rem, blk);
+      const uint64_t valid = cnt >= 64 ? ~0ull : ((1ull << cnt) - 1);
+      uint64_t cur = rm, kept = 0;
+      const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
+      uint64_t avail = ~cur & valid;
+      while (avail) {
+        const int t = __builtin_ctzll(avail);
+        kept |= 1ull << t;
+        const uint64_t row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, t) << 32) |
+                             (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, t);
+        cur |= row;
+        avail = ~cur & valid & ~((2ull << t) - 1ull);
+      }
+      if (lane < cnt && ((kept >> lane) & 1ull)) flags[svals[rbase + lane]] = 1;
+      kept_total += __popcll(kept);
+      // lane w > blk: OR of the kept rows' word w
+      if (lane > blk && lane < W) {
+        uint64_t acc = 0, k = kept;
+        while (k) {
+          const int t0 = __builtin_ctzll(k);
+          k &= k - 1;
+          const int t1 = k ? __builtin_ctzll(k) : t0;
+          k &= k ? k - 1 : 0ull;
+          const int t2 = k ? __builtin_ctzll(k) : t0;
+          k &= k ? k - 1 : 0ull;
+          const int t3 = k ? __builtin_ctzll(k) : t0;
+          k &= k ? k - 1 : 0ull;
+          acc |= rows[t0 * RS + lane] | rows[t1 * RS + lane] | rows[t2 * RS + lane] | rows[t3 * RS + lane];
+        }
+        rem |= acc;
+      }
+      if (blk + 1 < W) stash(blk + 1);
+    }
+    if (lane == 0 && kept_total) atomicAdd(nkeep, kept_total);
+  }
+}
+
 // final order: kept first by (group, score desc, index); the rest after
 __global__ void nms_final_keys_kernel(const float* __restrict__ scores, const int32_t* __restrict__ group,
                                       const int32_t* __restrict__ flags, int64_t n, uint64_t* __restrict__ keys,
@@ -488,7 +577,10 @@ extern "C" int mx_batched_nms(const float* boxes, const float* scores, const int
   nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask);
   MX_LAUNCH_CHECK();
   int sgrid = (int)std::min<int64_t>(n, 1024);
-  if (Wm <= SCAN_LDS_W)
+  if (Wm <= SCAN_WAVE_W)
+    nms_scan_wave_kernel<<<sgrid, 64, sizeof(uint64_t) * 2 * 64 * (size_t)(Wm + 1), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
+                                                                                   Wm, w.flags, w.nk);
+  else if (Wm <= SCAN_LDS_W)
     nms_scan_lds_kernel<<<sgrid, 256, sizeof(uint64_t) * (Wm + 64 * (size_t)Wm), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
                                                                                        Wm, w.flags, w.nk);
   else
@@ -551,7 +643,10 @@ extern "C" int mx_batched_nms_grouped(const float* boxes, const float* scores, c
   nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask);
   MX_LAUNCH_CHECK();
   const int sgrid = (int)std::min<int64_t>(n, 1024);
-  if (Wm <= SCAN_LDS_W)
+  if (Wm <= SCAN_WAVE_W)
+    nms_scan_wave_kernel<<<sgrid, 64, sizeof(uint64_t) * 2 * 64 * (size_t)(Wm + 1), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
+                                                                                   Wm, w.flags, w.nk);
+  else if (Wm <= SCAN_LDS_W)
     nms_scan_lds_kernel<<<sgrid, 256, sizeof(uint64_t) * (Wm + 64 * (size_t)Wm), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
                                                                                        Wm, w.flags, w.nk);
   else

@@ -303,7 +303,22 @@ class BalancedPositiveNegativeSampler:
         num_pos = pos.sum(1).clamp(max=P)
         num_neg = torch.minimum(neg.sum(1), self.batch - num_pos)
         r = self.rand(lab.shape, lab.device) if self.rand is not None else torch.rand(lab.shape, device=lab.device)
-        return self._pick(pos, r, min(P, L), num_pos, be), self._pick(neg, r, min(self.batch, L), num_neg, be)
+        kp, kn = min(P, L), min(self.batch, L)
+        if (be is None or not hasattr(be, "level_topk")) and kp > 0 and kn > 0:
+            # both draws in ONE torch.topk over the stacked [pos; neg] key rows (the RPN's 268k-anchor
+            # rows: one multi-kernel top-k sequence instead of two); the sorted ascending prefix of
+            # length kp is exactly topk(kp)'s answer
+            N = lab.shape[0]
+            keys = torch.cat([torch.where(pos, r, 2.0), torch.where(neg, r, 2.0)], 0)
+            _, idx = keys.topk(max(kp, kn), dim=1, largest=False)
+            return (self._mark(pos, idx[:N, :kp], num_pos), self._mark(neg, idx[N:, :kn], num_neg))
+        return self._pick(pos, r, kp, num_pos, be), self._pick(neg, r, kn, num_neg, be)
+
+    @staticmethod
+    def _mark(cand, idx, num):
+        m = torch.zeros_like(cand)
+        m.scatter_(1, idx, torch.arange(idx.shape[1], device=cand.device)[None, :] < num[:, None])
+        return m
 
     @staticmethod
     def _pick(cand, r, k, num, be=None):

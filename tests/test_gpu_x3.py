@@ -308,3 +308,18 @@ def test_x3_bottleneck_bn_partials_from_dgrad_epilogue(dev, monkeypatch):
         assert rel(res["1"][0], res["0"][0]) < 1e-5
         for n in res["0"][1]:
             assert rel(res["1"][1][n], res["0"][1][n]) < 1e-4, n
+
+
+@pytest.mark.parametrize("variant", [4, 5])
+@pytest.mark.parametrize("case", [CASES[i] for i in (0, 2, 4, 5, 7, 8, 9, 11)])
+def test_x3_wgrad_wide_tiles(dev, monkeypatch, variant, case):
+    """The wide wgrad tiles forced for every shape (4: 128 x 256 at 8 waves; 5: 256 x 256 at one wave
+    per SIMD, accumulators in AGPRs): K / column counts below or not a multiple of the tile, split and
+    unsplit pixel axes, strided gathers -- the same bar as the default kernel."""
+    from mx_det._lib import call
+    monkeypatch.setenv("MX_CONV_TUNE", "0")
+    call("mx_conv_set_wgrad_variant", variant)
+    try:
+        test_x3_dgrad_wgrad(dev, *case)
+    finally:
+        call("mx_conv_set_wgrad_variant", 3)
