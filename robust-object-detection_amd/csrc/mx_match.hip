@@ -29,12 +29,29 @@ __device__ __forceinline__ float iou_tv(float4 a, float area_a, float4 b, float 
 
 __device__ __forceinline__ float area_tv(float4 b) { return (b.z - b.x) * (b.w - b.y); }
 
-__global__ void __launch_bounds__(256) match_pass1(const float4* __restrict__ gt, int64_t G, const float4* __restrict__ boxes,
-                                                   int64_t A, float* __restrict__ best_val, int32_t* __restrict__ best_idx,
+// Batched form: image b = blockIdx.y has gt rows gt[b * G ..] of which gcount[b] (nullable: all G) are
+// real -- a padded, static-shape batch (graph capture) -- and its boxes at boxes + b * bstride
+// (bstride 0: the same anchors for every image); per-image outputs are [B][A].
+__device__ __forceinline__ int64_t match_g(int64_t G, const int32_t* gcount) {
+  if (!gcount) return G;
+  const int64_t c = gcount[blockIdx.y];
+  return c < G ? (c < 0 ? 0 : c) : G;
+}
+
+__global__ void __launch_bounds__(256) match_pass1(const float4* __restrict__ gt, int64_t G, const int32_t* __restrict__ gcount,
+                                                   const float4* __restrict__ boxes, int64_t bstride, int64_t A,
+                                                   float* __restrict__ best_val, int32_t* __restrict__ best_idx,
                                                    uint32_t* __restrict__ gmax) {
   __shared__ float4 sg[kTile];
   __shared__ float sga[kTile];
   __shared__ uint32_t smax[kTile];
+  const int64_t b = blockIdx.y;
+  gt += b * G;
+  gmax += b * G;
+  boxes += b * bstride;
+  best_val += b * A;
+  best_idx += b * A;
+  G = match_g(G, gcount);
   int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool valid = a < A;
   float4 bx = valid ? boxes[a] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -71,7 +88,8 @@ __global__ void __launch_bounds__(256) match_pass1(const float4* __restrict__ gt
 }
 
 __global__ void __launch_bounds__(256) match_pass2(const float4* __restrict__ gt, const int64_t* __restrict__ gt_labels,
-                                                   int64_t G, const float4* __restrict__ boxes, int64_t A, float high,
+                                                   int64_t G, const int32_t* __restrict__ gcount,
+                                                   const float4* __restrict__ boxes, int64_t bstride, int64_t A, float high,
                                                    float low, int allow_lq, int mode, float4 wts,
                                                    const float* __restrict__ best_val, const int32_t* __restrict__ best_idx,
                                                    const uint32_t* __restrict__ gmax, int64_t* __restrict__ matches,
@@ -79,6 +97,17 @@ __global__ void __launch_bounds__(256) match_pass2(const float4* __restrict__ gt
   __shared__ float4 sg[kTile];
   __shared__ float sga[kTile];
   __shared__ uint32_t sm[kTile];
+  const int64_t b = blockIdx.y;
+  gt += b * G;
+  if (gt_labels) gt_labels += b * G;
+  gmax += b * G;
+  boxes += b * bstride;
+  best_val += b * A;
+  best_idx += b * A;
+  matches += b * A;
+  if (labels) labels = (char*)labels + b * A * (mode == 1 ? 4 : 8);
+  if (targets) targets += b * A;
+  G = match_g(G, gcount);
   int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool valid = a < A;
   float4 bx = valid ? boxes[a] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -160,32 +189,56 @@ extern "C" size_t mx_match_workspace(int64_t G, int64_t A) {
   return c.off;
 }
 
-extern "C" int mx_match_assign(const float* gt, const int64_t* gt_labels, int64_t G, const float* boxes, int64_t A,
-                               float high, float low, int allow_lq, int mode, const float* enc_w, int64_t* matches,
-                               void* labels, float* targets, void* ws, size_t ws_bytes, mx_stream_t stream) {
-  MX_CHECK_ARG(G >= 0 && A >= 0, "mx_match_assign: negative sizes");
+extern "C" size_t mx_match_batched_workspace(int64_t B, int64_t G, int64_t A) {
+  Carver c(nullptr, 0);
+  c.take<float>(B * A);
+  c.take<int32_t>(B * A);
+  c.take<uint32_t>(B * G > 0 ? B * G : 1);
+  return c.off;
+}
+
+static int match_launch(const float* gt, const int64_t* gt_labels, const int32_t* gcount, int64_t B, int64_t G,
+                        const float* boxes, int64_t bstride, int64_t A, float high, float low, int allow_lq, int mode,
+                        const float* enc_w, int64_t* matches, void* labels, float* targets, void* ws, size_t ws_bytes,
+                        hipStream_t s) {
+  MX_CHECK_ARG(G >= 0 && A >= 0 && B >= 1 && B <= 65535, "mx_match_assign: bad sizes");
   MX_CHECK_ARG(mode >= 0 && mode <= 2, "mx_match_assign: bad mode %d", mode);
   MX_CHECK_ARG(mode == 0 || labels, "mx_match_assign: labels required for mode %d", mode);
   MX_CHECK_ARG(mode != 2 || G == 0 || gt_labels, "mx_match_assign: gt_labels required for mode 2");
   MX_CHECK_ARG(!targets || enc_w, "mx_match_assign: enc weights required with targets");
   if (A == 0) return MX_OK;
-  hipStream_t s = (hipStream_t)stream;
   Carver c(ws, ws_bytes);
-  float* bv = c.take<float>(A);
-  int32_t* bi = c.take<int32_t>(A);
-  uint32_t* gm = c.take<uint32_t>(G > 0 ? G : 1);
+  float* bv = c.take<float>(B * A);
+  int32_t* bi = c.take<int32_t>(B * A);
+  uint32_t* gm = c.take<uint32_t>(B * G > 0 ? B * G : 1);
   MX_CHECK_ARG(c.ok(), "mx_match_assign: workspace too small (%zu < %zu)", ws_bytes, c.off);
-  int blocks = (int)cdiv(A, 256);
+  const dim3 grid((unsigned)cdiv(A, 256), (unsigned)B);
   if (G > 0) {
-    MX_HIP(hipMemsetAsync(gm, 0, sizeof(uint32_t) * G, s));
-    match_pass1<<<blocks, 256, 0, s>>>((const float4*)gt, G, (const float4*)boxes, A, bv, bi, gm);
+    MX_HIP(hipMemsetAsync(gm, 0, sizeof(uint32_t) * B * G, s));
+    match_pass1<<<grid, 256, 0, s>>>((const float4*)gt, G, gcount, (const float4*)boxes, bstride, A, bv, bi, gm);
     MX_LAUNCH_CHECK();
   }
   float4 w = enc_w ? make_float4(enc_w[0], enc_w[1], enc_w[2], enc_w[3]) : make_float4(1.f, 1.f, 1.f, 1.f);
-  match_pass2<<<blocks, 256, 0, s>>>((const float4*)gt, gt_labels, G, (const float4*)boxes, A, high, low, allow_lq, mode,
-                                     w, bv, bi, gm, matches, labels, (float4*)targets);
+  match_pass2<<<grid, 256, 0, s>>>((const float4*)gt, gt_labels, G, gcount, (const float4*)boxes, bstride, A, high, low,
+                                   allow_lq, mode, w, bv, bi, gm, matches, labels, (float4*)targets);
   MX_LAUNCH_CHECK();
   return MX_OK;
+}
+
+extern "C" int mx_match_assign(const float* gt, const int64_t* gt_labels, int64_t G, const float* boxes, int64_t A,
+                               float high, float low, int allow_lq, int mode, const float* enc_w, int64_t* matches,
+                               void* labels, float* targets, void* ws, size_t ws_bytes, mx_stream_t stream) {
+  return match_launch(gt, gt_labels, nullptr, 1, G, boxes, 0, A, high, low, allow_lq, mode, enc_w, matches, labels,
+                      targets, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int mx_match_assign_batched(const float* gt, const int64_t* gt_labels, const int32_t* gcount, int64_t B,
+                                       int64_t G, const float* boxes, int64_t box_stride, int64_t A, float high, float low,
+                                       int allow_lq, int mode, const float* enc_w, int64_t* matches, void* labels,
+                                       float* targets, void* ws, size_t ws_bytes, mx_stream_t stream) {
+  MX_CHECK_ARG(box_stride == 0 || box_stride >= A, "mx_match_assign_batched: box_stride must be 0 or >= A");
+  return match_launch(gt, gt_labels, gcount, B, G, boxes, box_stride, A, high, low, allow_lq, mode, enc_w, matches,
+                      labels, targets, ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int mx_box_iou(const float* b1, int64_t n, const float* b2, int64_t m, float* out, mx_stream_t stream) {

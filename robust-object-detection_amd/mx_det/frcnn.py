@@ -22,6 +22,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from . import ops
 from .backend import default_backend
 from .conv import ACT_NONE, ACT_RELU, BatchNorm2d, Conv2d, ConvNormAct
 
@@ -271,6 +272,19 @@ class AnchorGenerator(nn.Module):
         return self._cache[key]
 
 
+def _gt_batch(targets, dev):
+    """(boxes [N, G, 4], labels [N, G], counts int32 [N]) of the step's targets, zero-padded to a
+    multiple of 32 GT slots (ops.pad_gt); built once per step and shared by the RPN and RoI heads."""
+    key = tuple((id(t["boxes"]), t["boxes"]._version, id(t["labels"]), t["labels"]._version) for t in targets)
+    c = _gt_batch.cache
+    if c is None or c[0] != key or c[1] != str(dev):
+        c = _gt_batch.cache = (key, str(dev), ops.pad_gt(targets, dev), targets)
+    return c[2]
+
+
+_gt_batch.cache = None
+
+
 def _compact(mask, total):
     """Indices of the True entries of a flat bool mask, ascending, when their number is already
     known on the host (torch.nonzero without its device->host sync)."""
@@ -423,14 +437,19 @@ class RegionProposalNetwork(nn.Module):
             if not self.training:
                 return {}
             # targets, sampling and losses never wait for the GPU
-            labels, reg_targets = [], []
-            for t in targets:
-                _, lab, tg = be.match_assign(t["boxes"], anchors, self.fg, self.bg, True, mode=1,
-                                             weights=RPN_WEIGHTS)
-                labels.append(lab)
-                reg_targets.append(tg)
-            lab = torch.stack(labels)                     # [N, A] 1 / 0 / -1
-            rt = torch.stack(reg_targets)                 # [N, A, 4]
+            if hasattr(be, "match_assign_batched"):  # every image in one launch pair, zero-padded GT
+                gtp, _, gcnt = _gt_batch(targets, anchors.device)
+                _, lab, rt = be.match_assign_batched(gtp, gcnt, anchors, self.fg, self.bg, True, 1,
+                                                     weights=RPN_WEIGHTS)
+            else:
+                labels, reg_targets = [], []
+                for t in targets:
+                    _, lab, tg = be.match_assign(t["boxes"], anchors, self.fg, self.bg, True, mode=1,
+                                                 weights=RPN_WEIGHTS)
+                    labels.append(lab)
+                    reg_targets.append(tg)
+                lab = torch.stack(labels)                 # [N, A] 1 / 0 / -1
+                rt = torch.stack(reg_targets)             # [N, A, 4]
             pm, nm = self.fg_bg_sampler(lab)
             # torchvision: BCE mean over the sampled anchors; smooth-L1 (beta 1/9) sum over the sampled
             # positives / number sampled
@@ -591,21 +610,26 @@ class RoIHeads(nn.Module):
             # reads the number of sampled RoIs
             pb, _, pvalid = proposals
             N, post = pvalid.shape
-            gts = [t["boxes"].float().to(dev) for t in targets]
-            gm = max(1, max(g.shape[0] for g in gts))
+            # GT slots padded to _gt_batch's width (a multiple of 32) on every backend, so the sampler
+            # draws keys over the same [N, post + gm] rows whichever path builds them
+            gtp, glp, gcnt = _gt_batch(targets, dev)
+            gm = gtp.shape[1]
             gslot = torch.arange(gm, device=dev)
-            box_p = torch.zeros((N, post + gm, 4), dtype=torch.float32, device=dev)
-            box_p[:, :post] = pb
-            lab_l, tg_l, val_l = [], [], []
-            for i, (gt, t) in enumerate(zip(gts, targets)):
-                box_p[i, post:post + gt.shape[0]] = gt
-                _, lab, tg = be.match_assign(gt, box_p[i], self.fg, self.bg, False, mode=2,
-                                             gt_labels=t["labels"], weights=ROI_WEIGHTS)
-                lab_l.append(lab.to(dev))
-                tg_l.append(tg.to(dev))
-                val_l.append(torch.cat([pvalid[i], gslot < gt.shape[0]]))
-            lab_p = torch.where(torch.stack(val_l), torch.stack(lab_l), -1)
-            tg_p = torch.stack(tg_l)
+            box_p = torch.cat([pb, gtp], 1)               # [N, post + gm, 4]
+            valid = torch.cat([pvalid, gslot[None, :] < gcnt[:, None]], 1)
+            if hasattr(be, "match_assign_batched"):       # both images in one launch pair
+                _, lab_b, tg_p = be.match_assign_batched(gtp, gcnt, box_p, self.fg, self.bg, False, 2,
+                                                         gt_labels=glp, weights=ROI_WEIGHTS)
+            else:
+                lab_l, tg_l = [], []
+                for i, t in enumerate(targets):
+                    g = int(t["boxes"].shape[0])
+                    _, lab, tg = be.match_assign(gtp[i, :g], box_p[i], self.fg, self.bg, False, mode=2,
+                                                 gt_labels=glp[i, :g], weights=ROI_WEIGHTS)
+                    lab_l.append(lab.to(dev))
+                    tg_l.append(tg.to(dev))
+                lab_b, tg_p = torch.stack(lab_l), torch.stack(tg_l)
+            lab_p = torch.where(valid, lab_b, -1)
             pos_m, neg_m = self.fg_bg_sampler(lab_p, be)
             sm = (pos_m | neg_m).flatten()
             idx = _compact(sm, int(sm.sum()))             # per image ascending, as torch.where per image

@@ -93,6 +93,49 @@ def match_assign(gt_boxes, boxes, high, low, allow_low_quality, mode=0, gt_label
     return matches, labels, targets
 
 
+def match_assign_batched(gt_pad, gcount, boxes, high, low, allow_low_quality, mode, gt_labels=None, weights=None):
+    """match_assign for B images in one launch pair: gt_pad [B, G, 4] (rows >= gcount[b] are padding),
+    gcount int32 [B] on the device, boxes [A, 4] shared by every image or [B, A, 4]. Returns
+    (matches [B, A], labels [B, A], targets [B, A, 4]) as match_assign's modes 1 / 2."""
+    _dev(gt_pad, boxes, gcount)
+    _check(gt_pad.dim() == 3 and gt_pad.shape[2] == 4, "gt_pad must be [B, G, 4]")
+    B, G = gt_pad.shape[0], gt_pad.shape[1]
+    gt = gt_pad.float().contiguous()
+    bx = boxes.float().contiguous()
+    shared = bx.dim() == 2
+    _check(shared or (bx.dim() == 3 and bx.shape[0] == B), "boxes must be [A, 4] or [B, A, 4]")
+    A = bx.shape[-2]
+    dev = bx.device
+    gc = gcount.to(torch.int32).contiguous()
+    matches = torch.empty((B, A), dtype=torch.int64, device=dev)
+    labels = torch.empty((B, A), dtype=torch.float32 if mode == 1 else torch.int64, device=dev) if mode else None
+    if mode == 2:
+        _check(gt_labels is not None and gt_labels.shape[:2] == (B, G), "mode 2 needs gt_labels [B, G]")
+        gt_labels = gt_labels.to(torch.int64).contiguous()
+    targets = torch.empty((B, A, 4), dtype=torch.float32, device=dev) if weights is not None else None
+    w = (_lib.F4)(*weights) if weights is not None else None
+    ws = _ws(_lib.load().mx_match_batched_workspace(B, G, A), dev)
+    call("mx_match_assign_batched", _p(gt), _p(gt_labels) if mode == 2 else None, _p(gc), B, G, _p(bx),
+         0 if shared else A, A, float(high), float(low), int(bool(allow_low_quality)), int(mode), w, _p(matches),
+         _p(labels), _p(targets), _p(ws), ws.numel(), _stream())
+    return matches, labels, targets
+
+
+def pad_gt(targets, dev, multiple=32):
+    """Per-image target boxes / labels -> zero-padded [B, G, 4] / [B, G] batches (G = the largest count
+    rounded up to `multiple`, so a few static shapes recur) + the real counts (int32 [B], device)."""
+    B = len(targets)
+    counts = [int(t["boxes"].shape[0]) for t in targets]
+    G = max(multiple, -(-max(counts) // multiple) * multiple) if B else multiple
+    boxes = torch.zeros((B, G, 4), dtype=torch.float32, device=dev)
+    labels = torch.zeros((B, G), dtype=torch.int64, device=dev)
+    for i, t in enumerate(targets):
+        if counts[i]:
+            boxes[i, :counts[i]] = t["boxes"]
+            labels[i, :counts[i]] = t["labels"]
+    return boxes, labels, torch.tensor(counts, dtype=torch.int32).to(dev, non_blocking=True)
+
+
 # ---------------------------------------------------------------------------------------------
 def batched_nms(boxes, scores, idxs, iou_threshold, group=None, max_seg=None, mode=0):
     """torchvision.ops.batched_nms (CPU dispatch semantics). idxs=None -> plain nms.

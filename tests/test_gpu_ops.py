@@ -101,6 +101,38 @@ def test_roi_matcher_labels(dev):
     np.testing.assert_allclose(tgt.cpu().numpy(), reft, rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("counts", [(0, 3), (55, 300), (33, 1), (0, 0)])
+def test_batched_matcher_equals_per_image(dev, counts):
+    """One launch pair over zero-padded GT (frcnn's RPN and RoI target path) == the per-image matcher,
+    bit for bit: RPN mode over shared anchors, RoI mode over per-image [B, A, 4] candidates."""
+    from mx_det import ops
+    rng = np.random.default_rng(sum(counts) + 7)
+    anchors = torch.from_numpy(_anchors_np()).to(dev)
+    targets = [{"boxes": torch.from_numpy(_rand_boxes(rng, g)).to(dev),
+                "labels": torch.from_numpy(rng.integers(1, 7, g).astype(np.int64)).to(dev)} for g in counts]
+    if counts[1] > 3:
+        targets[1]["boxes"][2] = targets[1]["boxes"][0]  # duplicate gt -> first index wins
+    gtp, glp, gc = ops.pad_gt(targets, dev)
+    assert gtp.shape[1] % 32 == 0 and gtp.shape[1] >= max(counts)
+    m, lab, tg = ops.match_assign_batched(gtp, gc, anchors, 0.7, 0.3, True, 1, weights=(1., 1., 1., 1.))
+    for i, t in enumerate(targets):
+        mi, li, ti = ops.match_assign(t["boxes"], anchors, 0.7, 0.3, True, mode=1, weights=(1., 1., 1., 1.))
+        assert torch.equal(m[i], mi) and torch.equal(lab[i], li)
+        pos = mi >= 0
+        assert torch.equal(tg[i][pos], ti[pos])
+    props = torch.stack([torch.from_numpy(_rand_boxes(rng, 2000, med=40)).to(dev) for _ in counts])
+    cand = torch.cat([props, gtp], 1)
+    m, lab, tg = ops.match_assign_batched(gtp, gc, cand, 0.5, 0.5, False, 2, gt_labels=glp,
+                                          weights=(10., 10., 5., 5.))
+    for i, t in enumerate(targets):
+        mi, li, ti = ops.match_assign(t["boxes"], cand[i], 0.5, 0.5, False, mode=2, gt_labels=t["labels"],
+                                      weights=(10., 10., 5., 5.))
+        real = slice(0, 2000 + counts[i])  # padded candidate rows are masked out by the caller
+        assert torch.equal(m[i][real], mi[real]) and torch.equal(lab[i][real], li[real])
+        pos = mi[real] >= 0
+        assert torch.equal(tg[i][real][pos], ti[real][pos])
+
+
 @pytest.mark.parametrize("n,thr", [(1, 0.7), (50, 0.7), (999, 0.5), (2000, 0.7), (6000, 0.5), (7200, 0.7)])
 def test_nms_bitexact(dev, n, thr):
     from mx_det import ops

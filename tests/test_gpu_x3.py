@@ -311,7 +311,7 @@ def test_x3_bottleneck_bn_partials_from_dgrad_epilogue(dev, monkeypatch):
 
 
 @pytest.mark.parametrize("variant", [4, 5])
-@pytest.mark.parametrize("case", [CASES[i] for i in (0, 2, 4, 5, 7, 8, 9, 11)])
+@pytest.mark.parametrize("case", [CASES[i] for i in (0, 2, 4, 7, 8, 9, 11)])
 def test_x3_wgrad_wide_tiles(dev, monkeypatch, variant, case):
     """The wide wgrad tiles forced for every shape (4: 128 x 256 at 8 waves; 5: 256 x 256 at one wave
     per SIMD, accumulators in AGPRs): K / column counts below or not a multiple of the tile, split and
