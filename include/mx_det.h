@@ -262,6 +262,26 @@ typedef struct {
 size_t mx_conv_pack_plan_bytes(int64_t njobs);
 int mx_conv_pack_batched(const mx_pack_desc* jobs, int64_t njobs, void* plan, size_t plan_bytes, int upload,
                          mx_stream_t stream);
+/* SGD step (torch.optim.SGD semantics, see mx_sgd_step) fused with the per-step conv operand pack:
+ * a parameter with `pack` >= 0 is the f32 weight packs[pack].w, and its update and its wk / wt layouts
+ * (exactly what mx_sgd_step followed by mx_conv_pack_batched would write) come out of one pass; the
+ * others take plain multi-tensor SGD blocks of the same launch (scripts/train_frcnn_baseline.py:149-153,
+ * 174-176: optimizer.step() then the next forward's weights). Fused packs take R*S <= 49.
+ * mx_sgd_pack_build fills a HOST buffer of mx_sgd_pack_plan_bytes(nparams) (no device calls) and
+ * returns the grid size and dynamic LDS bytes; the caller copies it to device memory (stream-ordered)
+ * and launches mx_sgd_pack_step with it and a device array of the nparams gradient pointers. */
+typedef struct {
+  float* p;
+  float* buf;    /* momentum buffer */
+  int64_t n;
+  int32_t first; /* 1: the buffer starts from this step's d (torch's first momentum step) */
+  int32_t pack;  /* index into packs[] or -1 */
+} mx_sgd_param;
+size_t mx_sgd_pack_plan_bytes(int64_t nparams);
+int mx_sgd_pack_build(const mx_sgd_param* params, int64_t nparams, const mx_pack_desc* packs, void* host_plan,
+                      size_t plan_bytes, int64_t* blocks, size_t* lds_bytes);
+int mx_sgd_pack_step(const void* plan, const float* const* grads, int64_t nparams, int64_t blocks, size_t lds_bytes,
+                     float lr, float momentum, float dampening, float weight_decay, int nesterov, mx_stream_t stream);
 /* [K][RS][C] -> [C][RS][K] bf16 (the stride-1 dgrad layout). */
 int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS, int64_t C, uint16_t* wt, mx_stream_t stream);
 int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx, void* ws,

@@ -125,6 +125,20 @@ __device__ __forceinline__ void split8(const float4 a, const float4 b, uint4& hi
     else F<float>(__VA_ARGS__);                                     \
   } while (0)
 
+// torch.optim.SGD's update of one element (scripts/train_frcnn_baseline.py:149-153):
+//   d = g + wd * p;  buf = first ? d : momentum * buf + (1 - dampening) * d;
+//   d = nesterov ? d + momentum * buf : buf;  p -= lr * d
+// Shared by sgd_kernel (mx_optim.hip) and the pack-fused sgd_pack_kernel (mx_conv.hip), both built with
+// the same flags, so the two paths produce the same bits.
+__device__ __forceinline__ float sgd_update(float& p, float g, float& b, bool first, float lr, float momentum,
+                                            float dampening, float wd, int nesterov) {
+  const float d = g + wd * p;
+  b = first ? d : momentum * b + (1.f - dampening) * d;
+  const float u = nesterov ? d + momentum * b : b;
+  p = p - lr * u;
+  return p;
+}
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t v, size_t a = 256) { return (v + a - 1) / a * a; }
 

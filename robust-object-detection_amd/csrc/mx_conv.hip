@@ -18,6 +18,7 @@
 // tiles are staged pixel-major (coalesced) and read transposed with ds_read_b64_tr_b16, split-K
 // over pixels with f32 atomic accumulation.
 #include "mx_common.h"
+#include "mx_dma.h"
 
 #include <vector>
 
@@ -26,7 +27,6 @@ namespace mx {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-#define LDS_AS __attribute__((address_space(3)))
 
 static constexpr int BM = 128, BK = 64, NT = 256;
 
@@ -559,44 +559,6 @@ __device__ __forceinline__ int tile_swz(int row) {
   if (CPR == 8) return row & 7;
   return (row >> 1) & 2;
 }
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  // gfx9 s_waitcnt encoding: vmcnt[3:0], expcnt[6:4], lgkmcnt[11:8], vmcnt_hi[15:14]
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
-
-// LDS-DMA (buffer_load_dwordx4 ... lds, 16 B per lane) issued from inline asm. Through the builtin
-// the compiler tracks the load as an LDS write it cannot place, so SIInsertWaitcnts puts an
-// s_waitcnt vmcnt(0) in front of the first later ds_read that may alias it: in the ring kernels that
-// is the current tile's fragment read, right after the next tiles' DMA was issued -- every K-tile
-// then waited for its successors' loads and the STAGES-deep ring never had more than one tile in
-// flight during the MFMAs. Hidden from the compiler, the loads are ordered only by the kernels'
-// own counted wait_vmcnt<> + barrier (the ring's protocol): ds_reads of tile t never alias the
-// slots being filled. `lds` (M0) and the descriptor are wave-uniform SGPRs; M0 -> LDS-DMA needs one
-// wait state.
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ i32x4 dma_rsrc(const void* base, uint32_t bytes) {
-  const uint64_t a = (uint64_t)base;
-  i32x4 r;
-  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
-  r[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xffffu));
-  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
-  r[3] = 0x00020000;
-  return r;
-}
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(LDS_AS const void*)p);
-}
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"  // M0 is reserved: the kernels using this set it only here
-__device__ __forceinline__ void lds_dma16(i32x4 rsrc, uint32_t lds, uint32_t voff, uint32_t soff) {
-  const int l = __builtin_amdgcn_readfirstlane((int)lds), so = __builtin_amdgcn_readfirstlane((int)soff);
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-               :: "s"(l), "v"(voff), "s"(rsrc), "s"(so) : "memory", "m0");
-}
-#pragma clang diagnostic pop
 
 __device__ __forceinline__ void block_barrier() {
   asm volatile("" ::: "memory");
@@ -2493,6 +2455,174 @@ __global__ void __launch_bounds__(256) pack_batched_kernel(const PackP* __restri
   pack_tile(p, b - prefix[lo]);
 }
 
+// ---------------------------------------------------------------------------------------------
+// SGD step fused with the operand pack: a conv weight's update and its bf16 operand layouts in ONE
+// pass (mx_sgd_pack_step). The per-step order was sgd_kernel (p, g, buf -> p, buf) and then
+// pack_batched_kernel re-reading every updated f32 weight twice (wk tile, wt tile); here a block owns
+// a kr x tc x (all taps) tile of w[K][C][R][S]: it updates the tile in registers (p, buf written back),
+// keeps the (hi, lo) bf16 pair of each new weight in LDS as one u32, and writes both the wk and the wt
+// layout from there. Each weight element is read once and written once per layout, as sgd + pack
+// would produce it (same sgd_update, same rounding). Non-conv parameters take the plain
+// multi-tensor SGD blocks of the same launch.
+struct SgdJob {
+  float* p;
+  float* b;
+  int64_t n;
+  int first, fused;
+  int kr, tc;    // fused tile: kr output rows x tc input channels x all taps (powers of two)
+  int64_t ncb;   // channel blocks (cdiv(Cpad, tc)) per row block
+  PackP pk;      // fused: pk.w == p
+};
+struct SgdHyper {
+  float lr, momentum, dampening, wd;
+  int nesterov;
+};
+static constexpr int SGDP_PER_BLOCK = 2048;
+
+__device__ __forceinline__ uint32_t hilo_word(float v) {  // bf16(v) | bf16(v - bf16(v)) << 16
+  const uint16_t h = f2bf(v);
+  return (uint32_t)h | ((uint32_t)f2bf(v - bf2f(h)) << 16);
+}
+
+__device__ __forceinline__ void sgd_plain_block(const SgdJob& J, const float* __restrict__ g, int64_t blk,
+                                                const SgdHyper& h) {
+  const int64_t e0 = blk * SGDP_PER_BLOCK, e1 = min<int64_t>(J.n, e0 + SGDP_PER_BLOCK);
+  float* __restrict__ p = J.p;
+  float* __restrict__ b = J.b;
+  const bool first = J.first;
+  if (((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)b)) & 15u) == 0) {
+    for (int64_t e = e0 + threadIdx.x * 4; e + 3 < e1; e += 256 * 4) {
+      float4 pv = *(float4*)(p + e), bv = *(float4*)(b + e);
+      const float4 gv = *(const float4*)(g + e);
+      sgd_update(pv.x, gv.x, bv.x, first, h.lr, h.momentum, h.dampening, h.wd, h.nesterov);
+      sgd_update(pv.y, gv.y, bv.y, first, h.lr, h.momentum, h.dampening, h.wd, h.nesterov);
+      sgd_update(pv.z, gv.z, bv.z, first, h.lr, h.momentum, h.dampening, h.wd, h.nesterov);
+      sgd_update(pv.w, gv.w, bv.w, first, h.lr, h.momentum, h.dampening, h.wd, h.nesterov);
+      *(float4*)(p + e) = pv;
+      *(float4*)(b + e) = bv;
+    }
+    const int64_t tail = e0 + ((e1 - e0) & ~(int64_t)3);
+    for (int64_t e = tail + threadIdx.x; e < e1; e += 256)
+      sgd_update(p[e], g[e], b[e], first, h.lr, h.momentum, h.dampening, h.wd, h.nesterov);
+  } else {
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += 256)
+      sgd_update(p[e], g[e], b[e], first, h.lr, h.momentum, h.dampening, h.wd, h.nesterov);
+  }
+}
+
+__device__ __forceinline__ void sgd_pack_tile(const SgdJob& J, const float* __restrict__ g, int64_t t,
+                                              const SgdHyper& h, uint32_t* T) {
+  const PackP& pk = J.pk;
+  const int RS = pk.R * pk.S;
+  const int kr = J.kr, tc = J.tc;
+  const int64_t k0 = (t / J.ncb) * kr, c0 = (t % J.ncb) * tc;
+  const int width = tc * RS, ldt = width + 1;  // odd row stride: column reads spread over the banks
+  const int64_t cend = pk.C < c0 + tc ? pk.C : c0 + tc;
+  const int nvalid = cend > c0 ? (int)((cend - c0) * RS) : 0;
+  const bool first = J.first;
+  float* __restrict__ p = J.p;
+  float* __restrict__ b = J.b;
+  // 1. update the tile: row k's run of nvalid weights starts at (k * C + c0) * RS
+  if ((pk.C & 3) == 0 && ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)b)) & 15u) == 0) {
+    const int w4 = width >> 2, nv4 = nvalid >> 2;
+    const float inv4 = 1.f / (float)w4;
+    for (int e = threadIdx.x; e < kr * w4; e += 256) {
+      const int row = (int)fdiv((uint32_t)e, (uint32_t)w4, inv4), j4 = e - row * w4;
+      const int64_t k = k0 + row;
+      uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
+      if (k < pk.K && j4 < nv4) {
+        const int64_t i = (k * pk.C + c0) * RS + 4 * j4;
+        float4 pv = *(float4*)(p + i), bv = *(float4*)(b + i);
+        const float4 gv = *(const float4*)(g + i);
+        sgd_update(pv.x, gv.x, bv.x, first, h.lr, h.momentum, h.dampening, h.wd, h.nesterov);
+        sgd_update(pv.y, gv.y, bv.y, first, h.lr, h.momentum, h.dampening, h.wd, h.nesterov);
+        sgd_update(pv.z, gv.z, bv.z, first, h.lr, h.momentum, h.dampening, h.wd, h.nesterov);
+        sgd_update(pv.w, gv.w, bv.w, first, h.lr, h.momentum, h.dampening, h.wd, h.nesterov);
+        *(float4*)(p + i) = pv;
+        *(float4*)(b + i) = bv;
+        o0 = hilo_word(pv.x); o1 = hilo_word(pv.y); o2 = hilo_word(pv.z); o3 = hilo_word(pv.w);
+      }
+      uint32_t* d = T + row * ldt + 4 * j4;
+      d[0] = o0; d[1] = o1; d[2] = o2; d[3] = o3;
+    }
+  } else {
+    const float inv = 1.f / (float)width;
+    for (int e = threadIdx.x; e < kr * width; e += 256) {
+      const int row = (int)fdiv((uint32_t)e, (uint32_t)width, inv), j = e - row * width;
+      const int64_t k = k0 + row;
+      uint32_t o = 0;
+      if (k < pk.K && j < nvalid) {
+        const int64_t i = (k * pk.C + c0) * RS + j;
+        float pv = p[i], bv = b[i];
+        sgd_update(pv, g[i], bv, first, h.lr, h.momentum, h.dampening, h.wd, h.nesterov);
+        p[i] = pv;
+        b[i] = bv;
+        o = hilo_word(pv);
+      }
+      T[row * ldt + j] = o;
+    }
+  }
+  __syncthreads();
+  const int np = pk.split ? 2 : 1;
+  // 2. wk [K][R][S][Cpad]: runs of tc channels per (row, tap), written as channel pairs
+  if (pk.wk) {
+    const int h2 = tc >> 1, per = RS * h2;
+    const float inv_per = 1.f / (float)per, inv_h = 1.f / (float)h2;
+    for (int e = threadIdx.x; e < kr * per; e += 256) {
+      const int row = (int)fdiv((uint32_t)e, (uint32_t)per, inv_per), rem = e - row * per;
+      const int rs = (int)fdiv((uint32_t)rem, (uint32_t)h2, inv_h), c2 = rem - rs * h2;
+      const int64_t k = k0 + row, c = c0 + 2 * c2;
+      if (k >= pk.K || c >= pk.Cpad) continue;
+      const uint32_t* tt = T + row * ldt + 2 * c2 * RS + rs;
+      const uint32_t a = tt[0], a2 = tt[RS];  // Cpad is even: c + 1 < Cpad
+      const int64_t dst = (k * RS + rs) * pk.Cpad + c;
+      for (int pl = 0; pl < np; ++pl)
+        *(uint32_t*)(pk.wk + pl * pk.wk_plane + dst) =
+            pl ? (a >> 16) | (a2 & 0xffff0000u) : (a & 0xffffu) | (a2 << 16);
+    }
+  }
+  // 3. wt (dgrad layout): runs along the output channels, written as output-channel pairs
+  if (pk.wt) {
+    const int kr2 = kr >> 1, per = RS * kr2;
+    const float inv_per = 1.f / (float)per, inv_k = 1.f / (float)kr2;
+    for (int e = threadIdx.x; e < tc * per; e += 256) {
+      const int cc = (int)fdiv((uint32_t)e, (uint32_t)per, inv_per), rem = e - cc * per;
+      const int rs = (int)fdiv((uint32_t)rem, (uint32_t)kr2, inv_k), k2 = rem - rs * kr2;
+      const int64_t k = k0 + 2 * k2, c = c0 + cc;
+      if (k >= pk.Kpad || c >= pk.Cpad) continue;
+      const uint32_t* tt = T + 2 * k2 * ldt + cc * RS + rs;
+      const uint32_t a = tt[0], a2 = tt[ldt];  // Kpad is even: k + 1 < Kpad
+      int64_t dst;
+      if (pk.dense) {
+        dst = ((int64_t)rs * pk.Cpad + c) * pk.Kpad + k;
+      } else {
+        const int r = rs / pk.S, sx = rs - r * pk.S;
+        const int q = (r % pk.st_h) * pk.st_w + (sx % pk.st_w);
+        dst = pk.off[q] + ((c * pk.Rc[q] + r / pk.st_h) * pk.Sc[q] + sx / pk.st_w) * pk.Kpad + k;
+      }
+      for (int pl = 0; pl < np; ++pl)
+        *(uint32_t*)(pk.wt + pl * pk.wt_plane + dst) =
+            pl ? (a >> 16) | (a2 & 0xffff0000u) : (a & 0xffffu) | (a2 << 16);
+    }
+  }
+}
+
+// block -> (job, tile or 2048-element chunk) through the prefix sums; grads by job index (their
+// pointers change more often than the job table)
+__global__ void __launch_bounds__(256) sgd_pack_kernel(const SgdJob* __restrict__ jobs, const int64_t* __restrict__ prefix,
+                                                       const float* const* __restrict__ grads, int njobs, SgdHyper h) {
+  extern __shared__ uint32_t Tsm[];
+  const int64_t bidx = blockIdx.x;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (prefix[mid] <= bidx) lo = mid; else hi = mid - 1;
+  }
+  const SgdJob J = jobs[lo];
+  if (J.fused) sgd_pack_tile(J, grads[lo], bidx - prefix[lo], h, Tsm);
+  else sgd_plain_block(J, grads[lo], bidx - prefix[lo], h);
+}
+
 // Host: tile sizes of one pack job (both tile kinds fit PACK_LDS, rows padded by 4 elements)
 static int pack_plan(PackP& p) {
   const int RS = p.R * p.S;
@@ -2969,6 +3099,71 @@ extern "C" int mx_conv_pack_batched(const mx_pack_desc* jobs, int64_t njobs, voi
   }
   if (total == 0) return MX_OK;
   pack_batched_kernel<<<(unsigned)total, 256, 0, st>>>(dj, dp, (int)njobs);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+// fused tile for R*S taps (sgd_pack_tile): 64x64 (1x1), 32x32 (<= 9 taps), 16x16 (<= 49 taps; FC6)
+static bool sgd_tile(int RS, int& kr, int& tc) {
+  if (RS == 1) { kr = 64; tc = 64; return true; }
+  if (RS <= 9) { kr = 32; tc = 32; return true; }
+  if (RS <= 49) { kr = 16; tc = 16; return true; }
+  return false;
+}
+
+extern "C" size_t mx_sgd_pack_plan_bytes(int64_t nparams) {
+  return nparams > 0 ? sizeof(SgdJob) * (size_t)nparams + sizeof(int64_t) * (size_t)(nparams + 1) : 0;
+}
+
+extern "C" int mx_sgd_pack_build(const mx_sgd_param* params, int64_t nparams, const mx_pack_desc* packs,
+                                 void* host_plan, size_t plan_bytes, int64_t* blocks, size_t* lds_bytes) {
+  MX_CHECK_ARG(params && nparams > 0 && nparams < (1 << 20) && blocks && lds_bytes, "sgd pack build: bad lists");
+  MX_CHECK_ARG(host_plan && plan_bytes >= mx_sgd_pack_plan_bytes(nparams), "sgd pack build: plan buffer too small");
+  SgdJob* jobs = (SgdJob*)host_plan;
+  int64_t* prefix = (int64_t*)((char*)host_plan + sizeof(SgdJob) * (size_t)nparams);
+  prefix[0] = 0;
+  size_t lds = 0;
+  for (int64_t j = 0; j < nparams; ++j) {
+    const mx_sgd_param& q = params[j];
+    MX_CHECK_ARG(q.p && q.buf && q.n > 0, "sgd pack build: parameter %lld empty or null", (long long)j);
+    SgdJob J{};
+    J.p = q.p; J.b = q.buf; J.n = q.n; J.first = q.first ? 1 : 0;
+    int64_t nb = cdiv(q.n, SGDP_PER_BLOCK);
+    if (q.pack >= 0) {
+      MX_CHECK_ARG(packs, "sgd pack build: pack index without pack list");
+      const mx_pack_desc& d = packs[q.pack];
+      int64_t tiles = 0;
+      int rc = make_pack(d, J.pk, tiles);
+      if (rc) return rc;
+      const int RS = d.R * d.S;
+      MX_CHECK_ARG(d.w == q.p && d.Kout * d.Cin * RS == q.n, "sgd pack build: pack %lld is not parameter %lld",
+                   (long long)q.pack, (long long)j);
+      MX_CHECK_ARG(sgd_tile(RS, J.kr, J.tc), "sgd pack build: %d taps (fused packing takes <= 49)", RS);
+      MX_CHECK_ARG(d.wk || d.wt, "sgd pack build: pack %lld has no layout", (long long)q.pack);
+      J.fused = 1;
+      J.ncb = cdiv(J.pk.Cpad, J.tc);
+      nb = cdiv(J.pk.Kpad, J.kr) * J.ncb;
+      const size_t need = sizeof(uint32_t) * (size_t)J.kr * (size_t)(J.tc * RS + 1);
+      if (need > lds) lds = need;
+    }
+    jobs[j] = J;
+    prefix[j + 1] = prefix[j] + nb;
+  }
+  MX_CHECK_ARG(prefix[nparams] < (1ll << 31), "sgd pack build: too many blocks");
+  *blocks = prefix[nparams];
+  *lds_bytes = lds;
+  return MX_OK;
+}
+
+extern "C" int mx_sgd_pack_step(const void* plan, const float* const* grads, int64_t nparams, int64_t blocks,
+                                size_t lds_bytes, float lr, float momentum, float dampening, float weight_decay,
+                                int nesterov, mx_stream_t stream) {
+  MX_CHECK_ARG(plan && grads && nparams > 0 && blocks > 0 && blocks < (1ll << 31) && lds_bytes <= 65536,
+               "sgd pack step: bad plan");
+  const SgdJob* jobs = (const SgdJob*)plan;
+  const int64_t* prefix = (const int64_t*)((const char*)plan + sizeof(SgdJob) * (size_t)nparams);
+  SgdHyper h{lr, momentum, dampening, weight_decay, nesterov};
+  sgd_pack_kernel<<<(unsigned)blocks, 256, lds_bytes, (hipStream_t)stream>>>(jobs, prefix, grads, (int)nparams, h);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

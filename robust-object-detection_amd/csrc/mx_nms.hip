@@ -18,6 +18,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "mx_common.h"
+#include "mx_dma.h"
 
 namespace mx {
 
@@ -275,20 +276,38 @@ __global__ void __launch_bounds__(256) nms_scan_lds_kernel(const uint64_t* __res
 }
 
 // Single-wave scan (segments of up to 64*SCAN_WAVE_W boxes): one 64-lane workgroup per segment and
-// no workgroup barriers. Lane w keeps the removed bits of word w in a register; per 64-row block the
-// rows' words blk..W-1 are double-buffered in LDS (lane t loads row t's words into registers for the
-// next block while this block is resolved; odd LDS row stride), the in-tile chain is walked wave-uniformly over the survivors (as in
-// nms_scan_lds_kernel), and lane w ORs the kept rows' word w from LDS, four independent reads at a
-// time. Same greedy result; ~1 us per 64-row block instead of ~4 with three barriers per block.
+// no workgroup barriers. A 64-row block's mask rows are one contiguous run of 64*Wm words; it is
+// copied whole into an LDS ring slot by LDS-DMA (16 coalesced 1 KiB buffer_load_dwordx4 ... lds, plus
+// one for the block's 64 box ids), SCAN_RING - 1 blocks ahead of the one being resolved, so the
+// dependent walk waits on L2/MALL latency once per segment instead of once per block. Lane w keeps the
+// removed bits of word w in a register; the in-tile chain is walked wave-uniformly over the survivors
+// (as in nms_scan_lds_kernel) and lanes w and w + 32 OR the kept rows' word w from LDS (half the rows
+// each, eight reads in flight), combined with one cross-lane permute.
+// Same greedy result as nms_scan_kernel. Every block issues exactly SCAN_DMA VMEM instructions
+// (slots past the rows read out of range -> zero) and one flags store, so the counted waits are exact.
 static constexpr int SCAN_WAVE_W = 32;
+static constexpr int SCAN_RING = 4;
+static constexpr int SCAN_SLOT = 64 * SCAN_WAVE_W * 8 + 256;  // bytes: rows + box ids
+static constexpr int SCAN_DMA = 17;
+
+__device__ __forceinline__ void scan_wait(int ahead) {  // DMA of the block `ahead` blocks before the newest done
+  if (ahead >= 2) wait_vmcnt<2 * SCAN_DMA>();
+  else if (ahead == 1) wait_vmcnt<SCAN_DMA>();
+  else wait_vmcnt<0>();
+}
+
 __global__ void __launch_bounds__(64) nms_scan_wave_kernel(const uint64_t* __restrict__ mask,
                                                            const int32_t* __restrict__ seg_start,
                                                            const int32_t* __restrict__ nseg_p,
                                                            const int32_t* __restrict__ svals, int Wm,
                                                            int32_t* __restrict__ flags, int32_t* __restrict__ nkeep) {
-  extern __shared__ uint64_t sm[];  // [2][64][Wm + 1]
+  extern __shared__ __attribute__((aligned(16))) uint8_t smb[];  // [SCAN_RING][SCAN_SLOT]
   const int lane = threadIdx.x;
   const int nseg = *nseg_p;
+  const int64_t ntot = seg_start[nseg];
+  const i32x4 mrs = dma_rsrc(mask, (uint32_t)(ntot * Wm * 8)), vrs = dma_rsrc(svals, (uint32_t)(ntot * 4));
+  const uint32_t lds0 = lds_addr(smb);
+  const int nrow_inst = (Wm + 1) >> 1;  // 1 KiB per instruction: 64 rows x Wm words = Wm / 2 KiB
   for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
     const int64_t s0 = seg_start[seg], len = seg_start[seg + 1] - s0;
     const int W = (int)((len + 63) / 64);
@@ -296,35 +315,24 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(const uint64_t* __res
       if (lane == 0) atomicExch(nkeep, (int32_t)0x80000000);
       continue;
     }
+    auto issue = [&](int b) {
+      const uint32_t dst = lds0 + (uint32_t)((b % SCAN_RING) * SCAN_SLOT);
+      const uint32_t src = (uint32_t)((s0 + 64 * (int64_t)b) * Wm * 8);
+#pragma unroll
+      for (int i = 0; i < SCAN_DMA - 1; ++i)
+        lds_dma16(mrs, dst + i * 1024, i < nrow_inst ? src + i * 1024 + lane * 16 : 0xfffffff0u, 0);
+      lds_dma4(vrs, dst + 64 * SCAN_WAVE_W * 8, (uint32_t)((s0 + 64 * (int64_t)b) * 4) + lane * 4, 0);
+    };
+    for (int b = 0; b < SCAN_RING - 1 && b < W; ++b) issue(b);
     uint64_t rem = 0;  // removed bits of word `lane`
-    uint64_t pre[SCAN_WAVE_W];
-    const int RS = Wm + 1;  // LDS row stride in words (odd: row-strided lane access is 2-way banked)
-    // block b: lane t loads its row's words b..W-1 (row-contiguous 8-B loads)
-    auto fetch = [&](int b) {
-      const int64_t rb = s0 + (int64_t)b * 64;
-      const int c = (int)min<int64_t>(64, len - (int64_t)b * 64), nw = W - b;
-      const uint64_t* src = mask + (rb + lane) * Wm + b;
-#pragma unroll
-      for (int i = 0; i < SCAN_WAVE_W; ++i)
-        if (i < nw && lane < c) pre[i] = src[i];
-    };
-    auto stash = [&](int b) {
-      uint64_t* rows = sm + (b & 1) * 64 * RS + lane * RS + b;
-      const int c = (int)min<int64_t>(64, len - (int64_t)b * 64), nw = W - b;
-#pragma unroll
-      for (int i = 0; i < SCAN_WAVE_W; ++i)
-        if (i < nw && lane < c) rows[i] = pre[i];
-    };
-    fetch(0);
-    stash(0);
     int kept_total = 0;
     for (int blk = 0; blk < W; ++blk) {
-      if (blk + 1 < W) fetch(blk + 1);  // in flight while this block is resolved
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this block's LDS rows are written
-      const uint64_t* rows = sm + (blk & 1) * 64 * RS;
-      const int64_t rbase = s0 + (int64_t)blk * 64;
+      scan_wait(min(W - 1, blk + SCAN_RING - 2) - blk);
+      const uint8_t* slot = smb + (blk % SCAN_RING) * SCAN_SLOT;
+      const uint64_t* rows = (const uint64_t*)slot;
+      const int32_t* ids = (const int32_t*)(slot + 64 * SCAN_WAVE_W * 8);
       const int cnt = (int)min<int64_t>(64, len - (int64_t)blk * 64);
-      const uint64_t diag = lane < cnt ? rows[lane * RS + blk] : 0ull;
+      const uint64_t diag = lane < cnt ? rows[lane * Wm + blk] : 0ull;
       const uint64_t rm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(rem >> 32), blk) << 32) |
                           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rem, blk);
       const uint64_t valid = cnt >= 64 ? ~0ull : ((1ull << cnt) - 1);
@@ -339,27 +347,44 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(const uint64_t* __res
         cur |= row;
         avail = ~cur & valid & ~((2ull << t) - 1ull);
       }
-      if (lane < cnt && ((kept >> lane) & 1ull)) flags[svals[rbase + lane]] = 1;
+      // flags were zeroed by the keys kernel: every lane < cnt (>= 1 of them) stores, so each block
+      // issues exactly one store instruction
+      if (lane < cnt) flags[ids[lane]] = (int32_t)((kept >> lane) & 1ull);
       kept_total += __popcll(kept);
-      // lane w > blk: OR of the kept rows' word w
-      if (lane > blk && lane < W) {
-        uint64_t acc = 0, k = kept;
-        while (k) {
-          const int t0 = __builtin_ctzll(k);
-          k &= k - 1;
-          const int t1 = k ? __builtin_ctzll(k) : t0;
-          k &= k ? k - 1 : 0ull;
-          const int t2 = k ? __builtin_ctzll(k) : t0;
-          k &= k ? k - 1 : 0ull;
-          const int t3 = k ? __builtin_ctzll(k) : t0;
-          k &= k ? k - 1 : 0ull;
-          acc |= rows[t0 * RS + lane] | rows[t1 * RS + lane] | rows[t2 * RS + lane] | rows[t3 * RS + lane];
+      // word w = lane & 31 of the kept rows: lanes < 32 take rows 0..31, lanes >= 32 rows 32..63 (per-lane
+      // bit walks, 8 independent LDS reads per round), then the halves are combined across lanes
+      uint64_t acc = 0;
+      const int w = lane & 31;
+      if (w > blk && w < W) {
+        uint32_t m = lane < 32 ? (uint32_t)kept : (uint32_t)(kept >> 32);
+        const uint64_t* base = rows + (lane < 32 ? 0 : 32) * Wm + w;
+        while (m) {
+          int t[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            t[i] = m ? __builtin_ctz(m) : -1;
+            m &= m - 1;
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (t[i] >= 0) acc |= base[t[i] * Wm];
         }
-        rem |= acc;
       }
-      if (blk + 1 < W) stash(blk + 1);
+      {
+        const int src = (lane ^ 32) << 2;
+        const uint32_t olo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)acc);
+        const uint32_t ohi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(acc >> 32));
+        rem |= acc | ((uint64_t)ohi << 32) | olo;  // lanes < 32 hold the removed words
+      }
+      // the slot refilled next is the one resolved in the previous iteration: its ds_reads returned
+      // (their results were consumed) before this point
+      if (blk + SCAN_RING - 1 < W) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this block's LDS reads are done
+        issue(blk + SCAN_RING - 1);
+      }
     }
     if (lane == 0 && kept_total) atomicAdd(nkeep, kept_total);
+    wait_vmcnt<0>();  // the next segment's DMA must not land while a straggling store is counted
   }
 }
 
@@ -578,7 +603,7 @@ extern "C" int mx_batched_nms(const float* boxes, const float* scores, const int
   MX_LAUNCH_CHECK();
   int sgrid = (int)std::min<int64_t>(n, 1024);
   if (Wm <= SCAN_WAVE_W)
-    nms_scan_wave_kernel<<<sgrid, 64, sizeof(uint64_t) * 2 * 64 * (size_t)(Wm + 1), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
+    nms_scan_wave_kernel<<<sgrid, 64, (size_t)SCAN_RING * SCAN_SLOT, s>>>(w.mask, w.seg_start, w.nseg, w.v1,
                                                                                    Wm, w.flags, w.nk);
   else if (Wm <= SCAN_LDS_W)
     nms_scan_lds_kernel<<<sgrid, 256, sizeof(uint64_t) * (Wm + 64 * (size_t)Wm), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
@@ -644,7 +669,7 @@ extern "C" int mx_batched_nms_grouped(const float* boxes, const float* scores, c
   MX_LAUNCH_CHECK();
   const int sgrid = (int)std::min<int64_t>(n, 1024);
   if (Wm <= SCAN_WAVE_W)
-    nms_scan_wave_kernel<<<sgrid, 64, sizeof(uint64_t) * 2 * 64 * (size_t)(Wm + 1), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
+    nms_scan_wave_kernel<<<sgrid, 64, (size_t)SCAN_RING * SCAN_SLOT, s>>>(w.mask, w.seg_start, w.nseg, w.v1,
                                                                                    Wm, w.flags, w.nk);
   else if (Wm <= SCAN_LDS_W)
     nms_scan_lds_kernel<<<sgrid, 256, sizeof(uint64_t) * (Wm + 64 * (size_t)Wm), s>>>(w.mask, w.seg_start, w.nseg, w.v1,

@@ -26,11 +26,7 @@ struct SgdArgs {
 };
 
 __device__ __forceinline__ float sgd1(float& p, float g, float& b, bool first, const SgdArgs& a) {
-  const float d = g + a.wd * p;
-  b = first ? d : a.momentum * b + (1.f - a.dampening) * d;
-  const float u = a.nesterov ? d + a.momentum * b : b;
-  p = p - a.lr * u;
-  return p;
+  return sgd_update(p, g, b, first, a.lr, a.momentum, a.dampening, a.wd, a.nesterov);
 }
 
 __global__ void __launch_bounds__(256) sgd_kernel(SgdArgs a) {

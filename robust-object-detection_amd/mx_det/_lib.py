@@ -134,6 +134,9 @@ _SIGS = {
     "mx_act_bias_bwd": (c_int, [c_vp, c_vp, c_int, c_i64, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp,
                                 ctypes.c_size_t, c_vp]),
     "mx_sgd_step": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_f, c_f, c_int, c_vp]),
+    "mx_sgd_pack_plan_bytes": (ctypes.c_size_t, [c_i64]),
+    "mx_sgd_pack_build": (c_int, [c_vp, c_i64, c_vp, c_vp, ctypes.c_size_t, c_vp, c_vp]),
+    "mx_sgd_pack_step": (c_int, [c_vp, c_vp, c_i64, c_i64, ctypes.c_size_t, c_f, c_f, c_f, c_f, c_int, c_vp]),
     "mx_bn_apply": (c_int, [c_vp, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
     "mx_bn_bwd_reduce": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
     "mx_bn_bwd_apply": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -323,6 +323,37 @@ class WeightPacker:
         self.entries[k] = e
         self.order.append(k)
 
+    @staticmethod
+    def desc(e):
+        K, C, R, S = e.w.shape
+        return PackDesc(e.w.data_ptr(), e.wk.data_ptr(), e.wt.data_ptr() if e.wt is not None else None,
+                        C, K, e.cp, e.kp, R, S, e.stride[0], e.stride[1], e.pad[0], e.pad[1],
+                        (1 if e.dense else 0) | (2 if e.split else 0))
+
+    def fusable(self, params):
+        """Per parameter: the entry whose packing mx_sgd_pack_step can fold into the parameter's SGD
+        update (the parameter's only entry, covering all of it, <= 49 taps), else None."""
+        by_ptr = {}
+        for k in self.order:
+            e = self.entries[k]
+            by_ptr.setdefault(e.w.data_ptr(), []).append(e)
+        out = []
+        for p in params:
+            es = by_ptr.get(p.data_ptr(), ())
+            e = es[0] if len(es) == 1 else None
+            if e is not None and not (e.w.numel() == p.numel() and e.w.is_contiguous() and p.is_contiguous()
+                                      and e.w.shape[2] * e.w.shape[3] <= 49):
+                e = None
+            out.append(e)
+        return out
+
+    @staticmethod
+    def mark_packed(entries):
+        """The optimizer wrote these entries' operands along with the update (mx_sgd_pack_step)."""
+        for e in entries:
+            if e is not None:
+                e.version = e.w._version
+
     def refresh(self):
         dirty = [k for k in self.order if self.entries[k].version != self.entries[k].w._version]
         if not dirty:
@@ -331,11 +362,7 @@ class WeightPacker:
         if upload:
             descs = (PackDesc * len(dirty))()
             for i, k in enumerate(dirty):
-                e = self.entries[k]
-                K, C, R, S = e.w.shape
-                descs[i] = PackDesc(e.w.data_ptr(), e.wk.data_ptr(), e.wt.data_ptr() if e.wt is not None else None,
-                                    C, K, e.cp, e.kp, R, S, e.stride[0], e.stride[1], e.pad[0], e.pad[1],
-                                    (1 if e.dense else 0) | (2 if e.split else 0))
+                descs[i] = self.desc(self.entries[k])
             nb = _lib.load().mx_conv_pack_plan_bytes(len(dirty))
             self._plan = torch.empty(nb, dtype=torch.uint8, device=self.entries[dirty[0]].w.device)
             self._descs = descs
@@ -359,6 +386,10 @@ _packer = None
 def set_packer(p):
     global _packer
     _packer = p
+
+
+def get_packer():
+    return _packer
 
 
 def operands(w, cin_pad, stride, pad, kpad, dgrad, dense=False, split=False):

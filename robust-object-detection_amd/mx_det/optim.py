@@ -8,11 +8,22 @@ instead of torch's foreach path (three multi_tensor_apply launches plus host-sid
 Parameters that are not f32 CUDA tensors (e.g. a CPU model) take torch's own implementation.
 """
 import ctypes
+import os
 
 import torch
 from torch.autograd.graph import increment_version
 
 from . import _lib
+
+
+# MX_SGD_PACK=0: keep the update and the conv operand repack as two launches (sgd_kernel, then
+# WeightPacker.refresh's pack_batched_kernel before the next forward)
+_SGD_PACK = int(os.environ.get("MX_SGD_PACK", "1"))
+
+
+class _SgdParam(ctypes.Structure):  # mx_sgd_param
+    _fields_ = [("p", ctypes.c_void_p), ("buf", ctypes.c_void_p), ("n", ctypes.c_int64), ("first", ctypes.c_int32),
+                ("pack", ctypes.c_int32)]
 
 
 class SGD(torch.optim.SGD):
@@ -28,6 +39,8 @@ class SGD(torch.optim.SGD):
                 loss = closure()
         fast = self.__dict__.setdefault("_fast", {})
         for group in self.param_groups:
+            if self._pack_step(group):
+                continue
             if self._fast_step(group, fast):
                 continue
             ps = [p for p in group["params"] if p.grad is not None]
@@ -63,6 +76,71 @@ class SGD(torch.optim.SGD):
                     group["params"], n, P, B, N, (ctypes.c_uint8 * n)(), bufs, [p.data_ptr() for p in ps],
                     [b.data_ptr() for b in bufs])
         return loss
+
+    def _pack_step(self, group):
+        """Conv weights registered with the current WeightPacker (mx_det.conv.get_packer) get their
+        bf16 operands written by the update itself (mx_sgd_pack_step: one launch for the whole group,
+        no separate repack of the new weights before the next forward). Returns False to take the
+        other paths (no packer, nothing to fold, or a case the multi-tensor kernel does not cover)."""
+        from . import conv as mc
+        pk = mc.get_packer()
+        if pk is None or _SGD_PACK == 0:
+            return False
+        ps = group["params"]
+        if (not ps or group.get("maximize") or group["momentum"] == 0 or
+                any(p.grad is None or not p.is_cuda or p.dtype != torch.float32 or p.grad.is_sparse or
+                    not p.is_contiguous() or not p.grad.is_contiguous() for p in ps)):
+            return False
+        cache = self.__dict__.setdefault("_pk", {})
+        c = cache.get(id(group))
+        if c is None or c["ps"] is not ps or c["packer"] is not pk or c["pptr"] != [p.data_ptr() for p in ps]:
+            entries = pk.fusable(ps)
+            if not any(e is not None for e in entries):
+                return False
+            c = cache[id(group)] = {"ps": ps, "packer": pk, "pptr": [p.data_ptr() for p in ps],
+                                    "entries": entries, "key": None, "gkey": None}
+        n = len(ps)
+        first = []
+        bufs = []
+        for p in ps:
+            st = self.state[p]
+            b = st.get("momentum_buffer")
+            if b is None:
+                b = st["momentum_buffer"] = torch.empty_like(p, memory_format=torch.contiguous_format)
+                first.append(1)
+            else:
+                first.append(0)
+            bufs.append(b)
+        key = (tuple(b.data_ptr() for b in bufs), tuple(first))
+        dev = ps[0].device
+        if key != c["key"]:
+            entries = c["entries"]
+            packs = [e for e in entries if e is not None]
+            descs = (mc.PackDesc * len(packs))(*[pk.desc(e) for e in packs])
+            prm = (_SgdParam * n)()
+            j = 0
+            for i, (p, b, e) in enumerate(zip(ps, bufs, entries)):
+                prm[i] = _SgdParam(p.data_ptr(), b.data_ptr(), p.numel(), first[i], j if e is not None else -1)
+                j += e is not None
+            lib = _lib.load()
+            nb = lib.mx_sgd_pack_plan_bytes(n)
+            host = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+            blocks, lds = ctypes.c_int64(0), ctypes.c_size_t(0)
+            _lib.call("mx_sgd_pack_build", prm, n, descs, host.data_ptr(), nb, ctypes.byref(blocks),
+                      ctypes.byref(lds))
+            c["plan"] = host.to(dev, non_blocking=True)
+            c["blocks"], c["lds"], c["key"], c["bufs"] = blocks.value, lds.value, key, bufs
+        gptr = [p.grad.data_ptr() for p in ps]
+        if gptr != c["gkey"]:
+            c["gdev"] = torch.tensor(gptr, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+            c["gkey"] = gptr
+        _lib.call("mx_sgd_pack_step", c["plan"].data_ptr(), c["gdev"].data_ptr(), n, c["blocks"], c["lds"],
+                  float(group["lr"]), float(group["momentum"]), float(group["dampening"]),
+                  float(group["weight_decay"]), int(group["nesterov"]), _lib.stream())
+        increment_version(ps)
+        increment_version(bufs)
+        pk.mark_packed(c["entries"])
+        return True
 
     def _fast_step(self, group, fast):
         """Steady state: every parameter of the group has a grad and a momentum buffer, and the

@@ -396,3 +396,62 @@ def test_conv_tuner_candidates(dev, monkeypatch, ci, N, H, W, C, K, k, st, pd):
     monkeypatch.setattr(mc, "_WG_CANDS", (mc._WG_CANDS[ci % len(mc._WG_CANDS)],))
     test_conv_fwd(dev, 7, N, H, W, C, K, k, st, pd)
     test_conv_dgrad_wgrad(dev, 7, N, H, W, C, K, k, st, pd)
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_sgd_fused_pack_equals_sgd_then_refresh(dev, split, monkeypatch):
+    """mx_sgd_pack_step (update + wk/wt written in one pass) == sgd_kernel followed by the packer's
+    batched repack, bit for bit: parameters, momentum buffers and every packed layout over 3 steps
+    (1x1, 3x3 s1/s2, a 1x1 s2 without dgrad layout, narrow K, odd C, FC6 as a dense 7x7 view, FC7, and
+    plain parameters sharing the launch); frozen / unregistered weights untouched."""
+    from mx_det import conv as mc, optim
+    g = torch.Generator().manual_seed(11)
+    specs = [((256, 64, 1, 1), (1, 1), (0, 0), True), ((128, 128, 3, 3), (2, 2), (1, 1), True),
+             ((64, 64, 3, 3), (1, 1), (1, 1), True), ((512, 256, 1, 1), (2, 2), (0, 0), False),
+             ((15, 256, 1, 1), (1, 1), (0, 0), True), ((32, 3, 3, 3), (1, 1), (1, 1), True)]
+
+    def build():
+        gg = torch.Generator().manual_seed(5)
+        ws = [torch.nn.Parameter((torch.randn(*shp, generator=gg) * 0.1).to(dev)) for shp, _, _, _ in specs]
+        fc6 = torch.nn.Parameter((torch.randn(1024, 256 * 49, generator=gg) * 0.01).to(dev))
+        fc7 = torch.nn.Parameter((torch.randn(1024, 1024, generator=gg) * 0.01).to(dev))
+        extra = [torch.nn.Parameter(torch.randn(n, generator=gg).to(dev)) for n in (1024, 77, 5)]
+        pk = mc.WeightPacker()
+        for w, (_, st, pd, dg) in zip(ws, specs):
+            pk.register(w, st, pd, dg, split=split)
+        pk.register(fc6.view(1024, 256, 7, 7), (1, 1), (0, 0), True, dense=True, split=split)
+        pk.register(fc7.view(1024, 1024, 1, 1), (1, 1), (0, 0), True, split=split)
+        params = ws + [fc6, fc7] + extra
+        return pk, params
+
+    grads = None
+    out = []
+    for fused in (1, 0):
+        monkeypatch.setattr(optim, "_SGD_PACK", fused)
+        pk, params = build()
+        mc.set_packer(pk)
+        pk.refresh()
+        opt = optim.SGD(params, lr=0.02, momentum=0.9, weight_decay=5e-4)
+        if grads is None:
+            grads = [[torch.randn(p.shape, generator=g).to(dev) * 0.1 for p in params] for _ in range(3)]
+        for step in range(3):
+            for p, gr in zip(params, grads[step]):
+                p.grad = gr.clone()
+            opt.step()
+            if fused:
+                assert all(pk.entries[k].version == pk.entries[k].w._version for k in pk.order)
+            pk.refresh()  # fused: nothing dirty, no launch
+        torch.cuda.synchronize()
+        packed = [(pk.entries[k].wk.clone(), None if pk.entries[k].wt is None else pk.entries[k].wt.clone())
+                  for k in pk.order]
+        out.append(([p.detach().clone() for p in params],
+                    [opt.state[p]["momentum_buffer"].clone() for p in params], packed))
+        mc.set_packer(None)
+    (pa, ba, ka), (pb, bb, kb) = out
+    for x, y in zip(pa, pb):
+        assert torch.equal(x, y)
+    for x, y in zip(ba, bb):
+        assert torch.equal(x, y)
+    for (wk1, wt1), (wk2, wt2) in zip(ka, kb):
+        assert torch.equal(wk1, wk2)
+        assert (wt1 is None) == (wt2 is None) and (wt1 is None or torch.equal(wt1, wt2))
