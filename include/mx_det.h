@@ -182,6 +182,15 @@ int mx_normalize_pad(const uint8_t* img, int64_t B, int64_t H, int64_t W, const 
 int mx_resize_normalize_pad(const uint8_t* const* imgs, const int64_t* Hs, const int64_t* Ws, const int64_t* nhs,
                             const int64_t* nws, int64_t B, const float* mean3_host, const float* std3_host,
                             int64_t Hp, int64_t Wp, int64_t Cp, int dtype, void* out, mx_stream_t stream);
+/* RPN head outputs -> torchvision's concatenated (objectness [N, Atot], pred_deltas [N, Atot, 4]) in
+ * one pass (concat_box_prediction_layers, rpn.py; the reference model's RPN via train_frcnn_baseline.py:171)
+ * and the reverse for the backward. o0: level 0's [N, H0, W0, 5A] head output (A logits then A x 4
+ * deltas per pixel); ocv: the [N, Hc, Wc, 5A] canvas holding levels 1..ncv at rects[l] = (y, x, h, w).
+ * merge writes every element of g0 / gcv (frame pixels 0; gobj / gdel nullable = zero). */
+int mx_rpn_head_split(const float* o0, int64_t H0, int64_t W0, const float* ocv, int64_t Hc, int64_t Wc,
+                      const int32_t* rects, int ncv, int64_t N, int A, float* obj, float* del, mx_stream_t stream);
+int mx_rpn_head_merge(const float* gobj, const float* gdel, int64_t H0, int64_t W0, int64_t Hc, int64_t Wc,
+                      const int32_t* rects, int ncv, int64_t N, int A, float* g0, float* gcv, mx_stream_t stream);
 /* The same for the reference loader's own image tensors: ToDtype(float32, scale=True) output, f32 CHW
  * [3, Hs[b], Ws[b]] contiguous (train_frcnn_baseline.py:50-54 build_transforms, fed to the model at :171).
  * A float image equal to u8 * (float)(1/255) gives the bit-identical batch of mx_resize_normalize_pad;

@@ -132,10 +132,12 @@ __device__ __forceinline__ void split8(const float4 a, const float4 b, uint4& hi
 // the same flags, so the two paths produce the same bits.
 __device__ __forceinline__ float sgd_update(float& p, float g, float& b, bool first, float lr, float momentum,
                                             float dampening, float wd, int nesterov) {
-  const float d = g + wd * p;
-  b = first ? d : momentum * b + (1.f - dampening) * d;
-  const float u = nesterov ? d + momentum * b : b;
-  p = p - lr * u;
+  // explicit fused multiply-adds: the same rounding in every kernel that inlines this, whatever
+  // contraction the compiler would pick around it
+  const float d = __fmaf_rn(wd, p, g);
+  b = first ? d : __fmaf_rn(momentum, b, __fmul_rn(1.f - dampening, d));
+  const float u = nesterov ? __fmaf_rn(momentum, b, d) : b;
+  p = __fmaf_rn(-lr, u, p);
   return p;
 }
 

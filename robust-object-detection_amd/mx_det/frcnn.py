@@ -210,42 +210,56 @@ class RPNHead(nn.Module):
                 t = t * mask  # zero frame between levels: the next 3x3 conv reads it as padding
         return be.conv(t, w, b, (1, 1), (0, 0), ACT_NONE, out_dtype=torch.float32)  # [N,H,W,A*5]
 
-    def forward(self, feats, be):
-        """torchvision RPNHead.forward per level. The small levels (all but the first, P3..P6) run as ONE
-        conv chain over a zero canvas that holds each level framed by zero rows / columns: a 3x3 conv
-        with padding 1 then sees exactly each level's own neighbourhood, and the ReLU outputs on the
-        frame are zeroed before the next 3x3 conv -- the same arithmetic per output element as per-level
-        convs, in 2 launches per conv instead of 5 (the P4..P6 maps are too small to fill the GPU alone).
-        The shared weights' gradients then sum the canvas pixels in one wgrad (frame pixels add exact
-        zeros). MX_RPN_CANVAS=0 runs every level separately."""
-        A = self.cls_logits.weight.shape[0]
+    def layout(self, feats):
+        """Static per input shape: (canvas?, level (h, w)s, canvas rectangles (y, x, h, w) of levels 1..,
+        canvas (Hc, Wc)). MX_RPN_CANVAS=0 runs every level separately."""
+        hws = [tuple(f.shape[1:3]) for f in feats]
+        canvas = len(feats) >= 3 and os.environ.get("MX_RPN_CANVAS", "1") != "0"
+        if not canvas:
+            return False, hws, [], (0, 0)
+        pos, Hc, Wc = self.canvas_layout(hws[1:])
+        return True, hws, [(y, x, h, w) for (y, x), (h, w) in zip(pos, hws[1:])], (Hc, Wc)
+
+    def raw(self, feats, be):
+        """The head's conv outputs [N, H, W, 5A] (A logits, A x 4 deltas per pixel): level 0 alone and, on
+        the canvas path, ONE map for the small levels (P3..P6) -- each framed by zero rows / columns on
+        a zero canvas, so a 3x3 conv with padding 1 sees exactly each level's own neighbourhood and the
+        ReLU outputs on the frame are zeroed before the next 3x3 conv: the same arithmetic per output
+        element as per-level convs, in 2 launches per conv instead of 5 (the P4..P6 maps are too small
+        to fill the GPU alone). The shared weights' gradients then sum the canvas pixels in one wgrad
+        (frame pixels add exact zeros). Without the canvas: one map per level."""
         w = torch.cat([self.cls_logits.weight, self.bbox_pred.weight])
         b = torch.cat([self.cls_logits.bias, self.bbox_pred.bias])
-        L = len(feats)
-        outs = [None] * L
-        canvas = L >= 3 and os.environ.get("MX_RPN_CANVAS", "1") != "0"
-        for i in ([0] if canvas else range(L)):
-            outs[i] = self._run(feats[i], be, w, b)
-        if canvas:
-            small = list(range(1, L))
-            hws = [tuple(feats[i].shape[1:3]) for i in small]
-            pos, Hc, Wc = self.canvas_layout(hws)
-            f0 = feats[small[0]]
-            N, C = f0.shape[0], f0.shape[3]
-            cv = f0.new_zeros((N, Hc, Wc, C))
-            mask = f0.new_zeros((1, Hc, Wc, 1))
-            for i, (h, wd), (y, x) in zip(small, hws, pos):
-                cv[:, y:y + h, x:x + wd] = feats[i]
-                mask[:, y:y + h, x:x + wd] = 1
-            o = self._run(cv, be, w, b, mask)
-            for i, (h, wd), (y, x) in zip(small, hws, pos):
-                outs[i] = o[:, y:y + h, x:x + wd]
-        logits, deltas = [], []
-        for o in outs:
-            N = o.shape[0]
-            logits.append(o[..., :A].reshape(N, -1))          # (h, w, a) order = torchvision permute
-            deltas.append(o[..., A:].reshape(N, -1, 4))
-        return logits, deltas
+        canvas, hws, rects, (Hc, Wc) = self.layout(feats)
+        if not canvas:
+            return [self._run(f, be, w, b) for f in feats]
+        f0 = feats[1]
+        N, C = f0.shape[0], f0.shape[3]
+        cv = f0.new_zeros((N, Hc, Wc, C))
+        mask = f0.new_zeros((1, Hc, Wc, 1))
+        for f, (y, x, h, wd) in zip(feats[1:], rects):
+            cv[:, y:y + h, x:x + wd] = f
+            mask[:, y:y + h, x:x + wd] = 1
+        return [self._run(feats[0], be, w, b), self._run(cv, be, w, b, mask)]
+
+    def split(self, raws, feats_layout, be):
+        """raw() outputs -> (objectness [N, Atot], pred_deltas [N, Atot, 4], anchors per level) in
+        torchvision's concat_box_prediction_layers order (per image: level, then (h, w, a))."""
+        A = self.cls_logits.weight.shape[0]
+        canvas, hws, rects, _ = feats_layout
+        num_per_level = [h * w * A for h, w in hws]
+        if canvas and raws[0].is_cuda and getattr(be, "name", "") == "hip" and raws[0].dtype == torch.float32:
+            obj, dl = ops.rpn_head_split(raws[0].contiguous(), raws[1].contiguous(), rects, A)
+            return obj, dl, num_per_level
+        outs = [raws[0]] + ([raws[1][:, y:y + h, x:x + wd] for (y, x, h, wd) in rects] if canvas else raws[1:])
+        logits = [o[..., :A].reshape(o.shape[0], -1) for o in outs]      # (h, w, a) = torchvision permute
+        deltas = [o[..., A:].reshape(o.shape[0], -1, 4) for o in outs]
+        return torch.cat(logits, 1), torch.cat(deltas, 1), num_per_level
+
+    def forward(self, feats, be):
+        """torchvision RPNHead.forward + concat_box_prediction_layers: (objectness, pred_deltas,
+        anchors per level)."""
+        return self.split(self.raw(feats, be), self.layout(feats), be)
 
 
 class AnchorGenerator(nn.Module):
@@ -424,13 +438,11 @@ class RegionProposalNetwork(nn.Module):
         / loss launches later (FasterRCNN.forward: right after the RoI sampler's host sync, so the GPU
         works on them while the host issues the RoI head instead of idling)."""
         feats = list(features.values())
-        logits, deltas = head if head is not None else self.head(feats, be)
+        # objectness [N, A], pred_deltas [N, A, 4], anchors per level
+        objectness, pred_deltas, num_per_level = head if head is not None else self.head(feats, be)
         grid = [(f.shape[1], f.shape[2]) for f in feats]
         anchors = self.anchor_generator(images.tensors.shape[1:3], grid, feats[0].device, be)
         N = feats[0].shape[0]
-        num_per_level = [l.shape[1] for l in logits]
-        objectness = torch.cat(logits, 1)                 # [N, A]
-        pred_deltas = torch.cat(deltas, 1)                # [N, A, 4]
         A = anchors.shape[0]
 
         def compute_losses():
@@ -842,7 +854,8 @@ class FasterRCNN(nn.Module):
         outs = g(x)
         nf = len(self.backbone.fpn.inner_blocks) + 1
         feats = OrderedDict(zip([str(i) for i in range(nf - 1)] + ["pool"], outs[:nf]))
-        return feats, (list(outs[nf:2 * nf]), list(outs[2 * nf:]))
+        head = self.rpn.head
+        return feats, head.split(list(outs[nf:]), head.layout(outs[:nf]), be)
 
     def forward(self, images, targets=None):
         be = self.be
@@ -909,8 +922,7 @@ class _Trunk(nn.Module):
 
     def forward(self, x):
         feats = self.backbone(x, self.be)
-        logits, deltas = self.head(list(feats.values()), self.be)
-        return tuple(feats.values()) + tuple(logits) + tuple(deltas)
+        return tuple(feats.values()) + tuple(self.head.raw(list(feats.values()), self.be))
 
 
 class _Graphs:
@@ -963,6 +975,25 @@ class _Graphs:
         return _GraphFn.apply(x, self.anchor, self)
 
 
+def _tag_outputs(tg):
+    """Fresh tensor objects over a graph's static outputs, each tagged with the static buffer its
+    gradient is copied into before the backward replay (ops.grad_buffer: the RoIAlign and RPN-head
+    backward kernels write there directly, and the copy is skipped)."""
+    outs = tuple(o.detach() for o in tg.static_out)
+    for o, b in zip(outs, tg.static_gout):
+        o._mx_gbuf = b
+    return outs
+
+
+def _load_gouts(tg, gouts):
+    for s, g in zip(tg.static_gout, gouts):
+        if g is None:
+            s.zero_()
+        elif not (g.data_ptr() == s.data_ptr() and g.shape == s.shape and g.stride() == s.stride()
+                  and g.dtype == s.dtype):
+            s.copy_(g)
+
+
 class _GraphFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, tg):
@@ -970,16 +1001,12 @@ class _GraphFn(torch.autograd.Function):
         tg.fwd.replay()
         ctx.tg = tg
         # fresh tensor objects over the graph's static outputs (overwritten by the next replay)
-        return tuple(o.detach() for o in tg.static_out)
+        return _tag_outputs(tg)
 
     @staticmethod
     def backward(ctx, *gouts):
         tg = ctx.tg
-        for s, g in zip(tg.static_gout, gouts):
-            if g is None:
-                s.zero_()
-            else:
-                s.copy_(g)
+        _load_gouts(tg, gouts)
         # A .grad still aliasing the graph's static buffer (adopted by the previous replay, kept by
         # zero_grad(set_to_none=False) or gradient accumulation) gets its own storage first: the
         # replay below overwrites the static buffer.
@@ -1086,8 +1113,7 @@ class _SegGraphs:
             cs.append(c)
         leaves.append(c.detach().requires_grad_(self.need[3]))
         feats = self.model.backbone.fpn(OrderedDict((str(i), l) for i, l in enumerate(leaves)), be)
-        logits, deltas = self.model.rpn.head(list(feats.values()), be)
-        return tuple(feats.values()) + tuple(logits) + tuple(deltas), leaves, cs
+        return tuple(feats.values()) + tuple(self.model.rpn.head.raw(list(feats.values()), be)), leaves, cs
 
     def _bwd_plan(self, outs, gouts, leaves, cs):
         """[(segment key, roots, () -> root gradients)] in backward order; a layer segment runs only
@@ -1113,16 +1139,12 @@ class _SegGraphFn(torch.autograd.Function):
         tg.static_x.copy_(x)
         tg.fwd.replay()
         ctx.tg = tg
-        return tuple(o.detach() for o in tg.static_out)
+        return _tag_outputs(tg)
 
     @staticmethod
     def backward(ctx, *gouts):
         tg = ctx.tg
-        for s, g in zip(tg.static_gout, gouts):
-            if g is None:
-                s.zero_()
-            else:
-                s.copy_(g)
+        _load_gouts(tg, gouts)
         for key, _ in tg.bwd:  # see _GraphFn.backward
             for p, g in zip(tg.seg_params[key], tg.static_grads[key]):
                 if g is not None and p.grad is g:

@@ -277,6 +277,60 @@ def roi_align(input, boxes, output_size, spatial_scale=1.0, sampling_ratio=2, al
     return _RoIAlign.apply(input, boxes, spatial_scale, output_size[0], output_size[1], sampling_ratio, aligned)
 
 
+def grad_buffer(t, dtype=torch.float32):
+    """The buffer a HIP-graph replay will copy `t`'s gradient into (frcnn._GraphFn tags the tensors it
+    returns with it): a backward that writes the gradient there directly saves that copy."""
+    b = getattr(t, "_mx_gbuf", None)
+    if b is not None and b.shape == t.shape and b.dtype == dtype and b.device == t.device and b.is_contiguous():
+        return b
+    return None
+
+
+class _RPNHeadSplit(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, o0, ocv, rects, A):
+        _dev(o0, *([ocv] if ocv is not None else []))
+        N, H0, W0, C = o0.shape
+        _check(C == 5 * A and o0.dtype == torch.float32 and o0.is_contiguous(), "rpn head split: o0 must be f32 [N,H,W,5A]")
+        ncv = len(rects)
+        Hc = Wc = 0
+        if ncv:
+            _check(ocv is not None and ocv.shape[0] == N and ocv.shape[3] == C and ocv.dtype == torch.float32
+                   and ocv.is_contiguous(), "rpn head split: bad canvas")
+            Hc, Wc = ocv.shape[1], ocv.shape[2]
+        r = (ctypes.c_int32 * max(1, 4 * ncv))(*[v for rc in rects for v in rc])
+        atot = H0 * W0 * A + sum(h * w * A for _, _, h, w in rects)
+        obj = torch.empty((N, atot), dtype=torch.float32, device=o0.device)
+        dl = torch.empty((N, atot, 4), dtype=torch.float32, device=o0.device)
+        call("mx_rpn_head_split", _p(o0), H0, W0, _p(ocv) if ncv else None, Hc, Wc, r, ncv, N, A, _p(obj), _p(dl),
+             _stream())
+        ctx.cfg = (N, H0, W0, Hc, Wc, r, ncv, A)
+        ctx.gbufs = (grad_buffer(o0), grad_buffer(ocv) if ncv else None)
+        ctx.shapes = (o0.shape, ocv.shape if ncv else None)
+        return obj, dl
+
+    @staticmethod
+    def backward(ctx, gobj, gdl):
+        N, H0, W0, Hc, Wc, r, ncv, A = ctx.cfg
+        s0, scv = ctx.shapes
+        b0, bcv = ctx.gbufs
+        dev = (gobj if gobj is not None else gdl).device
+        g0 = b0 if b0 is not None else torch.empty(s0, dtype=torch.float32, device=dev)
+        gcv = (bcv if bcv is not None else torch.empty(scv, dtype=torch.float32, device=dev)) if ncv else None
+        gobj = gobj.contiguous() if gobj is not None else None
+        gdl = gdl.contiguous() if gdl is not None else None
+        call("mx_rpn_head_merge", _p(gobj) if gobj is not None else None, _p(gdl) if gdl is not None else None,
+             H0, W0, Hc, Wc, r, ncv, N, A, _p(g0), _p(gcv) if ncv else None, _stream())
+        return g0, gcv, None, None
+
+
+def rpn_head_split(o0, ocv, rects, A):
+    """RPN head outputs (level 0 map, zero-framed canvas of the other levels at rects (y, x, h, w)) ->
+    (objectness [N, Atot], pred_deltas [N, Atot, 4]) in torchvision's concat_box_prediction_layers order;
+    autograd-aware (one launch each way)."""
+    return _RPNHeadSplit.apply(o0, ocv, [tuple(int(v) for v in rc) for rc in rects], int(A))
+
+
 class _MultiScaleRoIAlign(torch.autograd.Function):
     @staticmethod
     def forward(ctx, rois, scales, k_min, ph, pw, sampling, *feats):
@@ -300,23 +354,32 @@ class _MultiScaleRoIAlign(torch.autograd.Function):
                  pw, sampling, _p(out), _p(levels), _stream())
         ctx.save_for_backward(r, levels)
         ctx.cfg = ([tuple(f.shape) for f in fs], list(scales), ph, pw, sampling, dt)
+        ctx.gbufs = [grad_buffer(f) for f in feats] if dt == torch.float32 else None
         return out
 
     @staticmethod
     def backward(ctx, gout):
         r, levels = ctx.saved_tensors
         shapes, scales, ph, pw, sampling, dt = ctx.cfg
-        gfs = multiscale_roi_align_backward(gout, r, levels, shapes, scales, ph, pw, sampling)
+        gfs = multiscale_roi_align_backward(gout, r, levels, shapes, scales, ph, pw, sampling, out=ctx.gbufs)
         return (None, None, None, None, None, None) + tuple(x.to(dt) for x in gfs)
 
 
-def multiscale_roi_align_backward(gout, rois, levels, shapes, scales, ph=7, pw=7, sampling=2):
+def multiscale_roi_align_backward(gout, rois, levels, shapes, scales, ph=7, pw=7, sampling=2, out=None):
     """torchvision _roi_align_backward over the pyramid: grad_out [K,ph,pw,C] -> f32 NHWC gradients of
-    the level maps `shapes` (deterministic gather when the shape allows it, else atomics)."""
+    the level maps `shapes` (deterministic gather when the shape allows it, else atomics). out: optional
+    per-level f32 buffers to write into (None entries allocated)."""
     g = gout.contiguous()
     C, K = shapes[0][3], rois.shape[0]
     det = roi_align_deterministic(C, ph, pw, sampling)
-    gfs = [(torch.empty if det else torch.zeros)(s, dtype=torch.float32, device=g.device) for s in shapes]
+    gfs = []
+    for i, s in enumerate(shapes):
+        b = out[i] if out is not None and i < len(out) else None
+        if b is None or tuple(b.shape) != tuple(s):
+            b = (torch.empty if det else torch.zeros)(s, dtype=torch.float32, device=g.device)
+        elif not det:
+            b.zero_()
+        gfs.append(b)
     n = len(gfs)
     ws = _ws(_lib.load().mx_roi_align_bwd_workspace(K, ph, pw, sampling) if det else 0, g.device)
     ptrs = (ctypes.c_void_p * n)(*[f.data_ptr() for f in gfs])

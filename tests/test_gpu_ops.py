@@ -629,3 +629,25 @@ def test_random_corruption_matches_reference_golden(dev):
         np.random.seed(int(s))
         got = np.asarray(aug.RandomCorruption(p=0.5)(img))
         assert np.array_equal(got, out), int(s)
+
+
+def test_rpn_head_split_merge_equals_torch_slicing(dev):
+    """ops.rpn_head_split (one gather) / its backward (one scatter writing every element, frame pixels
+    0) == torchvision's per-level permute / reshape / cat over the level map and the canvas slices."""
+    from mx_det import frcnn, ops
+    torch.manual_seed(3)
+    A, N = 3, 2
+    hws = [(25, 42), (13, 21), (7, 11), (4, 6)]
+    pos, Hc, Wc = frcnn.RPNHead.canvas_layout(hws)
+    rects = [(y, x, h, w) for (y, x), (h, w) in zip(pos, hws)]
+    o0 = torch.randn(N, 50, 84, 5 * A, device=dev, requires_grad=True)
+    ocv = torch.randn(N, Hc, Wc, 5 * A, device=dev, requires_grad=True)
+    obj, dl = ops.rpn_head_split(o0, ocv, rects, A)
+    outs = [o0] + [ocv[:, y:y + h, x:x + w] for y, x, h, w in rects]
+    robj = torch.cat([o[..., :A].reshape(N, -1) for o in outs], 1)
+    rdl = torch.cat([o[..., A:].reshape(N, -1, 4) for o in outs], 1)
+    assert torch.equal(obj, robj) and torch.equal(dl, rdl)
+    go, gd = torch.randn_like(obj), torch.randn_like(dl)
+    g0, gcv = torch.autograd.grad((obj, dl), (o0, ocv), (go, gd))
+    r0, rcv = torch.autograd.grad((robj, rdl), (o0, ocv), (go, gd))
+    assert torch.equal(g0, r0) and torch.equal(gcv, rcv)

@@ -78,7 +78,8 @@ def _rpn_head_run(be, feats, canvas, monkeypatch, seed=0):
         torch.nn.init.normal_(p, std=0.05)
     head = head.to(feats[0].device)
     fs = [f.clone().requires_grad_(True) for f in feats]
-    logits, deltas = head(fs, be)
+    obj, dls, npl = head(fs, be)
+    logits, deltas = list(obj.split(npl, 1)), list(dls.split(npl, 1))
     loss = sum((lg * (i + 1)).sin().sum() + dl.cos().sum() for i, (lg, dl) in enumerate(zip(logits, deltas)))
     loss.backward()
     return ([t.detach() for t in logits + deltas], [f.grad for f in fs],
