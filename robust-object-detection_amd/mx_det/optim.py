@@ -21,6 +21,11 @@ from . import _lib
 _SGD_PACK = int(os.environ.get("MX_SGD_PACK", "1"))
 
 
+def mc_PackDesc():
+    from .conv import PackDesc
+    return PackDesc
+
+
 class _SgdParam(ctypes.Structure):  # mx_sgd_param
     _fields_ = [("p", ctypes.c_void_p), ("buf", ctypes.c_void_p), ("n", ctypes.c_int64), ("first", ctypes.c_int32),
                 ("pack", ctypes.c_int32)]
@@ -81,27 +86,59 @@ class SGD(torch.optim.SGD):
         """Conv weights registered with the current WeightPacker (mx_det.conv.get_packer) get their
         bf16 operands written by the update itself (mx_sgd_pack_step: one launch for the whole group,
         no separate repack of the new weights before the next forward). Returns False to take the
-        other paths (no packer, nothing to fold, or a case the multi-tensor kernel does not cover)."""
+        other paths (no packer, nothing to fold, or a case the multi-tensor kernel does not cover).
+        Steady state (same parameters, buffers and packer): only the gradients' pointers are gathered
+        on the host; the device plan is rebuilt when anything else changes."""
         from . import conv as mc
         pk = mc.get_packer()
         if pk is None or _SGD_PACK == 0:
             return False
         ps = group["params"]
-        if (not ps or group.get("maximize") or group["momentum"] == 0 or
-                any(p.grad is None or not p.is_cuda or p.dtype != torch.float32 or p.grad.is_sparse or
-                    not p.is_contiguous() or not p.grad.is_contiguous() for p in ps)):
-            return False
         cache = self.__dict__.setdefault("_pk", {})
         c = cache.get(id(group))
-        if c is None or c["ps"] is not ps or c["packer"] is not pk or c["pptr"] != [p.data_ptr() for p in ps]:
-            entries = pk.fusable(ps)
-            if not any(e is not None for e in entries):
+        if c is not None and c["ps"] is ps and c["packer"] is pk and c["ready"]:
+            grads = [p.grad for p in ps]
+            if any(g is None for g in grads):
                 return False
-            c = cache[id(group)] = {"ps": ps, "packer": pk, "pptr": [p.data_ptr() for p in ps],
-                                    "entries": entries, "key": None, "gkey": None}
+            st = self.state
+            if ([p.data_ptr() for p in ps] != c["pptr"] or
+                    any(st[p].get("momentum_buffer") is not b for p, b in zip(ps, c["bufs"]))):
+                c = None
+        if c is None or c["ps"] is not ps or c["packer"] is not pk or not c["ready"]:
+            if (not ps or group.get("maximize") or group["momentum"] == 0 or
+                    any(p.grad is None or not p.is_cuda or p.dtype != torch.float32 or p.grad.is_sparse or
+                        not p.is_contiguous() for p in ps)):
+                return False
+            c = self._pack_plan(group, pk)
+            if c is None:
+                return False
+            cache[id(group)] = c
+            grads = [p.grad for p in ps]
+        gptr = [g.data_ptr() for g in grads]
+        if gptr != c["gkey"]:
+            if any(not g.is_contiguous() or g.dtype != torch.float32 or g.is_sparse or not g.is_cuda for g in grads):
+                return False
+            c["gdev"] = torch.tensor(gptr, dtype=torch.int64).pin_memory().to(ps[0].device, non_blocking=True)
+            c["gkey"] = gptr
+        _lib.call("mx_sgd_pack_step", c["plan"].data_ptr(), c["gdev"].data_ptr(), len(ps), c["blocks"], c["lds"],
+                  float(group["lr"]), float(group["momentum"]), float(group["dampening"]),
+                  float(group["weight_decay"]), int(group["nesterov"]), _lib.stream())
+        increment_version(ps)
+        increment_version(c["bufs"])
+        pk.mark_packed(c["entries"])
+        if not c["ready"]:  # first momentum step done: the next plan has every first flag clear
+            c["ready"] = all(not f for f in c["first"])
+            if not c["ready"]:
+                cache.pop(id(group), None)
+        return True
+
+    def _pack_plan(self, group, pk):
+        ps = group["params"]
+        entries = pk.fusable(ps)
+        if not any(e is not None for e in entries):
+            return None
         n = len(ps)
-        first = []
-        bufs = []
+        first, bufs = [], []
         for p in ps:
             st = self.state[p]
             b = st.get("momentum_buffer")
@@ -111,36 +148,21 @@ class SGD(torch.optim.SGD):
             else:
                 first.append(0)
             bufs.append(b)
-        key = (tuple(b.data_ptr() for b in bufs), tuple(first))
-        dev = ps[0].device
-        if key != c["key"]:
-            entries = c["entries"]
-            packs = [e for e in entries if e is not None]
-            descs = (mc.PackDesc * len(packs))(*[pk.desc(e) for e in packs])
-            prm = (_SgdParam * n)()
-            j = 0
-            for i, (p, b, e) in enumerate(zip(ps, bufs, entries)):
-                prm[i] = _SgdParam(p.data_ptr(), b.data_ptr(), p.numel(), first[i], j if e is not None else -1)
-                j += e is not None
-            lib = _lib.load()
-            nb = lib.mx_sgd_pack_plan_bytes(n)
-            host = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
-            blocks, lds = ctypes.c_int64(0), ctypes.c_size_t(0)
-            _lib.call("mx_sgd_pack_build", prm, n, descs, host.data_ptr(), nb, ctypes.byref(blocks),
-                      ctypes.byref(lds))
-            c["plan"] = host.to(dev, non_blocking=True)
-            c["blocks"], c["lds"], c["key"], c["bufs"] = blocks.value, lds.value, key, bufs
-        gptr = [p.grad.data_ptr() for p in ps]
-        if gptr != c["gkey"]:
-            c["gdev"] = torch.tensor(gptr, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
-            c["gkey"] = gptr
-        _lib.call("mx_sgd_pack_step", c["plan"].data_ptr(), c["gdev"].data_ptr(), n, c["blocks"], c["lds"],
-                  float(group["lr"]), float(group["momentum"]), float(group["dampening"]),
-                  float(group["weight_decay"]), int(group["nesterov"]), _lib.stream())
-        increment_version(ps)
-        increment_version(bufs)
-        pk.mark_packed(c["entries"])
-        return True
+        packs = [e for e in entries if e is not None]
+        descs = (mc_PackDesc() * len(packs))(*[pk.desc(e) for e in packs])
+        prm = (_SgdParam * n)()
+        j = 0
+        for i, (p, b, e) in enumerate(zip(ps, bufs, entries)):
+            prm[i] = _SgdParam(p.data_ptr(), b.data_ptr(), p.numel(), first[i], j if e is not None else -1)
+            j += e is not None
+        lib = _lib.load()
+        nb = lib.mx_sgd_pack_plan_bytes(n)
+        host = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+        blocks, lds = ctypes.c_int64(0), ctypes.c_size_t(0)
+        _lib.call("mx_sgd_pack_build", prm, n, descs, host.data_ptr(), nb, ctypes.byref(blocks), ctypes.byref(lds))
+        return {"ps": ps, "packer": pk, "pptr": [p.data_ptr() for p in ps], "entries": entries, "bufs": bufs,
+                "first": first, "ready": not any(first), "plan": host.to(ps[0].device, non_blocking=True),
+                "blocks": blocks.value, "lds": lds.value, "gkey": None}
 
     def _fast_step(self, group, fast):
         """Steady state: every parameter of the group has a grad and a momentum buffer, and the
