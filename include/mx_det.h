@@ -191,6 +191,14 @@ int mx_rpn_head_split(const float* o0, int64_t H0, int64_t W0, const float* ocv,
                       const int32_t* rects, int ncv, int64_t N, int A, float* obj, float* del, mx_stream_t stream);
 int mx_rpn_head_merge(const float* gobj, const float* gdel, int64_t H0, int64_t W0, int64_t Hc, int64_t Wc,
                       const int32_t* rects, int ncv, int64_t N, int A, float* g0, float* gcv, mx_stream_t stream);
+/* Zero-framed canvas of n NHWC maps (frcnn.RPNHead: the small FPN levels as one conv input):
+ * pack writes every element of cv [N, Hc, Wc, C] (map l at rects[l] = (y, x, h, w), 0 elsewhere);
+ * unpack is its backward: grads[l] = the slice of gcv (+ add[l], nullable list / entries). C % 8 == 0;
+ * dtype MX_F32 / MX_BF16 for every buffer. */
+int mx_canvas_pack(const void* const* maps, const int32_t* rects, int n, int64_t N, int64_t Hc, int64_t Wc, int64_t C,
+                   int dtype, void* cv, mx_stream_t stream);
+int mx_canvas_unpack(const void* gcv, const int32_t* rects, int n, int64_t N, int64_t Hc, int64_t Wc, int64_t C,
+                     int dtype, const void* const* add, void* const* grads, mx_stream_t stream);
 /* The same for the reference loader's own image tensors: ToDtype(float32, scale=True) output, f32 CHW
  * [3, Hs[b], Ws[b]] contiguous (train_frcnn_baseline.py:50-54 build_transforms, fed to the model at :171).
  * A float image equal to u8 * (float)(1/255) gives the bit-identical batch of mx_resize_normalize_pad;

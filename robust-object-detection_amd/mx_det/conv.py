@@ -597,6 +597,51 @@ def act_bias_bwd(gy, y, act, K8, need_db, g_dtype=torch.bfloat16):
     return g, db
 
 
+class GradSlot:
+    """Root-gradient absorption inside a captured backward graph: a graph output whose gradient arrives
+    in a static buffer (frcnn._Graphs' static_gout) and whose only in-graph consumer can add it itself
+    -- a stride-1 conv in its dgrad epilogue (ConvAct), the RPN canvas unpack -- is left out of the
+    backward roots; the consumer reads `buf` (set after the forward capture) instead of autograd adding
+    the two gradients in a separate pass."""
+    __slots__ = ("buf",)
+
+    def __init__(self):
+        self.buf = None
+
+
+_absorb = {}
+_absorb_on = False
+
+
+class absorb_mode:
+    """Context of a graph capture's forward: modules that can take a root gradient into an in-graph
+    consumer create GradSlots (RPNHead.raw)."""
+
+    def __enter__(self):
+        global _absorb_on
+        self.prev, _absorb_on = _absorb_on, True
+        return self
+
+    def __exit__(self, *a):
+        global _absorb_on
+        _absorb_on = self.prev
+        _absorb.clear()
+
+
+def absorbing():
+    return _absorb_on
+
+
+def absorb_into(t, slot):
+    """The next ConvAct consuming tensor `t` adds slot.buf to its input gradient."""
+    _absorb[id(t)] = (weakref.ref(t), slot)
+
+
+def _absorb_take(t):
+    e = _absorb.pop(id(t), None)
+    return e[1] if e is not None and e[0]() is t else None
+
+
 class ConvAct(torch.autograd.Function):
     """y = act(conv(x, w) + b). x NHWC (bf16, or f32: bf16x3); w [K,C,R,S] f32 parameter; b f32 [K]
     or None."""
@@ -612,6 +657,7 @@ class ConvAct(torch.autograd.Function):
         ctx.save_for_backward(x, y, wt if need_dx else None)
         ctx.cfg = (stride, pad, act, w.shape, b is not None)
         ctx.wref, ctx.uses = weakref.ref(w), _count_use(w)
+        ctx.slot = _absorb_take(x) if _absorb else None
         return y
 
     @staticmethod
@@ -627,7 +673,11 @@ class ConvAct(torch.autograd.Function):
                 N, H, W, C = x.shape
                 dx = conv_dgrad(gk.view(N, 1, 1, K8), wt, (N, 1, 1, H * W * C), 1, 1, (1, 1), (0, 0)).view(N, H, W, C)
             else:
-                dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad)
+                extra = ctx.slot.buf if ctx.slot is not None else None
+                if extra is not None and not (tuple(stride) == (1, 1) and extra.dtype == gk.dtype and
+                                              extra.shape == x.shape and extra.is_contiguous()):
+                    raise RuntimeError("absorbed gradient needs a stride-1 conv and an input-shaped buffer")
+                dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad, residual=extra)
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad(gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1], side=side_wgrad_enabled(ctx))
         return dx, dw, db, None, None, None, None

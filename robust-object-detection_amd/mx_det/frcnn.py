@@ -24,6 +24,7 @@ from torch import nn
 
 from . import ops
 from .backend import default_backend
+from . import conv as mc
 from .conv import ACT_NONE, ACT_RELU, BatchNorm2d, Conv2d, ConvNormAct
 
 RPN_WEIGHTS = (1.0, 1.0, 1.0, 1.0)
@@ -231,16 +232,35 @@ class RPNHead(nn.Module):
         w = torch.cat([self.cls_logits.weight, self.bbox_pred.weight])
         b = torch.cat([self.cls_logits.bias, self.bbox_pred.bias])
         canvas, hws, rects, (Hc, Wc) = self.layout(feats)
+        hip = feats[0].is_cuda and getattr(be, "name", "") == "hip"
+        # inside a trunk-graph capture (HIP): the levels' root gradients (RoIAlign's) are taken by the
+        # level-0 conv's dgrad epilogue and the canvas unpack instead of separate autograd adds
+        slots = [mc.GradSlot() for _ in feats] if hip and canvas and mc.absorbing() else None
+        self._slots = slots
         if not canvas:
             return [self._run(f, be, w, b) for f in feats]
+        if slots is not None:
+            mc.absorb_into(feats[0], slots[0])
         f0 = feats[1]
         N, C = f0.shape[0], f0.shape[3]
-        cv = f0.new_zeros((N, Hc, Wc, C))
-        mask = f0.new_zeros((1, Hc, Wc, 1))
-        for f, (y, x, h, wd) in zip(feats[1:], rects):
-            cv[:, y:y + h, x:x + wd] = f
-            mask[:, y:y + h, x:x + wd] = 1
+        key = (Hc, Wc, tuple(rects), f0.dtype, str(f0.device))
+        mask = self.__dict__.setdefault("_masks", {}).get(key)
+        if mask is None:  # shape constant, built once (outside any capture: the first call is eager)
+            mask = f0.new_zeros((1, Hc, Wc, 1))
+            for (y, x, h, wd) in rects:
+                mask[:, y:y + h, x:x + wd] = 1
+            self._masks[key] = mask
+        if hip and C % 8 == 0:
+            cv = ops.canvas_pack(feats[1:], rects, Hc, Wc, slots[1:] if slots is not None else None)
+        else:
+            cv = f0.new_zeros((N, Hc, Wc, C))
+            for f, (y, x, h, wd) in zip(feats[1:], rects):
+                cv[:, y:y + h, x:x + wd] = f
         return [self._run(feats[0], be, w, b), self._run(cv, be, w, b, mask)]
+
+    def absorbed(self):
+        """GradSlots of the last raw() (per feature level), or None."""
+        return self.__dict__.get("_slots")
 
     def split(self, raws, feats_layout, be):
         """raw() outputs -> (objectness [N, Atot], pred_deltas [N, Atot, 4], anchors per level) in
@@ -924,6 +944,9 @@ class _Trunk(nn.Module):
         feats = self.backbone(x, self.be)
         return tuple(feats.values()) + tuple(self.head.raw(list(feats.values()), self.be))
 
+    def absorbed(self):
+        return self.head.absorbed()
+
 
 class _Graphs:
     """Forward and backward HIP graphs of a static-shape sub-network fn(x) -> tuple(tensors). The
@@ -953,12 +976,13 @@ class _Graphs:
         torch.cuda.current_stream().wait_stream(side)
         pool = torch.cuda.graph_pool_handle()
         self.fwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.fwd, pool=pool):
+        with torch.cuda.graph(self.fwd, pool=pool), mc.absorb_mode():
             self.static_out = fn(self.static_x)
         self.static_gout = [torch.zeros_like(o) for o in self.static_out]
+        roots, groots = _absorb_roots(fn, self.static_out, self.static_gout)
         self.bwd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.bwd, pool=pool):
-            torch.autograd.backward(self.static_out, self.static_gout)
+            torch.autograd.backward(roots, groots)
         self.static_grads = [p.grad for p in self.params]
         self.static_xgrad = self.static_x.grad
         self.static_out = tuple(o.detach() for o in self.static_out)
@@ -973,6 +997,23 @@ class _Graphs:
 
     def __call__(self, x):
         return _GraphFn.apply(x, self.anchor, self)
+
+
+def _absorb_roots(fn, outs, gouts):
+    """Backward roots of a captured trunk: the outputs whose gradient an in-graph consumer takes from
+    its static buffer (fn.absorbed(): conv.GradSlot per leading output) are left out; their slots get
+    the buffers."""
+    slots = fn.absorbed() if hasattr(fn, "absorbed") else None
+    if not slots:
+        return list(outs), list(gouts)
+    roots, groots = [], []
+    for i, (o, g) in enumerate(zip(outs, gouts)):
+        if i < len(slots) and slots[i] is not None:
+            slots[i].buf = g
+        else:
+            roots.append(o)
+            groots.append(g)
+    return roots, groots
 
 
 def _tag_outputs(tg):
@@ -1079,11 +1120,12 @@ class _SegGraphs:
         torch.cuda.current_stream().wait_stream(side)
         pool = torch.cuda.graph_pool_handle()
         self.fwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.fwd, pool=pool):
+        with torch.cuda.graph(self.fwd, pool=pool), mc.absorb_mode():
             outs, self.leaves, self.cs = self._fwd(self.static_x)
         self.static_gout = [torch.zeros_like(o) for o in outs]
+        r0, g0 = _absorb_roots(self.model.rpn.head, outs, self.static_gout)
         self.bwd = []  # (segment key, graph)
-        for key, roots, groots in self._bwd_plan(outs, self.static_gout, self.leaves, self.cs):
+        for key, roots, groots in self._bwd_plan(outs, self.static_gout, self.leaves, self.cs, (r0, g0)):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
                 torch.autograd.backward(roots, groots())
@@ -1115,11 +1157,12 @@ class _SegGraphs:
         feats = self.model.backbone.fpn(OrderedDict((str(i), l) for i, l in enumerate(leaves)), be)
         return tuple(feats.values()) + tuple(self.model.rpn.head.raw(list(feats.values()), be)), leaves, cs
 
-    def _bwd_plan(self, outs, gouts, leaves, cs):
+    def _bwd_plan(self, outs, gouts, leaves, cs, first=None):
         """[(segment key, roots, () -> root gradients)] in backward order; a layer segment runs only
         when its output leaf carries a gradient (read lazily: the leaf's .grad exists once the
-        segments before it have run)."""
-        plan = [("fpn+rpn_head", outs, lambda: gouts)]
+        segments before it have run). first: the FPN + RPN-head roots after gradient absorption."""
+        r0, g0 = first if first is not None else (outs, gouts)
+        plan = [("fpn+rpn_head", r0, lambda: g0)]
         for k, key in zip((3, 2, 1, 0), ("layer4", "layer3", "layer2", "stem+layer1")):
             if self.need[k]:
                 plan.append((key, [cs[k]], (lambda lf: (lambda: [lf.grad]))(leaves[k])))

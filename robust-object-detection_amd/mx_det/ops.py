@@ -286,6 +286,44 @@ def grad_buffer(t, dtype=torch.float32):
     return None
 
 
+class _CanvasPack(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, rects, Hc, Wc, slots, *maps):
+        _dev(*maps)
+        N, C, dt = maps[0].shape[0], maps[0].shape[3], maps[0].dtype
+        for m in maps:
+            _check(m.dim() == 4 and m.shape[0] == N and m.shape[3] == C and m.dtype == dt and m.is_contiguous(),
+                   "canvas: maps must be contiguous NHWC of one N, C and dtype")
+        n = len(maps)
+        r = (ctypes.c_int32 * (4 * n))(*[v for rc in rects for v in rc])
+        cv = torch.empty((N, Hc, Wc, C), dtype=dt, device=maps[0].device)
+        call("mx_canvas_pack", (ctypes.c_void_p * n)(*[m.data_ptr() for m in maps]), r, n, N, Hc, Wc, C,
+             _dtype_code(maps[0]), _p(cv), _stream())
+        ctx.cfg = (r, n, N, Hc, Wc, C, [tuple(m.shape) for m in maps], slots)
+        return cv
+
+    @staticmethod
+    def backward(ctx, gcv):
+        r, n, N, Hc, Wc, C, shapes, slots = ctx.cfg
+        g = gcv.contiguous()
+        grads = [torch.empty(s, dtype=g.dtype, device=g.device) for s in shapes]
+        adds = [s.buf if s is not None and s.buf is not None else None for s in (slots or [None] * n)]
+        for a, s in zip(adds, shapes):
+            _check(a is None or (tuple(a.shape) == s and a.dtype == g.dtype and a.is_contiguous()),
+                   "canvas: absorbed gradient must match its map")
+        addp = (ctypes.c_void_p * n)(*[a.data_ptr() if a is not None else None for a in adds])
+        call("mx_canvas_unpack", _p(g), r, n, N, Hc, Wc, C, _dtype_code(g), addp,
+             (ctypes.c_void_p * n)(*[x.data_ptr() for x in grads]), _stream())
+        return (None, None, None, None) + tuple(grads)
+
+
+def canvas_pack(maps, rects, Hc, Wc, slots=None):
+    """Zero canvas [N, Hc, Wc, C] holding maps[l] at rects[l] = (y, x, h, w) (one launch each way);
+    slots[l].buf, when set, is added to map l's gradient in the backward (conv.GradSlot)."""
+    return _CanvasPack.apply([tuple(int(v) for v in rc) for rc in rects], int(Hc), int(Wc), slots,
+                             *[m.contiguous() for m in maps])
+
+
 class _RPNHeadSplit(torch.autograd.Function):
     @staticmethod
     def forward(ctx, o0, ocv, rects, A):

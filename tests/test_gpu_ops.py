@@ -651,3 +651,31 @@ def test_rpn_head_split_merge_equals_torch_slicing(dev):
     g0, gcv = torch.autograd.grad((obj, dl), (o0, ocv), (go, gd))
     r0, rcv = torch.autograd.grad((robj, rdl), (o0, ocv), (go, gd))
     assert torch.equal(g0, r0) and torch.equal(gcv, rcv)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_canvas_pack_unpack_equals_torch(dev, dtype):
+    """ops.canvas_pack: the zero-framed canvas of the small levels (frcnn.RPNHead) == zeros + slice
+    copies; its backward == the slices of the canvas gradient, plus the absorbed root gradients
+    (conv.GradSlot) when given."""
+    from mx_det import conv as mc, frcnn, ops
+    torch.manual_seed(5)
+    hws = [(25, 42), (13, 21), (7, 11), (4, 6)]
+    pos, Hc, Wc = frcnn.RPNHead.canvas_layout(hws)
+    rects = [(y, x, h, w) for (y, x), (h, w) in zip(pos, hws)]
+    maps = [torch.randn(2, h, w, 256, device=dev).to(dtype).requires_grad_(True) for h, w in hws]
+    slots = [mc.GradSlot() for _ in hws]
+    for s, (h, w) in zip(slots[::2], hws[::2]):
+        s.buf = torch.randn(2, h, w, 256, device=dev).to(dtype)
+    cv = ops.canvas_pack(maps, rects, Hc, Wc, slots)
+    ref = torch.zeros(2, Hc, Wc, 256, device=dev, dtype=dtype)
+    for m, (y, x, h, w) in zip(maps, rects):
+        ref[:, y:y + h, x:x + w] = m.detach()
+    assert torch.equal(cv, ref)
+    g = torch.randn_like(cv)
+    grads = torch.autograd.grad(cv, maps, g)
+    for gr, s, (y, x, h, w) in zip(grads, slots, rects):
+        want = g[:, y:y + h, x:x + w]
+        if s.buf is not None:
+            want = (want.float() + s.buf.float()).to(dtype)
+        assert torch.equal(gr, want)
