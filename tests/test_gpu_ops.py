@@ -679,3 +679,26 @@ def test_canvas_pack_unpack_equals_torch(dev, dtype):
         if s.buf is not None:
             want = (want.float() + s.buf.float()).to(dtype)
         assert torch.equal(gr, want)
+
+
+@pytest.mark.parametrize("C", [64, 256])
+def test_roi_align_fwd_window_path_bitexact(dev, C):
+    """C % 64 == 0: the windowed forward (roi_align_fwd_win_kernel: RoI pixel window staged in LDS,
+    64-channel passes) for small RoIs, the in-block v8 loop for windows over 224 pixels, RoIs partly
+    or wholly outside the map -- all bit-identical to the oracle (same per-element op order)."""
+    from mx_det import ops
+    rng = np.random.default_rng(C)
+    N, H, W, scale = 2, 100, 168, 1 / 8
+    feat = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    small = _rand_boxes(rng, 150, H=H / scale, W=W / scale, med=40)
+    large = _rand_boxes(rng, 40, H=H / scale, W=W / scale, med=400)
+    b = np.concatenate([small, large])
+    b[0] = [-20, -30, 5, 5]
+    b[1] = [3, 3, 3.2, 3.1]
+    b[2] = [-400, -400, -300, -300]  # no sample inside the map: zeros
+    bi = rng.integers(0, N, len(b)).astype(np.float32)[:, None]
+    rois = np.concatenate([bi, b], 1).astype(np.float32)
+    ref = orc.roi_align(feat, rois, scale, (7, 7), 2, False)
+    f = torch.from_numpy(feat).to(dev).permute(0, 2, 3, 1).contiguous()
+    got = ops.roi_align(f, torch.from_numpy(rois).to(dev), (7, 7), scale, 2, False).permute(0, 3, 1, 2).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
