@@ -56,12 +56,15 @@ int mx_match_assign(const float* gt, const int64_t* gt_labels, int64_t G, const 
 /* The same for B images in one launch (grid.y = image): gt [B][G][4] of which gcount[b] (device int32,
  * nullable = all G) rows are real -- a zero-padded, static-shape GT batch -- gt_labels [B][G]; boxes
  * [B][box_stride rows] (box_stride 0: one [A,4] set shared by every image, the RPN anchors);
- * matches / labels [B][A], targets [B][A][4]. Workspace mx_match_batched_workspace(B, G, A). */
+ * matches / labels [B][A], targets [B][A][4]; counts (nullable) [B][2] int32 = per image the number of
+ * boxes matched (label >= 1) and background (label 0) -- BalancedPositiveNegativeSampler's pos / neg
+ * counts without a reduction pass. Workspace mx_match_batched_workspace(B, G, A). */
 size_t mx_match_batched_workspace(int64_t B, int64_t G, int64_t A);
 int mx_match_assign_batched(const float* gt, const int64_t* gt_labels, const int32_t* gcount, int64_t B, int64_t G,
                             const float* boxes, int64_t box_stride, int64_t A, float high, float low,
                             int allow_low_quality, int mode, const float* enc_weights4_host, int64_t* matches,
-                            void* labels, float* targets, void* ws, size_t ws_bytes, mx_stream_t stream);
+                            void* labels, float* targets, int32_t* counts, void* ws, size_t ws_bytes,
+                            mx_stream_t stream);
 
 /* torchvision.ops.box_iou -> out[n,m] (test/diagnostic entry). */
 int mx_box_iou(const float* b1, int64_t n, const float* b2, int64_t m, float* out, mx_stream_t stream);

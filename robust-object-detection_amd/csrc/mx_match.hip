@@ -93,7 +93,8 @@ __global__ void __launch_bounds__(256) match_pass2(const float4* __restrict__ gt
                                                    float low, int allow_lq, int mode, float4 wts,
                                                    const float* __restrict__ best_val, const int32_t* __restrict__ best_idx,
                                                    const uint32_t* __restrict__ gmax, int64_t* __restrict__ matches,
-                                                   void* __restrict__ labels, float4* __restrict__ targets) {
+                                                   void* __restrict__ labels, float4* __restrict__ targets,
+                                                   int32_t* __restrict__ counts) {
   __shared__ float4 sg[kTile];
   __shared__ float sga[kTile];
   __shared__ uint32_t sm[kTile];
@@ -140,6 +141,13 @@ __global__ void __launch_bounds__(256) match_pass2(const float4* __restrict__ gt
         }
     }
     if (lq) m = bi;
+  }
+  if (counts) {  // per image: anchors labelled positive (m >= 0) / negative (m == -1), one atomic per wave
+    const uint64_t bp = __ballot(valid && m >= 0), bn = __ballot(valid && m == -1);
+    if ((threadIdx.x & 63) == 0) {
+      if (bp) atomicAdd(&counts[2 * b], (int32_t)__popcll(bp));
+      if (bn) atomicAdd(&counts[2 * b + 1], (int32_t)__popcll(bn));
+    }
   }
   if (!valid) return;
   matches[a] = m;
@@ -200,12 +208,13 @@ extern "C" size_t mx_match_batched_workspace(int64_t B, int64_t G, int64_t A) {
 static int match_launch(const float* gt, const int64_t* gt_labels, const int32_t* gcount, int64_t B, int64_t G,
                         const float* boxes, int64_t bstride, int64_t A, float high, float low, int allow_lq, int mode,
                         const float* enc_w, int64_t* matches, void* labels, float* targets, void* ws, size_t ws_bytes,
-                        hipStream_t s) {
+                        hipStream_t s, int32_t* counts = nullptr) {
   MX_CHECK_ARG(G >= 0 && A >= 0 && B >= 1 && B <= 65535, "mx_match_assign: bad sizes");
   MX_CHECK_ARG(mode >= 0 && mode <= 2, "mx_match_assign: bad mode %d", mode);
   MX_CHECK_ARG(mode == 0 || labels, "mx_match_assign: labels required for mode %d", mode);
   MX_CHECK_ARG(mode != 2 || G == 0 || gt_labels, "mx_match_assign: gt_labels required for mode 2");
   MX_CHECK_ARG(!targets || enc_w, "mx_match_assign: enc weights required with targets");
+  if (counts) MX_HIP(hipMemsetAsync(counts, 0, sizeof(int32_t) * 2 * B, s));
   if (A == 0) return MX_OK;
   Carver c(ws, ws_bytes);
   float* bv = c.take<float>(B * A);
@@ -220,7 +229,7 @@ static int match_launch(const float* gt, const int64_t* gt_labels, const int32_t
   }
   float4 w = enc_w ? make_float4(enc_w[0], enc_w[1], enc_w[2], enc_w[3]) : make_float4(1.f, 1.f, 1.f, 1.f);
   match_pass2<<<grid, 256, 0, s>>>((const float4*)gt, gt_labels, G, gcount, (const float4*)boxes, bstride, A, high, low,
-                                   allow_lq, mode, w, bv, bi, gm, matches, labels, (float4*)targets);
+                                   allow_lq, mode, w, bv, bi, gm, matches, labels, (float4*)targets, counts);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }
@@ -235,10 +244,11 @@ extern "C" int mx_match_assign(const float* gt, const int64_t* gt_labels, int64_
 extern "C" int mx_match_assign_batched(const float* gt, const int64_t* gt_labels, const int32_t* gcount, int64_t B,
                                        int64_t G, const float* boxes, int64_t box_stride, int64_t A, float high, float low,
                                        int allow_lq, int mode, const float* enc_w, int64_t* matches, void* labels,
-                                       float* targets, void* ws, size_t ws_bytes, mx_stream_t stream) {
+                                       float* targets, int32_t* counts, void* ws, size_t ws_bytes,
+                                       mx_stream_t stream) {
   MX_CHECK_ARG(box_stride == 0 || box_stride >= A, "mx_match_assign_batched: box_stride must be 0 or >= A");
   return match_launch(gt, gt_labels, gcount, B, G, boxes, box_stride, A, high, low, allow_lq, mode, enc_w, matches,
-                      labels, targets, ws, ws_bytes, (hipStream_t)stream);
+                      labels, targets, ws, ws_bytes, (hipStream_t)stream, counts);
 }
 
 extern "C" int mx_box_iou(const float* b1, int64_t n, const float* b2, int64_t m, float* out, mx_stream_t stream) {

@@ -286,7 +286,7 @@ __global__ void __launch_bounds__(256) roi_align_fwd_v8_kernel(Levels L, int64_t
 // ---- windowed forward: the RoI's pixel window staged in LDS ----------------------------------------
 // A P2 RoI of ~12 x 12 cells reads its 14 x 14 samples' 784 bilinear corners from ~200 distinct
 // pixels: the v8 kernel fetches every corner's channel row from L2 (784 KiB per RoI at C = 256), this
-// one copies the window (rows of the NHWC map, WIN_CQ channels per pass) into LDS once and gathers
+// one copies the window (rows of the NHWC map, one WIN_CQ-channel slice per block) into LDS once and gathers
 // the corners from there. Same per-element arithmetic and order as roi_align_fwd_kernel (bit-identical
 // output); windows above WIN_PX pixels (large RoIs: little corner reuse) take the v8 loop in the same
 // block.
@@ -317,19 +317,23 @@ template <typename T>
 __global__ void __launch_bounds__(256) roi_align_fwd_win_kernel(Levels L, int64_t C, const float* __restrict__ rois, int PH,
                                                                 int PW, int sampling, int aligned, int multiscale,
                                                                 T* __restrict__ out, int32_t* __restrict__ lv_out) {
+  // block = (RoI k, channel slice q of WIN_CQ channels): the slices of one RoI run as separate blocks, so
+  // window loads of some overlap the gathers of others
   __shared__ Samp tab[WIN_MAXSAMP];
   __shared__ RoiGeo sg;
   __shared__ int slv, bnd[4];
   extern __shared__ __attribute__((aligned(16))) char wsm[];
   T* win = (T*)wsm;
   const int tid = threadIdx.x;
-  const int64_t k = blockIdx.x;
+  const int nq = (int)(C / WIN_CQ);
+  const int64_t k = blockIdx.x / nq;
+  const int64_t cq = (int64_t)(blockIdx.x - k * nq) * WIN_CQ;
   const float* r = rois + 5 * k;
   if (tid == 0) {
     int lv = multiscale ? level_of(r, L.k_min, L.n) : 0;
     slv = lv;
     sg = roi_geo(r, L.scale[lv], PH, PW, sampling, aligned);
-    if (lv_out) lv_out[k] = lv;
+    if (lv_out && cq == 0) lv_out[k] = lv;
     bnd[0] = bnd[2] = 0x7fffffff;
     bnd[1] = bnd[3] = -1;
   }
@@ -352,15 +356,23 @@ __global__ void __launch_bounds__(256) roi_align_fwd_win_kernel(Levels L, int64_
   __syncthreads();
   const T* f = (const T*)L.f[lv] + g.b * H * W * C;
   const int y0 = bnd[0], x0 = bnd[2], wh = bnd[1] - y0 + 1, ww = bnd[3] - x0 + 1;
-  const int C8 = (int)(C / 8);
+  constexpr int Q8 = WIN_CQ / 8, U4 = 8 * (int)sizeof(T) / 16;  // 16-B pieces per 8 channels
   if (bnd[1] < 0 || wh * ww > WIN_PX) {  // no sample inside the map (all zero) or a large window: v8 loop
-    for (int e = tid; e < nbins * C8; e += blockDim.x) {
-      const int bin = e / C8, c0 = (e - bin * C8) * 8;
+    for (int e = tid; e < nbins * Q8; e += blockDim.x) {
+      const int bin = e / Q8, c0 = (int)cq + (e - bin * Q8) * 8;
       float v[8];
       roi_bin8(tab, bin, per_bin, f, C, c0, 0.f, g.count, v);
       st8(out + (k * nbins + bin) * C + c0, v);
     }
     return;
+  }
+  const int npx = wh * ww;
+  for (int e = tid; e < npx * Q8; e += blockDim.x) {
+    const int px = e / Q8, c0 = (e - px * Q8) * 8, py = px / ww, pxx = px - py * ww;
+    const uint4* src = (const uint4*)(f + ((int64_t)(y0 + py) * W + (x0 + pxx)) * C + cq + c0);
+    uint4* dst = (uint4*)(win + px * WIN_STRIDE + c0);
+#pragma unroll
+    for (int u = 0; u < U4; ++u) dst[u] = src[u];
   }
   for (int i = tid; i < ns; i += blockDim.x) {  // corner offsets relative to the window
     Samp& sp = tab[i];
@@ -368,24 +380,12 @@ __global__ void __launch_bounds__(256) roi_align_fwd_win_kernel(Levels L, int64_
     const int yl = sp.p1 / (int)W - y0, xl = sp.p1 % (int)W - x0, yh = sp.p4 / (int)W - y0, xh = sp.p4 % (int)W - x0;
     sp.p1 = yl * ww + xl; sp.p2 = yl * ww + xh; sp.p3 = yh * ww + xl; sp.p4 = yh * ww + xh;
   }
-  const int npx = wh * ww;
-  constexpr int Q8 = WIN_CQ / 8, U4 = 8 * (int)sizeof(T) / 16;  // 16-B pieces per 8 channels
-  for (int64_t cq = 0; cq < C; cq += WIN_CQ) {
-    __syncthreads();  // the table is final / the previous pass has read the window
-    for (int e = tid; e < npx * Q8; e += blockDim.x) {
-      const int px = e / Q8, c0 = (e - px * Q8) * 8, py = px / ww, pxx = px - py * ww;
-      const uint4* src = (const uint4*)(f + ((int64_t)(y0 + py) * W + (x0 + pxx)) * C + cq + c0);
-      uint4* dst = (uint4*)(win + px * WIN_STRIDE + c0);
-#pragma unroll
-      for (int u = 0; u < U4; ++u) dst[u] = src[u];
-    }
-    __syncthreads();
-    for (int e = tid; e < nbins * Q8; e += blockDim.x) {
-      const int bin = e / Q8, c0 = (e - bin * Q8) * 8;
-      float v[8];
-      roi_bin8(tab, bin, per_bin, (const T*)win, WIN_STRIDE, c0, 0.f, g.count, v);
-      st8(out + (k * nbins + bin) * C + cq + c0, v);
-    }
+  __syncthreads();
+  for (int e = tid; e < nbins * Q8; e += blockDim.x) {
+    const int bin = e / Q8, c0 = (e - bin * Q8) * 8;
+    float v[8];
+    roi_bin8(tab, bin, per_bin, (const T*)win, WIN_STRIDE, c0, 0.f, g.count, v);
+    st8(out + (k * nbins + bin) * C + cq + c0, v);
   }
 }
 
@@ -724,10 +724,10 @@ static int launch_fwd(const Levels& L, int dtype, int64_t C, const float* rois, 
   if (C % WIN_CQ == 0 && PH * PW * sampling * sampling <= WIN_MAXSAMP && g_roi_fwd_win) {
     const size_t lds = (size_t)WIN_PX * WIN_STRIDE * (dtype == MX_F32 ? 4 : 2);
     if (dtype == MX_F32)
-      roi_align_fwd_win_kernel<float><<<(unsigned)K, 256, lds, s>>>(L, C, rois, PH, PW, sampling, aligned, ms,
+      roi_align_fwd_win_kernel<float><<<(unsigned)(K * (C / WIN_CQ)), 256, lds, s>>>(L, C, rois, PH, PW, sampling, aligned, ms,
                                                                     (float*)out, lv);
     else
-      roi_align_fwd_win_kernel<uint16_t><<<(unsigned)K, 256, lds, s>>>(L, C, rois, PH, PW, sampling, aligned, ms,
+      roi_align_fwd_win_kernel<uint16_t><<<(unsigned)(K * (C / WIN_CQ)), 256, lds, s>>>(L, C, rois, PH, PW, sampling, aligned, ms,
                                                                        (uint16_t*)out, lv);
   } else if (C % 8 == 0 && dtype == MX_F32)
     roi_align_fwd_v8_kernel<float><<<(unsigned)K, 256, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms, (float*)out, lv);

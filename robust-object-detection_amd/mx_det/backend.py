@@ -145,8 +145,10 @@ class HipBackend:
     def match_assign(self, gt, boxes, high, low, allow_lq, mode, gt_labels=None, weights=None):
         return ops.match_assign(gt, boxes, high, low, allow_lq, mode, gt_labels, weights)
 
-    def match_assign_batched(self, gt_pad, gcount, boxes, high, low, allow_lq, mode, gt_labels=None, weights=None):
-        return ops.match_assign_batched(gt_pad, gcount, boxes, high, low, allow_lq, mode, gt_labels, weights)
+    def match_assign_batched(self, gt_pad, gcount, boxes, high, low, allow_lq, mode, gt_labels=None, weights=None,
+                             with_counts=False):
+        return ops.match_assign_batched(gt_pad, gcount, boxes, high, low, allow_lq, mode, gt_labels, weights,
+                                        with_counts)
 
     def batched_nms(self, boxes, scores, idxs, thr, group=None, max_seg=None, mode=0):
         return ops.batched_nms(boxes, scores, idxs, thr, group=group, max_seg=max_seg, mode=mode)

@@ -341,15 +341,21 @@ class BalancedPositiveNegativeSampler:
         self.batch, self.frac = batch_size_per_image, positive_fraction
         self.rand = None
 
-    def __call__(self, lab, be=None):
+    def __call__(self, lab, be=None, counts=None):
         """be: a backend with level_topk draws the k smallest keys with it (used for the RoI sampler's
         ~2k-wide rows; the RPN's 268k-anchor rows stay on torch.topk, which splits a row over many
-        workgroups)."""
+        workgroups). counts: per-row (#label >= 1, #label == 0) when the matcher already produced them
+        (int [N, 2]), sparing two reductions over the rows."""
         L = lab.shape[1]
         pos, neg = lab >= 1, lab == 0
         P = int(self.batch * self.frac)
-        num_pos = pos.sum(1).clamp(max=P)
-        num_neg = torch.minimum(neg.sum(1), self.batch - num_pos)
+        if counts is not None:
+            c = counts.to(torch.int64)
+            num_pos = c[:, 0].clamp(max=P)
+            num_neg = torch.minimum(c[:, 1], self.batch - num_pos)
+        else:
+            num_pos = pos.sum(1).clamp(max=P)
+            num_neg = torch.minimum(neg.sum(1), self.batch - num_pos)
         r = self.rand(lab.shape, lab.device) if self.rand is not None else torch.rand(lab.shape, device=lab.device)
         kp, kn = min(P, L), min(self.batch, L)
         if (be is None or not hasattr(be, "level_topk")) and kp > 0 and kn > 0:
@@ -471,9 +477,10 @@ class RegionProposalNetwork(nn.Module):
             # targets, sampling and losses never wait for the GPU
             if hasattr(be, "match_assign_batched"):  # every image in one launch pair, zero-padded GT
                 gtp, _, gcnt = _gt_batch(targets, anchors.device)
-                _, lab, rt = be.match_assign_batched(gtp, gcnt, anchors, self.fg, self.bg, True, 1,
-                                                     weights=RPN_WEIGHTS)
+                _, lab, rt, lcnt = be.match_assign_batched(gtp, gcnt, anchors, self.fg, self.bg, True, 1,
+                                                           weights=RPN_WEIGHTS, with_counts=True)
             else:
+                lcnt = None
                 labels, reg_targets = [], []
                 for t in targets:
                     _, lab, tg = be.match_assign(t["boxes"], anchors, self.fg, self.bg, True, mode=1,
@@ -482,7 +489,7 @@ class RegionProposalNetwork(nn.Module):
                     reg_targets.append(tg)
                 lab = torch.stack(labels)                 # [N, A] 1 / 0 / -1
                 rt = torch.stack(reg_targets)             # [N, A, 4]
-            pm, nm = self.fg_bg_sampler(lab)
+            pm, nm = self.fg_bg_sampler(lab, counts=lcnt)
             # torchvision: BCE mean over the sampled anchors; smooth-L1 (beta 1/9) sum over the sampled
             # positives / number sampled
             if hasattr(be, "rpn_loss"):  # HIP: one fused launch each way

@@ -93,10 +93,12 @@ def match_assign(gt_boxes, boxes, high, low, allow_low_quality, mode=0, gt_label
     return matches, labels, targets
 
 
-def match_assign_batched(gt_pad, gcount, boxes, high, low, allow_low_quality, mode, gt_labels=None, weights=None):
+def match_assign_batched(gt_pad, gcount, boxes, high, low, allow_low_quality, mode, gt_labels=None, weights=None,
+                         with_counts=False):
     """match_assign for B images in one launch pair: gt_pad [B, G, 4] (rows >= gcount[b] are padding),
     gcount int32 [B] on the device, boxes [A, 4] shared by every image or [B, A, 4]. Returns
-    (matches [B, A], labels [B, A], targets [B, A, 4]) as match_assign's modes 1 / 2."""
+    (matches [B, A], labels [B, A], targets [B, A, 4]) as match_assign's modes 1 / 2, plus with_counts
+    the per-image (matched, background) counts int32 [B, 2]."""
     _dev(gt_pad, boxes, gcount)
     _check(gt_pad.dim() == 3 and gt_pad.shape[2] == 4, "gt_pad must be [B, G, 4]")
     B, G = gt_pad.shape[0], gt_pad.shape[1]
@@ -115,10 +117,11 @@ def match_assign_batched(gt_pad, gcount, boxes, high, low, allow_low_quality, mo
     targets = torch.empty((B, A, 4), dtype=torch.float32, device=dev) if weights is not None else None
     w = (_lib.F4)(*weights) if weights is not None else None
     ws = _ws(_lib.load().mx_match_batched_workspace(B, G, A), dev)
+    counts = torch.empty((B, 2), dtype=torch.int32, device=dev) if with_counts else None
     call("mx_match_assign_batched", _p(gt), _p(gt_labels) if mode == 2 else None, _p(gc), B, G, _p(bx),
          0 if shared else A, A, float(high), float(low), int(bool(allow_low_quality)), int(mode), w, _p(matches),
-         _p(labels), _p(targets), _p(ws), ws.numel(), _stream())
-    return matches, labels, targets
+         _p(labels), _p(targets), _p(counts) if counts is not None else None, _p(ws), ws.numel(), _stream())
+    return (matches, labels, targets, counts) if with_counts else (matches, labels, targets)
 
 
 def pad_gt(targets, dev, multiple=32):

@@ -114,7 +114,9 @@ def test_batched_matcher_equals_per_image(dev, counts):
         targets[1]["boxes"][2] = targets[1]["boxes"][0]  # duplicate gt -> first index wins
     gtp, glp, gc = ops.pad_gt(targets, dev)
     assert gtp.shape[1] % 32 == 0 and gtp.shape[1] >= max(counts)
-    m, lab, tg = ops.match_assign_batched(gtp, gc, anchors, 0.7, 0.3, True, 1, weights=(1., 1., 1., 1.))
+    m, lab, tg, cnt = ops.match_assign_batched(gtp, gc, anchors, 0.7, 0.3, True, 1, weights=(1., 1., 1., 1.),
+                                               with_counts=True)
+    assert torch.equal(cnt.long(), torch.stack([(lab == 1).sum(1), (lab == 0).sum(1)], 1))
     for i, t in enumerate(targets):
         mi, li, ti = ops.match_assign(t["boxes"], anchors, 0.7, 0.3, True, mode=1, weights=(1., 1., 1., 1.))
         assert torch.equal(m[i], mi) and torch.equal(lab[i], li)
@@ -122,8 +124,9 @@ def test_batched_matcher_equals_per_image(dev, counts):
         assert torch.equal(tg[i][pos], ti[pos])
     props = torch.stack([torch.from_numpy(_rand_boxes(rng, 2000, med=40)).to(dev) for _ in counts])
     cand = torch.cat([props, gtp], 1)
-    m, lab, tg = ops.match_assign_batched(gtp, gc, cand, 0.5, 0.5, False, 2, gt_labels=glp,
-                                          weights=(10., 10., 5., 5.))
+    m, lab, tg, cnt = ops.match_assign_batched(gtp, gc, cand, 0.5, 0.5, False, 2, gt_labels=glp,
+                                               weights=(10., 10., 5., 5.), with_counts=True)
+    assert torch.equal(cnt.long(), torch.stack([(lab >= 1).sum(1), (lab == 0).sum(1)], 1))
     for i, t in enumerate(targets):
         mi, li, ti = ops.match_assign(t["boxes"], cand[i], 0.5, 0.5, False, mode=2, gt_labels=t["labels"],
                                       weights=(10., 10., 5., 5.))
