@@ -283,112 +283,6 @@ __global__ void __launch_bounds__(256) roi_align_fwd_v8_kernel(Levels L, int64_t
   }
 }
 
-// ---- windowed forward: the RoI's pixel window staged in LDS ----------------------------------------
-// A P2 RoI of ~12 x 12 cells reads its 14 x 14 samples' 784 bilinear corners from ~200 distinct
-// pixels: the v8 kernel fetches every corner's channel row from L2 (784 KiB per RoI at C = 256), this
-// one copies the window (rows of the NHWC map, one WIN_CQ-channel slice per block) into LDS once and gathers
-// the corners from there. Same per-element arithmetic and order as roi_align_fwd_kernel (bit-identical
-// output); windows above WIN_PX pixels (large RoIs: little corner reuse) take the v8 loop in the same
-// block.
-static constexpr int WIN_CQ = 64, WIN_STRIDE = WIN_CQ + 8, WIN_PX = 224, WIN_MAXSAMP = 256;
-
-template <typename T>
-__device__ __forceinline__ void roi_bin8(const Samp* tab, int bin, int per_bin, const T* base, int64_t pstride, int c0,
-                                         float inv_unused, float count, float (&v)[8]) {
-  (void)inv_unused;
-#pragma unroll
-  for (int t = 0; t < 8; ++t) v[t] = 0.f;
-  for (int s = 0; s < per_bin; ++s) {
-    const Samp p = tab[bin * per_bin + s];
-    if (p.p1 < 0) continue;
-    float f1[8], f2[8], f3[8], f4[8];
-    ld8(base + (int64_t)p.p1 * pstride + c0, f1);
-    ld8(base + (int64_t)p.p2 * pstride + c0, f2);
-    ld8(base + (int64_t)p.p3 * pstride + c0, f3);
-    ld8(base + (int64_t)p.p4 * pstride + c0, f4);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) v[t] += ((p.w1 * f1[t] + p.w2 * f2[t]) + p.w3 * f3[t]) + p.w4 * f4[t];
-  }
-#pragma unroll
-  for (int t = 0; t < 8; ++t) v[t] = v[t] / count;
-}
-
-template <typename T>
-__global__ void __launch_bounds__(256) roi_align_fwd_win_kernel(Levels L, int64_t C, const float* __restrict__ rois, int PH,
-                                                                int PW, int sampling, int aligned, int multiscale,
-                                                                T* __restrict__ out, int32_t* __restrict__ lv_out) {
-  // block = (RoI k, channel slice q of WIN_CQ channels): the slices of one RoI run as separate blocks, so
-  // window loads of some overlap the gathers of others
-  __shared__ Samp tab[WIN_MAXSAMP];
-  __shared__ RoiGeo sg;
-  __shared__ int slv, bnd[4];
-  extern __shared__ __attribute__((aligned(16))) char wsm[];
-  T* win = (T*)wsm;
-  const int tid = threadIdx.x;
-  const int nq = (int)(C / WIN_CQ);
-  const int64_t k = blockIdx.x / nq;
-  const int64_t cq = (int64_t)(blockIdx.x - k * nq) * WIN_CQ;
-  const float* r = rois + 5 * k;
-  if (tid == 0) {
-    int lv = multiscale ? level_of(r, L.k_min, L.n) : 0;
-    slv = lv;
-    sg = roi_geo(r, L.scale[lv], PH, PW, sampling, aligned);
-    if (lv_out && cq == 0) lv_out[k] = lv;
-    bnd[0] = bnd[2] = 0x7fffffff;
-    bnd[1] = bnd[3] = -1;
-  }
-  __syncthreads();
-  const int lv = slv;
-  const RoiGeo g = sg;
-  const int64_t H = L.H[lv], W = L.W[lv];
-  const int per_bin = g.gh * g.gw, nbins = PH * PW, ns = nbins * per_bin;
-  for (int i = tid; i < ns; i += blockDim.x) {
-    const int bin = i / per_bin, sidx = i % per_bin;
-    const Samp sp = make_samp(g, H, W, bin / PW, bin % PW, sidx / g.gw, sidx % g.gw);
-    tab[i] = sp;
-    if (sp.p1 >= 0) {
-      atomicMin(&bnd[0], (int)(sp.p1 / W));
-      atomicMax(&bnd[1], (int)(sp.p4 / W));
-      atomicMin(&bnd[2], (int)(sp.p1 % W));
-      atomicMax(&bnd[3], (int)(sp.p4 % W));
-    }
-  }
-  __syncthreads();
-  const T* f = (const T*)L.f[lv] + g.b * H * W * C;
-  const int y0 = bnd[0], x0 = bnd[2], wh = bnd[1] - y0 + 1, ww = bnd[3] - x0 + 1;
-  constexpr int Q8 = WIN_CQ / 8, U4 = 8 * (int)sizeof(T) / 16;  // 16-B pieces per 8 channels
-  if (bnd[1] < 0 || wh * ww > WIN_PX) {  // no sample inside the map (all zero) or a large window: v8 loop
-    for (int e = tid; e < nbins * Q8; e += blockDim.x) {
-      const int bin = e / Q8, c0 = (int)cq + (e - bin * Q8) * 8;
-      float v[8];
-      roi_bin8(tab, bin, per_bin, f, C, c0, 0.f, g.count, v);
-      st8(out + (k * nbins + bin) * C + c0, v);
-    }
-    return;
-  }
-  const int npx = wh * ww;
-  for (int e = tid; e < npx * Q8; e += blockDim.x) {
-    const int px = e / Q8, c0 = (e - px * Q8) * 8, py = px / ww, pxx = px - py * ww;
-    const uint4* src = (const uint4*)(f + ((int64_t)(y0 + py) * W + (x0 + pxx)) * C + cq + c0);
-    uint4* dst = (uint4*)(win + px * WIN_STRIDE + c0);
-#pragma unroll
-    for (int u = 0; u < U4; ++u) dst[u] = src[u];
-  }
-  for (int i = tid; i < ns; i += blockDim.x) {  // corner offsets relative to the window
-    Samp& sp = tab[i];
-    if (sp.p1 < 0) continue;
-    const int yl = sp.p1 / (int)W - y0, xl = sp.p1 % (int)W - x0, yh = sp.p4 / (int)W - y0, xh = sp.p4 % (int)W - x0;
-    sp.p1 = yl * ww + xl; sp.p2 = yl * ww + xh; sp.p3 = yh * ww + xl; sp.p4 = yh * ww + xh;
-  }
-  __syncthreads();
-  for (int e = tid; e < nbins * Q8; e += blockDim.x) {
-    const int bin = e / Q8, c0 = (e - bin * Q8) * 8;
-    float v[8];
-    roi_bin8(tab, bin, per_bin, (const T*)win, WIN_STRIDE, c0, 0.f, g.count, v);
-    st8(out + (k * nbins + bin) * C + cq + c0, v);
-  }
-}
-
 // ---- deterministic backward (gather form, no atomics) ---------------------------------------------
 // grad_feat[n, y, x, :] = sum over the RoIs k of image n at this level, their bins and the bilinear
 // corners landing on (y, x) of gout[k, bin, :] / count * w. Pass 1 (one block per RoI) merges each
@@ -700,12 +594,6 @@ static int check_grid(int PH, int PW, int sampling) {
 
 using namespace mx;
 
-// MX_ROI_FWD_WIN=0: the v8 gather kernel for every RoI (A/B switch; read once)
-static const int g_roi_fwd_win = [] {
-  const char* e = getenv("MX_ROI_FWD_WIN");
-  return e && e[0] == '0' ? 0 : 1;
-}();
-
 static int launch_fwd(const Levels& L, int dtype, int64_t C, const float* rois, int64_t K, int PH, int PW, int sampling,
                       int aligned, int ms, void* out, int32_t* lv, hipStream_t s) {
   MX_CHECK_ARG(check_grid(PH, PW, sampling), "roi_align: unsupported pooled %dx%d sampling %d", PH, PW, sampling);
@@ -721,15 +609,7 @@ static int launch_fwd(const Levels& L, int dtype, int64_t C, const float* rois, 
     return MX_OK;
   }
   int threads = C >= 256 ? 256 : (int)(cdiv(C, 64) * 64);
-  if (C % WIN_CQ == 0 && PH * PW * sampling * sampling <= WIN_MAXSAMP && g_roi_fwd_win) {
-    const size_t lds = (size_t)WIN_PX * WIN_STRIDE * (dtype == MX_F32 ? 4 : 2);
-    if (dtype == MX_F32)
-      roi_align_fwd_win_kernel<float><<<(unsigned)(K * (C / WIN_CQ)), 256, lds, s>>>(L, C, rois, PH, PW, sampling, aligned, ms,
-                                                                    (float*)out, lv);
-    else
-      roi_align_fwd_win_kernel<uint16_t><<<(unsigned)(K * (C / WIN_CQ)), 256, lds, s>>>(L, C, rois, PH, PW, sampling, aligned, ms,
-                                                                       (uint16_t*)out, lv);
-  } else if (C % 8 == 0 && dtype == MX_F32)
+  if (C % 8 == 0 && dtype == MX_F32)
     roi_align_fwd_v8_kernel<float><<<(unsigned)K, 256, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms, (float*)out, lv);
   else if (C % 8 == 0)
     roi_align_fwd_v8_kernel<uint16_t><<<(unsigned)K, 256, 0, s>>>(L, C, rois, PH, PW, sampling, aligned, ms,

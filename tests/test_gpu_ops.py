@@ -685,10 +685,9 @@ def test_canvas_pack_unpack_equals_torch(dev, dtype):
 
 
 @pytest.mark.parametrize("C", [64, 256])
-def test_roi_align_fwd_window_path_bitexact(dev, C):
-    """C % 64 == 0: the windowed forward (roi_align_fwd_win_kernel: RoI pixel window staged in LDS,
-    64-channel passes) for small RoIs, the in-block v8 loop for windows over 224 pixels, RoIs partly
-    or wholly outside the map -- all bit-identical to the oracle (same per-element op order)."""
+def test_roi_align_fwd_wide_channels_bitexact(dev, C):
+    """The 8-channel-vector forward (roi_align_fwd_v8_kernel) at C = 64 / 256 over small and large RoIs,
+    RoIs partly or wholly outside the map: bit-identical to the oracle (same per-element op order)."""
     from mx_det import ops
     rng = np.random.default_rng(C)
     N, H, W, scale = 2, 100, 168, 1 / 8
