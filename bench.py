@@ -213,19 +213,22 @@ _SCRUB = {}
 
 def time_cold(fn, reps=10, scrub_mb=4096):
     """Device time of fn() as it runs inside a train step: caches cold and no host gap. Before every
-    rep a 4 GiB fill (~0.8 ms) evicts the 4 MiB L2s and the 256 MiB Infinity Cache (the operands come from HBM,
-    as in the step where other kernels run between producer and consumer) and keeps the GPU busy
-    while the host enqueues fn's launches, so the HIP events bracket only fn's kernels (no Python /
-    allocation time). Returns the mean in microseconds."""
+    rep a 4 GiB read (~0.6 ms) evicts the 4 MiB L2s and the 256 MiB Infinity Cache (the operands come
+    from HBM, as in the step where other kernels run between producer and consumer) and keeps the GPU
+    busy while the host enqueues fn's launches, so the HIP events bracket only fn's kernels (no Python /
+    allocation time). A read, not a fill: a 4 GiB write left the caches full of dirty lines whose
+    write-back then ran inside fn's window (the round-2 backward figure's 2.5x). Returns the mean in
+    microseconds."""
     dev = torch.device("cuda", torch.cuda.current_device())
     buf = _SCRUB.get(dev)
     if buf is None:
-        buf = _SCRUB[dev] = torch.empty(scrub_mb * 2 ** 20 // 4, dtype=torch.float32, device=dev)
+        buf = _SCRUB[dev] = torch.zeros(scrub_mb * 2 ** 20 // 4, dtype=torch.float32, device=dev)
     fn()
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    sink = torch.empty((), dtype=torch.float32, device=dev)
     for a, b in ev:
-        buf.fill_(1.0)
+        torch.amax(buf, dim=0, out=sink)
         a.record()
         fn()
         b.record()

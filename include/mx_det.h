@@ -307,8 +307,9 @@ int mx_conv_transpose_weight(const uint16_t* w, int64_t K, int64_t RS, int64_t C
 int mx_conv2d_dgrad_t(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, uint16_t* dx, void* ws,
                       size_t ws_bytes, mx_stream_t stream);
 /* mx_conv2d_dgrad_t plus a bf16 [N][H][W][C] tensor added to dx in the epilogue before the single
- * bf16 rounding (stride 1): the gradient of an input that also feeds a residual branch (ResNet
- * bottleneck x -> conv1 and x -> + identity) without a separate add pass. */
+ * bf16 rounding (strides 1 and 2: each parity class adds it at the pixels it writes): the gradient of
+ * an input that also feeds another branch (ResNet bottleneck x -> conv1 and x -> + identity, a stage
+ * output read by the next stage and the FPN) without a separate add pass. */
 int mx_conv2d_dgrad_ex(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, const uint16_t* residual,
                        uint16_t* dx, void* ws, size_t ws_bytes, mx_stream_t stream);
 /* mx_conv2d_dgrad_ex whose output dx is the incoming gradient of a train-mode BatchNorm (+act)

@@ -3205,8 +3205,8 @@ extern "C" int mx_conv2d_dgrad_bnb(const mx_conv_shape* s, const uint16_t* dy, c
 
 static int dgrad_impl(const mx_conv_shape* s, const uint16_t* dy, const uint16_t* wt, const uint16_t* residual,
                       uint16_t* dx, const BnbArgs* bnb, void* ws, size_t ws_bytes, mx_stream_t stream) {
-  MX_CHECK_ARG(!residual || (s && s->stride_h == 1 && s->stride_w == 1),
-               "conv dgrad: a residual (gradient accumulated in the epilogue) needs stride 1");
+  // residual: a gradient accumulated in the epilogue; under stride 2 each parity class adds it at the
+  // pixels it writes (classes without taps write it alone), so every pixel gets it exactly once
   int rc = conv_check(s);
   if (rc) return rc;
   MX_CHECK_ARG(s->K % 8 == 0, "conv dgrad: K=%lld must be a multiple of 8", (long long)s->K);
@@ -3590,7 +3590,6 @@ extern "C" int mx_conv2d_dgrad_x3(const mx_conv_shape* s, const float* dy, const
   if (rc) return rc;
   MX_CHECK_ARG(s->K % 8 == 0 && s->C % 8 == 0, "conv dgrad x3: K and C must be multiples of 8");
   MX_CHECK_ARG(s->stride_h <= 2 && s->stride_w <= 2, "conv dgrad x3: strides 1 and 2 are supported");
-  MX_CHECK_ARG(!residual || (s->stride_h == 1 && s->stride_w == 1), "conv dgrad x3: a residual needs stride 1");
   const bool bnb = part != nullptr;
   if (bnb) {
     MX_CHECK_ARG(s->stride_h == 1 && s->stride_w == 1, "conv dgrad x3 bnb: stride 1 only");

@@ -421,7 +421,7 @@ def _is_dense(x_shape, R, S, stride, pad):
 def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
     """dy NHWC [N,Ho,Wo,K] (K = the wt's padded output channels), wt from pack_weight(dgrad=True)
     -> dx NHWC [N,H,W,C] of dy's dtype (+ residual, a tensor of dx's shape and dtype added in the
-    epilogue; stride 1). f32 dy: bf16x3 kernels on the split wt."""
+    epilogue, at every pixel once under either stride). f32 dy: bf16x3 kernels on the split wt."""
     N, H, W, C = x_shape
     K = dy.shape[3]
     x3 = is_x3(dy)
@@ -631,10 +631,59 @@ class absorb_mode:
         global _absorb_on
         _absorb_on = self.prev
         _absorb.clear()
+        _chains.clear()
 
 
 def absorbing():
     return _absorb_on
+
+
+class GradChain:
+    """A tensor read by several convs inside a captured graph (a backbone stage output: the next
+    stage's first conv and downsample, and the FPN lateral conv): their backwards run in a fixed
+    order; each adds the running sum of the earlier ones' input gradients in its own dgrad epilogue
+    (conv_dgrad residual) and hands it on; the last returns the total to autograd, the others None --
+    no separate accumulation passes. Consumers join at forward time (n counts them), so a consumer
+    that does not see the chain simply returns its gradient to autograd as usual."""
+    __slots__ = ("n", "seen", "acc")
+
+    def __init__(self):
+        self.n, self.seen, self.acc = 0, 0, None
+
+    def last(self):
+        return self.seen + 1 >= self.n
+
+    def hand(self, dx):
+        self.seen += 1
+        if self.seen >= self.n:
+            self.seen, self.acc = 0, None
+            return dx
+        self.acc = dx
+        return None
+
+
+_chains = {}
+
+
+def chain_over(t):
+    """Inside a graph capture (absorb_mode): the convs consuming `t` from here on accumulate its
+    gradient through one GradChain."""
+    _chains[id(t)] = (weakref.ref(t), GradChain())
+
+
+def _chain_join(t):
+    e = _chains.get(id(t))
+    if e is None or e[0]() is not t:
+        return None
+    e[1].n += 1
+    return e[1]
+
+
+def _chain_res(chain, res):
+    """A dgrad's residual with the chain's running sum added."""
+    if chain is None or chain.acc is None:
+        return res
+    return chain.acc if res is None else res + chain.acc
 
 
 def absorb_into(t, slot):
@@ -663,6 +712,7 @@ class ConvAct(torch.autograd.Function):
         ctx.cfg = (stride, pad, act, w.shape, b is not None)
         ctx.wref, ctx.uses = weakref.ref(w), _count_use(w)
         ctx.slot = _absorb_take(x) if _absorb else None
+        ctx.chain = _chain_join(x) if _chains and need_dx else None
         return y
 
     @staticmethod
@@ -677,12 +727,16 @@ class ConvAct(torch.autograd.Function):
             if _is_dense(x.shape, R, S, stride, pad):  # 1x1-GEMM form: dX[N, R*S*C] = dY[N, K8] wt
                 N, H, W, C = x.shape
                 dx = conv_dgrad(gk.view(N, 1, 1, K8), wt, (N, 1, 1, H * W * C), 1, 1, (1, 1), (0, 0)).view(N, H, W, C)
+                if ctx.chain is not None and ctx.chain.acc is not None:
+                    dx = dx + ctx.chain.acc
             else:
                 extra = ctx.slot.buf if ctx.slot is not None else None
-                if extra is not None and not (tuple(stride) == (1, 1) and extra.dtype == gk.dtype and
-                                              extra.shape == x.shape and extra.is_contiguous()):
-                    raise RuntimeError("absorbed gradient needs a stride-1 conv and an input-shaped buffer")
-                dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad, residual=extra)
+                if extra is not None and not (extra.dtype == gk.dtype and extra.shape == x.shape and
+                                              extra.is_contiguous()):
+                    raise RuntimeError("absorbed gradient needs an input-shaped buffer of the gradient's dtype")
+                dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad, residual=_chain_res(ctx.chain, extra))
+            if ctx.chain is not None:
+                dx = ctx.chain.hand(dx)
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad(gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1], side=side_wgrad_enabled(ctx))
         return dx, dw, db, None, None, None, None
@@ -733,6 +787,7 @@ class ConvBNAct(torch.autograd.Function):
         if bnb_own is not None:  # the next conv's dgrad will produce this BN's backward partials
             bnb_own.y, bnb_own.z, bnb_own.mean, bnb_own.invstd, bnb_own.act = y, z, mean, invstd, act
         ctx.wref, ctx.uses = weakref.ref(w), _count_use(w)
+        ctx.chain = _chain_join(x) if _chains and need_dx else None
         return y
 
     @staticmethod
@@ -774,9 +829,13 @@ class ConvBNAct(torch.autograd.Function):
             if ctx.role == "src":
                 res, link.dres = link.dres, None
             feed = ctx.bnb_feed
+            chain = ctx.chain
+            # BN-backward partials from this epilogue only when it produces the input's whole gradient
             bnb = feed if (feed is not None and feed.y is not None and tuple(stride) == (1, 1)
-                           and feed.y.shape == x.shape) else None
-            dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad, residual=res, bnb=bnb)
+                           and feed.y.shape == x.shape and (chain is None or chain.last())) else None
+            dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad, residual=_chain_res(chain, res), bnb=bnb)
+            if chain is not None:
+                dx = chain.hand(dx)
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad(dz, x, K, R, S, stride, pad, cin=wshape[1], side=side_wgrad_enabled(ctx))
         dgamma = sums[1] if ctx.needs_input_grad[2] else None

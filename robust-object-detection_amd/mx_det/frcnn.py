@@ -120,6 +120,8 @@ class ResNet50Body(nn.Module):
         out = OrderedDict()
         for i, name in enumerate(self.LAYERS):
             x = self.run_layer(name, x, be)
+            if mc.absorbing() and 0 < i < len(self.LAYERS) - 1:
+                mc.chain_over(x)  # C3 / C4: next stage's conv1 + downsample and the FPN lateral conv
             out[str(i)] = x
         return out
 
@@ -1157,6 +1159,8 @@ class _SegGraphs:
         leaves, cs = [], [c]
         for k, name in enumerate(("layer2", "layer3", "layer4")):
             leaf = c.detach().requires_grad_(self.need[k])
+            if k > 0 and self.need[k] and mc.absorbing():
+                mc.chain_over(leaf)  # C3 / C4 leaves: next stage's conv1 + downsample and the FPN lateral
             leaves.append(leaf)
             c = body.run_layer(name, leaf, be)
             cs.append(c)

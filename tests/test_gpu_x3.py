@@ -323,3 +323,27 @@ def test_x3_wgrad_wide_tiles(dev, monkeypatch, variant, case):
         test_x3_dgrad_wgrad(dev, *case)
     finally:
         call("mx_conv_set_wgrad_variant", 3)
+
+
+@pytest.mark.parametrize("k,st,pd,tile", [(1, 2, 0, (0, 0)), (3, 2, 1, (0, 0)), (3, 2, 1, (64, 64)), (1, 2, 0, (64, 64))])
+def test_x3_dgrad_residual_stride2(dev, k, st, pd, tile, monkeypatch):
+    """Stride-2 dgrad with a residual (conv.GradChain: a stage output's gradient accumulated through
+    the next stage's downsample): every parity class adds the residual at the pixels it writes, the
+    tap-less classes of a 1x1 stride-2 conv write it alone -- equal to dgrad + residual."""
+    from mx_det._lib import call
+    from mx_det import conv as mc
+    monkeypatch.setenv("MX_CONV_TUNE", "0")
+    call("mx_conv_set_tile", *tile)
+    try:
+        g = torch.Generator().manual_seed(11 + k)
+        N, H, W, C, K = 2, 21, 26, 64, 128
+        w = torch.randn(K, C, k, k, generator=g) * 0.05
+        Ho, Wo = (H + 2 * pd - k) // st + 1, (W + 2 * pd - k) // st + 1
+        dy = torch.randn(N, Ho, Wo, K, generator=g).to(dev)
+        res = torch.randn(N, H, W, C, generator=g).to(dev)
+        _, wt = mc.pack_weight(w.to(dev), C, (st, st), (pd, pd), krsc=False, dgrad=True, split=True)
+        a = mc.conv_dgrad(dy, wt, (N, H, W, C), k, k, (st, st), (pd, pd), residual=res)
+        b = mc.conv_dgrad(dy, wt, (N, H, W, C), k, k, (st, st), (pd, pd)) + res
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    finally:
+        call("mx_conv_set_tile", 0, 0)
