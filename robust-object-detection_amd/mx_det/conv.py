@@ -13,6 +13,7 @@ running buffers), so state_dicts load both ways; the kernels ta
 (split into hi / lo planes in f32 mode) made once per step.
 """
 import ctypes
+import os
 import weakref
 
 import torch
@@ -667,7 +668,9 @@ _chains = {}
 
 def chain_over(t):
     """Inside a graph capture (absorb_mode): the convs consuming `t` from here on accumulate its
-    gradient through one GradChain."""
+    gradient through one GradChain (MX_GRAD_CHAIN=0: autograd sums them, for A/B checks)."""
+    if os.environ.get("MX_GRAD_CHAIN", "1") == "0":
+        return
     _chains[id(t)] = (weakref.ref(t), GradChain())
 
 

@@ -148,9 +148,14 @@ def test_filter_proposals_matches_cpu_backend(dev, levels, tiny):
 
 def test_graphed_trunk_matches_eager(dev, monkeypatch):
     """The HIP-graph replay of backbone + FPN + RPN head gives the eager step's losses, gradients and
-    parameter updates (same kernels, replayed): 3 train steps each way from the same init and RNG
-    state. The only run-to-run noise is the float-atomic order of the RoIAlign backward, amplified by
-    a random-init network; it is measured by a second eager run and bounds the graph-vs-eager gap."""
+    parameter updates: 3 train steps each way from the same init and RNG state. The eager step is
+    deterministic (a second eager run is bit-identical); the captured graphs sum some gradients in
+    other places (GradChain: a stage output's three consumer gradients added in dgrad epilogues,
+    root-gradient absorption), i.e. in another f32 rounding order, so the step-1 gradients agree to
+    rounding (rel 1e-4) and the 3-step losses to 3e-2. Later parameter states are not compared
+    element-wise: a random-init network amplifies a 1e-5 perturbation chaotically over 3 steps
+    (BN biases drift by up to ~0.3 rel, measured with tools/graph_vs_eager.py; with MX_GRAD_CHAIN=0
+    the graph run is bit-identical to eager, as is a second eager run)."""
     import copy
     from mx_det.data import synth_batch
     from mx_det.optim import SGD
@@ -158,8 +163,9 @@ def test_graphed_trunk_matches_eager(dev, monkeypatch):
     base = _model(dev).train()
     imgs, tg = synth_batch(0, 2, H=320, W=480, device=dev)
     res = {}
-    for run, mode in (("eager", "0"), ("eager2", "0"), ("graph", "1")):
+    for run, mode in (("eager", "0"), ("eager2", "0"), ("graph", "1"), ("graph_nochain", "1")):
         monkeypatch.setenv("MX_GRAPHS", mode)
+        monkeypatch.setenv("MX_GRAD_CHAIN", "0" if run == "graph_nochain" else "1")
         m = copy.deepcopy(base)
         opt = SGD([p for p in m.parameters() if p.requires_grad], lr=0.005, momentum=0.9, weight_decay=5e-4)
         torch.manual_seed(5)
@@ -183,18 +189,17 @@ def test_graphed_trunk_matches_eager(dev, monkeypatch):
         return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
 
     for k in ge:  # step-1 gradients of every trainable parameter
-        assert rel(gg[k], ge[k]) <= max(5e-2, 3 * rel(g2[k], ge[k])), (k, rel(gg[k], ge[k]), rel(g2[k], ge[k]))
-    for a, b, c in zip(le, l2, lg):
-        assert abs(c - a) <= max(3e-2 * abs(a), 3 * abs(b - a)), (le, l2, lg)
-    # after 3 steps the atomic-order noise has been amplified chaotically (eager vs eager reaches
-    # ~0.6 on some BN biases and its per-parameter size is itself random): each parameter is held to
-    # max(0.1, 3x its own eager noise), and the mean drift over all parameters to 1.5x the eager one
-    dg, de = [], []
+        assert rel(g2[k], ge[k]) == 0.0, k  # eager is deterministic
+        assert rel(gg[k], ge[k]) <= 1e-4, (k, rel(gg[k], ge[k]))
+    assert le == l2, (le, l2)
+    lc, gc, _ = res["graph_nochain"]  # the same summation order as eager: bit-identical
+    assert lc == le, (lc, le)
+    for k in ge:
+        assert torch.equal(gc[k], ge[k]), k
+    for a, c in zip(le, lg):
+        assert abs(c - a) <= 3e-2 * abs(a), (le, lg)
     for k in se:
         if k.endswith("num_batches_tracked"):
             assert int(se[k]) == int(sg[k]) == 3, k
         else:
-            dg.append(rel(sg[k], se[k]))
-            de.append(rel(s2[k], se[k]))
-            assert dg[-1] <= max(0.1, 3 * de[-1]), (k, dg[-1], de[-1])
-    assert sum(dg) <= 1.5 * sum(de) + 0.01 * len(de), (sum(dg) / len(dg), sum(de) / len(de))
+            assert torch.isfinite(sg[k].float()).all(), k

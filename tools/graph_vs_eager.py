@@ -26,17 +26,24 @@ def main():
         m = copy.deepcopy(base)
         opt = SGD([p for p in m.parameters() if p.requires_grad], lr=0.005, momentum=0.9, weight_decay=5e-4)
         torch.manual_seed(5)
-        losses = []
+        losses, g1 = [], None
         for it in range(3):
             loss = sum(m(imgs, tg).values())
             opt.zero_grad(set_to_none=True)
             loss.backward()
+            if it == 0:
+                g1 = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
             opt.step()
             losses.append(float(loss.detach()))
-        res[run] = (losses, {k: v.detach().clone() for k, v in m.state_dict().items()})
+        res[run] = (losses, {k: v.detach().clone() for k, v in m.state_dict().items()}, g1)
     rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()  # noqa: E731
-    (le, se), (l2, s2), (lg, sg) = res["eager"], res["eager2"], res["graph"]
+    (le, se, ge), (l2, s2, g2), (lg, sg, gg) = res["eager"], res["eager2"], res["graph"]
     print("losses", le, l2, lg)
+    rows = sorted(((rel(gg[k], ge[k]), rel(g2[k], ge[k]), k) for k in ge), reverse=True)
+    print("step-1 gradients, worst graph-vs-eager:")
+    for g, e, k in rows[:12]:
+        print(f"{k:60s} graph {g:.3e} eager2 {e:.3e}")
+    print("after 3 steps:")
     rows = sorted(((rel(sg[k], se[k]), rel(s2[k], se[k]), k) for k in se if not k.endswith("num_batches_tracked")),
                   reverse=True)
     for g, e, k in rows[:12]:
