@@ -123,6 +123,9 @@ int mx_batched_nms(const float* boxes, const float* scores, const int64_t* idxs,
  *     backward with deterministic = 0 only (atomics, as torchvision's CUDA kernel).
  * ------------------------------------------------------------------------------------------- */
 size_t mx_roi_align_bwd_workspace(int64_t K, int PH, int PW, int sampling);
+/* deterministic-gather tile width (pixels per wave strip): 2 (default), 4 or 8. Results are identical;
+ * 4-wide tiles shorten the tail of tiles that many RoIs overlap. Not thread-safe (a process setting). */
+int mx_roi_bwd_set_strip(int sw);
 int mx_roi_align_fwd(const void* feat, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, const float* rois,
                      int64_t K, float spatial_scale, int PH, int PW, int sampling, int aligned, void* out,
                      mx_stream_t stream);

@@ -275,13 +275,55 @@ __global__ void __launch_bounds__(256) nms_scan_lds_kernel(const uint64_t* __res
   }
 }
 
+// OR of a 64-bit value over the 64 lanes of the wave (DPP: pairs, quads, half-rows, rows, then the
+// row broadcasts; lane 63 ends up with the total), returned wave-uniform
+__device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
+  int x = (int)v;
+  x |= __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  x |= __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  x |= __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  x |= __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false);  // row_mirror
+  x |= __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x |= __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return (uint32_t)__builtin_amdgcn_readlane(x, 63);
+}
+
+// Greedy NMS inside one 64 x 64 diagonal tile: lane l holds row l's suppression bits (bit t: box l
+// suppresses box t > l); `live` = the candidates (in range, not removed by earlier blocks). The
+// greedy set G is the unique fixpoint of K -> live & ~OR{row s : s in K}: each Jacobi step fixes at
+// least one more leading position, and a repeated K is that fixpoint. A few wave-wide ORs replace
+// the walk's one dependent readlane pair per survivor; chains still unresolved after 8 steps
+// finish with the walk (the same greedy result either way).
+__device__ __forceinline__ uint64_t tile_greedy(uint64_t diag, uint64_t live, int lane) {
+  uint64_t k = live;
+  for (int it = 0; it < 8; ++it) {
+    const uint64_t c = ((k >> lane) & 1ull) ? diag : 0ull;
+    const uint64_t sup = ((uint64_t)wave_or32((uint32_t)(c >> 32)) << 32) | wave_or32((uint32_t)c);
+    const uint64_t nk = live & ~sup;
+    if (nk == k) return k;
+    k = nk;
+  }
+  const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
+  uint64_t cur = ~live, kept = 0;
+  uint64_t avail = live;
+  while (avail) {
+    const int t = __builtin_ctzll(avail);
+    kept |= 1ull << t;
+    const uint64_t row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, t) << 32) |
+                         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, t);
+    cur |= row;
+    avail = ~cur & ~((2ull << t) - 1ull);
+  }
+  return kept;
+}
+
 // Single-wave scan (segments of up to 64*SCAN_WAVE_W boxes): one 64-lane workgroup per segment and
 // no workgroup barriers. A 64-row block's mask rows are one contiguous run of 64*Wm words; it is
 // copied whole into an LDS ring slot by LDS-DMA (16 coalesced 1 KiB buffer_load_dwordx4 ... lds, plus
 // one for the block's 64 box ids), SCAN_RING - 1 blocks ahead of the one being resolved, so the
 // dependent walk waits on L2/MALL latency once per segment instead of once per block. Lane w keeps the
-// removed bits of word w in a register; the in-tile chain is walked wave-uniformly over the survivors
-// (as in nms_scan_lds_kernel) and lanes w and w + 32 OR the kept rows' word w from LDS (half the rows
+// removed bits of word w in a register; the in-tile chain is resolved by tile_greedy (Jacobi steps of
+// wave-wide ORs, the survivor walk as the fallback) and lanes w and w + 32 OR the kept rows' word w from LDS (half the rows
 // each, eight reads in flight), combined with one cross-lane permute.
 // Same greedy result as nms_scan_kernel. Every block issues exactly SCAN_DMA VMEM instructions
 // (slots past the rows read out of range -> zero) and one flags store, so the counted waits are exact.
@@ -336,17 +378,7 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(const uint64_t* __res
       const uint64_t rm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(rem >> 32), blk) << 32) |
                           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rem, blk);
       const uint64_t valid = cnt >= 64 ? ~0ull : ((1ull << cnt) - 1);
-      uint64_t cur = rm, kept = 0;
-      const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
-      uint64_t avail = ~cur & valid;
-      while (avail) {
-        const int t = __builtin_ctzll(avail);
-        kept |= 1ull << t;
-        const uint64_t row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, t) << 32) |
-                             (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, t);
-        cur |= row;
-        avail = ~cur & valid & ~((2ull << t) - 1ull);
-      }
+      const uint64_t kept = tile_greedy(diag, ~rm & valid, lane);
       // flags were zeroed by the keys kernel: every lane < cnt (>= 1 of them) stores, so each block
       // issues exactly one store instruction
       if (lane < cnt) flags[ids[lane]] = (int32_t)((kept >> lane) & 1ull);

@@ -369,9 +369,10 @@ __device__ __forceinline__ float4 ld4f(const T* p) {
 // are listed in ascending k (one ordered block compaction per 1024 RoIs); each wave then walks them
 // independently (no barriers): a ballot over the RoI's bins picks those whose pixel bbox meets the
 // wave's strip, 64/S4 (<= 4) such bins are loaded at once -- their corner slots one per lane and their
-// gout rows one quad per lane, the next group prefetched while the current one is applied -- and
-// the hit bits are walked in slot order with readlane: fixed order per output element.
-template <typename T>
+// gout rows one quad per lane, the next group (of this or a later RoI) prefetched while the current
+// one is applied -- and the hit bits are walked in slot order with readlane: fixed order per output
+// element.
+template <typename T, int SW>
 __global__ void __launch_bounds__(512, 2) roi_bwd_gather_kernel(Levels L, TileGrid TG, int64_t C, int64_t K, int nbins, int S4,
                                                              float count, const BwdEnt* __restrict__ ent,
                                                              const int2* __restrict__ binbox, const int4* __restrict__ box,
@@ -385,7 +386,7 @@ __global__ void __launch_bounds__(512, 2) roi_bwd_gather_kernel(Levels L, TileGr
   const int64_t rem = id - TG.first[lv];
   const int per_img = TG.th[lv] * TG.tw[lv];
   const int n = (int)(rem / per_img), t = (int)(rem % per_img);
-  const int ty0 = (t / TG.tw[lv]) * 8, tx0 = (t % TG.tw[lv]) * 8;
+  const int ty0 = (t / TG.tw[lv]) * 8, tx0 = (t % TG.tw[lv]) * SW;
   const int64_t H = L.H[lv], W = L.W[lv];
   const int Q = (int)(C / 4);
   const bool qa = lane < Q;  // this lane's channel quad exists
@@ -394,7 +395,7 @@ __global__ void __launch_bounds__(512, 2) roi_bwd_gather_kernel(Levels L, TileGr
   const float inv = 1.f / count;
   const bool pow2 = inv * count == 1.f && (__float_as_uint(count) & 0x7fffffu) == 0;
   const int32_t want = n * 8 + lv;
-  const int sy0 = ty0 + wave;  // this wave's strip: row sy0, cols tx0..tx0+7
+  const int sy0 = ty0 + wave;  // this wave's strip: row sy0, cols tx0..tx0+SW-1
   const int NBC = min(4, 64 / S4);  // bins per load group
   const int sub = lane / S4, sj = lane - sub * S4;
   for (int64_t c0 = 0; c0 < K; c0 += 1024) {
@@ -405,7 +406,7 @@ __global__ void __launch_bounds__(512, 2) roi_bwd_gather_kernel(Levels L, TileGr
       hit[r] = false;
       if (kq < K && meta[kq] == want) {
         const int4 b = box[kq];
-        hit[r] = b.x <= ty0 + 7 && b.y >= ty0 && b.z <= tx0 + 7 && b.w >= tx0;
+        hit[r] = b.x <= ty0 + 7 && b.y >= ty0 && b.z <= tx0 + SW - 1 && b.w >= tx0;
       }
     }
     uint64_t m[2];
@@ -428,46 +429,78 @@ __global__ void __launch_bounds__(512, 2) roi_bwd_gather_kernel(Levels L, TileGr
     }
     const int nl = base;
     __syncthreads();
-    for (int li = 0; li < nl; ++li) {
-      const int64_t kk = list[li];
-      // bins of this RoI whose pixel bbox meets the strip (nbins <= 64 for the deterministic path)
-      bool bh = false;
-      if (lane < nbins) {
-        const int2 bb = binbox[kk * nbins + lane];
-        const int by0 = (int)(int16_t)(bb.x & 0xffff), by1 = bb.x >> 16;
-        const int bx0 = (int)(int16_t)(bb.y & 0xffff), bx1 = bb.y >> 16;
-        bh = by0 <= sy0 && by1 >= sy0 && bx0 <= tx0 + 7 && bx1 >= tx0;
+    // Pipelined walk over the listed RoIs (ascending k: the fixed summation order), 64 at a time.
+    // Phase 1: each RoI's bins on this strip as a 64-bit mask in lane (j - j0), from binbox rows of 8
+    // RoIs per round trip. Phase 2: the RoIs with hits in order, as a stream of (RoI, bin group)
+    // loads double-buffered in two named register sets: the next group (of this or a later RoI) is in
+    // flight while the current one is applied. Every load is unconditional (clamped indices, results
+    // masked after) so the compiler's counted waits stay exact across the loop.
+    for (int j0 = 0; j0 < nl; j0 += 64) {
+      const int nb = min(64, nl - j0);
+      uint32_t bml = 0, bmh = 0;
+      const int bl = min(lane, nbins - 1);
+      for (int r0 = 0; r0 < nb; r0 += 8) {
+        int2 bb[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) bb[r] = binbox[(int64_t)list[j0 + min(r0 + r, nb - 1)] * nbins + bl];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int by0 = (int)(int16_t)(bb[r].x & 0xffff), by1 = bb[r].x >> 16;
+          const int bx0 = (int)(int16_t)(bb[r].y & 0xffff), bx1 = bb[r].y >> 16;
+          const bool bh = lane < nbins && r0 + r < nb && by0 <= sy0 && by1 >= sy0 && bx0 <= tx0 + SW - 1 && bx1 >= tx0;
+          const uint64_t bmr = __ballot(bh);
+          if (lane == r0 + r) {
+            bml = (uint32_t)bmr;
+            bmh = (uint32_t)(bmr >> 32);
+          }
+        }
       }
-      uint64_t bm = __ballot(bh);
-      // load group: up to NBC (<= 4) bins of bm in order; lane (sub, sj) holds slot sj of bin sub,
-      // lane q holds channel quad q of each bin's gout row
-      int gb0 = -1, gb1 = -1, gb2 = -1, gb3 = -1;
-      BwdEnt e;
-      float4 go0, go1, go2, go3;
+      uint64_t todo = __ballot((bml | bmh) != 0u);  // RoIs of this batch with a bin on the strip
+      int cj = 0;                                    // cursor: RoI (batch lane) and its bins not yet loaded
+      uint64_t cbm = 0;
+      auto advance = [&]() -> bool {
+        if (cbm == 0) {
+          if (todo == 0) return false;
+          cj = __builtin_ctzll(todo);
+          todo &= todo - 1;
+          cbm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)bmh, cj) << 32) |
+                (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)bml, cj);
+        }
+        return true;
+      };
+      // a load group: up to NBC (<= 4) bins of the cursor RoI in order; lane (sub, sj) holds corner
+      // slot sj of bin sub, lane q channel quad q of each bin's gout row
+      struct Grp {
+        int g0, g1, g2, g3;
+        bool ev;  // this lane's corner slot belongs to a loaded bin
+        BwdEnt e;
+        float4 o0, o1, o2, o3;  // raw rows: slots without a bin have no hits, lanes >= Q are never stored
+      };
+      const int qc = min(lane, Q - 1);
+      auto load_group = [&](Grp& G, bool valid) {
+        const int64_t kk = list[j0 + (valid ? cj : 0)];
+        G.g0 = G.g1 = G.g2 = G.g3 = -1;
+        if (valid) {
 #define MX_TAKE(gbv, s)                        \
-  if (s < NBC && bm) {                         \
-    gbv = __builtin_ctzll(bm);                 \
-    bm &= bm - 1;                              \
+  if (s < NBC && cbm) {                        \
+    gbv = __builtin_ctzll(cbm);                \
+    cbm &= cbm - 1;                            \
   }
-#define MX_ROW(gbv) (gbv >= 0 && qa ? ld4f(gout + (kk * nbins + gbv) * C + 4 * lane) : make_float4(0.f, 0.f, 0.f, 0.f))
-#define MX_LOAD_GROUP()                                                                        \
-  {                                                                                            \
-    gb0 = gb1 = gb2 = gb3 = -1;                                                                \
-    MX_TAKE(gb0, 0) MX_TAKE(gb1, 1) MX_TAKE(gb2, 2) MX_TAKE(gb3, 3)                            \
-    const int mb = sub == 0 ? gb0 : sub == 1 ? gb1 : sub == 2 ? gb2 : sub == 3 ? gb3 : -1;   \
-    e.yx = -1;                                                                                 \
-    e.w = 0.f;                                                                                 \
-    if (sub < NBC && mb >= 0) e = ent[(kk * nbins + mb) * S4 + sj];                            \
-    go0 = MX_ROW(gb0); go1 = MX_ROW(gb1); go2 = MX_ROW(gb2); go3 = MX_ROW(gb3);                \
-  }
-      MX_LOAD_GROUP();
-      while (gb0 >= 0) {
-        const BwdEnt ce = e;
-        const float4 c0g = go0, c1g = go1, c2g = go2, c3g = go3;
-        if (bm) MX_LOAD_GROUP()  // prefetch the next group
-        else gb0 = -1;
+          MX_TAKE(G.g0, 0) MX_TAKE(G.g1, 1) MX_TAKE(G.g2, 2) MX_TAKE(G.g3, 3)
+#undef MX_TAKE
+        }
+        const int mb = sub == 0 ? G.g0 : sub == 1 ? G.g1 : sub == 2 ? G.g2 : sub == 3 ? G.g3 : -1;
+        G.ev = sub < NBC && mb >= 0;
+        G.e = ent[(kk * nbins + max(mb, 0)) * S4 + (sub < NBC ? sj : 0)];
+        G.o0 = ld4f(gout + (kk * nbins + max(G.g0, 0)) * C + 4 * qc);
+        G.o1 = ld4f(gout + (kk * nbins + max(G.g1, 0)) * C + 4 * qc);
+        G.o2 = ld4f(gout + (kk * nbins + max(G.g2, 0)) * C + 4 * qc);
+        G.o3 = ld4f(gout + (kk * nbins + max(G.g3, 0)) * C + 4 * qc);
+      };
+      auto apply = [&](const Grp& G) {
+        const BwdEnt ce = G.e;
         const int y = (ce.yx >> 16) - sy0, x = (ce.yx & 0xffff) - tx0;
-        const bool inb = ce.yx >= 0 && y == 0 && (unsigned)x < 8u;
+        const bool inb = G.ev && ce.yx >= 0 && y == 0 && (unsigned)x < (unsigned)SW;
         const int plv = inb ? x : -1;  // pixel within the wave's 1x8 strip
         const uint64_t hm = __ballot(inb);
         if (hm) {
@@ -475,7 +508,7 @@ __global__ void __launch_bounds__(512, 2) roi_bwd_gather_kernel(Levels L, TileGr
           // every accumulator and gout quad in named registers
           uint64_t pm[8];
 #pragma unroll
-          for (int p = 0; p < 8; ++p) pm[p] = __ballot(plv == p);
+          for (int p = 0; p < SW; ++p) pm[p] = __ballot(plv == p);
           const uint64_t sl = S4 >= 64 ? ~0ull : ((1ull << S4) - 1);
 #define MX_RUN(sv, cgv)                                                            \
   {                                                                                \
@@ -486,7 +519,7 @@ __global__ void __launch_bounds__(512, 2) roi_bwd_gather_kernel(Levels L, TileGr
     }                                                                              \
   }
 #define MX_PIX(pp)                                                                  \
-  {                                                                                 \
+  if (pp < SW) {                                                                    \
     uint64_t m = sm & pm[pp];                                                       \
     while (m) {                                                                     \
       const int b = __builtin_ctzll(m);                                             \
@@ -498,14 +531,23 @@ __global__ void __launch_bounds__(512, 2) roi_bwd_gather_kernel(Levels L, TileGr
       a##pp.x += vx; a##pp.y += vy; a##pp.z += vz; a##pp.w += vw;                   \
     }                                                                               \
   }
-          MX_RUN(0, c0g) MX_RUN(1, c1g) MX_RUN(2, c2g) MX_RUN(3, c3g)
+          MX_RUN(0, G.o0) MX_RUN(1, G.o1) MX_RUN(2, G.o2) MX_RUN(3, G.o3)
 #undef MX_PIX
 #undef MX_RUN
         }
+      };
+      Grp ga, gb;
+      bool ha = advance();
+      load_group(ga, ha);
+      while (ha) {
+        const bool hb = advance();
+        load_group(gb, hb);  // prefetch (a dummy load past the end: keeps the wait counts exact)
+        apply(ga);
+        if (!hb) break;
+        ha = advance();
+        load_group(ga, ha);
+        apply(gb);
       }
-#undef MX_LOAD_GROUP
-#undef MX_ROW
-#undef MX_TAKE
     }
     __syncthreads();  // list rebuilt for the next 1024 RoIs
   }
@@ -513,7 +555,7 @@ __global__ void __launch_bounds__(512, 2) roi_bwd_gather_kernel(Levels L, TileGr
   if (qa) {
     const float4 av[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < SW; ++i) {
       const int y = sy0, x = tx0 + i;
       if (y < H && x < W) *((float4*)(gmap + ((int64_t)y * W + x) * C) + lane) = av[i];
     }
@@ -633,6 +675,16 @@ static size_t det_ws_bytes(int64_t K, int PH, int PW, int sampling) {
 // one channel quad per lane (C <= 256); 16 pixels x 4 channels of f32 accumulators per lane
 static bool det_supported(int64_t C) { return C >= 4 && C <= 256 && C % 4 == 0; }
 
+// deterministic gather tile: 8 rows x g_roi_strip columns (one wave per row strip). Narrower strips cut
+// the work of the block and of each wave on tiles that many RoIs overlap (the kernel's tail) at more
+// blocks (each re-scans the RoI list): mx_roi_bwd_set_strip
+static int g_roi_strip = 2;
+extern "C" int mx_roi_bwd_set_strip(int sw) {
+  MX_CHECK_ARG(sw == 2 || sw == 4 || sw == 8, "mx_roi_bwd_set_strip: 2, 4 or 8");
+  g_roi_strip = sw;
+  return MX_OK;
+}
+
 static int launch_bwd(const Levels& L, int64_t N, int dtype, int64_t C, const float* rois, const int32_t* lv, int64_t K,
                       int PH, int PW, int sampling, int aligned, const void* gout, int deterministic, void* ws,
                       size_t ws_bytes, hipStream_t s) {
@@ -676,19 +728,26 @@ static int launch_bwd(const Levels& L, int64_t N, int dtype, int64_t C, const fl
     for (int i = 0; i < L.n; ++i) {
       tg.first[i] = tot;
       tg.th[i] = (int)cdiv(L.H[i], 8);
-      tg.tw[i] = (int)cdiv(L.W[i], 8);
+      tg.tw[i] = (int)cdiv(L.W[i], g_roi_strip);
       tot += N * tg.th[i] * tg.tw[i];
     }
     tg.first[L.n] = tot;
     MX_CHECK_ARG(tot < (1ll << 31), "roi_align_bwd deterministic: grid too large");
     if (tot == 0) return MX_OK;
     const float count = (float)(sampling * sampling);
-    if (dtype == MX_F32)
-      roi_bwd_gather_kernel<float><<<(unsigned)tot, 512, 0, s>>>(L, tg, C, K, nbins, S4, count, ent, cnt, box, meta,
-                                                                 (const float*)gout);
-    else
-      roi_bwd_gather_kernel<uint16_t><<<(unsigned)tot, 512, 0, s>>>(L, tg, C, K, nbins, S4, count, ent, cnt, box, meta,
-                                                                    (const uint16_t*)gout);
+#define MX_GATHER(T_, SW_)                                                                               \
+  roi_bwd_gather_kernel<T_, SW_><<<(unsigned)tot, 512, 0, s>>>(L, tg, C, K, nbins, S4, count, ent, cnt, box, meta, \
+                                                                (const T_*)gout)
+    if (dtype == MX_F32) {
+      if (g_roi_strip == 2) MX_GATHER(float, 2);
+      else if (g_roi_strip == 4) MX_GATHER(float, 4);
+      else MX_GATHER(float, 8);
+    } else {
+      if (g_roi_strip == 2) MX_GATHER(uint16_t, 2);
+      else if (g_roi_strip == 4) MX_GATHER(uint16_t, 4);
+      else MX_GATHER(uint16_t, 8);
+    }
+#undef MX_GATHER
     MX_LAUNCH_CHECK();
     return MX_OK;
   }

@@ -148,6 +148,24 @@ def test_nms_bitexact(dev, n, thr):
     assert np.array_equal(got, orc.nms(b, s, thr))
 
 
+@pytest.mark.parametrize("chain", [3, 40, 1500])
+def test_nms_suppression_chains(dev, chain):
+    """Boxes on a line where each suppresses the next but not the one after (keep every other one):
+    chains longer than the tile resolver's Jacobi steps take its survivor-walk fallback; short ones
+    converge in the Jacobi steps. Mixed with random boxes; bit-exact vs the oracle."""
+    from mx_det import ops
+    rng = np.random.default_rng(chain)
+    x = np.arange(chain, dtype=np.float32) * 7.0
+    line = np.stack([x, np.zeros_like(x), x + 30, np.full_like(x, 20)], 1)  # IoU(i, i+1) .62, (i, i+2) .36
+    b = np.concatenate([line, _rand_boxes(rng, 1900 - chain if chain < 1900 else 0, med=40)]).astype(np.float32)
+    s = rng.random(len(b)).astype(np.float32) * 0.5
+    s[:chain] = 1.0 - np.arange(chain, dtype=np.float32) / (4 * chain)  # the chain first, in line order
+    got = ops.nms(torch.from_numpy(b).to(dev), torch.from_numpy(s).to(dev), 0.5).cpu().numpy()
+    ref = orc.nms(b, s, 0.5)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(ref[: (chain + 1) // 2], np.arange(0, chain, 2))
+
+
 @pytest.mark.parametrize("n,ncls", [(700, 6), (1000, 5), (1001, 5), (8819, 5), (5000, 6)])
 def test_batched_nms_paths(dev, n, ncls):
     """CPU dispatch: 4n > 4000 -> per-class loop; else coordinate trick (both bit-exact)."""
@@ -277,6 +295,40 @@ def test_multiscale_roi_align_backward_deterministic(dev, monkeypatch, C, gdt):
         r = orc.roi_align_backward(gn[sel], rois[sel], scales[l], (N, C) + shapes[l], 2, False)
         r = torch.from_numpy(r).to(gdt).float().numpy()  # the returned grad is in the feature dtype
         assert np.array_equal(a[l].float().permute(0, 3, 1, 2).cpu().numpy(), r), l
+
+
+def test_multiscale_roi_align_backward_heavy_overlap(dev, monkeypatch):
+    """Deterministic gather on a tile that ~1,100 RoIs overlap (more than one 1,024-RoI list chunk;
+    the pipelined walk crosses RoI and batch boundaries with prefetched groups): still BIT-EXACT vs
+    the oracle's loop order, and bitwise reproducible."""
+    from mx_det import ops
+    monkeypatch.setenv("MX_ROI_DETERMINISTIC", "1")
+    rng = np.random.default_rng(77)
+    N, C = 1, 256
+    shapes = [(60, 101), (30, 51), (15, 26), (8, 13)]
+    scales = [0.25, 0.125, 0.0625, 0.03125]
+    feats = [torch.from_numpy(rng.standard_normal((N, h, w, C)).astype(np.float32)) for h, w in shapes]
+    K = 1100
+    ctr = rng.uniform(90, 110, (K, 2))
+    wh = rng.uniform(20, 90, (K, 2))
+    boxes = np.concatenate([ctr - wh / 2, ctr + wh / 2], 1).astype(np.float32)
+    rois = np.concatenate([np.zeros((K, 1), np.float32), boxes], 1)
+    lv = _level_mapper_np(boxes)
+    g = torch.from_numpy(rng.standard_normal((K, 7, 7, C)).astype(np.float32))
+    rt = torch.from_numpy(rois).to(dev)
+
+    def run():
+        ft = [f.to(dev).requires_grad_(True) for f in feats]
+        out = ops.multiscale_roi_align(ft, rt, scales, 2)
+        return torch.autograd.grad(out, ft, g.to(dev))
+    a, b = run(), run()
+    gn = g.permute(0, 3, 1, 2).numpy()
+    assert (lv == 0).sum() > 1000
+    for l in range(4):
+        assert torch.equal(a[l], b[l]), l
+        sel = np.where(lv == l)[0]
+        r = orc.roi_align_backward(gn[sel], rois[sel], scales[l], (N, C) + shapes[l], 2, False)
+        assert np.array_equal(a[l].permute(0, 3, 1, 2).cpu().numpy(), r), l
 
 
 def test_roi_align_backward_no_rois_writes_zeros(dev):

@@ -33,6 +33,13 @@ SHAPES = [  # name, N, H, W, C, K, k, stride, pad
     ("L3 1x1 256->1024", 2, 50, 84, 256, 1024, 1, 1, 0),
     ("stem 7x7 s2 (8->64)", 2, 800, 1344, 8, 64, 7, 2, 3),
     ("L3.0 3x3 s2 128->256 (dgrad s2)", 2, 100, 168, 256, 256, 3, 2, 1),
+    # thin (memory-bound) 1x1 convs of the f32 step
+    ("thin L1 1x1 64->256", 2, 200, 336, 64, 256, 1, 1, 0),
+    ("thin L1 1x1 256->64", 2, 200, 336, 256, 64, 1, 1, 0),
+    ("thin L2 1x1 512->128", 2, 100, 168, 512, 128, 1, 1, 0),
+    ("thin L3 1x1 1024->256", 2, 50, 84, 1024, 256, 1, 1, 0),
+    ("thin predictor 1024->40", 1024, 1, 1, 1024, 40, 1, 1, 0),
+    ("thin RPN P2 cls+box 256->16", 2, 200, 336, 256, 16, 1, 1, 0),
 ]
 
 
@@ -118,6 +125,9 @@ def run(args):
         Ho, Wo = mc.out_hw(H, W, k, k, (st, st), (pd, pd))
         dy = torch.randn(N, Ho, Wo, K, device=dev).to(dt)
         fl = 2.0 * N * Ho * Wo * K * k * k * C
+        es = 4 if args.dtype == "f32" else 2
+        nb = {"fwd": es * (x.numel() + dy.numel()), "dgrad": es * (x.numel() + dy.numel()),
+              "wgrad": es * (x.numel() + dy.numel()) + 4 * w.numel()}  # operands read once, output written once
         res = []
         for kind, fn in (("fwd", lambda: mc.conv_fwd(x, wk, (st, st), (pd, pd), stats=True)),
                          ("dgrad", lambda: mc.conv_dgrad(dy, wt, x.shape, k, k, (st, st), (pd, pd))),
@@ -125,7 +135,7 @@ def run(args):
             ms = timeit(fn, args.reps)
             tot[kind][0] += fl
             tot[kind][1] += ms
-            res.append(f"{kind} {ms * 1000:8.1f}us {fl / ms / 1e9:7.1f}TF")
+            res.append(f"{kind} {ms * 1000:8.1f}us {fl / ms / 1e9:7.1f}TF {nb[kind] / ms / 1e6:6.0f}GB/s")
         print(f"{name:34s} {fl / 1e9:7.1f} GF | " + " | ".join(res), flush=True)
     print("aggregate: " + " | ".join(f"{k} {v[0] / v[1] / 1e9:.1f} TF/s" for k, v in tot.items() if v[1]))
 

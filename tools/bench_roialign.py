@@ -40,13 +40,16 @@ def main():
         return orig(self, feats, rois, scales, k_min, output_size, sampling_ratio)
 
     HipBackend.multiscale_roi_align = hook
+    if os.environ.get("MX_ROI_STRIP"):
+        from mx_det import _lib
+        _lib.call("mx_roi_bwd_set_strip", int(os.environ["MX_ROI_STRIP"]))
     torch.manual_seed(42)
     precision = os.environ.get("MX_PRECISION", "f32")
     model = bench.build_model(dev, precision=precision).train()
     opt = bench.make_optimizer(model)
     imgs, tg = synth_batch(0, 2, device=dev)
     os.environ["MX_GRAPHS"] = "0"  # eager, so the hook sees the call
-    for _ in range(2):
+    for _ in range(int(os.environ.get("MX_PROBE_STEPS", "2"))):  # RoIs concentrate as the RPN trains
         bench.train_step(model, opt, imgs, tg)
     HipBackend.multiscale_roi_align = orig
     feats, rois, scales, k_min = cap["feats"], cap["rois"], cap["scales"], cap["k_min"]
