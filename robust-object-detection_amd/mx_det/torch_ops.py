@@ -18,7 +18,9 @@ namespace. CUDA (= HIP on ROCm) implementations call libmx_det; roi_align's auto
 _roi_align_backward (the deterministic gather: bit-exact with torchvision's CPU kernel, see
 ops.roi_align_deterministic); fake (meta) implementations give shapes for tracing. There is no CPU
 implementation: a CPU tensor raises NotImplementedError from the dispatcher, as the product path
-has no fallback. sampling_ratio <= 0 (adaptive) is rejected.
+has no fallback. sampling_ratio <= 0 is torchvision's adaptive grid (ceil(roi_h / PH) x ceil(roi_w / PW)
+samples per bin): forward bit-exact like the fixed grid, backward by float atomics (torchvision's CUDA
+scheme; the deterministic gather needs a fixed grid).
 """
 import torch
 
