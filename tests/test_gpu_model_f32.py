@@ -214,3 +214,35 @@ def test_f32_train_losses_and_grads_match_cpu_backend(dev, monkeypatch):
     assert mh * 5 < mt_, (mh, mt_)
     bad = [(n, a, b) for n, a, b in zip(names, eh, et) if a > b]
     assert not bad, bad[:5]
+
+
+def test_f32_rpn_proposal_drift_bounded(dev):
+    """The HIP RPN's own proposal set vs the fp32 CPU restatement's on the scaled-logit RPN (eval,
+    post_nms_top_n = 1000 per image): both backends run filter_proposals on their own objectness and
+    decoded boxes. Float noise can flip a 0.7-IoU NMS decision between near-equal proposals, so the
+    sets are compared as sets: per image the proposal counts agree within 1 %, and at least 99 % of
+    the CPU proposals have a HIP proposal with the same box (1e-3) and score (1e-3) -- the bound the
+    unpinned end-to-end test inherits."""
+    from mx_det import frcnn
+    orig = frcnn.RegionProposalNetwork.filter_proposals_padded
+    cap = {}
+
+    def fp(self, proposals, objectness, image_sizes, num_per_level, be):
+        out = orig(self, proposals, objectness, image_sizes, num_per_level, be)
+        cap.setdefault(proposals.device.type, out)
+        return out
+    frcnn.RegionProposalNetwork.filter_proposals_padded = fp
+    try:
+        _eval_pair(dev)
+    finally:
+        frcnn.RegionProposalNetwork.filter_proposals_padded = orig
+    (hb, hs, hv), (cb, cs, cv) = [tuple(t.cpu() for t in cap[k][:3]) for k in ("cuda", "cpu")]
+    for i in range(cb.shape[0]):
+        rb, rs = cb[i][cv[i].bool()], cs[i][cv[i].bool()]
+        ob, os_ = hb[i][hv[i].bool()], hs[i][hv[i].bool()]
+        n = rs.numel()
+        assert n > 500 and abs(os_.numel() - n) <= max(2, n // 100), (os_.numel(), n)
+        d = (rb[:, None, :] - ob[None, :, :]).abs() <= 1e-3 + 1e-3 * rb[:, None, :].abs()
+        ok = d.all(-1) & ((rs[:, None] - os_[None, :]).abs() <= 1e-3 + 1e-3 * rs[:, None].abs())
+        hit = int(ok.any(1).sum())
+        assert hit >= 0.99 * n, (hit, n)

@@ -1,9 +1,10 @@
 set -o pipefail
-mkdir -p gpurun_out/tr
-export TMPDIR=/tmp PYTHONUNBUFFERED=1
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tr/raw -o t -- python3 bench.py --steps 6 --warmup 3 --precision f32 --no-cpu-baseline --no-roofline --no-augment-variant > gpurun_out/tr/log 2>&1 || { tail gpurun_out/tr/log; exit 1; }
-f=$(find gpurun_out/tr/raw -name '*kernel_trace.csv' | head -n 1)
-python3 tools/step_gaps.py $f 20 > gpurun_out/tr/gaps.txt
-python3 tools/gap_analysis.py $f 20 > gpurun_out/tr/gaps2.txt 2>&1 || true
-rm -rf gpurun_out/tr/raw
-head -50 gpurun_out/tr/gaps.txt
+export PYTHONUNBUFFERED=1
+mkdir -p gpurun_out/pmc3
+timeout -k 10 300 python -u -m pytest tests/test_gpu_model_f32.py -x -q --timeout 200 --timeout-method thread -k "drift or unpinned" > gpurun_out/pmc3/t.log 2>&1; tail -15 gpurun_out/pmc3/t.log
+
+MX_PMC_PRECISION=f32 timeout -k 10 500 bash tools/pmc_traffic.sh > gpurun_out/pmc3/f32.log 2>&1 || { tail -20 gpurun_out/pmc3/f32.log; exit 1; }
+cp gpurun_out/pmc_traffic/traffic.json gpurun_out/pmc3/f32.json
+MX_PMC_PRECISION=bf16 timeout -k 10 500 bash tools/pmc_traffic.sh > gpurun_out/pmc3/bf16.log 2>&1 || { tail -20 gpurun_out/pmc3/bf16.log; exit 1; }
+cp gpurun_out/pmc_traffic/traffic.json gpurun_out/pmc3/bf16.json
+ls -la gpurun_out/pmc3
