@@ -1,10 +1,8 @@
 set -o pipefail
+T=${TAG:-r03m32}
+mkdir -p gpurun_out/$T
 export PYTHONUNBUFFERED=1
-mkdir -p gpurun_out/pmc3
-timeout -k 10 300 python -u -m pytest tests/test_gpu_model_f32.py -x -q --timeout 200 --timeout-method thread -k "drift or unpinned" > gpurun_out/pmc3/t.log 2>&1; tail -15 gpurun_out/pmc3/t.log
-
-MX_PMC_PRECISION=f32 timeout -k 10 500 bash tools/pmc_traffic.sh > gpurun_out/pmc3/f32.log 2>&1 || { tail -20 gpurun_out/pmc3/f32.log; exit 1; }
-cp gpurun_out/pmc_traffic/traffic.json gpurun_out/pmc3/f32.json
-MX_PMC_PRECISION=bf16 timeout -k 10 500 bash tools/pmc_traffic.sh > gpurun_out/pmc3/bf16.log 2>&1 || { tail -20 gpurun_out/pmc3/bf16.log; exit 1; }
-cp gpurun_out/pmc_traffic/traffic.json gpurun_out/pmc3/bf16.json
-ls -la gpurun_out/pmc3
+timeout -k 10 400 python -u -m pytest tests/test_gpu_x3.py -x -q --timeout 120 --timeout-method thread > gpurun_out/$T/t.log 2>&1 || { tail -30 gpurun_out/$T/t.log; exit 1; }
+tail -2 gpurun_out/$T/t.log
+timeout -k 10 500 python -u tools/bench_conv.py --dtype f32 --graph --stages 0,7 --tiles 0x0,128x128 > gpurun_out/$T/bc.log 2>&1 || { tail -20 gpurun_out/$T/bc.log; exit 1; }
+grep -v amdgpu gpurun_out/$T/bc.log
