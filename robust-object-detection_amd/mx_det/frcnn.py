@@ -886,19 +886,41 @@ class FasterRCNN(nn.Module):
         head = self.rpn.head
         return feats, head.split(list(outs[nf:]), head.layout(outs[:nf]), be)
 
+    def _flag_async(self, flags):
+        """(pinned host bool, event) of any(flags) copied without waiting, or None."""
+        if not flags:
+            return None
+        f = torch.stack(flags).any() if len(flags) > 1 else flags[0]
+        host = self.__dict__.get("_degenerate_host")
+        if host is None:
+            host = self.__dict__["_degenerate_host"] = torch.empty((), dtype=torch.bool, pin_memory=True)
+        host.copy_(f, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return host, ev
+
     def forward(self, images, targets=None):
         be = self.be
         if hasattr(be, "prepare"):
             be.prepare(self)  # per-step operand preparation (HIP: every conv weight packed in one launch)
+        degenerate = None
         if self.training:
             if targets is None:
                 raise ValueError("In training mode, targets should be passed")
+            flags = []
             for t in targets:
                 b = t["boxes"]
                 if not (isinstance(b, torch.Tensor) and b.dim() == 2 and b.shape[-1] == 4):
                     raise ValueError(f"Expected target boxes to be a tensor of shape [N, 4], got {b.shape}.")
-                if b.numel() and bool(((b[:, 2:] <= b[:, :2]).any())):
-                    raise ValueError("All bounding boxes should have positive height and width.")
+                if b.numel():
+                    if b.is_cuda:
+                        flags.append((b[:, 2:] <= b[:, :2]).any())
+                    elif bool(((b[:, 2:] <= b[:, :2]).any())):
+                        raise ValueError("All bounding boxes should have positive height and width.")
+            # GeneralizedRCNN.forward's degenerate-box check without its per-image host round trips:
+            # the device flag is copied to pinned memory asynchronously and read after the RPN's own
+            # host sync (filter_proposals' per-image counts), where it is already complete
+            degenerate = self._flag_async(flags)
         if isinstance(images, torch.Tensor) and images.dim() == 4 and images.dtype == torch.uint8:
             original = [(images.shape[1], images.shape[2])] * images.shape[0]
         else:  # float CHW (reference ToDtype output) or uint8 HWC tensors
@@ -914,6 +936,11 @@ class FasterRCNN(nn.Module):
         # measured 0.5 % slower than issuing them while the trunk runs (A/B on one box), so off
         defer = os.environ.get("MX_RPN_DEFER_LOSSES", "0") != "0"
         proposals, rpn_losses = self.rpn(il, features, targets, be, head=head, defer_losses=defer)
+        if degenerate is not None:
+            host, ev = degenerate
+            ev.synchronize()
+            if bool(host):
+                raise ValueError("All bounding boxes should have positive height and width.")
         detections, det_losses = self.roi_heads(features, proposals, il.image_sizes, targets, be)
         if self.training:
             losses = {}

@@ -203,3 +203,16 @@ def test_graphed_trunk_matches_eager(dev, monkeypatch):
             assert int(se[k]) == int(sg[k]) == 3, k
         else:
             assert torch.isfinite(sg[k].float()).all(), k
+
+
+def test_degenerate_target_box_raises(dev):
+    """GeneralizedRCNN.forward's check (x2 <= x1 or y2 <= y1 -> ValueError) still raises on the device
+    path, where the flag is read after the RPN's host sync instead of with a round trip per image."""
+    from mx_det.data import synth_batch
+    m = _model(dev).train()
+    imgs, tg = synth_batch(0, 2, H=256, W=320, device=dev)
+    tg[1]["boxes"][0, 2] = tg[1]["boxes"][0, 0]  # zero width
+    with pytest.raises(ValueError, match="positive height and width"):
+        m(imgs, tg)
+    imgs, tg = synth_batch(0, 2, H=256, W=320, device=dev)
+    assert torch.isfinite(sum(m(imgs, tg).values()))
