@@ -126,6 +126,9 @@ size_t mx_roi_align_bwd_workspace(int64_t K, int PH, int PW, int sampling);
 /* deterministic-gather tile width (pixels per wave strip): 2 (default), 4 or 8. Results are identical;
  * 4-wide tiles shorten the tail of tiles that many RoIs overlap. Not thread-safe (a process setting). */
 int mx_roi_bwd_set_strip(int sw);
+/* forward: channel slices per RoI (1, 2, 4 (default) or 8 when C / 8 divides): more, shorter blocks.
+ * A process setting, results identical. */
+int mx_roi_fwd_set_split(int n);
 int mx_roi_align_fwd(const void* feat, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, const float* rois,
                      int64_t K, float spatial_scale, int PH, int PW, int sampling, int aligned, void* out,
                      mx_stream_t stream);

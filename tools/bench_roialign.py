@@ -40,6 +40,9 @@ def main():
         return orig(self, feats, rois, scales, k_min, output_size, sampling_ratio)
 
     HipBackend.multiscale_roi_align = hook
+    if os.environ.get("MX_ROI_SPLIT"):
+        from mx_det import _lib
+        _lib.call("mx_roi_fwd_set_split", int(os.environ["MX_ROI_SPLIT"]))
     if os.environ.get("MX_ROI_STRIP"):
         from mx_det import _lib
         _lib.call("mx_roi_bwd_set_strip", int(os.environ["MX_ROI_STRIP"]))

@@ -18,6 +18,9 @@ from mx_det.data import synth_batch  # noqa: E402
 
 def main():
     dev = torch.device("cuda")
+    if os.environ.get("MX_ROI_SPLIT"):
+        from mx_det import _lib
+        _lib.call("mx_roi_fwd_set_split", int(os.environ["MX_ROI_SPLIT"]))
     torch.manual_seed(42)
     model = bench.build_model(dev, precision="f32").train()
     opt = bench.make_optimizer(model)

@@ -1,19 +1,14 @@
 set -o pipefail
-mkdir -p gpurun_out/tr
-export TMPDIR=/tmp PYTHONUNBUFFERED=1
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tr/raw -o t -- python3 bench.py --steps 4 --warmup 3 --precision f32 --no-cpu-baseline --no-roofline --no-augment-variant > gpurun_out/tr/log 2>&1 || { tail gpurun_out/tr/log; exit 1; }
-f=$(find gpurun_out/tr/raw -name '*kernel_trace.csv' | head -n 1)
-python3 - $f <<'PY'
-import csv, sys
-rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-names=[r["Kernel_Name"] for r in rows]
-mk=[i for i,n in enumerate(names) if "trace_marker" in n]
-sub=rows[mk[0]:mk[1]+1]
-import csv as c2
-w=c2.writer(open('gpurun_out/tr/steps.csv','w'))
-w.writerow(["Kernel_Name","Start_Timestamp","End_Timestamp"])
-for r in sub: w.writerow([r["Kernel_Name"][:120],r["Start_Timestamp"],r["End_Timestamp"]])
-PY
-python3 tools/all_gaps.py gpurun_out/tr/steps.csv > gpurun_out/tr/allgaps.txt
-rm -rf gpurun_out/tr/raw
-cat gpurun_out/tr/allgaps.txt
+T=${TAG:-r03split2}
+mkdir -p gpurun_out/$T
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py tests/test_torch_ops.py -x -q --timeout 120 --timeout-method thread -k "roi" > gpurun_out/$T/t.log 2>&1 || { tail -30 gpurun_out/$T/t.log; exit 1; }
+tail -1 gpurun_out/$T/t.log
+for sp in 4 8 4 8; do
+MX_ROI_SPLIT=$sp timeout -k 10 300 python -u tools/hbm_ops_probe.py > gpurun_out/$T/p$sp.log 2>&1 || { tail -20 gpurun_out/$T/p$sp.log; exit 1; }
+echo "split $sp $(grep -m1 avg_launch_us gpurun_out/$T/p$sp.log)"
+done
+for sp in 1 4 8; do
+MX_ROI_SPLIT=$sp timeout -k 10 300 python -u tools/bench_roialign.py > gpurun_out/$T/roi$sp.log 2>&1 || exit 1
+echo "hot split $sp $(grep '^fwd' gpurun_out/$T/roi$sp.log)"
+done
