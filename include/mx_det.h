@@ -11,6 +11,11 @@
  *  - Every pointer argument is a device pointer owned by the caller; the library never allocates
  *    or frees on these paths. Scratch comes from a caller workspace sized by *_workspace().
  *  - Work is enqueued on `stream` (a hipStream_t) and is stream-ordered; nothing synchronises.
+ *  - Exceptions, off the hot path and marked at their declarations: the convenience forms
+ *    (mx_conv2d_fwd / _dgrad / _wgrad, mx_bn_finalize, mx_bn_bwd_reduce / _apply) allocate their
+ *    temporaries with hipMallocAsync / hipFreeAsync on `stream` (the _ex forms take a workspace);
+ *    mx_conv_pack_batched with upload = 1 synchronises `stream` once to copy a NEW job plan to the
+ *    device (the steady state passes upload = 0 and only launches).
  *  - Return 0 on success, negative MX_E* on error; mx_last_error() gives the message (thread-local).
  *  - Activations are NHWC; conv weights are KRSC (Cout, kh, kw, Cin); dtype codes below.
  */
