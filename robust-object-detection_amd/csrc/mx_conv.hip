@@ -3103,11 +3103,13 @@ extern "C" int mx_conv_pack_batched(const mx_pack_desc* jobs, int64_t njobs, voi
   return MX_OK;
 }
 
-// fused tile for R*S taps (sgd_pack_tile): 64x64 (1x1), 32x32 (<= 9 taps), 16x16 (<= 49 taps; FC6)
+// fused tile for R*S taps (sgd_pack_tile): 64x64 (1x1), 32x32 (<= 9 taps), 16x8 (<= 49 taps; FC6).
+// One launch reserves the largest tile's LDS for every block: FC6's 16x16 (50 KiB) held the whole
+// launch to 3 blocks per CU; 16x8 (25 KiB) leaves the 3x3 tile (37 KiB) as the bound (4 per CU).
 static bool sgd_tile(int RS, int& kr, int& tc) {
   if (RS == 1) { kr = 64; tc = 64; return true; }
   if (RS <= 9) { kr = 32; tc = 32; return true; }
-  if (RS <= 49) { kr = 16; tc = 16; return true; }
+  if (RS <= 49) { kr = 16; tc = 8; return true; }
   return false;
 }
 
