@@ -11,13 +11,17 @@ Arithmetic: the headline runs the reference's precision -- an fp32 model (train_
 no autocast; TF32 convs on its Ampere GPU): HipBackend("f32"), f32 activations / gradients / BN /
 RoIAlign, every conv product as the bf16x3 split on MFMA (~2^-16 relative, finer than TF32's 2^-11;
 tests/test_gpu_x3.py). The bf16 mode (bf16 activations and operands) is timed after it and reported
-inside the same line under "bf16_variant" (--precision f32|bf16 picks one mode only).
+inside the same line under "bf16_variant" (--precision f32|bf16 picks one mode only). The same line
+also carries "augment_variant" (configs[2]'s step with on-GPU RandomCorruption), and the metric's
+"+ eval" half: "eval_variant" (eval_all.py per-image eval forward) and "eval_restored_variant"
+(configs[3]: U-Net restore + eval), K images each after W warmup (--no-eval-variant skips them;
+mAP@50 is parity-unpinned: no trained checkpoint ships with the reference).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
-One process per GPU; gradients all-reduced over RCCL (torch.distributed "nccl") by DDP buckets;
+One process per GPU; gradients all-reduced over RCCL (torch.distributed "nccl") by mx_det.dp.DataParallel;
 per-GPU BatchNorm statistics (no SyncBN: each GPU sees the reference's bs=2). Rank 0 prints one
 JSON line. Weak scaling: per-GPU work is fixed.
 """
@@ -621,6 +625,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-augment-variant", action="store_true")
+    ap.add_argument("--no-eval-variant", action="store_true", help="skip the eval / eval_restored legs of the train run")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -708,6 +713,22 @@ def main():
                                               "the same train step", "dtype": DTYPE_TEXT[head],
                                   "value": round(images / dt3, 3), "ms_per_step": round(1000 * dt3 / args.steps, 3)}
         del m3
+    if not args.no_eval_variant:
+        # the metric's "+ eval" half, in the same driver run: eval_all.py:97-143 per-image eval forward
+        # and configs[3] (eval_restored.py: U-Net restore fused in front), headline precision, each rank
+        # on its own images (eval is embarrassingly parallel per image), K images timed after W warmup
+        for restored, key, what in ((False, "eval_variant", "eval_all.py per-image eval forward (1000 proposals)"),
+                                    (True, "eval_restored_variant", "configs[3]: U-Net restore + eval forward")):
+            try:
+                del ddp, opt
+            except NameError:
+                pass
+            torch.cuda.empty_cache()
+            m4, u4, dt4 = _time_eval(head, args, world, rank, dev, imgs, restored)
+            rec[key] = {"workload": what, "dtype": DTYPE_TEXT[head], "unit": "images/sec",
+                        "value": round(args.steps * world / dt4, 3), "ms_per_image": round(1000 * dt4 / args.steps, 3),
+                        "map50": "parity unpinned: no trained checkpoint ships with the reference (random-init weights)"}
+            del m4, u4
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(cpu_model)
     if rank == 0:
