@@ -748,14 +748,22 @@ class ConvAct(torch.autograd.Function):
 _scratch = {}
 
 
+_scratch_kept = []
+
+
 def bn_scratch(nbytes, device):
-    """Persistent per-device workspace of the one-launch BN reductions: zero-filled when allocated;
-    its leading arrival counters are left zero by every launch, so it is reused across calls (all of
-    them are stream-ordered on the current stream)."""
-    t = _scratch.get(device)
+    """Persistent per-(device, stream) workspace of the one-launch reductions (BN, bias gradients, RPN
+    loss): zero-filled when allocated; its leading arrival counters are left zero by every launch, so
+    it is reused by every call on that stream (they are stream-ordered). Per stream: launches on two
+    streams may overlap and must not share counters. A grown workspace keeps the old one alive (a
+    captured graph may still address it)."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    t = _scratch.get(key)
     if t is None or t.numel() < nbytes:
+        if t is not None:
+            _scratch_kept.append(t)
         t = torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
-        _scratch[device] = t
+        _scratch[key] = t
     return t
 
 

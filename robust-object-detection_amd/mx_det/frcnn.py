@@ -144,15 +144,39 @@ class FeaturePyramidNetwork(nn.Module):
     def forward(self, x, be):
         names = list(x.keys())
         feats = list(x.values())
+        side = None
+        if feats[0].is_cuda and getattr(be, "name", "") == "hip" and os.environ.get("MX_FPN_STREAMS", "1") != "0":
+            # the small levels' 3x3 output blocks (and P6) on a side stream beside the top-down chain
+            main = torch.cuda.current_stream()
+            side = self.__dict__.get("_side")
+            if side is None or side.device != feats[0].device:
+                side = self.__dict__["_side"] = torch.cuda.Stream(device=feats[0].device)
+
+        def block(idx, t):
+            if side is None or idx == 0:
+                return self.layer_blocks[idx](t, be)
+            side.wait_stream(main)
+            t.record_stream(side)
+            with torch.cuda.stream(side):
+                return self.layer_blocks[idx](t, be)
         last_inner = self.inner_blocks[-1](feats[-1], be)
-        results = [self.layer_blocks[-1](last_inner, be)]
+        results = [block(len(feats) - 1, last_inner)]
+        if side is not None:
+            with torch.cuda.stream(side):
+                pool = be.maxpool(results[-1], 1, 2, 0)
         for idx in range(len(feats) - 2, -1, -1):
             lat = feats[idx]
             top_down = be.upsample_add(last_inner, None, (lat.shape[1], lat.shape[2]))
             # inner_lateral + top_down fused into the lateral conv's BN epilogue
             last_inner = self.inner_blocks[idx](lat, be, residual=top_down)
-            results.insert(0, self.layer_blocks[idx](last_inner, be))
-        results.append(be.maxpool(results[-1], 1, 2, 0))  # LastLevelMaxPool: max_pool2d(x, 1, 2, 0)
+            results.insert(0, block(idx, last_inner))
+        if side is None:
+            pool = be.maxpool(results[-1], 1, 2, 0)  # LastLevelMaxPool: max_pool2d(x, 1, 2, 0)
+        else:
+            main.wait_stream(side)
+            for t in results[1:] + [pool]:
+                t.record_stream(main)
+        results.append(pool)
         return OrderedDict(zip(names + ["pool"], results))
 
 
@@ -258,6 +282,21 @@ class RPNHead(nn.Module):
             cv = f0.new_zeros((N, Hc, Wc, C))
             for f, (y, x, h, wd) in zip(feats[1:], rects):
                 cv[:, y:y + h, x:x + wd] = f
+        if hip and os.environ.get("MX_RPN_STREAMS", "1") != "0":
+            # the canvas chain (P3..P6) on a side stream beside level 0's: independent convs that fill
+            # each other's tail rounds; autograd runs each backward on its forward's stream
+            main = torch.cuda.current_stream()
+            side = self.__dict__.get("_side")
+            if side is None or side.device != cv.device:
+                side = self.__dict__["_side"] = torch.cuda.Stream(device=cv.device)
+            side.wait_stream(main)
+            cv.record_stream(side)
+            with torch.cuda.stream(side):
+                r1 = self._run(cv, be, w, b, mask)
+            r0 = self._run(feats[0], be, w, b)
+            main.wait_stream(side)
+            r1.record_stream(main)
+            return [r0, r1]
         return [self._run(feats[0], be, w, b), self._run(cv, be, w, b, mask)]
 
     def absorbed(self):

@@ -1,9 +1,10 @@
 set -o pipefail
-T=${TAG:-r03sgd}
+T=${TAG:-r03str2}
 mkdir -p gpurun_out/$T
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_bn.py tests/test_gpu_ops.py -x -q --timeout 120 --timeout-method thread -k "sgd or roi" > gpurun_out/$T/t.log 2>&1 || { tail -30 gpurun_out/$T/t.log; exit 1; }
+MX_RPN_STREAMS=1 MX_FPN_STREAMS=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_rpn_canvas.py tests/test_gpu_graphs.py -x -q --timeout 200 --timeout-method thread > gpurun_out/$T/t.log 2>&1 || { tail -30 gpurun_out/$T/t.log; exit 1; }
 tail -1 gpurun_out/$T/t.log
-bash tools/gpu_check.sh $T prof > gpurun_out/$T/prof.out 2>&1 || { tail -20 gpurun_out/$T/prof.out; exit 1; }
-grep -E "sgd_pack|roi_align_fwd|roi_bwd" gpurun_out/$T/step_kernels.csv | cut -c1-60,150-
-tail -1 gpurun_out/$T/step_kernels.log
+for v in 0 1 0 1; do
+MX_RPN_STREAMS=$v MX_FPN_STREAMS=$v timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-roofline --no-augment-variant --no-eval-variant --precision f32 --steps 30 > gpurun_out/$T/b$v.log 2>&1 || { tail -20 gpurun_out/$T/b$v.log; exit 1; }
+echo "streams $v $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/$T/b$v.log)"
+done
