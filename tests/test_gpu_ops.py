@@ -543,15 +543,23 @@ def _level_topk_np(scores, num_per_level, k):
     return np.concatenate(out, 1)
 
 
-@pytest.mark.parametrize("case", ["train", "ties", "edges"])
+@pytest.mark.parametrize("case", ["train", "logits", "uniform", "ties", "edges"])
 def test_level_topk(dev, case):
     """mx_level_topk == the per-level topk of RegionProposalNetwork._get_top_n_idx: exact indices vs
-    the definition (value desc, index asc) and exact values vs torch.topk on the CPU."""
+    the definition (value desc, index asc) and exact values vs torch.topk on the CPU. "logits" (one
+    exponent band, an untrained RPN's objectness) and "uniform" (the samplers' keys) put most lanes of
+    a wave on a few first-digit bins of the radix select."""
     from mx_det import ops
     rng = np.random.default_rng(21)
     if case == "train":  # bs=2 at 1344x800: P2..P6 anchors per level, pre_nms_top_n=2000
         levels, k = [201600, 50400, 12600, 3150, 819], 2000
         s = rng.standard_normal((2, sum(levels))).astype(np.float32)
+    elif case == "logits":
+        levels, k = [201600, 50400, 12600, 3150, 819], 2000
+        s = (0.01 + 0.001 * rng.standard_normal((2, sum(levels)))).astype(np.float32)
+    elif case == "uniform":
+        levels, k = [268569], 256
+        s = rng.random((2, sum(levels))).astype(np.float32)
     elif case == "ties":  # heavy ties at every threshold (quantised logits), eval k=1000
         levels, k = [40000, 10000, 2500, 700], 1000
         s = (np.round(rng.standard_normal((3, sum(levels))) * 4) / 4).astype(np.float32)

@@ -34,6 +34,12 @@ def torch_loop(ob, levels, k):
 def main():
     levels, k = [201600, 50400, 12600, 3150, 819], 2000
     ob = torch.randn(2, sum(levels), device="cuda")
+    dists = {"randn": ob, "logits(0.01+-0.001)": 0.01 + 0.001 * torch.randn_like(ob),
+             "uniform": torch.rand_like(ob)}
+    for name, t in dists.items():
+        print(f"{name:20s} proposals k=2000: {timeit(lambda: ops.level_topk(t, levels, k)):6.1f} us"
+              f"   sampler k=256 one level: {timeit(lambda: ops.level_topk(t, [sum(levels)], 256)):6.1f} us",
+              flush=True)
     print(f"mx_level_topk {timeit(lambda: ops.level_topk(ob, levels, k)):.1f} us")
     print(f"torch.topk loop {timeit(lambda: torch_loop(ob, levels, k)):.1f} us")
     for lv in ([201600], [50400], [3150]):

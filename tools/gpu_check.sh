@@ -32,6 +32,8 @@ for s in $STEPS; do
       for f in $(find "$OUT/prof" -name '*_stats.csv'); do cp "$f" "$OUT/"; done
       python3 tools/prof_steps.py "$OUT/prof" --steps 10 --out "$OUT/step_kernels.csv" > "$OUT/step_kernels.log" 2>&1 \
         || { echo "prof_steps failed"; tail -5 "$OUT/step_kernels.log"; }
+      tr=$(find "$OUT/prof" -name '*kernel_trace.csv' | head -n 1)
+      [ -n "$tr" ] && python3 tools/step_gaps.py "$tr" 20 > "$OUT/step_gaps.log" 2>&1
       rm -rf "$OUT/prof"
       tail -1 "$OUT/prof.log" ;;
     pmc)
