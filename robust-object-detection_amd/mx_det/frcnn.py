@@ -126,6 +126,14 @@ class ResNet50Body(nn.Module):
         return out
 
 
+def _side_streams(knob):
+    """Concurrent small levels (the FPN's P3..P6 output blocks, the RPN head's canvas chain) on side
+    streams: on by default (knob "0" turns it off) and off while mc's per-launch timer is installed
+    (bench.py's roofline step), so every timed conv runs alone and its event-timed duration is the
+    kernel's own (the side-stream wgrad follows the same rule, conv.side_wgrad_enabled)."""
+    return os.environ.get(knob, "1") != "0" and mc._timer is None
+
+
 class FeaturePyramidNetwork(nn.Module):
     """torchvision.ops.FeaturePyramidNetwork(norm_layer=BatchNorm2d) + LastLevelMaxPool."""
 
@@ -145,7 +153,7 @@ class FeaturePyramidNetwork(nn.Module):
         names = list(x.keys())
         feats = list(x.values())
         side = None
-        if feats[0].is_cuda and getattr(be, "name", "") == "hip" and os.environ.get("MX_FPN_STREAMS", "1") != "0":
+        if feats[0].is_cuda and getattr(be, "name", "") == "hip" and _side_streams("MX_FPN_STREAMS"):
             # the small levels' 3x3 output blocks (and P6) on a side stream beside the top-down chain
             main = torch.cuda.current_stream()
             side = self.__dict__.get("_side")
@@ -282,7 +290,7 @@ class RPNHead(nn.Module):
             cv = f0.new_zeros((N, Hc, Wc, C))
             for f, (y, x, h, wd) in zip(feats[1:], rects):
                 cv[:, y:y + h, x:x + wd] = f
-        if hip and os.environ.get("MX_RPN_STREAMS", "1") != "0":
+        if hip and _side_streams("MX_RPN_STREAMS"):
             # the canvas chain (P3..P6) on a side stream beside level 0's: independent convs that fill
             # each other's tail rounds; autograd runs each backward on its forward's stream
             main = torch.cuda.current_stream()
