@@ -28,6 +28,8 @@ JSON line. Weak scaling: per-GPU work is fixed.
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -358,6 +360,12 @@ def _time_precision(precision, args, world, rank, dev, imgs, tg):
     return model, ddp, opt, dt
 
 
+def _barrier(world):
+    if world > 1:
+        torch.cuda.synchronize()
+        dist.barrier()
+
+
 def eval_step(model, img, unet=None):
     """One image of the reference's evaluation loop (eval_all.py:106-124, batch_size=1): model([image])
     in eval mode, the detections copied to the host; with unet, the corrupted uint8 image is first
@@ -447,7 +455,7 @@ def eval_main(args, world, rank, dev, imgs):
     if rank == 0 and not args.no_roofline:
         rec["roofline"] = conv_roofline(model, None, None, None, peak,
                                         step_fn=lambda: eval_step(model, imgs[0], unet))
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_eval_baseline(model, unet, imgs[0])
     if rank == 0:
         print(json.dumps(rec), flush=True)
@@ -609,6 +617,20 @@ def visdrone_main(args, world, rank, dev):
         print(json.dumps(rec), flush=True)
 
 
+def _launch_ranks(n):
+    """torch.distributed.run --nproc-per-node n over 127.0.0.1 re-running this script with the same
+    arguments; returns the launcher's exit code."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL / CUDA IPC)
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -628,7 +650,15 @@ def main():
     ap.add_argument("--no-eval-variant", action="store_true", help="skip the eval / eval_restored legs of the train run")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` run directly: one rank per GPU needs a launcher. Start torch.distributed.run
+        # as a child process BEFORE this process makes any HIP call (no exec from a GPU-initialised
+        # process) and exit with its return code; the child ranks re-enter main() with WORLD_SIZE set.
+        raise SystemExit(_launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU "
+                         f"(torch.distributed.run --nproc-per-node {args.gpus}) or pass --gpus {world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():
@@ -685,9 +715,15 @@ def main():
                    "parallelism": f"dp{world}", "trainable_backbone_layers": 3},
     }
     peak = {"f32": X3_PEAK_TFLOPS, "bf16": BF16_PEAK_TFLOPS}
-    if rank == 0 and not args.no_roofline:
-        rec["roofline"] = conv_roofline(ddp, opt, imgs[0:2], tg[0:2], peak[head])
-        rec["hbm_ops"] = hbm_ops_roofline(ddp, opt, imgs[0:2], tg[0:2])
+    # the measurement legs run a train step through the data-parallel wrapper, whose gradient
+    # all-reduces RCCL pairs by issue order: EVERY rank runs them (same collectives, same order) and
+    # only rank 0 records; a barrier closes each leg
+    if not args.no_roofline:
+        rf = conv_roofline(ddp, opt, imgs[0:2], tg[0:2], peak[head])
+        ho = hbm_ops_roofline(ddp, opt, imgs[0:2], tg[0:2])
+        if rank == 0:
+            rec["roofline"], rec["hbm_ops"] = rf, ho
+        _barrier(world)
     cpu_model = model  # the CPU baseline starts from the headline model's weights
     for p in precs[1:]:
         del ddp, opt
@@ -695,8 +731,11 @@ def main():
         m2, ddp, opt, dt2 = _time_precision(p, args, world, rank, dev, imgs, tg)
         var = {"dtype": DTYPE_TEXT[p], "arithmetic": ARITH_TEXT[p], "value": round(images / dt2, 3),
                "ms_per_step": round(1000 * dt2 / args.steps, 3)}
-        if rank == 0 and not args.no_roofline:
-            var["roofline"] = conv_roofline(ddp, opt, imgs[0:2], tg[0:2], peak[p])
+        if not args.no_roofline:
+            rf = conv_roofline(ddp, opt, imgs[0:2], tg[0:2], peak[p])
+            if rank == 0:
+                var["roofline"] = rf
+            _barrier(world)
         rec[p + "_variant"] = var
         del m2
     if not args.augment and not args.no_augment_variant:
@@ -729,7 +768,9 @@ def main():
                         "value": round(args.steps * world / dt4, 3), "ms_per_image": round(1000 * dt4 / args.steps, 3),
                         "map50": "parity unpinned: no trained checkpoint ships with the reference (random-init weights)"}
             del m4, u4
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        # host-only, after every timed leg (the other ranks wait at the closing barrier); the same
+        # one-node CPU port at any N (per-image work does not shard on the host)
         rec["cpu_baseline"] = cpu_baseline(cpu_model)
     if rank == 0:
         print(json.dumps(rec), flush=True)

@@ -38,7 +38,10 @@ struct Huff {
   uint8_t look_len[512], look_val[512];  // 0 length: code longer than 9 bits
 };
 
+bool huff_counts_ok(const uint8_t* bits);
+
 bool build_huff(const uint8_t* bits, const uint8_t* vals, Huff* h) {
+  if (!huff_counts_ok(bits)) return false;
   int code = 0, k = 0;
   int total = 0;
   for (int l = 1; l <= 16; ++l) total += bits[l];
@@ -65,13 +68,18 @@ bool build_huff(const uint8_t* bits, const uint8_t* vals, Huff* h) {
   return true;
 }
 
-// T.81 C.2 code assignment: false when the counts over-subscribe some code length (a table no
-// encoder can produce; libjpeg rejects it as JERR_BAD_HUFF_TABLE)
+// T.81 C.2 code assignment, checked as libjpeg's jpeg_make_d_derived_tbl does when a scan USES the
+// table: after the codes of length l (l up to the longest length in use) the next code must still fit
+// in l bits -- no code may be all ones, so a complete table (e.g. two 1-bit codes) is rejected too
+// (JERR_BAD_HUFF_TABLE). Tables a scan never uses are not checked (libjpeg derives only used ones).
 bool huff_counts_ok(const uint8_t* bits) {
+  int last = 0;
+  for (int l = 1; l <= 16; ++l)
+    if (bits[l]) last = l;
   int code = 0;
-  for (int l = 1; l <= 16; ++l) {
+  for (int l = 1; l <= last; ++l) {
     code += bits[l];
-    if (code > (1 << l)) return false;
+    if (code >= (1 << l)) return false;
     code <<= 1;
   }
   return true;
@@ -200,7 +208,7 @@ extern "C" int mx_jpeg_parse(const uint8_t* d, int64_t n, mx_jpeg_info* info) {
           info->hbits[t][l] = s[o + l];
           tot += s[o + l];
         }
-        if (tot > 256 || o + 17 + tot > sl || !huff_counts_ok(info->hbits[t]))
+        if (tot > 256 || o + 17 + tot > sl)
           return fail(MX_EINVAL, "jpeg: bad DHT counts");
         memcpy(info->hval[t], s + o + 17, tot);
         info->hdef[t] = 1;

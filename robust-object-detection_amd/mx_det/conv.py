@@ -608,11 +608,18 @@ class GradSlot:
     in a static buffer (frcnn._Graphs' static_gout) and whose only in-graph consumer can add it itself
     -- a stride-1 conv in its dgrad epilogue (ConvAct), the RPN canvas unpack -- is left out of the
     backward roots; the consumer reads `buf` (set after the forward capture) instead of autograd adding
-    the two gradients in a separate pass."""
-    __slots__ = ("buf",)
+    the two gradients in a separate pass. `taken` is set when the consumer claims the slot at forward
+    time (frcnn._absorb_roots keeps an unclaimed output as an ordinary backward root), `stream` is the
+    stream the slot was opened on: the consumer must run there (its backward then reads `buf` in stream
+    order; a consumer on another stream would read it outside autograd's cross-stream edges)."""
+    __slots__ = ("buf", "taken", "stream")
 
     def __init__(self):
-        self.buf = None
+        self.buf, self.taken, self.stream = None, False, None
+
+    def claim(self):
+        self.taken = True
+        return self
 
 
 _absorb = {}
@@ -645,11 +652,15 @@ class GradChain:
     order; each adds the running sum of the earlier ones' input gradients in its own dgrad epilogue
     (conv_dgrad residual) and hands it on; the last returns the total to autograd, the others None --
     no separate accumulation passes. Consumers join at forward time (n counts them), so a consumer
-    that does not see the chain simply returns its gradient to autograd as usual."""
-    __slots__ = ("n", "seen", "acc")
+    that does not see the chain simply returns its gradient to autograd as usual.
+    Every consumer must run on ONE stream (recorded at the first join): the running sum passes between
+    their backwards outside autograd's edges, so autograd would insert no cross-stream wait for it (the
+    downsample-branch side-stream attempt of round 3 crashed the backward capture exactly so); a join
+    from another stream raises at forward time."""
+    __slots__ = ("n", "seen", "acc", "stream")
 
     def __init__(self):
-        self.n, self.seen, self.acc = 0, 0, None
+        self.n, self.seen, self.acc, self.stream = 0, 0, None, None
 
     def last(self):
         return self.seen + 1 >= self.n
@@ -674,12 +685,24 @@ def chain_over(t):
     _chains[id(t)] = (weakref.ref(t), GradChain())
 
 
+def _cur_stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream if t.is_cuda else None
+
+
 def _chain_join(t):
     e = _chains.get(id(t))
     if e is None or e[0]() is not t:
         return None
-    e[1].n += 1
-    return e[1]
+    ch = e[1]
+    st = _cur_stream(t)
+    if ch.n == 0:
+        ch.stream = st
+    elif st != ch.stream:
+        raise RuntimeError("GradChain: a consumer of a chained tensor runs on a different stream than the "
+                           "chain's first consumer; the running gradient sum would cross streams outside "
+                           "autograd's edges. Run every consumer of the tensor on one stream.")
+    ch.n += 1
+    return ch
 
 
 def _chain_res(chain, res):
@@ -690,13 +713,19 @@ def _chain_res(chain, res):
 
 
 def absorb_into(t, slot):
-    """The next ConvAct consuming tensor `t` adds slot.buf to its input gradient."""
+    """The next ConvAct consuming tensor `t` (on this stream) adds slot.buf to its input gradient."""
+    slot.stream = _cur_stream(t)
     _absorb[id(t)] = (weakref.ref(t), slot)
 
 
 def _absorb_take(t):
     e = _absorb.pop(id(t), None)
-    return e[1] if e is not None and e[0]() is t else None
+    if e is None or e[0]() is not t:
+        return None
+    if _cur_stream(t) != e[1].stream:
+        raise RuntimeError("GradSlot: the consumer of an absorbed graph output runs on a different stream "
+                           "than the slot was opened on; run it on the producer's stream")
+    return e[1].claim()
 
 
 class ConvAct(torch.autograd.Function):
@@ -732,6 +761,8 @@ class ConvAct(torch.autograd.Function):
                 dx = conv_dgrad(gk.view(N, 1, 1, K8), wt, (N, 1, 1, H * W * C), 1, 1, (1, 1), (0, 0)).view(N, H, W, C)
                 if ctx.chain is not None and ctx.chain.acc is not None:
                     dx = dx + ctx.chain.acc
+                if ctx.slot is not None and ctx.slot.buf is not None:  # claimed slot: its gradient too
+                    dx = dx + ctx.slot.buf
             else:
                 extra = ctx.slot.buf if ctx.slot is not None else None
                 if extra is not None and not (extra.dtype == gk.dtype and extra.shape == x.shape and
@@ -746,6 +777,18 @@ class ConvAct(torch.autograd.Function):
 
 
 _scratch = {}
+_capture_streams = {}
+
+
+def capture_stream(device):
+    """The stream graph captures (frcnn._Graphs / _SegGraphs) warm up AND capture on, one per device:
+    the warm-up allocates this stream's reduction scratch (bn_scratch) outside any capture, so no
+    workspace is ever allocated from a graph's private pool."""
+    device = torch.device(device)
+    s = _capture_streams.get(device)
+    if s is None:
+        s = _capture_streams[device] = torch.cuda.Stream(device=device)
+    return s
 
 
 _scratch_kept = []
@@ -760,6 +803,12 @@ def bn_scratch(nbytes, device):
     key = (device, torch.cuda.current_stream(device).cuda_stream)
     t = _scratch.get(key)
     if t is None or t.numel() < nbytes:
+        if torch.cuda.is_current_stream_capturing():
+            # allocated inside a capture it would come from that graph's private pool and be shared
+            # with every later graph on the stream: captures warm up on their capture stream first
+            # (capture_stream), so every workspace exists before the capture begins
+            raise RuntimeError("bn_scratch: first use of a stream inside a graph capture (warm the capture "
+                               "up on conv.capture_stream(device) first)")
         if t is not None:
             _scratch_kept.append(t)
         t = torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)

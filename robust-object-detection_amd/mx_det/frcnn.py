@@ -966,7 +966,16 @@ class FasterRCNN(nn.Module):
                         raise ValueError("All bounding boxes should have positive height and width.")
             # GeneralizedRCNN.forward's degenerate-box check without its per-image host round trips:
             # the device flag is copied to pinned memory asynchronously and read after the RPN's own
-            # host sync (filter_proposals' per-image counts), where it is already complete
+            # host sync (filter_proposals' per-image counts), where it is already complete.
+            # Divergence: torchvision raises BEFORE any forward; here the backbone / FPN / RPN forward of
+            # the rejected batch has already run, so its BatchNorm running statistics (v2 has BN in the
+            # FPN and box head too) and the graphs' static buffers are updated by it. A loop that catches
+            # the error and skips the batch should set MX_STRICT_TARGETS=1 (one host sync per step,
+            # torchvision's order and state).
+            if flags and os.environ.get("MX_STRICT_TARGETS", "0") == "1":
+                if bool(torch.stack(flags).any()):
+                    raise ValueError("All bounding boxes should have positive height and width.")
+                flags = []
             degenerate = self._flag_async(flags)
         if isinstance(images, torch.Tensor) and images.dim() == 4 and images.dtype == torch.uint8:
             original = [(images.shape[1], images.shape[2])] * images.shape[0]
@@ -1046,7 +1055,7 @@ class _Graphs:
         grads = [p.grad for p in self.params]
         self.input_grad = input_grad
         self.static_x = x.detach().clone().requires_grad_(input_grad)
-        side = torch.cuda.Stream()
+        side = mc.capture_stream(x.device)  # warm-up and capture share it (bn_scratch)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(2):
@@ -1059,12 +1068,12 @@ class _Graphs:
         torch.cuda.current_stream().wait_stream(side)
         pool = torch.cuda.graph_pool_handle()
         self.fwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.fwd, pool=pool), mc.absorb_mode():
+        with torch.cuda.graph(self.fwd, pool=pool, stream=side), mc.absorb_mode():
             self.static_out = fn(self.static_x)
         self.static_gout = [torch.zeros_like(o) for o in self.static_out]
         roots, groots = _absorb_roots(fn, self.static_out, self.static_gout)
         self.bwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.bwd, pool=pool):
+        with torch.cuda.graph(self.bwd, pool=pool, stream=side):
             torch.autograd.backward(roots, groots)
         self.static_grads = [p.grad for p in self.params]
         self.static_xgrad = self.static_x.grad
@@ -1091,7 +1100,9 @@ def _absorb_roots(fn, outs, gouts):
         return list(outs), list(gouts)
     roots, groots = [], []
     for i, (o, g) in enumerate(zip(outs, gouts)):
-        if i < len(slots) and slots[i] is not None:
+        # only a slot whose consumer claimed it at forward time replaces the root (an unclaimed one --
+        # e.g. a copy in front of the consumer broke the tensor identity -- stays an ordinary root)
+        if i < len(slots) and slots[i] is not None and slots[i].taken:
             slots[i].buf = g
         else:
             roots.append(o)
@@ -1191,7 +1202,7 @@ class _SegGraphs:
                  if k.endswith(("running_mean", "running_var", "num_batches_tracked"))}
         grads = [p.grad for p in self.params]
         self.static_x = x.detach().clone()
-        side = torch.cuda.Stream()
+        side = mc.capture_stream(x.device)  # warm-up and capture share it (bn_scratch)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(2):
@@ -1203,14 +1214,14 @@ class _SegGraphs:
         torch.cuda.current_stream().wait_stream(side)
         pool = torch.cuda.graph_pool_handle()
         self.fwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.fwd, pool=pool), mc.absorb_mode():
+        with torch.cuda.graph(self.fwd, pool=pool, stream=side), mc.absorb_mode():
             outs, self.leaves, self.cs = self._fwd(self.static_x)
         self.static_gout = [torch.zeros_like(o) for o in outs]
         r0, g0 = _absorb_roots(self.model.rpn.head, outs, self.static_gout)
         self.bwd = []  # (segment key, graph)
         for key, roots, groots in self._bwd_plan(outs, self.static_gout, self.leaves, self.cs, (r0, g0)):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, stream=side):
                 torch.autograd.backward(roots, groots())
             self.bwd.append((key, g))
         self.static_out = tuple(o.detach() for o in outs)

@@ -322,7 +322,14 @@ class _CanvasPack(torch.autograd.Function):
 
 def canvas_pack(maps, rects, Hc, Wc, slots=None):
     """Zero canvas [N, Hc, Wc, C] holding maps[l] at rects[l] = (y, x, h, w) (one launch each way);
-    slots[l].buf, when set, is added to map l's gradient in the backward (conv.GradSlot)."""
+    slots[l].buf, when set, is added to map l's gradient in the backward (conv.GradSlot; the slots are
+    claimed here, on the stream the backward's unpack will run on)."""
+    if slots is not None and maps and maps[0].is_cuda:
+        st = torch.cuda.current_stream(maps[0].device).cuda_stream
+        for sl in slots:
+            if sl is not None:
+                sl.stream = st
+                sl.claim()
     return _CanvasPack.apply([tuple(int(v) for v in rc) for rc in rects], int(Hc), int(Wc), slots,
                              *[m.contiguous() for m in maps])
 

@@ -138,12 +138,13 @@ class SGD(torch.optim.SGD):
         if not any(e is not None for e in entries):
             return None
         n = len(ps)
-        first, bufs = [], []
+        # new momentum buffers stay local until the plan is built: a failed build must not leave
+        # uninitialised buffers in self.state (a retried step / state_dict would read them as momentum)
+        first, bufs, fresh = [], [], {}
         for p in ps:
-            st = self.state[p]
-            b = st.get("momentum_buffer")
+            b = self.state[p].get("momentum_buffer") if p in self.state else None
             if b is None:
-                b = st["momentum_buffer"] = torch.empty_like(p, memory_format=torch.contiguous_format)
+                b = fresh[p] = torch.empty_like(p, memory_format=torch.contiguous_format)
                 first.append(1)
             else:
                 first.append(0)
@@ -160,6 +161,8 @@ class SGD(torch.optim.SGD):
         host = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
         blocks, lds = ctypes.c_int64(0), ctypes.c_size_t(0)
         _lib.call("mx_sgd_pack_build", prm, n, descs, host.data_ptr(), nb, ctypes.byref(blocks), ctypes.byref(lds))
+        for p, b in fresh.items():
+            self.state[p]["momentum_buffer"] = b
         return {"ps": ps, "packer": pk, "pptr": [p.data_ptr() for p in ps], "entries": entries, "bufs": bufs,
                 "first": first, "ready": not any(first), "plan": host.to(ps[0].device, non_blocking=True),
                 "blocks": blocks.value, "lds": lds.value, "gkey": None}

@@ -216,3 +216,18 @@ def test_degenerate_target_box_raises(dev):
         m(imgs, tg)
     imgs, tg = synth_batch(0, 2, H=256, W=320, device=dev)
     assert torch.isfinite(sum(m(imgs, tg).values()))
+
+
+def test_strict_targets_raise_before_forward(dev, monkeypatch):
+    """MX_STRICT_TARGETS=1: the degenerate-box ValueError comes before any forward, as in torchvision,
+    so a rejected batch leaves the BatchNorm running statistics untouched."""
+    from mx_det.data import synth_batch
+    monkeypatch.setenv("MX_STRICT_TARGETS", "1")
+    m = _model(dev).train()
+    imgs, tg = synth_batch(0, 2, H=256, W=320, device=dev)
+    before = {k: v.clone() for k, v in m.state_dict().items() if k.endswith(("running_mean", "running_var"))}
+    tg[0]["boxes"][0, 3] = tg[0]["boxes"][0, 1]  # zero height
+    with pytest.raises(ValueError, match="positive height and width"):
+        m(imgs, tg)
+    after = m.state_dict()
+    assert all(torch.equal(v, after[k]) for k, v in before.items())

@@ -130,8 +130,10 @@ def test_oversubscribed_dht_rejected_before_table_writes():
     k = next(l for l in range(16) if d[bits + l] >= 3 and l > 0)
     d[bits + 0] += 3          # three more 1-bit codes (only two exist)...
     d[bits + k] -= 3          # ...same total, so only the code-space check can catch it
-    with pytest.raises(ValueError):
-        jpeg.parse(bytes(d))
+    with pytest.raises(ValueError):  # checked where a scan uses the table, as libjpeg does
+        jpeg.decode_coefs(bytes(d))
+    with pytest.raises(OSError):
+        _pil(bytes(d))
     # the entropy decoder's own table builder refuses it too (a caller handing it a crafted info)
     good = _base()
     info = jpeg.parse(bytes(good))
@@ -139,6 +141,24 @@ def test_oversubscribed_dht_rejected_before_table_writes():
         info.hbits[t][1] = 255
     with pytest.raises(ValueError):
         jpeg.decode_coefs(bytes(good), info)
+
+
+def test_complete_code_space_dht_rejected_like_libjpeg():
+    """A table whose codes fill the whole code space (Kraft sum 1: the last code is all ones) is legal
+    prefix code but libjpeg's jpeg_make_d_derived_tbl rejects it (`code >= 1 << si`): so must we."""
+    from mx_det import jpeg
+    d = _base()
+    m, o, e = next(s for s in _segs(d) if s[0] == 0xC4)
+    bits = o + 5
+    counts = list(d[bits:bits + 16])
+    assert counts == [0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0], counts  # T.81 K.3 DC luminance
+    assert sum(c / 2 ** (l + 1) for l, c in enumerate(counts)) == 1 - 2 ** -9
+    d[bits + 7] += 1  # one 9-bit code becomes an 8-bit one: Kraft sum exactly 1, same total
+    d[bits + 8] -= 1
+    with pytest.raises(OSError):
+        _pil(bytes(d))
+    with pytest.raises(ValueError):
+        jpeg.decode_coefs(bytes(d))
 
 
 def test_short_sos_and_undefined_quant_table_rejected():
