@@ -47,3 +47,35 @@ def synth_batch(start, n, H=800, W=1333, device="cpu"):
     imgs = torch.from_numpy(np.stack([synth_image(start + k, H, W) for k in range(n)])).to(device)
     tg = [{k: v.to(device) for k, v in synth_target(start + k, H, W).items()} for k in range(n)]
     return imgs, tg
+
+
+VISDRONE_CATEGORIES = ["pedestrian", "car", "van", "truck", "bus", "motor"]  # convert_visdrone_to_coco.py:24-31
+
+
+def write_coco_split(root, split, start, n, H=800, W=1333, mean_boxes=55, quality=95):
+    """A synthetic VisDrone-COCO split on disk in the layout the reference's scripts read
+    (data/processed/visdrone_coco6: images/<split>/*.jpg as PIL JPEG q95 and
+    annotations/instances_<split>.json, bbox xywh, the six VisDrone categories). Returns the json path."""
+    import json
+    from pathlib import Path
+    from PIL import Image
+    root = Path(root)
+    img_dir = root / "images" / split
+    img_dir.mkdir(parents=True, exist_ok=True)
+    images, anns, aid = [], [], 1
+    for i in range(n):
+        name = f"{start + i:05d}.jpg"
+        Image.fromarray(synth_image(start + i, H, W)).save(img_dir / name, quality=quality)
+        images.append({"id": start + i, "file_name": name, "width": W, "height": H})
+        t = synth_target(start + i, H, W, mean_boxes=mean_boxes)
+        for b, lab in zip(t["boxes"].tolist(), t["labels"].tolist()):
+            anns.append({"id": aid, "image_id": start + i, "category_id": lab,
+                         "bbox": [b[0], b[1], b[2] - b[0], b[3] - b[1]], "area": (b[2] - b[0]) * (b[3] - b[1]),
+                         "iscrowd": 0})
+            aid += 1
+    cats = [{"id": k, "name": nm} for k, nm in enumerate(VISDRONE_CATEGORIES, 1)]
+    (root / "annotations").mkdir(parents=True, exist_ok=True)
+    ann = root / "annotations" / f"instances_{split}.json"
+    with open(ann, "w") as f:
+        json.dump({"images": images, "annotations": anns, "categories": cats}, f)
+    return ann

@@ -166,15 +166,26 @@ def train_frcnn(cfg):
         print("Device:", dev, f"(world {world})", flush=True)
         if cfg.get("AUGMENT"):
             print("Mode: AUGMENTED training (corruption p=0.5, on GPU)\n", flush=True)
-    train_ds = COCODetectionDataset(str(cfg["TRAIN_IMG"]), str(cfg["TRAIN_ANN"]), transforms=uint8_transform)
-    val_ds = COCODetectionDataset(str(cfg["VAL_IMG"]), str(cfg["VAL_ANN"]), transforms=uint8_transform)
+    # device input pipeline (MX_DEVICE_JPEG, default on): the loader yields file bytes, the host
+    # entropy decode is prefetched on threads and the pixel stage runs on the GPU (PrefetchJpegLoader)
+    device_jpeg = cfg.get("DEVICE_JPEG", os.environ.get("MX_DEVICE_JPEG", "1") != "0")
+    train_ds = COCODetectionDataset(str(cfg["TRAIN_IMG"]), str(cfg["TRAIN_ANN"]), transforms=uint8_transform,
+                                    raw=device_jpeg)
+    val_ds = COCODetectionDataset(str(cfg["VAL_IMG"]), str(cfg["VAL_ANN"]), transforms=uint8_transform,
+                                  raw=device_jpeg)
     sampler = (DistributedSampler(train_ds, world, rank, shuffle=True, seed=cfg["SEED"], drop_last=True)
                if world > 1 else None)
     train_loader = DataLoader(train_ds, batch_size=cfg["BATCH_SIZE"], shuffle=sampler is None, sampler=sampler,
-                              num_workers=cfg.get("NUM_WORKERS", 0), collate_fn=collate_fn, pin_memory=True)
+                              num_workers=cfg.get("NUM_WORKERS", 0), collate_fn=collate_fn,
+                              pin_memory=not device_jpeg)
+    if device_jpeg:
+        train_loader = PrefetchJpegLoader(train_loader, dev, workers=cfg.get("DECODE_THREADS", 4))
     val_sampler = ShardSampler(len(val_ds), world, rank) if world > 1 else None
     val_loader = DataLoader(val_ds, batch_size=1, shuffle=False, sampler=val_sampler,
-                            num_workers=cfg.get("NUM_WORKERS", 0), collate_fn=collate_fn, pin_memory=True)
+                            num_workers=cfg.get("NUM_WORKERS", 0), collate_fn=collate_fn,
+                            pin_memory=not device_jpeg)
+    if device_jpeg:
+        val_loader = PrefetchJpegLoader(val_loader, dev, workers=cfg.get("DECODE_THREADS", 4))
     model = build_frcnn(7, cfg.get("WEIGHTS"), trainable_backbone_layers=cfg.get("TRAINABLE_LAYERS")).to(dev)
     ddp = model
     if world > 1:  # DDP(broadcast_buffers=False) semantics, HIP graphs kept (gradients averaged after backward)
@@ -196,6 +207,9 @@ def train_frcnn(cfg):
     corrupt = RandomCorruptionGPU(p=0.5) if cfg.get("AUGMENT") else None
     history, best_ckpt, last_ckpt = out_dir / "history.jsonl", out_dir / "best.pth", out_dir / "last.pth"
     t0 = time.time()
+    # cfg["TIMER"] = {"warmup": W}: bench.py --mode script's clock -- after W optimizer steps the device
+    # is synchronised and t0 taken, at the end of training t1 and the number of timed steps
+    timer = cfg.get("TIMER")
     n_batches = len(train_loader)
     for epoch in range(1, cfg["EPOCHS"] + 1):
         if sampler is not None:
@@ -203,7 +217,7 @@ def train_frcnn(cfg):
         ddp.train()
         epoch_loss = 0.0
         for i, (images, targets) in enumerate(train_loader):
-            imgs, tgs = _to_device_batch(images, targets, dev)
+            imgs, tgs = _to_device_batch(images, targets, dev)  # no-op copies for device images
             if corrupt is not None:
                 imgs = [corrupt(im) for im in imgs]
             loss_dict = ddp(imgs, tgs)
@@ -218,6 +232,11 @@ def train_frcnn(cfg):
             it_global += 1
             optimizer.step()
             epoch_loss += float(losses.item())
+            if timer is not None and it_global == timer["warmup"]:
+                torch.cuda.synchronize()
+                if world > 1:
+                    dist.barrier()
+                timer["t0"] = time.perf_counter()
             if rank == 0 and ((i + 1) % 100 == 0 or (i + 1) == n_batches):
                 print(f"  [Epoch {epoch:03d}] batch {i + 1}/{n_batches}", flush=True)
         sched.step()
@@ -231,6 +250,11 @@ def train_frcnn(cfg):
                                     "elapsed_sec": int(time.time() - t0)})
             print(f"[Epoch {epoch:03d}/{cfg['EPOCHS']}] loss_sum={epoch_loss:.4f}", flush=True)
             torch.save({"model": model.state_dict(), "epoch": epoch}, last_ckpt)
+    if timer is not None:
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        timer["t1"], timer["steps"] = time.perf_counter(), it_global - timer["warmup"]
     if rank == 0:
         print("\nEvaluating on clean val set (final)...", flush=True)
     metrics = evaluate(model, val_loader, str(cfg["VAL_ANN"]), dev)
@@ -296,6 +320,61 @@ class DeviceJpegLoader:
 
     def __len__(self):
         return len(self.loader)
+
+
+def _host_decode(b):
+    """Host half of one image's decode (a prefetch thread): JPEG -> (info, pinned coefficients), or
+    for files the hybrid decoder does not handle, PIL's RGB pixels (the reference's decode)."""
+    from . import jpeg
+    try:
+        return jpeg.host_stage(b)
+    except (jpeg.JpegUnsupported, ValueError):
+        import io
+        from PIL import Image
+        return None, np.asarray(Image.open(io.BytesIO(b.tobytes())).convert("RGB")).copy()
+
+
+class PrefetchJpegLoader:
+    """The training input pipeline on the device (coco_detection_dataset.py:23 + train_frcnn_*.py's
+    DataLoader): a loader of (file bytes, target) batches -> (uint8 HWC device images, targets).
+    The host entropy decode of the next `depth` batches runs on `workers` threads (the ctypes decoder
+    releases the GIL) while the GPU trains on the current one; the main thread only issues each image's
+    pinned -> HBM copy and the device IDCT / upsampling / colour launch (mx_det.jpeg.device_stage) on
+    the current stream, so the step never waits for a host decode that had a step's time to finish.
+    Pixels are bit-identical to PIL's decode (tests/test_jpeg.py)."""
+
+    def __init__(self, loader, dev, workers=4, depth=2):
+        self.loader, self.dev, self.workers, self.depth = loader, dev, int(workers), int(depth)
+
+    def __len__(self):
+        return len(self.loader)
+
+    def __iter__(self):
+        from collections import deque
+        from concurrent.futures import ThreadPoolExecutor
+        from . import jpeg
+        it = iter(self.loader)
+        pending = deque()
+        with ThreadPoolExecutor(max(1, self.workers)) as pool:
+            def submit():
+                try:
+                    images, targets = next(it)
+                except StopIteration:
+                    return False
+                pending.append(([pool.submit(_host_decode, b) for b in images], targets))
+                return True
+            for _ in range(max(1, self.depth)):
+                if not submit():
+                    break
+            while pending:
+                futs, targets = pending.popleft()
+                submit()
+                imgs = []
+                for f in futs:
+                    info, host = f.result()
+                    imgs.append(torch.from_numpy(host).to(self.dev) if info is None
+                                else jpeg.device_stage(info, host, self.dev))
+                yield imgs, targets
 
 
 class _RestoredLoader:

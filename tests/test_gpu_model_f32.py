@@ -73,7 +73,7 @@ def test_f32_eval_detections_match_cpu_backend(dev, monkeypatch):
 
 
 def test_f32_eval_detections_unpinned(dev):
-    """The same call end to end with each backend running its own RPN: at least 97 % of the CPU
+    """The same call end to end with each backend running its own RPN: at least 99 % of the CPU
     detections have a HIP detection with the same label, score and box within 1e-3 (a flipped
     proposal-NMS decision moves the odd detection by a few pixels: measured 1 of 200 on one box)."""
     out, ref = _eval_pair(dev)
@@ -86,7 +86,7 @@ def test_f32_eval_detections_unpinned(dev):
             ok = (ol == lab) & ((os_ - s).abs() <= 1e-3 + 1e-3 * s.abs()) & \
                  ((ob - b).abs() <= 1e-3 + 1e-3 * b.abs()).all(1)
             hit += bool(ok.any())
-        assert hit >= 0.97 * n, (hit, n)
+        assert hit >= 0.99 * n, (hit, n)
 
 
 def _tf32(t):
@@ -164,7 +164,9 @@ def _pin_proposals():
     return fp
 
 
-def test_f32_train_losses_and_grads_match_cpu_backend(dev, monkeypatch):
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("hw", [(512, 672), (800, 1333)])
+def test_f32_train_losses_and_grads_match_cpu_backend(dev, monkeypatch, hw):
     """One train forward + backward: all four losses within 1e-3 relative of the CPU fp32 path, and
     every trainable gradient closer to it than the reference's own arithmetic is (the CPU path with
     TF32-rounded conv operands, its Ampere GPU run), >= 5x closer on average over the parameters
@@ -176,7 +178,8 @@ def test_f32_train_losses_and_grads_match_cpu_backend(dev, monkeypatch):
     (one pair within float noise of IoU 0.7, or two near-equal scores in swapped order) through its
     neighbourhood -- measured (tools/debug_f32_parity.py) ~70 % of the sets agree whether the trunk
     features differ by 1e-3 or 5e-5, i.e. the divergence is the NMS cascade, not the size of the
-    perturbation."""
+    perturbation. Sizes: 512 x 672 frames (resized to 800 x 1050) and configs[1]'s own 1333 x 800
+    (padded 1344 x 800, no resize)."""
     import copy
     from mx_det import frcnn
     from mx_det.data import synth_batch
@@ -187,7 +190,7 @@ def test_f32_train_losses_and_grads_match_cpu_backend(dev, monkeypatch):
         mod.rpn.fg_bg_sampler.rand = _keys(7)
         mod.roi_heads.fg_bg_sampler.rand = _keys(8)
     monkeypatch.setattr(frcnn.RegionProposalNetwork, "filter_proposals_padded", _pin_proposals())
-    imgs, tg = synth_batch(30, 2, H=512, W=672)
+    imgs, tg = synth_batch(30, 2, H=hw[0], W=hw[1])
     ldc = mc(list(imgs), tg)
     ldt = mt(list(imgs), tg)
     ld = m(list(imgs.to(dev)), [{k: v.to(dev) for k, v in t.items()} for t in tg])

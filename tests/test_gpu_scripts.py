@@ -13,24 +13,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _write_split(root, split, start, n, H=200, W=280):
-    from mx_det.data import synth_image, synth_target
-    img_dir = root / "images" / split
-    img_dir.mkdir(parents=True, exist_ok=True)
-    images, anns, aid = [], [], 1
-    for i in range(n):
-        Image.fromarray(synth_image(start + i, H, W)).save(img_dir / f"{start + i:05d}.jpg", quality=95)
-        images.append({"id": start + i, "file_name": f"{start + i:05d}.jpg", "width": W, "height": H})
-        t = synth_target(start + i, H, W, mean_boxes=8)
-        for b, lab in zip(t["boxes"].tolist(), t["labels"].tolist()):
-            anns.append({"id": aid, "image_id": start + i, "category_id": lab,
-                         "bbox": [b[0], b[1], b[2] - b[0], b[3] - b[1]], "area": (b[2] - b[0]) * (b[3] - b[1]),
-                         "iscrowd": 0})
-            aid += 1
-    cats = [{"id": k, "name": n} for k, n in enumerate(["pedestrian", "car", "van", "truck", "bus", "motor"], 1)]
-    (root / "annotations").mkdir(parents=True, exist_ok=True)
-    ann = root / "annotations" / f"instances_{split}.json"
-    json.dump({"images": images, "annotations": anns, "categories": cats}, open(ann, "w"))
-    return ann
+    from mx_det.data import write_coco_split
+    return write_coco_split(root, split, start, n, H, W, mean_boxes=8)
 
 
 def test_train_eval_scripts(dev, tmp_path, monkeypatch):

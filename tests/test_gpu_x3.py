@@ -29,6 +29,18 @@ CASES = [
     (2, 64, 80, 256, 256, 3, 1, 1),    # 128x128 tiles, no split
 ]
 
+# configs[1]'s exact shapes (1333x800 padded to 1344x800, bs=2): the P2-level 3x3 (FPN output block
+# and RPN head convs, 2x200x336x256), layer3 / layer4 3x3 and 1x1 convs, the layer4 downsample and the
+# P5 lateral -- the launches the tuner maps to the 128x128 / 64x128 tiles and split-K in the bench
+HEADLINE = [
+    (2, 200, 336, 256, 256, 3, 1, 1),
+    (2, 50, 84, 256, 256, 3, 1, 1),
+    (2, 25, 42, 512, 512, 3, 1, 1),
+    (2, 50, 84, 1024, 256, 1, 1, 0),
+    (2, 50, 84, 1024, 2048, 1, 2, 0),
+    (2, 25, 42, 2048, 256, 1, 1, 0),
+]
+
 
 def tf32(t):
     """Round f32 to TF32 (10 explicit mantissa bits, RNE): the operand precision of the reference's
@@ -75,7 +87,7 @@ def test_split_pack_planes(dev):
     assert ((hi + lo - ref).abs() <= ref.abs() * 2 ** -16).all()
 
 
-@pytest.mark.parametrize("N,H,W,C,K,k,st,pd", CASES)
+@pytest.mark.parametrize("N,H,W,C,K,k,st,pd", CASES + HEADLINE)
 def test_x3_fwd(dev, N, H, W, C, K, k, st, pd):
     from mx_det import conv as mc
     g = torch.Generator().manual_seed(N * 1000 + C + K)
@@ -110,7 +122,8 @@ def test_x3_fwd_residual_leaky(dev):
     assert rel(y, ref) < 1e-5
 
 
-@pytest.mark.parametrize("N,H,W,C,K,k,st,pd", [c for c in CASES if c[4] % 8 == 0])
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("N,H,W,C,K,k,st,pd", [c for c in CASES + HEADLINE if c[4] % 8 == 0])
 def test_x3_dgrad_wgrad(dev, N, H, W, C, K, k, st, pd):
     from mx_det import conv as mc
     g = torch.Generator().manual_seed(7 + C + K)

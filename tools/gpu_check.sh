@@ -10,7 +10,7 @@ export TMPDIR=/tmp PYTHONUNBUFFERED=1
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
         > "$OUT/tests.log" 2>&1 || { echo "tests failed rc=$?"; tail -40 "$OUT/tests.log"; exit 1; }
       tail -3 "$OUT/tests.log" ;;
     smoke)
@@ -21,6 +21,14 @@ for s in $STEPS; do
       timeout -k 10 400 python -u bench.py > "$OUT/bench.log" 2>&1 \
         || { echo "bench failed rc=$?"; tail -30 "$OUT/bench.log"; exit 1; }
       tail -1 "$OUT/bench.log" ;;
+    script)
+      timeout -k 10 400 python -u bench.py --mode script --steps 20 --warmup 5 > "$OUT/script.log" 2>&1 \
+        || { echo "script bench failed rc=$?"; tail -30 "$OUT/script.log"; exit 1; }
+      tail -1 "$OUT/script.log" ;;
+    breakdown)
+      timeout -k 10 300 python -u tools/step_breakdown.py --top 60 > "$OUT/breakdown.log" 2>&1 \
+        || { echo "breakdown failed rc=$?"; tail -30 "$OUT/breakdown.log"; exit 1; }
+      tail -5 "$OUT/breakdown.log" ;;
     benchfast)
       timeout -k 10 300 python -u bench.py --no-cpu-baseline > "$OUT/bench.log" 2>&1 \
         || { echo "bench failed rc=$?"; tail -30 "$OUT/bench.log"; exit 1; }
