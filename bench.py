@@ -251,7 +251,7 @@ def hbm_ops_roofline(model, opt, imgs, tg, reps=10):
     from mx_det import ops
     from mx_det.backend import HipBackend
     cap = {}
-    o_ra, o_nms = HipBackend.multiscale_roi_align, HipBackend.proposal_nms
+    o_ra, o_nms, o_sel = HipBackend.multiscale_roi_align, HipBackend.proposal_nms, HipBackend.proposal_nms_select
 
     def ra(self, feats, rois, scales, k_min, output_size=(7, 7), sampling_ratio=2):
         cap["ra"] = ([f.detach() for f in feats], rois.detach().clone(), list(scales), k_min)
@@ -261,13 +261,18 @@ def hbm_ops_roofline(model, opt, imgs, tg, reps=10):
         cap["nms"] = (boxes.detach().clone(), scores.detach().clone(), lvl.clone(), group.clone(), G, L, thr, max_seg)
         return o_nms(self, boxes, scores, lvl, group, G, L, thr, max_seg)
 
-    HipBackend.multiscale_roi_align, HipBackend.proposal_nms = ra, pn
+    def ps(self, boxes, scores, lvl, group, G, L, thr, max_seg, post):
+        cap["nms_sel"] = (boxes.detach().clone(), scores.detach().clone(), lvl.clone(), group.clone(), G, L, thr,
+                          max_seg, post)
+        return o_sel(self, boxes, scores, lvl, group, G, L, thr, max_seg, post)
+
+    HipBackend.multiscale_roi_align, HipBackend.proposal_nms, HipBackend.proposal_nms_select = ra, pn, ps
     graphs = os.environ.get("MX_GRAPHS")
     os.environ["MX_GRAPHS"] = "0"  # eager: the RoI head graph would replay past the hook
     try:
         train_step(model, opt, imgs, tg)
     finally:
-        HipBackend.multiscale_roi_align, HipBackend.proposal_nms = o_ra, o_nms
+        HipBackend.multiscale_roi_align, HipBackend.proposal_nms, HipBackend.proposal_nms_select = o_ra, o_nms, o_sel
         if graphs is None:
             del os.environ["MX_GRAPHS"]
         else:
@@ -307,7 +312,19 @@ def hbm_ops_roofline(model, opt, imgs, tg, reps=10):
                                 "channels": C, "avg_call_us": round(us, 2), "level_map_mb": round(maps / 1e6, 2),
                                 "algorithmic_mb": round(byts / 1e6, 2), "achieved": round(gbs, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
-    if "nms" in cap:
+    if "nms_sel" in cap:  # the sort-free form on filter_proposals' presorted candidates (default)
+        boxes, scores, lvl, group, G, L, thr, max_seg, post = cap["nms_sel"]
+        n = boxes.shape[0]
+        us = timed(lambda: ops.batched_nms_grouped_sorted(boxes, scores, lvl, group, G, L, thr, max_seg, post))
+        us_general = timed(lambda: ops.batched_nms_grouped(boxes, scores, lvl, group, G, L, thr, max_seg))
+        byts = n * (16 + 4 + 8 + 4 + 8)
+        gbs = byts / (us * 1e-6) / 1e9
+        res["proposal_nms"] = {"kernel": "mx_batched_nms_grouped_sorted (pre + mask + scan + post)", "boxes": n,
+                               "images": G, "avg_call_us": round(us, 2), "general_path_us": round(us_general, 2),
+                               "algorithmic_mb": round(byts / 1e6, 3),
+                               "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(gbs / HBM_PEAK_GBS, 5), "bound": "latency (dependent scan)"}
+    elif "nms" in cap:
         boxes, scores, lvl, group, G, L, thr, max_seg = cap["nms"]
         n = boxes.shape[0]
         us = timed(lambda: ops.batched_nms_grouped(boxes, scores, lvl, group, G, L, thr, max_seg))

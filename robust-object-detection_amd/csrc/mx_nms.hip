@@ -540,6 +540,295 @@ __global__ void nms_group_out_kernel(const uint64_t* __restrict__ skeys, const i
   if (i == 0 && !live) *num_keep = *nk32 < 0 ? -1 : 0;
 }
 
+// ---- presorted grouped dispatch (mx_batched_nms_grouped_sorted) --------------------------------
+// filter_proposals' candidates are already ordered: image-major, level-major, and within each
+// (image, level) run by the per-level top-k's value order (score = sigmoid(logit) of a descending
+// logit list). Then the segment sort of mx_batched_nms_grouped is a stable compaction plus, for a
+// coordinate-trick image, a merge of its level runs -- and the final (image, score desc, index)
+// order of the survivors is a merge of their level runs. One workgroup per image does each with a
+// block scan in list order and merge ranks by binary search over the runs' score keys in LDS:
+// 2 launches replace the two radix sorts, the scans and their helper kernels (4 launches in all with
+// the mask and scan kernels). Exactness does not rest on the presorted order: every run's key order
+// is checked in LDS, and a run found out of order (e.g. a non-monotone sigmoid at ulp level) is ranked
+// by counting instead of binary search -- the result is always the stable (segment, score desc,
+// index) order of mx_batched_nms_grouped.
+static constexpr int PS_T = 1024, PS_NMAX = 32768, PS_GMAX = 64, PS_LMAX = 8;
+
+// wave-aggregated LDS counters: cnt[key] += #lanes with that key, mx[key / L] = max(m) (key < 0: none)
+__device__ __forceinline__ void ps_wave_add(int key, uint32_t m, int lane, uint32_t* cnt, uint32_t* mx, int L) {
+  bool todo = key >= 0;
+  while (__ballot(todo)) {
+    const uint64_t act = __ballot(todo);
+    const int leader = __ffsll((unsigned long long)act) - 1;
+    const int kk = __shfl(key, leader);
+    const bool mine = todo && key == kk;
+    const uint64_t sel = __ballot(mine);
+    if (mx) {
+      uint32_t v = mine ? m : 0u;
+      for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+      if (lane == leader) atomicMax(mx + kk / L, v);
+    }
+    if (lane == leader) atomicAdd(cnt + kk, (uint32_t)__popcll(sel));
+    todo = todo && !mine;
+  }
+}
+
+// block-wide ordered compaction step over one 1024-entry tile: returns the entry's index among the
+// flagged entries so far (valid where flag), advances *run by the tile's count; wsum = [16] LDS
+__device__ __forceinline__ int ps_compact(bool flag, int lane, int wave, int* wsum, int& run) {
+  const uint64_t bal = __ballot(flag);
+  if (lane == 0) wsum[wave] = __popcll(bal);
+  __syncthreads();
+  int before = run, tot = 0;
+#pragma unroll
+  for (int w = 0; w < PS_T / 64; ++w) {
+    const int c = wsum[w];
+    before += w < wave ? c : 0;
+    tot += c;
+  }
+  __syncthreads();  // wsum is rewritten by the next tile
+  run += tot;
+  return before + __popcll(bal & ((1ull << lane) - 1ull));
+}
+
+// entries of run [lo, hi) (keys non-increasing unless `bad`) ranked before key x at compacted index q:
+// key greater, or equal and earlier in list order (index below q)
+__device__ __forceinline__ int ps_before(const uint32_t* key, int lo, int hi, uint32_t x, int q, bool bad) {
+  if (bad) {
+    int c = 0;
+    for (int j = lo; j < hi; ++j) {
+      const uint32_t y = key[j];
+      c += (y > x || (y == x && j < q)) ? 1 : 0;
+    }
+    return c;
+  }
+  if (q >= hi) {  // whole run earlier in list order: ties precede
+    int a = lo, b = hi;
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if (key[mid] >= x) a = mid + 1; else b = mid;
+    }
+    return a - lo;
+  }
+  if (q < lo) {  // whole run later: ties follow
+    int a = lo, b = hi;
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if (key[mid] > x) a = mid + 1; else b = mid;
+    }
+    return a - lo;
+  }
+  return q - lo;  // x's own sorted run
+}
+
+__device__ __forceinline__ int ps_run_of(const int* rs, int L, int q) {
+  int l = 0;
+  while (l + 1 < L && q >= rs[l + 1]) ++l;
+  return l;
+}
+
+// one workgroup per image g: segment layout (positions, segment ids, offset boxes) for the mask /
+// scan kernels -- the outputs of nms_group_keys + sort + gather + scan + seg of the general path
+__global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
+    const float4* __restrict__ boxes, const float* __restrict__ scores, const int64_t* __restrict__ lvl,
+    const int32_t* __restrict__ group, int n, int G, int L, float4* __restrict__ sbox, float* __restrict__ sarea,
+    int32_t* __restrict__ v1, int32_t* __restrict__ incl, int32_t* __restrict__ seg_start, int32_t* __restrict__ nseg_out,
+    int32_t* __restrict__ flags, int32_t* __restrict__ nk, int32_t* __restrict__ scratch) {
+  extern __shared__ uint32_t key[];  // [n] score keys of this image's live entries, list order
+  __shared__ uint32_t cnt[PS_GMAX * PS_LMAX], gmx[PS_GMAX], bad;
+  __shared__ int wsum[PS_T / 64], rs[PS_LMAX + 1], runseg[PS_LMAX];
+  __shared__ int s_gbase, s_segbase, s_gcnt, s_trick, s_nlive, s_nseg;
+  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int k = tid; k < G * L; k += PS_T) cnt[k] = 0;
+  for (int k = tid; k < G; k += PS_T) gmx[k] = 0;
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  // pass 1: live counts per (image, level) and max coordinate per image, for every image (each block
+  // needs the earlier images' counts for its base); the flags are zeroed, each block a share of tiles
+  for (int i0 = 0; i0 < n; i0 += PS_T) {
+    const int i = i0 + tid;
+    int k = -1;
+    uint32_t m = 0;
+    if (i < n) {
+      const int gi = group[i];
+      if (gi >= 0 && gi < G) {
+        const float4 b = boxes[i];
+        m = max(max(ord_f32(b.x), ord_f32(b.y)), max(ord_f32(b.z), ord_f32(b.w)));
+        k = gi * L + (int)lvl[i];
+      }
+      if ((i0 / PS_T) % G == g) flags[i] = 0;
+    }
+    ps_wave_add(k, m, lane, cnt, gmx, L);
+  }
+  if (g == 0 && tid == 0) *nk = 0;
+  __syncthreads();
+  if (tid == 0) {
+    int nl = 0, ns = 0;
+    for (int gg = 0; gg < G; ++gg) {
+      int gc = 0, nr = 0;
+      for (int l = 0; l < L; ++l) {
+        gc += (int)cnt[gg * L + l];
+        nr += cnt[gg * L + l] ? 1 : 0;
+      }
+      const int tr = gc * 4 <= 4000;  // torchvision's CPU dispatch rule, per image
+      if (gg == g) {
+        s_gbase = nl;
+        s_segbase = ns;
+        s_gcnt = gc;
+        s_trick = tr;
+        int r = 0, sid = 0;
+        for (int l = 0; l < L; ++l) {
+          rs[l] = r;
+          runseg[l] = tr ? 0 : sid;
+          sid += cnt[gg * L + l] ? 1 : 0;
+          r += (int)cnt[gg * L + l];
+        }
+        rs[L] = r;
+      }
+      nl += gc;
+      ns += tr ? (gc > 0 ? 1 : 0) : nr;
+    }
+    s_nlive = nl;
+    s_nseg = ns;
+  }
+  __syncthreads();
+  const int gbase = s_gbase, gc = s_gcnt, trick = s_trick, nlive = s_nlive, nseg = s_nseg;
+  // segment starts: one per non-empty level run, or one for a coordinate-trick image
+  if (trick) {
+    if (tid == 0 && gc > 0) seg_start[s_segbase] = gbase;
+  } else if (tid < L && cnt[g * L + tid]) {
+    seg_start[s_segbase + runseg[tid]] = gbase + rs[tid];
+  }
+  if (g == G - 1 && tid == 0) {
+    *nseg_out = nseg;
+    seg_start[nseg] = nlive;
+    if (nlive < n) seg_start[nseg + 1] = nlive;  // the tail's empty pseudo-segment
+  }
+  // pass 2: this image's live entries in list order -> keys in LDS, list index in scratch
+  int run = 0;
+  for (int i0 = 0; i0 < n; i0 += PS_T) {
+    const int i = i0 + tid;
+    const bool mine = i < n && group[i] == g;
+    const int q = ps_compact(mine, lane, wave, wsum, run);
+    if (mine) {
+      key[q] = ord_f32(scores[i]);  // larger score, larger key
+      scratch[gbase + q] = i;
+    }
+  }
+  __syncthreads();
+  // every run's key order checked (presorted input: non-increasing within a run)
+  for (int q = tid + 1; q < gc; q += PS_T) {
+    const int l = ps_run_of(rs, L, q);
+    if (q > rs[l] && key[q] > key[q - 1]) atomicOr(&bad, 1u << l);
+  }
+  __syncthreads();
+  const uint32_t badm = bad;
+  const float step = unord_f32(gmx[g]) + 1.0f;
+  for (int q = tid; q < gc; q += PS_T) {
+    const int l = ps_run_of(rs, L, q);
+    const uint32_t x = key[q];
+    int rank;
+    if (trick) {  // one segment: the merge of the level runs
+      rank = 0;
+      for (int l2 = 0; l2 < L; ++l2) rank += ps_before(key, rs[l2], rs[l2 + 1], x, q, (badm >> l2) & 1u);
+    } else {
+      rank = rs[l] + ps_before(key, rs[l], rs[l + 1], x, q, (badm >> l) & 1u);
+    }
+    const int pos = gbase + rank;
+    const int i = scratch[gbase + q];
+    float4 b = boxes[i];
+    if (trick) {  // boxes + idxs * (max_coordinate + 1), as nms_group_keys_kernel
+      const float off = (float)lvl[i] * step;
+      b.x = b.x + off; b.y = b.y + off; b.z = b.z + off; b.w = b.w + off;
+    }
+    sbox[pos] = b;
+    sarea[pos] = (b.z - b.x) * (b.w - b.y);
+    v1[pos] = i;
+    incl[pos] = s_segbase + runseg[l] + 1;
+  }
+  for (int p = nlive + g * PS_T + tid; p < n; p += G * PS_T) incl[p] = nseg + 1;  // empty pseudo-segment
+}
+
+// one workgroup per image: survivors (flags) -> keep in (image, score desc, index) order, num_keep,
+// and optionally the padded per-image selection sel [G, post] / valid [G, post] of filter_proposals
+__global__ void __launch_bounds__(PS_T) nms_sorted_post_kernel(
+    const float* __restrict__ scores, const int64_t* __restrict__ lvl, const int32_t* __restrict__ group,
+    const int32_t* __restrict__ flags, int n, int G, int L, const int32_t* __restrict__ nk32, int32_t* __restrict__ scratch,
+    int64_t* __restrict__ keep, int64_t* __restrict__ num_keep, int post, int64_t* __restrict__ sel,
+    uint8_t* __restrict__ valid) {
+  extern __shared__ uint32_t key[];
+  __shared__ uint32_t cnt[PS_GMAX * PS_LMAX], bad;
+  __shared__ int wsum[PS_T / 64], rs[PS_LMAX + 1];
+  __shared__ int s_sbase, s_sc, s_total;
+  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int k = tid; k < G * L; k += PS_T) cnt[k] = 0;
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  for (int i0 = 0; i0 < n; i0 += PS_T) {
+    const int i = i0 + tid;
+    int k = -1;
+    if (i < n && flags[i]) {
+      const int gi = group[i];
+      if (gi >= 0 && gi < G) k = gi * L + (int)lvl[i];
+    }
+    ps_wave_add(k, 0u, lane, cnt, nullptr, L);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int tot = 0;
+    for (int gg = 0; gg < G; ++gg) {
+      int gc = 0;
+      for (int l = 0; l < L; ++l) gc += (int)cnt[gg * L + l];
+      if (gg == g) {
+        s_sbase = tot;
+        s_sc = gc;
+        int r = 0;
+        for (int l = 0; l < L; ++l) {
+          rs[l] = r;
+          r += (int)cnt[gg * L + l];
+        }
+        rs[L] = r;
+      }
+      tot += gc;
+    }
+    s_total = tot;
+  }
+  __syncthreads();
+  const int sbase = s_sbase, sc = s_sc, total = s_total;
+  int run = 0;
+  for (int i0 = 0; i0 < n; i0 += PS_T) {
+    const int i = i0 + tid;
+    const bool mine = i < n && flags[i] && group[i] == g;
+    const int q = ps_compact(mine, lane, wave, wsum, run);
+    if (mine) {
+      key[q] = ord_f32(scores[i]);
+      scratch[sbase + q] = i;
+    }
+  }
+  __syncthreads();
+  for (int q = tid + 1; q < sc; q += PS_T) {
+    const int l = ps_run_of(rs, L, q);
+    if (q > rs[l] && key[q] > key[q - 1]) atomicOr(&bad, 1u << l);
+  }
+  __syncthreads();
+  const uint32_t badm = bad;
+  for (int q = tid; q < sc; q += PS_T) {
+    const uint32_t x = key[q];
+    int rank = 0;
+    for (int l2 = 0; l2 < L; ++l2) rank += ps_before(key, rs[l2], rs[l2 + 1], x, q, (badm >> l2) & 1u);
+    keep[sbase + rank] = scratch[sbase + q];
+  }
+  if (g == 0 && tid == 0) *num_keep = *nk32 < 0 ? -1 : total;
+  for (int p = total + g * PS_T + tid; p < n; p += G * PS_T) keep[p] = 0;
+  if (sel) {
+    __syncthreads();  // this block's keep entries
+    for (int r = tid; r < post; r += PS_T) {
+      sel[(int64_t)g * post + r] = r < sc ? keep[sbase + r] : 0;
+      valid[(int64_t)g * post + r] = r < sc ? 1 : 0;
+    }
+  }
+}
+
 struct NmsWs {
   uint64_t *k0, *k1, *mask;
   int32_t *v0, *v1, *head, *incl, *seg_start, *nseg, *flags, *nk;
@@ -648,6 +937,56 @@ extern "C" int mx_batched_nms(const float* boxes, const float* scores, const int
   cb = w.cub_bytes;
   MX_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.k0, w.k1, w.v0, w.v1, (int)n, 0, 64, s));
   nms_out_kernel<<<nb, T, 0, s>>>(w.v1, n, w.nk, keep, num_keep);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" int mx_batched_nms_grouped_sorted(const float* boxes, const float* scores, const int64_t* lvl,
+                                             const int32_t* group, int64_t n, int64_t G, int64_t L, int64_t max_seg,
+                                             double thr, int64_t* keep, int64_t* num_keep, int64_t post, int64_t* sel,
+                                             uint8_t* valid, void* ws, size_t ws_bytes, mx_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  MX_CHECK_ARG(n >= 0 && n <= PS_NMAX && G > 0 && G <= PS_GMAX && L > 0 && L <= PS_LMAX,
+               "mx_batched_nms_grouped_sorted: bad sizes n=%lld (<= %d) G=%lld (<= %d) L=%lld (<= %d)", (long long)n,
+               PS_NMAX, (long long)G, PS_GMAX, (long long)L, PS_LMAX);
+  MX_CHECK_ARG(num_keep && (n == 0 || (boxes && scores && lvl && group && keep)),
+               "mx_batched_nms_grouped_sorted: null pointer");
+  MX_CHECK_ARG(post >= 0 && (post == 0 || (sel && valid)), "mx_batched_nms_grouped_sorted: sel / valid needed for post > 0");
+  if (n == 0) {
+    MX_HIP(hipMemsetAsync(num_keep, 0, sizeof(int64_t), s));
+    if (post > 0) {
+      MX_HIP(hipMemsetAsync(sel, 0, sizeof(int64_t) * (size_t)(G * post), s));
+      MX_HIP(hipMemsetAsync(valid, 0, (size_t)(G * post), s));
+    }
+    return MX_OK;
+  }
+  if (max_seg <= 0 || max_seg > n) max_seg = n;
+  const int Wm = (int)cdiv(max_seg, 64);
+  Carver c(ws, ws_bytes);
+  NmsWs w;
+  carve(c, n, Wm, &w, (int)G);
+  MX_CHECK_ARG(c.ok(), "mx_batched_nms_grouped_sorted: workspace too small (%zu < %zu)", ws_bytes, c.off);
+  MX_CHECK_ARG(Wm * 8 <= 64 * 1024, "mx_batched_nms_grouped_sorted: segment bound %lld too large", (long long)max_seg);
+  const size_t lds = sizeof(uint32_t) * (size_t)n;
+  nms_sorted_pre_kernel<<<(int)G, PS_T, lds, s>>>((const float4*)boxes, scores, lvl, group, (int)n, (int)G, (int)L, w.sbox,
+                                                  w.sarea, w.v1, w.incl, w.seg_start, w.nseg, w.flags, w.nk, w.v0);
+  MX_LAUNCH_CHECK();
+  dim3 mg((unsigned)cdiv(n, 64), (unsigned)Wm);
+  nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask);
+  MX_LAUNCH_CHECK();
+  const int sgrid = (int)std::min<int64_t>(n, 1024);
+  if (Wm <= SCAN_WAVE_W)
+    nms_scan_wave_kernel<<<sgrid, 64, (size_t)SCAN_RING * SCAN_SLOT, s>>>(w.mask, w.seg_start, w.nseg, w.v1,
+                                                                                   Wm, w.flags, w.nk);
+  else if (Wm <= SCAN_LDS_W)
+    nms_scan_lds_kernel<<<sgrid, 256, sizeof(uint64_t) * (Wm + 64 * (size_t)Wm), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
+                                                                                       Wm, w.flags, w.nk);
+  else
+    nms_scan_kernel<<<sgrid, 64, sizeof(uint64_t) * Wm, s>>>(w.mask, w.seg_start, w.nseg, w.v1, Wm, w.flags, w.nk);
+  MX_LAUNCH_CHECK();
+  nms_sorted_post_kernel<<<(int)G, PS_T, lds, s>>>(scores, lvl, group, w.flags, (int)n, (int)G, (int)L, w.nk, w.v0, keep,
+                                                   num_keep, (int)post, post > 0 ? sel : nullptr,
+                                                   post > 0 ? valid : nullptr);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

@@ -52,6 +52,8 @@ _SIGS = {
     "mx_box_iou": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "mx_nms_workspace": (c_sz, [c_i64, c_i64]),
     "mx_nms_grouped_workspace": (c_sz, [c_i64, c_i64, c_i64]),
+    "mx_batched_nms_grouped_sorted": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_d, c_vp, c_vp, c_i64,
+                                              c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_batched_nms_grouped": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_d, c_vp, c_vp, c_vp, c_sz,
                                        c_vp]),
     "mx_level_topk": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_i64, c_vp, c_vp]),

@@ -165,6 +165,12 @@ class HipBackend:
     def proposal_nms(self, boxes, scores, lvl, group, G, L, thr, max_seg):
         return ops.batched_nms_grouped(boxes, scores, lvl, group, G, L, thr, max_seg)
 
+    def proposal_nms_select(self, boxes, scores, lvl, group, G, L, thr, max_seg, post):
+        """filter_proposals' NMS on its presorted candidates plus the padded per-image selection:
+        (sel [G, post], valid [G, post]) (mx_batched_nms_grouped_sorted)."""
+        _, _, sel, valid = ops.batched_nms_grouped_sorted(boxes, scores, lvl, group, G, L, thr, max_seg, post)
+        return sel, valid
+
     def box_decode(self, rel, boxes, weights):
         return ops.box_decode(rel, boxes, weights)
 

@@ -487,6 +487,13 @@ class RegionProposalNetwork(nn.Module):
         T = keep.shape[1]
         n = N * T
         grp = torch.where(keep, bi, N).reshape(-1)
+        post = self.post_nms_top_n()
+        if hasattr(be, "proposal_nms_select") and os.environ.get("MX_SORTED_NMS", "1") != "0":
+            # the candidates are presorted (image, level, score desc: the per-level top-k order): the
+            # sort-free NMS also emits the padded per-image selection
+            sel, valid = be.proposal_nms_select(boxes.reshape(-1, 4), prob.reshape(-1), lvl.reshape(-1), grp, N,
+                                                len(num_per_level), self.nms_thresh, max(pre, 1000), post)
+            return boxes.reshape(-1, 4)[sel], prob.reshape(-1)[sel], valid
         kk, nk = be.proposal_nms(boxes.reshape(-1, 4), prob.reshape(-1), lvl.reshape(-1), grp, N,
                                  len(num_per_level), self.nms_thresh, max(pre, 1000))
         kk, nk = kk.to(dev), nk.to(dev)
@@ -494,7 +501,6 @@ class RegionProposalNetwork(nn.Module):
         cnt = torch.zeros(N + 1, dtype=torch.int64, device=dev)
         cnt.scatter_add_(0, torch.where(live, grp[kk], N), live.to(torch.int64))
         cnt = cnt[:N]
-        post = self.post_nms_top_n()
         r = torch.arange(post, device=dev)
         sel = kk[((torch.cumsum(cnt, 0) - cnt)[:, None] + r[None, :]).clamp(max=n - 1)]  # [N, post]
         valid = r[None, :] < cnt[:, None]                 # survivors are a prefix of each row

@@ -191,6 +191,45 @@ def batched_nms_grouped(boxes, scores, lvl, group, G, L, iou_threshold, max_seg)
     return keep, nk
 
 
+SORTED_NMS_MAX = (32768, 64, 8)  # n, G, L bounds of mx_batched_nms_grouped_sorted
+
+
+def batched_nms_grouped_sorted(boxes, scores, lvl, group, G, L, iou_threshold, max_seg, post=0):
+    """batched_nms_grouped for presorted candidates (mx_batched_nms_grouped_sorted: live entries
+    image-major, level-major, score-descending per (image, level) run -- filter_proposals' per-level
+    top-k layout; a run out of order is still ranked exactly). Same (keep, num_keep); with post > 0
+    also (sel [G, post] int64, valid [G, post] bool): per image its first `post` survivors (score
+    order), 0 / False past its count. Falls back to batched_nms_grouped outside the size bounds."""
+    _dev(boxes, scores)
+    n = boxes.shape[0]
+    dev = boxes.device
+    if n > SORTED_NMS_MAX[0] or G > SORTED_NMS_MAX[1] or L > SORTED_NMS_MAX[2]:
+        keep, nk = batched_nms_grouped(boxes, scores, lvl, group, G, L, iou_threshold, max_seg)
+        if not post:
+            return keep, nk
+        cnt = torch.zeros(G + 1, dtype=torch.int64, device=dev)
+        live = torch.arange(n, device=dev) < nk
+        cnt.scatter_add_(0, torch.where(live, group.to(torch.int64)[keep], G), live.to(torch.int64))
+        cnt = cnt[:G]
+        r = torch.arange(post, device=dev)
+        valid = r[None, :] < cnt[:, None]
+        sel = torch.where(valid, keep[((torch.cumsum(cnt, 0) - cnt)[:, None] + r[None, :]).clamp(max=max(n - 1, 0))], 0)
+        return keep, nk, sel, valid
+    keep = torch.empty(n, dtype=torch.int64, device=dev)
+    nk = torch.zeros(1, dtype=torch.int64, device=dev)
+    sel = torch.empty((G, post), dtype=torch.int64, device=dev) if post else None
+    valid = torch.empty((G, post), dtype=torch.bool, device=dev) if post else None
+    b = boxes.float().contiguous()
+    s = scores.float().contiguous()
+    lv = lvl.to(torch.int64).contiguous()
+    g = group.to(torch.int32).contiguous()
+    ws = _ws(_lib.load().mx_nms_grouped_workspace(max(n, 1), G, max_seg), dev)
+    call("mx_batched_nms_grouped_sorted", _p(b), _p(s), _p(lv), _p(g), n, G, L, int(max_seg), float(iou_threshold),
+         _p(keep), _p(nk), int(post), _p(sel) if post else None, _p(valid) if post else None, _p(ws), ws.numel(),
+         _stream())
+    return (keep, nk) if not post else (keep, nk, sel, valid)
+
+
 def level_topk(scores, num_per_level, k):
     """RegionProposalNetwork._get_top_n_idx (torchvision rpn.py): per image row of scores [N, A] and
     per level, the indices of the min(k, n_l) largest scores (value descending, ties by index) plus

@@ -120,10 +120,14 @@ def test_postprocess_matches_cpu_backend(dev):
     ([200, 100, 60, 30, 9], 0.0),        # <= 1000 boxes per image: coordinate-trick dispatch
     ([900, 500, 200, 60, 20], 0.8),      # image 0 per level, image 1 (80% removed as small) trick
 ])
-def test_filter_proposals_matches_cpu_backend(dev, levels, tiny):
+@pytest.mark.parametrize("sorted_nms", ["1", "0"])
+def test_filter_proposals_matches_cpu_backend(dev, levels, tiny, sorted_nms, monkeypatch):
     """RPN filter_proposals (per-level top-k, sigmoid, clip, remove_small, one grouped NMS with
     torchvision's per-image dispatch rule evaluated on the device, top-2000) on identical decoded
-    proposals and logits: identical proposal sets as the CPU restatement (per-image batched_nms)."""
+    proposals and logits: identical proposal sets as the CPU restatement (per-image batched_nms).
+    Both device NMS forms: the sort-free one on the presorted candidates (default) and the general
+    grouped one (MX_SORTED_NMS=0)."""
+    monkeypatch.setenv("MX_SORTED_NMS", sorted_nms)
     from oracle.cpu_backend import CpuBackend
     from mx_det.backend import default_backend
     g = torch.Generator().manual_seed(4)

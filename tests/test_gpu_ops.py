@@ -199,6 +199,83 @@ def test_batched_nms_grouped(dev):
     assert np.array_equal(got, np.concatenate(ref))
 
 
+def _presorted(rng, G, runs, dead_frac, ties):
+    """filter_proposals-shaped candidates: per image, per level a run of `runs[l]` slots with scores
+    descending (ties every `ties` slots), a fraction of slots dead (group G), boxes random."""
+    b, s, lv, gr = [], [], [], []
+    for g in range(G):
+        for l, k in enumerate(runs):
+            sc = np.sort(rng.random(k).astype(np.float32))[::-1].copy()
+            if ties:
+                sc[1::ties] = sc[0::ties][:len(sc[1::ties])]
+            b.append(_rand_boxes(rng, k, med=40))
+            s.append(sc)
+            lv.append(np.full(k, l))
+            gg = np.full(k, g, np.int32)
+            gg[rng.random(k) < dead_frac] = G
+            gr.append(gg)
+    return (np.concatenate(b).astype(np.float32), np.concatenate(s), np.concatenate(lv).astype(np.int64),
+            np.concatenate(gr))
+
+
+@pytest.mark.parametrize("G,runs,dead,ties,shuffle", [
+    (2, [2000, 2000, 2000, 2000, 819], 0.0, 0, False),   # the bs=2 training call: per-level NMS
+    (2, [2000, 2000, 2000, 2000, 819], 0.1, 5, False),   # dead slots + score ties
+    (3, [200, 100, 60, 30, 9], 0.2, 3, False),           # <= 1000 live per image: coordinate trick
+    (2, [900, 500, 200, 60, 20], 0.5, 0, False),         # one image per level, one trick (mixed)
+    (1, [1000, 1000, 1000, 1000, 273], 0.0, 0, False),   # eval: one image
+    (2, [700, 600, 300, 50, 10], 0.05, 0, True),         # runs NOT sorted: exact by the counting path
+    (2, [300, 200, 100, 20, 5], 0.05, 0, True),          # unsorted trick images
+])
+def test_batched_nms_grouped_sorted(dev, G, runs, dead, ties, shuffle):
+    """The sort-free grouped NMS on presorted candidates == the general grouped NMS (two radix sorts)
+    == per-image torchvision batched_nms (oracle): keep[:num_keep] bit-exact, and the padded
+    per-image selection equals the survivors' prefix. Shuffled runs break the presorted order: the
+    counting fallback must still give the exact stable order."""
+    from mx_det import ops
+    rng = np.random.default_rng(sum(runs) + G)
+    b, s, lv, gr = _presorted(rng, G, runs, dead, ties)
+    if shuffle:
+        perm = np.arange(len(s))
+        o = 0
+        for _ in range(G):
+            for k in runs:
+                perm[o:o + k] = o + rng.permutation(k)
+                o += k
+        b, s, lv, gr = b[perm], s[perm], lv[perm], gr[perm]
+    t = [torch.from_numpy(a).to(dev) for a in (b, s, lv, gr)]
+    L = len(runs)
+    k0, n0 = ops.batched_nms_grouped(*t, G, L, 0.7, 2000)
+    k1, n1, sel, valid = ops.batched_nms_grouped_sorted(*t, G, L, 0.7, 2000, post=1500)
+    nk = int(n0.item())
+    assert int(n1.item()) == nk
+    got = k1[:nk].cpu().numpy()
+    assert np.array_equal(got, k0[:nk].cpu().numpy())
+    ref = []
+    for g in range(G):
+        idx = np.where(gr == g)[0]
+        if idx.size:
+            ref.append(idx[orc.batched_nms(b[idx], s[idx], lv[idx], 0.7)])
+    assert np.array_equal(got, np.concatenate(ref) if ref else np.zeros(0, np.int64))
+    sel, valid = sel.cpu().numpy(), valid.cpu().numpy()
+    o = 0
+    for g in range(G):
+        c = len(ref[g]) if g < len(ref) else 0
+        assert valid[g].sum() == min(c, 1500) and valid[g][:min(c, 1500)].all()
+        assert np.array_equal(sel[g][:min(c, 1500)], got[o:o + min(c, 1500)])
+        o += c
+
+
+def test_batched_nms_grouped_sorted_empty(dev):
+    from mx_det import ops
+    z = torch.zeros((0, 4), device=dev)
+    k, nk, sel, valid = ops.batched_nms_grouped_sorted(z, torch.zeros(0, device=dev),
+                                                       torch.zeros(0, dtype=torch.int64, device=dev),
+                                                       torch.zeros(0, dtype=torch.int32, device=dev), 2, 5, 0.7, 2000,
+                                                       post=10)
+    assert int(nk.item()) == 0 and not valid.any() and (sel == 0).all()
+
+
 def test_nms_empty(dev):
     from mx_det import ops
     k = ops.nms(torch.zeros((0, 4), device=dev), torch.zeros(0, device=dev), 0.5)
