@@ -336,12 +336,13 @@ def _host_decode(b):
 
 class PrefetchJpegLoader:
     """The training input pipeline on the device (coco_detection_dataset.py:23 + train_frcnn_*.py's
-    DataLoader): a loader of (file bytes, target) batches -> (uint8 HWC device images, targets).
-    The host entropy decode of the next `depth` batches runs on `workers` threads (the ctypes decoder
-    releases the GIL) while the GPU trains on the current one; the main thread only issues each image's
-    pinned -> HBM copy and the device IDCT / upsampling / colour launch (mx_det.jpeg.device_stage) on
-    the current stream, so the step never waits for a host decode that had a step's time to finish.
-    Pixels are bit-identical to PIL's decode (tests/test_jpeg.py)."""
+    DataLoader): a loader of (file bytes, target) batches -> (uint8 HWC device images, device targets).
+    A producer thread runs the loader (file reads, COCO target tensors), pins the targets and hands
+    each image's host entropy decode to `workers` threads (the ctypes decoder releases the GIL), up to
+    `depth` batches ahead; the main thread only issues each batch's pinned -> HBM copies and the
+    device IDCT / upsampling / colour launches (mx_det.jpeg.device_stage) on the current stream, so
+    the training step never waits for host data work that had a step's time to finish. Pixels are
+    bit-identical to PIL's decode (tests/test_jpeg.py)."""
 
     def __init__(self, loader, dev, workers=4, depth=2):
         self.loader, self.dev, self.workers, self.depth = loader, dev, int(workers), int(depth)
@@ -350,31 +351,59 @@ class PrefetchJpegLoader:
         return len(self.loader)
 
     def __iter__(self):
-        from collections import deque
+        import queue
+        import sys
+        import threading
         from concurrent.futures import ThreadPoolExecutor
         from . import jpeg
-        it = iter(self.loader)
-        pending = deque()
-        with ThreadPoolExecutor(max(1, self.workers)) as pool:
-            def submit():
+        q = queue.Queue(maxsize=max(1, self.depth))
+        stop = threading.Event()
+        # the producer's Python work must not hold the GIL for a whole 5 ms switch interval while
+        # the training thread waits to issue launches
+        old_switch = sys.getswitchinterval()
+        sys.setswitchinterval(min(old_switch, 0.0005))
+
+        def put(item):
+            while not stop.is_set():
                 try:
-                    images, targets = next(it)
-                except StopIteration:
-                    return False
-                pending.append(([pool.submit(_host_decode, b) for b in images], targets))
-                return True
-            for _ in range(max(1, self.depth)):
-                if not submit():
+                    q.put(item, timeout=0.1)
+                    return True
+                except queue.Full:
+                    pass
+            return False
+
+        def produce():
+            try:
+                with ThreadPoolExecutor(max(1, self.workers)) as pool:
+                    for images, targets in self.loader:
+                        futs = [pool.submit(_host_decode, b) for b in images]
+                        tgs = [{k: v.pin_memory() for k, v in t.items()} for t in targets]
+                        if not put((futs, tgs)):
+                            return
+            except BaseException as e:  # surfaced in the consuming thread
+                put(e)
+                return
+            put(None)
+
+        th = threading.Thread(target=produce, name="mx-prefetch", daemon=True)
+        th.start()
+        try:
+            while True:
+                item = q.get()
+                if item is None:
                     break
-            while pending:
-                futs, targets = pending.popleft()
-                submit()
+                if isinstance(item, BaseException):
+                    raise item
+                futs, tgs = item
                 imgs = []
                 for f in futs:
                     info, host = f.result()
                     imgs.append(torch.from_numpy(host).to(self.dev) if info is None
                                 else jpeg.device_stage(info, host, self.dev))
-                yield imgs, targets
+                yield imgs, [{k: v.to(self.dev, non_blocking=True) for k, v in t.items()} for t in tgs]
+        finally:
+            stop.set()
+            sys.setswitchinterval(old_switch)
 
 
 class _RestoredLoader:

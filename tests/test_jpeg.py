@@ -8,6 +8,7 @@ files (progressive) raise. GPU: mx_jpeg_reconstruct on the device == PIL on the 
 import io
 
 import numpy as np
+import torch
 import pytest
 from PIL import Image
 
@@ -228,3 +229,27 @@ def test_extraneous_bytes_before_marker_skipped_like_libjpeg():
     junk = d[:o] + b"\x00\x12\x34" + d[o:]
     info, coefs = jpeg.decode_coefs(junk)
     assert np.array_equal(orc.jpeg_reconstruct(coefs, info), _pil(d))
+
+
+@pytest.mark.gpu
+def test_prefetch_loader_matches_pil(dev, tmp_path):
+    """engine.PrefetchJpegLoader (producer thread, threaded host entropy decode, device pixel stage,
+    pinned targets) over an on-disk COCO split: every image bit-identical to PIL's decode, targets
+    identical to the reference dataset's, batches in the loader's order."""
+    from torch.utils.data import DataLoader
+    from mx_det.data import write_coco_split
+    from mx_det.dataset import COCODetectionDataset, collate_fn, uint8_transform
+    from mx_det.engine import PrefetchJpegLoader
+    ann = write_coco_split(tmp_path, "train", 0, 5, H=120, W=176, mean_boxes=6)
+    raw = COCODetectionDataset(str(tmp_path / "images/train"), str(ann), transforms=uint8_transform, raw=True)
+    ref = COCODetectionDataset(str(tmp_path / "images/train"), str(ann), transforms=uint8_transform)
+    loader = PrefetchJpegLoader(DataLoader(raw, batch_size=2, shuffle=False, collate_fn=collate_fn), dev, workers=3)
+    seen = 0
+    for images, targets in loader:
+        for im, t in zip(images, targets):
+            r_img, r_t = ref[seen]
+            assert im.device.type == "cuda" and torch.equal(im.cpu(), r_img)
+            for k in r_t:
+                assert torch.equal(t[k].cpu(), r_t[k]), k
+            seen += 1
+    assert seen == 5
