@@ -552,9 +552,10 @@ __global__ void nms_group_out_kernel(const uint64_t* __restrict__ skeys, const i
 // is checked in LDS, and a run found out of order (e.g. a non-monotone sigmoid at ulp level) is ranked
 // by counting instead of binary search -- the result is always the stable (segment, score desc,
 // index) order of mx_batched_nms_grouped.
-static constexpr int PS_T = 1024, PS_NMAX = 32768, PS_GMAX = 64, PS_LMAX = 8;
+static constexpr int PS_T = 1024, PS_NMAX = 32768, PS_GMAX = 64, PS_LMAX = 8, PS_CH = PS_NMAX / PS_T;
 
-// wave-aggregated LDS counters: cnt[key] += #lanes with that key, mx[key / L] = max(m) (key < 0: none)
+// wave-aggregated counters: cnt[key] += #lanes with that key, mx[key / L] = max(m) (key < 0: none);
+// LDS or global (agent-scope atomics) alike
 __device__ __forceinline__ void ps_wave_add(int key, uint32_t m, int lane, uint32_t* cnt, uint32_t* mx, int L) {
   bool todo = key >= 0;
   while (__ballot(todo)) {
@@ -573,22 +574,26 @@ __device__ __forceinline__ void ps_wave_add(int key, uint32_t m, int lane, uint3
   }
 }
 
-// block-wide ordered compaction step over one 1024-entry tile: returns the entry's index among the
-// flagged entries so far (valid where flag), advances *run by the tile's count; wsum = [16] LDS
-__device__ __forceinline__ int ps_compact(bool flag, int lane, int wave, int* wsum, int& run) {
-  const uint64_t bal = __ballot(flag);
-  if (lane == 0) wsum[wave] = __popcll(bal);
+// block-wide exclusive scan of one int per thread (16 waves); *total = the block's sum
+__device__ __forceinline__ int ps_excl_scan(int v, int lane, int wave, int* wsum, int* total) {
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
   __syncthreads();
-  int before = run, tot = 0;
+  int wb = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < PS_T / 64; ++w) {
     const int c = wsum[w];
-    before += w < wave ? c : 0;
+    wb += w < wave ? c : 0;
     tot += c;
   }
-  __syncthreads();  // wsum is rewritten by the next tile
-  run += tot;
-  return before + __popcll(bal & ((1ull << lane) - 1ull));
+  __syncthreads();
+  *total = tot;
+  return wb + x - v;
 }
 
 // entries of run [lo, hi) (keys non-increasing unless `bad`) ranked before key x at compacted index q:
@@ -627,48 +632,92 @@ __device__ __forceinline__ int ps_run_of(const int* rs, int L, int q) {
   return l;
 }
 
+// pass over the list by many blocks: live entries per (image, level) and the max coordinate per image
+// into tab (zeroed by a memset; tab[G*L .. G*L+G) = max bits), flags zeroed, keep count reset
+__global__ void __launch_bounds__(256) nms_sorted_stats_kernel(const float4* __restrict__ boxes,
+                                                               const int64_t* __restrict__ lvl,
+                                                               const int32_t* __restrict__ group, int n, int G, int L,
+                                                               uint32_t* __restrict__ tab, int32_t* __restrict__ flags,
+                                                               int32_t* __restrict__ nk) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  int k = -1;
+  uint32_t m = 0;
+  if (i < n) {
+    flags[i] = 0;
+    const int gi = group[i];
+    if (gi >= 0 && gi < G) {
+      const float4 b = boxes[i];
+      m = max(max(ord_f32(b.x), ord_f32(b.y)), max(ord_f32(b.z), ord_f32(b.w)));
+      k = gi * L + (int)lvl[i];
+    }
+  }
+  if (i == 0) *nk = 0;
+  ps_wave_add(k, m, threadIdx.x & 63, tab, tab + G * L, L);
+}
+
+// survivors per (image, level) into tab2 (zeroed by nms_sorted_pre_kernel)
+__global__ void __launch_bounds__(256) nms_sorted_post_stats_kernel(const int64_t* __restrict__ lvl,
+                                                                    const int32_t* __restrict__ group,
+                                                                    const int32_t* __restrict__ flags, int n, int G,
+                                                                    int L, uint32_t* __restrict__ tab2) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  int k = -1;
+  if (i < n && flags[i]) {
+    const int gi = group[i];
+    if (gi >= 0 && gi < G) k = gi * L + (int)lvl[i];
+  }
+  ps_wave_add(k, 0u, threadIdx.x & 63, tab2, nullptr, L);
+}
+
+// the block's image entries in list order: thread t owns [t*ch, t*ch + ch); returns the compacted
+// index of its first selected entry; sel = selected bits of its chunk
+__device__ __forceinline__ int ps_compact_chunks(const int32_t* __restrict__ group, const int32_t* __restrict__ flags,
+                                                 int n, int g, int ch, int tid, int lane, int wave, int* wsum,
+                                                 uint32_t* sel_bits, int* total) {
+  const int b0 = tid * ch;
+  int gv[PS_CH], fv[PS_CH];
+#pragma unroll
+  for (int u = 0; u < PS_CH; ++u) {
+    const int i = b0 + u;
+    const bool in = u < ch && i < n;
+    gv[u] = in ? group[i] : -1;
+    fv[u] = (in && flags) ? flags[i] : 1;
+  }
+  uint32_t bits = 0;
+  int own = 0;
+#pragma unroll
+  for (int u = 0; u < PS_CH; ++u) {
+    const bool m = gv[u] == g && fv[u] != 0;
+    bits |= m ? (1u << u) : 0u;
+    own += m ? 1 : 0;
+  }
+  *sel_bits = bits;
+  return ps_excl_scan(own, lane, wave, wsum, total);
+}
+
 // one workgroup per image g: segment layout (positions, segment ids, offset boxes) for the mask /
 // scan kernels -- the outputs of nms_group_keys + sort + gather + scan + seg of the general path
 __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
     const float4* __restrict__ boxes, const float* __restrict__ scores, const int64_t* __restrict__ lvl,
-    const int32_t* __restrict__ group, int n, int G, int L, float4* __restrict__ sbox, float* __restrict__ sarea,
-    int32_t* __restrict__ v1, int32_t* __restrict__ incl, int32_t* __restrict__ seg_start, int32_t* __restrict__ nseg_out,
-    int32_t* __restrict__ flags, int32_t* __restrict__ nk, int32_t* __restrict__ scratch) {
+    const int32_t* __restrict__ group, int n, int G, int L, const uint32_t* __restrict__ tab, uint32_t* __restrict__ tab2,
+    float4* __restrict__ sbox, float* __restrict__ sarea, int32_t* __restrict__ v1, int32_t* __restrict__ incl,
+    int32_t* __restrict__ seg_start, int32_t* __restrict__ nseg_out, int32_t* __restrict__ scratch,
+    int32_t* __restrict__ err) {
   extern __shared__ uint32_t key[];  // [n] score keys of this image's live entries, list order
-  __shared__ uint32_t cnt[PS_GMAX * PS_LMAX], gmx[PS_GMAX], bad;
+  __shared__ uint32_t bad;
   __shared__ int wsum[PS_T / 64], rs[PS_LMAX + 1], runseg[PS_LMAX];
   __shared__ int s_gbase, s_segbase, s_gcnt, s_trick, s_nlive, s_nseg;
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int k = tid; k < G * L; k += PS_T) cnt[k] = 0;
-  for (int k = tid; k < G; k += PS_T) gmx[k] = 0;
-  if (tid == 0) bad = 0;
-  __syncthreads();
-  // pass 1: live counts per (image, level) and max coordinate per image, for every image (each block
-  // needs the earlier images' counts for its base); the flags are zeroed, each block a share of tiles
-  for (int i0 = 0; i0 < n; i0 += PS_T) {
-    const int i = i0 + tid;
-    int k = -1;
-    uint32_t m = 0;
-    if (i < n) {
-      const int gi = group[i];
-      if (gi >= 0 && gi < G) {
-        const float4 b = boxes[i];
-        m = max(max(ord_f32(b.x), ord_f32(b.y)), max(ord_f32(b.z), ord_f32(b.w)));
-        k = gi * L + (int)lvl[i];
-      }
-      if ((i0 / PS_T) % G == g) flags[i] = 0;
-    }
-    ps_wave_add(k, m, lane, cnt, gmx, L);
-  }
-  if (g == 0 && tid == 0) *nk = 0;
-  __syncthreads();
+  if (g == 0)
+    for (int k = tid; k < G * L; k += PS_T) tab2[k] = 0;  // the post pass's counters
   if (tid == 0) {
+    bad = 0;
     int nl = 0, ns = 0;
     for (int gg = 0; gg < G; ++gg) {
       int gc = 0, nr = 0;
       for (int l = 0; l < L; ++l) {
-        gc += (int)cnt[gg * L + l];
-        nr += cnt[gg * L + l] ? 1 : 0;
+        gc += (int)tab[gg * L + l];
+        nr += tab[gg * L + l] ? 1 : 0;
       }
       const int tr = gc * 4 <= 4000;  // torchvision's CPU dispatch rule, per image
       if (gg == g) {
@@ -680,8 +729,8 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
         for (int l = 0; l < L; ++l) {
           rs[l] = r;
           runseg[l] = tr ? 0 : sid;
-          sid += cnt[gg * L + l] ? 1 : 0;
-          r += (int)cnt[gg * L + l];
+          sid += tab[gg * L + l] ? 1 : 0;
+          r += (int)tab[gg * L + l];
         }
         rs[L] = r;
       }
@@ -696,7 +745,7 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
   // segment starts: one per non-empty level run, or one for a coordinate-trick image
   if (trick) {
     if (tid == 0 && gc > 0) seg_start[s_segbase] = gbase;
-  } else if (tid < L && cnt[g * L + tid]) {
+  } else if (tid < L && tab[g * L + tid]) {
     seg_start[s_segbase + runseg[tid]] = gbase + rs[tid];
   }
   if (g == G - 1 && tid == 0) {
@@ -704,38 +753,46 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
     seg_start[nseg] = nlive;
     if (nlive < n) seg_start[nseg + 1] = nlive;  // the tail's empty pseudo-segment
   }
-  // pass 2: this image's live entries in list order -> keys in LDS, list index in scratch
-  int run = 0;
-  for (int i0 = 0; i0 < n; i0 += PS_T) {
-    const int i = i0 + tid;
-    const bool mine = i < n && group[i] == g;
-    const int q = ps_compact(mine, lane, wave, wsum, run);
-    if (mine) {
-      key[q] = ord_f32(scores[i]);  // larger score, larger key
-      scratch[gbase + q] = i;
-    }
+  // this image's live entries in list order -> keys in LDS, list index in scratch
+  const int ch = (n + PS_T - 1) / PS_T;
+  uint32_t bits;
+  int tot;
+  int q = ps_compact_chunks(group, nullptr, n, g, ch, tid, lane, wave, wsum, &bits, &tot);
+  for (int u = 0; bits; ++u, bits >>= 1) {
+    if (!(bits & 1u)) continue;
+    const int i = tid * ch + u;
+    key[q] = ord_f32(scores[i]);
+    scratch[gbase + q] = i;
+    if ((int)lvl[i] != ps_run_of(rs, L, q) || q >= gc) atomicOr(&bad, 0x80000000u);  // layout contract
+    ++q;
   }
   __syncthreads();
   // every run's key order checked (presorted input: non-increasing within a run)
-  for (int q = tid + 1; q < gc; q += PS_T) {
-    const int l = ps_run_of(rs, L, q);
-    if (q > rs[l] && key[q] > key[q - 1]) atomicOr(&bad, 1u << l);
+  for (int q2 = tid + 1; q2 < gc; q2 += PS_T) {
+    const int l = ps_run_of(rs, L, q2);
+    if (q2 > rs[l] && key[q2] > key[q2 - 1]) atomicOr(&bad, 1u << l);
   }
   __syncthreads();
-  const uint32_t badm = bad;
-  const float step = unord_f32(gmx[g]) + 1.0f;
-  for (int q = tid; q < gc; q += PS_T) {
-    const int l = ps_run_of(rs, L, q);
-    const uint32_t x = key[q];
+  uint32_t badm = bad;
+  if (badm & 0x80000000u) {
+    // not image-major / level-major: reported (num_keep = -2); every run is then ranked by counting,
+    // so the positions stay a permutation and every later index stays in range
+    if (tid == 0) atomicExch(err, 1);
+    badm = 0xffffffffu;
+  }
+  const float step = unord_f32(tab[G * L + g]) + 1.0f;
+  for (int q2 = tid; q2 < gc; q2 += PS_T) {
+    const int l = ps_run_of(rs, L, q2);
+    const uint32_t x = key[q2];
     int rank;
     if (trick) {  // one segment: the merge of the level runs
       rank = 0;
-      for (int l2 = 0; l2 < L; ++l2) rank += ps_before(key, rs[l2], rs[l2 + 1], x, q, (badm >> l2) & 1u);
+      for (int l2 = 0; l2 < L; ++l2) rank += ps_before(key, rs[l2], rs[l2 + 1], x, q2, (badm >> l2) & 1u);
     } else {
-      rank = rs[l] + ps_before(key, rs[l], rs[l + 1], x, q, (badm >> l) & 1u);
+      rank = rs[l] + ps_before(key, rs[l], rs[l + 1], x, q2, (badm >> l) & 1u);
     }
     const int pos = gbase + rank;
-    const int i = scratch[gbase + q];
+    const int i = scratch[gbase + q2];
     float4 b = boxes[i];
     if (trick) {  // boxes + idxs * (max_coordinate + 1), as nms_group_keys_kernel
       const float off = (float)lvl[i] * step;
@@ -752,40 +809,28 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
 // one workgroup per image: survivors (flags) -> keep in (image, score desc, index) order, num_keep,
 // and optionally the padded per-image selection sel [G, post] / valid [G, post] of filter_proposals
 __global__ void __launch_bounds__(PS_T) nms_sorted_post_kernel(
-    const float* __restrict__ scores, const int64_t* __restrict__ lvl, const int32_t* __restrict__ group,
-    const int32_t* __restrict__ flags, int n, int G, int L, const int32_t* __restrict__ nk32, int32_t* __restrict__ scratch,
-    int64_t* __restrict__ keep, int64_t* __restrict__ num_keep, int post, int64_t* __restrict__ sel,
-    uint8_t* __restrict__ valid) {
+    const float* __restrict__ scores, const int32_t* __restrict__ group, const int32_t* __restrict__ flags, int n, int G,
+    int L, const uint32_t* __restrict__ tab2, const int32_t* __restrict__ nk32, const int32_t* __restrict__ err,
+    int32_t* __restrict__ scratch, int64_t* __restrict__ keep, int64_t* __restrict__ num_keep, int post,
+    int64_t* __restrict__ sel, uint8_t* __restrict__ valid) {
   extern __shared__ uint32_t key[];
-  __shared__ uint32_t cnt[PS_GMAX * PS_LMAX], bad;
+  __shared__ uint32_t bad;
   __shared__ int wsum[PS_T / 64], rs[PS_LMAX + 1];
   __shared__ int s_sbase, s_sc, s_total;
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int k = tid; k < G * L; k += PS_T) cnt[k] = 0;
-  if (tid == 0) bad = 0;
-  __syncthreads();
-  for (int i0 = 0; i0 < n; i0 += PS_T) {
-    const int i = i0 + tid;
-    int k = -1;
-    if (i < n && flags[i]) {
-      const int gi = group[i];
-      if (gi >= 0 && gi < G) k = gi * L + (int)lvl[i];
-    }
-    ps_wave_add(k, 0u, lane, cnt, nullptr, L);
-  }
-  __syncthreads();
   if (tid == 0) {
+    bad = 0;
     int tot = 0;
     for (int gg = 0; gg < G; ++gg) {
       int gc = 0;
-      for (int l = 0; l < L; ++l) gc += (int)cnt[gg * L + l];
+      for (int l = 0; l < L; ++l) gc += (int)tab2[gg * L + l];
       if (gg == g) {
         s_sbase = tot;
         s_sc = gc;
         int r = 0;
         for (int l = 0; l < L; ++l) {
           rs[l] = r;
-          r += (int)cnt[gg * L + l];
+          r += (int)tab2[gg * L + l];
         }
         rs[L] = r;
       }
@@ -795,36 +840,40 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_post_kernel(
   }
   __syncthreads();
   const int sbase = s_sbase, sc = s_sc, total = s_total;
-  int run = 0;
-  for (int i0 = 0; i0 < n; i0 += PS_T) {
-    const int i = i0 + tid;
-    const bool mine = i < n && flags[i] && group[i] == g;
-    const int q = ps_compact(mine, lane, wave, wsum, run);
-    if (mine) {
-      key[q] = ord_f32(scores[i]);
-      scratch[sbase + q] = i;
-    }
+  const bool failed = *err != 0;
+  const int ch = (n + PS_T - 1) / PS_T;
+  uint32_t bits;
+  int tot;
+  int q = ps_compact_chunks(group, flags, n, g, ch, tid, lane, wave, wsum, &bits, &tot);
+  for (int u = 0; bits; ++u, bits >>= 1) {
+    if (!(bits & 1u)) continue;
+    const int i = tid * ch + u;
+    key[q] = ord_f32(scores[i]);
+    scratch[sbase + q] = i;
+    ++q;
   }
   __syncthreads();
-  for (int q = tid + 1; q < sc; q += PS_T) {
-    const int l = ps_run_of(rs, L, q);
-    if (q > rs[l] && key[q] > key[q - 1]) atomicOr(&bad, 1u << l);
+  for (int q2 = tid + 1; q2 < sc; q2 += PS_T) {
+    const int l = ps_run_of(rs, L, q2);
+    if (q2 > rs[l] && key[q2] > key[q2 - 1]) atomicOr(&bad, 1u << l);
   }
   __syncthreads();
   const uint32_t badm = bad;
-  for (int q = tid; q < sc; q += PS_T) {
-    const uint32_t x = key[q];
+  for (int q2 = tid; q2 < sc; q2 += PS_T) {
+    const uint32_t x = key[q2];
     int rank = 0;
-    for (int l2 = 0; l2 < L; ++l2) rank += ps_before(key, rs[l2], rs[l2 + 1], x, q, (badm >> l2) & 1u);
-    keep[sbase + rank] = scratch[sbase + q];
+    for (int l2 = 0; l2 < L; ++l2) rank += ps_before(key, rs[l2], rs[l2 + 1], x, q2, (badm >> l2) & 1u);
+    keep[sbase + rank] = scratch[sbase + q2];
   }
-  if (g == 0 && tid == 0) *num_keep = *nk32 < 0 ? -1 : total;
+  // -1: a segment exceeded max_seg (the scan's overflow flag); -2: the presorted layout contract broken
+  if (g == 0 && tid == 0) *num_keep = failed ? -2 : (*nk32 < 0 ? -1 : total);
   for (int p = total + g * PS_T + tid; p < n; p += G * PS_T) keep[p] = 0;
   if (sel) {
     __syncthreads();  // this block's keep entries
     for (int r = tid; r < post; r += PS_T) {
-      sel[(int64_t)g * post + r] = r < sc ? keep[sbase + r] : 0;
-      valid[(int64_t)g * post + r] = r < sc ? 1 : 0;
+      const bool ok = r < sc && !failed;
+      sel[(int64_t)g * post + r] = ok ? keep[sbase + r] : 0;
+      valid[(int64_t)g * post + r] = ok ? 1 : 0;
     }
   }
 }
@@ -833,6 +882,7 @@ struct NmsWs {
   uint64_t *k0, *k1, *mask;
   int32_t *v0, *v1, *head, *incl, *seg_start, *nseg, *flags, *nk;
   uint32_t* maxbits;
+  uint32_t* tab;
   int32_t* gcnt;
   uint32_t* gmax;
   float4 *obox, *sbox;
@@ -852,6 +902,8 @@ static size_t cub_bytes_needed(int64_t n) {
 static size_t carve(Carver& c, int64_t n, int Wm, NmsWs* w, int G = 0) {
   int64_t m = n > 0 ? n : 1;
   w->gcnt = G > 0 ? c.take<int32_t>(2 * (size_t)G) : nullptr;  // [G] counts then [G] max bits
+  // the presorted path's tables: [G*L] live counts, [G] max bits, [G*L] survivor counts, error word
+  w->tab = G > 0 ? c.take<uint32_t>(2 * (size_t)PS_GMAX * PS_LMAX + PS_GMAX + 1) : nullptr;
   w->gmax = G > 0 ? (uint32_t*)(w->gcnt + G) : nullptr;
   w->k0 = c.take<uint64_t>(m); w->k1 = c.take<uint64_t>(m);
   w->v0 = c.take<int32_t>(m); w->v1 = c.take<int32_t>(m);
@@ -965,11 +1017,20 @@ extern "C" int mx_batched_nms_grouped_sorted(const float* boxes, const float* sc
   Carver c(ws, ws_bytes);
   NmsWs w;
   carve(c, n, Wm, &w, (int)G);
+  // small tables in the (unused here) sort-key buffer: [G*L] counts + [G] max bits, [G*L] survivor
+  // counts, one error word
   MX_CHECK_ARG(c.ok(), "mx_batched_nms_grouped_sorted: workspace too small (%zu < %zu)", ws_bytes, c.off);
   MX_CHECK_ARG(Wm * 8 <= 64 * 1024, "mx_batched_nms_grouped_sorted: segment bound %lld too large", (long long)max_seg);
+  uint32_t* tab = w.tab;
+  uint32_t* tab2 = tab + G * L + G;
+  int32_t* err = (int32_t*)(tab2 + G * L);
+  MX_HIP(hipMemsetAsync(tab, 0, sizeof(uint32_t) * (size_t)(G * L + G) + sizeof(uint32_t) * (size_t)(G * L) + 4, s));
+  const int nb = (int)cdiv(n, 256);
+  nms_sorted_stats_kernel<<<nb, 256, 0, s>>>((const float4*)boxes, lvl, group, (int)n, (int)G, (int)L, tab, w.flags, w.nk);
+  MX_LAUNCH_CHECK();
   const size_t lds = sizeof(uint32_t) * (size_t)n;
-  nms_sorted_pre_kernel<<<(int)G, PS_T, lds, s>>>((const float4*)boxes, scores, lvl, group, (int)n, (int)G, (int)L, w.sbox,
-                                                  w.sarea, w.v1, w.incl, w.seg_start, w.nseg, w.flags, w.nk, w.v0);
+  nms_sorted_pre_kernel<<<(int)G, PS_T, lds, s>>>((const float4*)boxes, scores, lvl, group, (int)n, (int)G, (int)L, tab,
+                                                  tab2, w.sbox, w.sarea, w.v1, w.incl, w.seg_start, w.nseg, w.v0, err);
   MX_LAUNCH_CHECK();
   dim3 mg((unsigned)cdiv(n, 64), (unsigned)Wm);
   nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask);
@@ -984,8 +1045,10 @@ extern "C" int mx_batched_nms_grouped_sorted(const float* boxes, const float* sc
   else
     nms_scan_kernel<<<sgrid, 64, sizeof(uint64_t) * Wm, s>>>(w.mask, w.seg_start, w.nseg, w.v1, Wm, w.flags, w.nk);
   MX_LAUNCH_CHECK();
-  nms_sorted_post_kernel<<<(int)G, PS_T, lds, s>>>(scores, lvl, group, w.flags, (int)n, (int)G, (int)L, w.nk, w.v0, keep,
-                                                   num_keep, (int)post, post > 0 ? sel : nullptr,
+  nms_sorted_post_stats_kernel<<<nb, 256, 0, s>>>(lvl, group, w.flags, (int)n, (int)G, (int)L, tab2);
+  MX_LAUNCH_CHECK();
+  nms_sorted_post_kernel<<<(int)G, PS_T, lds, s>>>(scores, group, w.flags, (int)n, (int)G, (int)L, tab2, w.nk, err, w.v0,
+                                                   keep, num_keep, (int)post, post > 0 ? sel : nullptr,
                                                    post > 0 ? valid : nullptr);
   MX_LAUNCH_CHECK();
   return MX_OK;

@@ -226,6 +226,7 @@ def _presorted(rng, G, runs, dead_frac, ties):
     (1, [1000, 1000, 1000, 1000, 273], 0.0, 0, False),   # eval: one image
     (2, [700, 600, 300, 50, 10], 0.05, 0, True),         # runs NOT sorted: exact by the counting path
     (2, [300, 200, 100, 20, 5], 0.05, 0, True),          # unsorted trick images
+    (2, [3, 0, 2, 0, 1], 0.0, 0, False),                 # tiny, empty levels
 ])
 def test_batched_nms_grouped_sorted(dev, G, runs, dead, ties, shuffle):
     """The sort-free grouped NMS on presorted candidates == the general grouped NMS (two radix sorts)
@@ -264,6 +265,20 @@ def test_batched_nms_grouped_sorted(dev, G, runs, dead, ties, shuffle):
         assert valid[g].sum() == min(c, 1500) and valid[g][:min(c, 1500)].all()
         assert np.array_equal(sel[g][:min(c, 1500)], got[o:o + min(c, 1500)])
         o += c
+
+
+def test_batched_nms_grouped_sorted_layout_violation(dev):
+    """Levels not contiguous within an image (outside the presorted contract): num_keep = -2 and an
+    empty selection -- reported, never an out-of-range index."""
+    from mx_det import ops
+    rng = np.random.default_rng(3)
+    b, s, lv, gr = _presorted(rng, 2, [300, 300, 300], 0.0, 0)
+    lv = lv.copy()
+    lv[:600] = np.tile([0, 1], 300)  # image 0's first two runs interleaved
+    t = [torch.from_numpy(a).to(dev) for a in (b, s, lv, gr)]
+    k, nk, sel, valid = ops.batched_nms_grouped_sorted(*t, 2, 3, 0.7, 2000, post=100)
+    assert int(nk.item()) == -2 and not valid.any()
+    assert int(k.min()) >= 0 and int(k.max()) < len(s)
 
 
 def test_batched_nms_grouped_sorted_empty(dev):
