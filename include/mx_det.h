@@ -99,7 +99,7 @@ int mx_batched_nms_grouped(const float* boxes, const float* scores, const int64_
 /* Presorted form of mx_batched_nms_grouped, same result (bit-identical keep[0:num_keep]) in 4
  * launches instead of ~20 (no radix sorts): meant for filter_proposals' candidates, whose live entries
  * come image-major, level-major, and score-descending within each (image, level) run (the per-level
- * top-k order; a run found out of order is still ranked exactly, by counting). n <= 32768, G <= 64,
+ * top-k order; a run found out of order is still ranked exactly, by counting). n <= 24576, G <= 64,
  * L <= 8. keep[num_keep:n] is filled with 0. post > 0: also sel [G, post] int64 = per image the first
  * post survivors (0 past the image's count) and valid [G, post] uint8 -- filter_proposals' padded
  * selection. Workspace from mx_nms_grouped_workspace(n, G, max_seg). Replaces the per-image
@@ -146,6 +146,10 @@ int mx_roi_bwd_set_strip(int sw);
 /* forward: channel slices per RoI (1, 2, 4 (default) or 8 when C / 8 divides): more, shorter blocks.
  * A process setting, results identical. */
 int mx_roi_fwd_set_split(int n);
+/* forward kernel: 1 (default) = one wave per bin row with whole-pixel (C = 256) loads and column reuse
+ * where it applies (C == 256, sampling_ratio 2, pooled width <= 8, height <= 16), else and 0 = the
+ * per-RoI v8 kernel. A process setting; results bit-identical. */
+int mx_roi_fwd_set_variant(int v);
 int mx_roi_align_fwd(const void* feat, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, const float* rois,
                      int64_t K, float spatial_scale, int PH, int PW, int sampling, int aligned, void* out,
                      mx_stream_t stream);

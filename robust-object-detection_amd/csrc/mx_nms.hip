@@ -552,7 +552,7 @@ __global__ void nms_group_out_kernel(const uint64_t* __restrict__ skeys, const i
 // is checked in LDS, and a run found out of order (e.g. a non-monotone sigmoid at ulp level) is ranked
 // by counting instead of binary search -- the result is always the stable (segment, score desc,
 // index) order of mx_batched_nms_grouped.
-static constexpr int PS_T = 1024, PS_NMAX = 32768, PS_GMAX = 64, PS_LMAX = 8, PS_CH = PS_NMAX / PS_T;
+static constexpr int PS_T = 1024, PS_NMAX = 24576, PS_GMAX = 64, PS_LMAX = 8, PS_CH = PS_NMAX / PS_T;
 
 // wave-aggregated counters: cnt[key] += #lanes with that key, mx[key / L] = max(m) (key < 0: none);
 // LDS or global (agent-scope atomics) alike
@@ -669,30 +669,63 @@ __global__ void __launch_bounds__(256) nms_sorted_post_stats_kernel(const int64_
   ps_wave_add(k, 0u, threadIdx.x & 63, tab2, nullptr, L);
 }
 
-// the block's image entries in list order: thread t owns [t*ch, t*ch + ch); returns the compacted
-// index of its first selected entry; sel = selected bits of its chunk
-__device__ __forceinline__ int ps_compact_chunks(const int32_t* __restrict__ group, const int32_t* __restrict__ flags,
-                                                 int n, int g, int ch, int tid, int lane, int wave, int* wsum,
-                                                 uint32_t* sel_bits, int* total) {
+// The block's image entries in list order: thread t owns [t*ch, t*ch + ch) (ch a multiple of 4, so
+// its group / flag / score words come as 16-B loads, all in flight at once). Entries of group g (and,
+// with flags, flagged) are compacted in list order: key[q] = ord_f32(score), idx[q] = list index.
+// Returns the block's count.
+__device__ __forceinline__ int ps_compact(const int32_t* __restrict__ group, const int32_t* __restrict__ flags,
+                                          const float* __restrict__ scores, int n, int g, int ch, int tid, int lane,
+                                          int wave, int* wsum, uint32_t* key, uint16_t* idx) {
   const int b0 = tid * ch;
   int gv[PS_CH], fv[PS_CH];
+  float sv[PS_CH];
 #pragma unroll
-  for (int u = 0; u < PS_CH; ++u) {
-    const int i = b0 + u;
-    const bool in = u < ch && i < n;
-    gv[u] = in ? group[i] : -1;
-    fv[u] = (in && flags) ? flags[i] : 1;
+  for (int v = 0; v < PS_CH / 4; ++v) {
+    const int i = b0 + 4 * v;
+    if (4 * v < ch && i + 3 < n) {
+      const int4 a = *(const int4*)(group + i);
+      gv[4 * v] = a.x; gv[4 * v + 1] = a.y; gv[4 * v + 2] = a.z; gv[4 * v + 3] = a.w;
+      const float4 b = *(const float4*)(scores + i);
+      sv[4 * v] = b.x; sv[4 * v + 1] = b.y; sv[4 * v + 2] = b.z; sv[4 * v + 3] = b.w;
+      if (flags) {
+        const int4 c = *(const int4*)(flags + i);
+        fv[4 * v] = c.x; fv[4 * v + 1] = c.y; fv[4 * v + 2] = c.z; fv[4 * v + 3] = c.w;
+      } else {
+        fv[4 * v] = fv[4 * v + 1] = fv[4 * v + 2] = fv[4 * v + 3] = 1;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bool in = 4 * v + t < ch && i + t < n;
+        gv[4 * v + t] = in ? group[i + t] : -1;
+        sv[4 * v + t] = in ? scores[i + t] : 0.f;
+        fv[4 * v + t] = (in && flags) ? flags[i + t] : 1;
+      }
+    }
   }
-  uint32_t bits = 0;
   int own = 0;
 #pragma unroll
+  for (int u = 0; u < PS_CH; ++u) own += (gv[u] == g && fv[u] != 0) ? 1 : 0;
+  int tot;
+  int q = ps_excl_scan(own, lane, wave, wsum, &tot);
+#pragma unroll
   for (int u = 0; u < PS_CH; ++u) {
-    const bool m = gv[u] == g && fv[u] != 0;
-    bits |= m ? (1u << u) : 0u;
-    own += m ? 1 : 0;
+    if (gv[u] == g && fv[u] != 0) {
+      key[q] = ord_f32(sv[u]);
+      idx[q] = (uint16_t)(b0 + u);
+      ++q;
+    }
   }
-  *sel_bits = bits;
-  return ps_excl_scan(own, lane, wave, wsum, total);
+  return tot;
+}
+
+// run-order check of the compacted keys: bit l of the result = run l out of order (non-increasing
+// expected); LDS only
+__device__ __forceinline__ void ps_check_runs(const uint32_t* key, const int* rs, int L, int cnt, int tid, uint32_t* bad) {
+  for (int q = tid + 1; q < cnt; q += PS_T) {
+    const int l = ps_run_of(rs, L, q);
+    if (q > rs[l] && key[q] > key[q - 1]) atomicOr(bad, 1u << l);
+  }
 }
 
 // one workgroup per image g: segment layout (positions, segment ids, offset boxes) for the mask /
@@ -701,9 +734,9 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
     const float4* __restrict__ boxes, const float* __restrict__ scores, const int64_t* __restrict__ lvl,
     const int32_t* __restrict__ group, int n, int G, int L, const uint32_t* __restrict__ tab, uint32_t* __restrict__ tab2,
     float4* __restrict__ sbox, float* __restrict__ sarea, int32_t* __restrict__ v1, int32_t* __restrict__ incl,
-    int32_t* __restrict__ seg_start, int32_t* __restrict__ nseg_out, int32_t* __restrict__ scratch,
-    int32_t* __restrict__ err) {
-  extern __shared__ uint32_t key[];  // [n] score keys of this image's live entries, list order
+    int32_t* __restrict__ seg_start, int32_t* __restrict__ nseg_out, int32_t* __restrict__ err) {
+  extern __shared__ uint32_t key[];  // [n] score keys of this image's live entries, list order; then [n] u16 indices
+  uint16_t* idx = (uint16_t*)(key + n);
   __shared__ uint32_t bad;
   __shared__ int wsum[PS_T / 64], rs[PS_LMAX + 1], runseg[PS_LMAX];
   __shared__ int s_gbase, s_segbase, s_gcnt, s_trick, s_nlive, s_nseg;
@@ -741,67 +774,70 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
     s_nseg = ns;
   }
   __syncthreads();
-  const int gbase = s_gbase, gc = s_gcnt, trick = s_trick, nlive = s_nlive, nseg = s_nseg;
+  const int gbase = s_gbase, gc = s_gcnt, trick = s_trick, nlive = s_nlive, nseg = s_nseg, segbase = s_segbase;
   // segment starts: one per non-empty level run, or one for a coordinate-trick image
   if (trick) {
-    if (tid == 0 && gc > 0) seg_start[s_segbase] = gbase;
+    if (tid == 0 && gc > 0) seg_start[segbase] = gbase;
   } else if (tid < L && tab[g * L + tid]) {
-    seg_start[s_segbase + runseg[tid]] = gbase + rs[tid];
+    seg_start[segbase + runseg[tid]] = gbase + rs[tid];
   }
   if (g == G - 1 && tid == 0) {
     *nseg_out = nseg;
     seg_start[nseg] = nlive;
     if (nlive < n) seg_start[nseg + 1] = nlive;  // the tail's empty pseudo-segment
   }
-  // this image's live entries in list order -> keys in LDS, list index in scratch
-  const int ch = (n + PS_T - 1) / PS_T;
-  uint32_t bits;
-  int tot;
-  int q = ps_compact_chunks(group, nullptr, n, g, ch, tid, lane, wave, wsum, &bits, &tot);
-  for (int u = 0; bits; ++u, bits >>= 1) {
-    if (!(bits & 1u)) continue;
-    const int i = tid * ch + u;
-    key[q] = ord_f32(scores[i]);
-    scratch[gbase + q] = i;
-    if ((int)lvl[i] != ps_run_of(rs, L, q) || q >= gc) atomicOr(&bad, 0x80000000u);  // layout contract
-    ++q;
-  }
+  const int ch = ((n + PS_T - 1) / PS_T + 3) & ~3;
+  ps_compact(group, nullptr, scores, n, g, ch, tid, lane, wave, wsum, key, idx);
   __syncthreads();
-  // every run's key order checked (presorted input: non-increasing within a run)
-  for (int q2 = tid + 1; q2 < gc; q2 += PS_T) {
-    const int l = ps_run_of(rs, L, q2);
-    if (q2 > rs[l] && key[q2] > key[q2 - 1]) atomicOr(&bad, 1u << l);
-  }
+  ps_check_runs(key, rs, L, gc, tid, &bad);
   __syncthreads();
-  uint32_t badm = bad;
-  if (badm & 0x80000000u) {
-    // not image-major / level-major: reported (num_keep = -2); every run is then ranked by counting,
-    // so the positions stay a permutation and every later index stays in range
-    if (tid == 0) atomicExch(err, 1);
-    badm = 0xffffffffu;
-  }
+  const uint32_t badm = bad;
   const float step = unord_f32(tab[G * L + g]) + 1.0f;
-  for (int q2 = tid; q2 < gc; q2 += PS_T) {
-    const int l = ps_run_of(rs, L, q2);
-    const uint32_t x = key[q2];
-    int rank;
-    if (trick) {  // one segment: the merge of the level runs
-      rank = 0;
-      for (int l2 = 0; l2 < L; ++l2) rank += ps_before(key, rs[l2], rs[l2 + 1], x, q2, (badm >> l2) & 1u);
-    } else {
-      rank = rs[l] + ps_before(key, rs[l], rs[l + 1], x, q2, (badm >> l) & 1u);
+  // positions, 8 entries per thread per round: ranks from LDS, then all 8 gathers in flight
+  for (int q0 = 0; q0 < gc; q0 += 8 * PS_T) {
+    int pos[8], ii[8], ll[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int q = q0 + e * PS_T + tid;
+      pos[e] = -1;
+      ii[e] = 0;
+      ll[e] = 0;
+      if (q < gc) {
+        const int l = ps_run_of(rs, L, q);
+        const uint32_t x = key[q];
+        int rank;
+        if (trick) {  // one segment: the merge of the level runs
+          rank = 0;
+          for (int l2 = 0; l2 < L; ++l2) rank += ps_before(key, rs[l2], rs[l2 + 1], x, q, (badm >> l2) & 1u);
+        } else {
+          rank = rs[l] + ps_before(key, rs[l], rs[l + 1], x, q, (badm >> l) & 1u);
+        }
+        pos[e] = gbase + rank;
+        ii[e] = idx[q];
+        ll[e] = l;
+      }
     }
-    const int pos = gbase + rank;
-    const int i = scratch[gbase + q2];
-    float4 b = boxes[i];
-    if (trick) {  // boxes + idxs * (max_coordinate + 1), as nms_group_keys_kernel
-      const float off = (float)lvl[i] * step;
-      b.x = b.x + off; b.y = b.y + off; b.z = b.z + off; b.w = b.w + off;
+    float4 b[8];
+    int lvv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      b[e] = boxes[ii[e]];
+      lvv[e] = (int)lvl[ii[e]];
     }
-    sbox[pos] = b;
-    sarea[pos] = (b.z - b.x) * (b.w - b.y);
-    v1[pos] = i;
-    incl[pos] = s_segbase + runseg[l] + 1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (pos[e] < 0) continue;
+      if (lvv[e] != ll[e]) atomicExch(err, 1);  // layout contract: levels contiguous in list order
+      float4 bb = b[e];
+      if (trick) {  // boxes + idxs * (max_coordinate + 1), as nms_group_keys_kernel
+        const float off = (float)lvv[e] * step;
+        bb.x = bb.x + off; bb.y = bb.y + off; bb.z = bb.z + off; bb.w = bb.w + off;
+      }
+      sbox[pos[e]] = bb;
+      sarea[pos[e]] = (bb.z - bb.x) * (bb.w - bb.y);
+      v1[pos[e]] = ii[e];
+      incl[pos[e]] = segbase + runseg[ll[e]] + 1;
+    }
   }
   for (int p = nlive + g * PS_T + tid; p < n; p += G * PS_T) incl[p] = nseg + 1;  // empty pseudo-segment
 }
@@ -811,9 +847,10 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
 __global__ void __launch_bounds__(PS_T) nms_sorted_post_kernel(
     const float* __restrict__ scores, const int32_t* __restrict__ group, const int32_t* __restrict__ flags, int n, int G,
     int L, const uint32_t* __restrict__ tab2, const int32_t* __restrict__ nk32, const int32_t* __restrict__ err,
-    int32_t* __restrict__ scratch, int64_t* __restrict__ keep, int64_t* __restrict__ num_keep, int post,
-    int64_t* __restrict__ sel, uint8_t* __restrict__ valid) {
+    int64_t* __restrict__ keep, int64_t* __restrict__ num_keep, int post, int64_t* __restrict__ sel,
+    uint8_t* __restrict__ valid) {
   extern __shared__ uint32_t key[];
+  uint16_t* idx = (uint16_t*)(key + n);
   __shared__ uint32_t bad;
   __shared__ int wsum[PS_T / 64], rs[PS_LMAX + 1];
   __shared__ int s_sbase, s_sc, s_total;
@@ -841,29 +878,17 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_post_kernel(
   __syncthreads();
   const int sbase = s_sbase, sc = s_sc, total = s_total;
   const bool failed = *err != 0;
-  const int ch = (n + PS_T - 1) / PS_T;
-  uint32_t bits;
-  int tot;
-  int q = ps_compact_chunks(group, flags, n, g, ch, tid, lane, wave, wsum, &bits, &tot);
-  for (int u = 0; bits; ++u, bits >>= 1) {
-    if (!(bits & 1u)) continue;
-    const int i = tid * ch + u;
-    key[q] = ord_f32(scores[i]);
-    scratch[sbase + q] = i;
-    ++q;
-  }
+  const int ch = ((n + PS_T - 1) / PS_T + 3) & ~3;
+  ps_compact(group, flags, scores, n, g, ch, tid, lane, wave, wsum, key, idx);
   __syncthreads();
-  for (int q2 = tid + 1; q2 < sc; q2 += PS_T) {
-    const int l = ps_run_of(rs, L, q2);
-    if (q2 > rs[l] && key[q2] > key[q2 - 1]) atomicOr(&bad, 1u << l);
-  }
+  ps_check_runs(key, rs, L, sc, tid, &bad);
   __syncthreads();
   const uint32_t badm = bad;
-  for (int q2 = tid; q2 < sc; q2 += PS_T) {
-    const uint32_t x = key[q2];
+  for (int q = tid; q < sc; q += PS_T) {
+    const uint32_t x = key[q];
     int rank = 0;
-    for (int l2 = 0; l2 < L; ++l2) rank += ps_before(key, rs[l2], rs[l2 + 1], x, q2, (badm >> l2) & 1u);
-    keep[sbase + rank] = scratch[sbase + q2];
+    for (int l2 = 0; l2 < L; ++l2) rank += ps_before(key, rs[l2], rs[l2 + 1], x, q, (badm >> l2) & 1u);
+    keep[sbase + rank] = idx[q];
   }
   // -1: a segment exceeded max_seg (the scan's overflow flag); -2: the presorted layout contract broken
   if (g == 0 && tid == 0) *num_keep = failed ? -2 : (*nk32 < 0 ? -1 : total);
@@ -1028,9 +1053,9 @@ extern "C" int mx_batched_nms_grouped_sorted(const float* boxes, const float* sc
   const int nb = (int)cdiv(n, 256);
   nms_sorted_stats_kernel<<<nb, 256, 0, s>>>((const float4*)boxes, lvl, group, (int)n, (int)G, (int)L, tab, w.flags, w.nk);
   MX_LAUNCH_CHECK();
-  const size_t lds = sizeof(uint32_t) * (size_t)n;
+  const size_t lds = (sizeof(uint32_t) + sizeof(uint16_t)) * (size_t)n + 16;
   nms_sorted_pre_kernel<<<(int)G, PS_T, lds, s>>>((const float4*)boxes, scores, lvl, group, (int)n, (int)G, (int)L, tab,
-                                                  tab2, w.sbox, w.sarea, w.v1, w.incl, w.seg_start, w.nseg, w.v0, err);
+                                                  tab2, w.sbox, w.sarea, w.v1, w.incl, w.seg_start, w.nseg, err);
   MX_LAUNCH_CHECK();
   dim3 mg((unsigned)cdiv(n, 64), (unsigned)Wm);
   nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask);
@@ -1047,7 +1072,7 @@ extern "C" int mx_batched_nms_grouped_sorted(const float* boxes, const float* sc
   MX_LAUNCH_CHECK();
   nms_sorted_post_stats_kernel<<<nb, 256, 0, s>>>(lvl, group, w.flags, (int)n, (int)G, (int)L, tab2);
   MX_LAUNCH_CHECK();
-  nms_sorted_post_kernel<<<(int)G, PS_T, lds, s>>>(scores, group, w.flags, (int)n, (int)G, (int)L, tab2, w.nk, err, w.v0,
+  nms_sorted_post_kernel<<<(int)G, PS_T, lds, s>>>(scores, group, w.flags, (int)n, (int)G, (int)L, tab2, w.nk, err,
                                                    keep, num_keep, (int)post, post > 0 ? sel : nullptr,
                                                    post > 0 ? valid : nullptr);
   MX_LAUNCH_CHECK();

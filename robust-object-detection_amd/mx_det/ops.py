@@ -191,7 +191,7 @@ def batched_nms_grouped(boxes, scores, lvl, group, G, L, iou_threshold, max_seg)
     return keep, nk
 
 
-SORTED_NMS_MAX = (32768, 64, 8)  # n, G, L bounds of mx_batched_nms_grouped_sorted
+SORTED_NMS_MAX = (24576, 64, 8)  # n, G, L bounds of mx_batched_nms_grouped_sorted
 
 
 def batched_nms_grouped_sorted(boxes, scores, lvl, group, G, L, iou_threshold, max_seg, post=0):

@@ -27,6 +27,14 @@ for s in "$@"; do
         --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 4 --warmup 2 --precision f32 \
         --no-roofline > "$OUT/rehearse.log" 2>&1 || { echo "rehearse failed"; tail -30 "$OUT/rehearse.log"; exit 1; }
       tail -1 "$OUT/rehearse.log" ;;
+    hbm)
+      timeout -k 10 300 python -u bench.py --precision f32 --no-augment-variant --no-eval-variant --no-cpu-baseline \
+        --steps 10 --warmup 3 > "$OUT/hbm.log" 2>&1 || { echo "hbm bench failed"; tail -30 "$OUT/hbm.log"; exit 1; }
+      tail -1 "$OUT/hbm.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], json.dumps(d.get('hbm_ops')))" ;;
+    script)
+      timeout -k 10 400 python -u bench.py --mode script --steps 20 --warmup 5 > "$OUT/script.log" 2>&1 \
+        || { echo "script bench failed"; tail -30 "$OUT/script.log"; exit 1; }
+      tail -1 "$OUT/script.log" ;;
     bench)
       timeout -k 10 400 python -u bench.py > "$OUT/bench.log" 2>&1 \
         || { echo "bench failed"; tail -30 "$OUT/bench.log"; exit 1; }
