@@ -146,10 +146,6 @@ int mx_roi_bwd_set_strip(int sw);
 /* forward: channel slices per RoI (1, 2, 4 (default) or 8 when C / 8 divides): more, shorter blocks.
  * A process setting, results identical. */
 int mx_roi_fwd_set_split(int n);
-/* forward kernel: 1 (default) = one wave per bin row with whole-pixel (C = 256) loads and column reuse
- * where it applies (C == 256, sampling_ratio 2, pooled width <= 8, height <= 16), else and 0 = the
- * per-RoI v8 kernel. A process setting; results bit-identical. */
-int mx_roi_fwd_set_variant(int v);
 int mx_roi_align_fwd(const void* feat, int dtype, int64_t N, int64_t H, int64_t W, int64_t C, const float* rois,
                      int64_t K, float spatial_scale, int PH, int PW, int sampling, int aligned, void* out,
                      mx_stream_t stream);

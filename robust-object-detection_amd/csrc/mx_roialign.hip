@@ -284,162 +284,6 @@ __global__ void __launch_bounds__(256) roi_align_fwd_v8_kernel(Levels L, int64_t
   }
 }
 
-// ---- row forward: one wave per bin row, all C = 256 channels per pixel load ----------------------
-// Block = one RoI, wave = one bin row (PH waves), lane = 4 channels: every corner read is one pixel's
-// whole 256-channel row (1 KiB f32, fully coalesced) and every output bin one 1 KiB store. A bin row's
-// samples share their pixel rows (2 sample rows -> <= 4 distinct pixel rows, loaded once per column)
-// and consecutive sample columns share pixel columns (xh of one = xl of the next whenever samples are
-// >= 1 px apart; the same pair when closer): the wave walks its 2*PW sample columns left to right
-// keeping the current column pair of the distinct rows in registers, so each distinct pixel of the
-// bin row is read ~once instead of once per (sample, corner) -- for the small P2 RoIs of a VisDrone
-// step ~3x fewer loads. Per output element the arithmetic is roi_align_fwd_kernel's, op for op:
-// v = 0; v += ((w1 f1 + w2 f2) + w3 f3) + w4 f4 per valid sample in (iy, ix) order; v / count
-// (sample_corners' coordinates, clamps and weights restated per axis with the same float ops).
-// sampling_ratio 2, C == 256, PW <= 8, PH <= 16.
-template <typename T>
-struct Px4;
-template <>
-struct Px4<float> {
-  static __device__ __forceinline__ float4 ld(const float* p) { return *(const float4*)p; }
-  static __device__ __forceinline__ void st(float* p, float4 v) { *(float4*)p = v; }
-};
-template <>
-struct Px4<uint16_t> {
-  static __device__ __forceinline__ float4 ld(const uint16_t* p) {
-    const uint2 u = *(const uint2*)p;
-    return make_float4(bf2f((uint16_t)(u.x & 0xffff)), bf2f((uint16_t)(u.x >> 16)), bf2f((uint16_t)(u.y & 0xffff)),
-                       bf2f((uint16_t)(u.y >> 16)));
-  }
-  static __device__ __forceinline__ void st(uint16_t* p, float4 v) {
-    uint2 u;
-    u.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
-    u.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
-    *(uint2*)p = u;
-  }
-};
-
-// one axis of sample_corners: coordinate t in [-1, n] -> (lo, hi, l, h); false outside
-__device__ __forceinline__ bool axis_corners(float t, int64_t n, int& lo, int& hi, float& l, float& h) {
-  if (t < -1.0f || t > (float)n) return false;
-  if (t <= 0) t = 0;
-  lo = (int)t;
-  if (lo >= n - 1) { hi = lo = (int)n - 1; t = (float)lo; } else hi = lo + 1;
-  l = t - (float)lo;
-  h = 1.f - l;
-  return true;
-}
-
-__device__ __forceinline__ float4 samp4(float w1, float w2, float w3, float w4, float4 a, float4 b, float4 c, float4 d) {
-  return make_float4(((w1 * a.x + w2 * b.x) + w3 * c.x) + w4 * d.x, ((w1 * a.y + w2 * b.y) + w3 * c.y) + w4 * d.y,
-                     ((w1 * a.z + w2 * b.z) + w3 * c.z) + w4 * d.z, ((w1 * a.w + w2 * b.w) + w3 * c.w) + w4 * d.w);
-}
-
-__device__ __forceinline__ void acc4(float4& v, float4 s) {
-  v.x += s.x; v.y += s.y; v.z += s.z; v.w += s.w;
-}
-
-// register slot s (0..3, wave-uniform) of a 4-entry float4 set
-__device__ __forceinline__ float4 pick4(const float4 (&r)[4], int s) {
-  return s == 0 ? r[0] : (s == 1 ? r[1] : (s == 2 ? r[2] : r[3]));
-}
-
-template <typename T>
-__global__ void __launch_bounds__(1024) roi_align_fwd_row_kernel(Levels L, const float* __restrict__ rois, int PH, int PW,
-                                                                 int aligned, int multiscale, T* __restrict__ out,
-                                                                 int32_t* __restrict__ lv_out) {
-  constexpr int C = 256;
-  const int64_t k = blockIdx.x;
-  const int ph = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const float* r = rois + 5 * k;
-  const int lv = multiscale ? level_of(r, L.k_min, L.n) : 0;
-  if (threadIdx.x == 0 && lv_out) lv_out[k] = lv;
-  const RoiGeo g = roi_geo(r, L.scale[lv], PH, PW, 2, aligned);
-  const int64_t H = L.H[lv], W = L.W[lv];
-  const T* f = (const T*)L.f[lv] + g.b * H * W * C + 4 * lane;
-  // the bin row's two sample rows (sample_corners' y arithmetic)
-  int yl[2], yh[2];
-  float ly[2], hy[2];
-  bool yok[2];
-#pragma unroll
-  for (int iy = 0; iy < 2; ++iy) {
-    const float y = (g.sh + (float)ph * g.bh) + ((float)iy + .5f) * g.bh / (float)g.gh;
-    yok[iy] = axis_corners(y, H, yl[iy], yh[iy], ly[iy], hy[iy]);
-    if (!yok[iy]) { yl[iy] = yh[iy] = 0; ly[iy] = hy[iy] = 0.f; }
-  }
-  // distinct pixel rows: slot of each (iy, corner); rows[] = their pixel rows
-  int rows[4], nrow = 0, sl[2], sh_[2];
-  {
-    const int cand[4] = {yl[0], yh[0], yl[1], yh[1]};
-    int slot[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      int f_ = -1;
-      for (int u = 0; u < nrow; ++u)
-        if (rows[u] == cand[q]) f_ = u;
-      if (f_ < 0) {
-        rows[nrow] = cand[q];
-        f_ = nrow++;
-      }
-      slot[q] = f_;
-    }
-    sl[0] = slot[0]; sh_[0] = slot[1]; sl[1] = slot[2]; sh_[1] = slot[3];
-  }
-  float4 vl[4], vh[4];  // current column pair (xl, xh) at the distinct rows
-  int cur_xl = -1, cur_xh = -1;
-  float4 s00 = make_float4(0.f, 0.f, 0.f, 0.f), s10 = s00;
-  bool ok00 = false, ok10 = false;
-  for (int j = 0; j < 2 * PW; ++j) {
-    const int pw = j >> 1, ix = j & 1;
-    const float x = (g.sw + (float)pw * g.bw) + ((float)ix + .5f) * g.bw / (float)g.gw;
-    int xl = 0, xh = 0;
-    float lx = 0.f, hx = 0.f;
-    const bool xok = axis_corners(x, W, xl, xh, lx, hx);
-    const bool any = xok && (yok[0] || yok[1]);
-    if (any && !(xl == cur_xl && xh == cur_xh)) {
-      if (xl == cur_xh) {  // slide: the old right column is the new left one
-#pragma unroll
-        for (int u = 0; u < 4; ++u) vl[u] = vh[u];
-      } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (u < nrow) vl[u] = Px4<T>::ld(f + ((int64_t)rows[u] * W + xl) * C);
-      }
-      if (xh == xl) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) vh[u] = vl[u];
-      } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (u < nrow) vh[u] = Px4<T>::ld(f + ((int64_t)rows[u] * W + xh) * C);
-      }
-      cur_xl = xl;
-      cur_xh = xh;
-    }
-    float4 sv[2];
-    bool okv[2];
-#pragma unroll
-    for (int iy = 0; iy < 2; ++iy) {
-      okv[iy] = xok && yok[iy];
-      const float w1 = hy[iy] * hx, w2 = hy[iy] * lx, w3 = ly[iy] * hx, w4 = ly[iy] * lx;
-      sv[iy] = okv[iy] ? samp4(w1, w2, w3, w4, pick4(vl, sl[iy]), pick4(vh, sl[iy]), pick4(vl, sh_[iy]),
-                               pick4(vh, sh_[iy]))
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if (ix == 0) {
-      s00 = sv[0]; ok00 = okv[0];
-      s10 = sv[1]; ok10 = okv[1];
-    } else {  // bin (ph, pw) complete: the samples in (iy, ix) order, as the scalar kernel adds them
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok00) acc4(v, s00);
-      if (okv[0]) acc4(v, sv[0]);
-      if (ok10) acc4(v, s10);
-      if (okv[1]) acc4(v, sv[1]);
-      v.x = v.x / g.count; v.y = v.y / g.count; v.z = v.z / g.count; v.w = v.w / g.count;
-      Px4<T>::st(out + ((k * PH + ph) * PW + pw) * C + 4 * lane, v);
-    }
-  }
-}
-
 // ---- deterministic backward (gather form, no atomics) ---------------------------------------------
 // grad_feat[n, y, x, :] = sum over the RoIs k of image n at this level, their bins and the bilinear
 // corners landing on (y, x) of gout[k, bin, :] / count * w. Pass 1 (one block per RoI) merges each
@@ -796,13 +640,6 @@ using namespace mx;
 // forward: channel slices per RoI block (mx_roi_fwd_set_split: 1, 2, 4 or 8; 4 measured 65 vs 76 us cold on the
 // step's 1,024 RoIs: four 64-channel blocks per RoI keep more gathers in flight per CU)
 static int g_roi_fwd_split = 4;
-// forward variant: 1 = the row kernel where it applies (C 256, sampling 2, PW <= 8, PH <= 16), 0 = v8
-static int g_roi_fwd_variant = 1;
-extern "C" int mx_roi_fwd_set_variant(int v) {
-  MX_CHECK_ARG(v == 0 || v == 1, "mx_roi_fwd_set_variant: 0 (v8) or 1 (row kernel)");
-  g_roi_fwd_variant = v;
-  return MX_OK;
-}
 extern "C" int mx_roi_fwd_set_split(int n) {
   MX_CHECK_ARG(n == 1 || n == 2 || n == 4 || n == 8, "mx_roi_fwd_set_split: 1, 2, 4 or 8");
   g_roi_fwd_split = n;
@@ -820,14 +657,6 @@ static int launch_fwd(const Levels& L, int dtype, int64_t C, const float* rois, 
     else
       roi_align_fwd_adaptive_kernel<uint16_t><<<(unsigned)K, 256, 0, s>>>(L, C, rois, PH, PW, aligned, ms,
                                                                           (uint16_t*)out, lv);
-    MX_LAUNCH_CHECK();
-    return MX_OK;
-  }
-  if (g_roi_fwd_variant == 1 && C == 256 && sampling == 2 && PW <= 8 && PH <= 16) {
-    if (dtype == MX_F32)
-      roi_align_fwd_row_kernel<float><<<(unsigned)K, 64 * PH, 0, s>>>(L, rois, PH, PW, aligned, ms, (float*)out, lv);
-    else
-      roi_align_fwd_row_kernel<uint16_t><<<(unsigned)K, 64 * PH, 0, s>>>(L, rois, PH, PW, aligned, ms, (uint16_t*)out, lv);
     MX_LAUNCH_CHECK();
     return MX_OK;
   }

@@ -65,7 +65,6 @@ _SIGS = {
     "mx_roi_align_bwd_workspace": (c_sz, [c_i64, c_int, c_int, c_int]),
     "mx_roi_bwd_set_strip": (c_int, [c_int]),
     "mx_roi_fwd_set_split": (c_int, [c_int]),
-    "mx_roi_fwd_set_variant": (c_int, [c_int]),
     "mx_multiscale_roi_align_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_i64, c_vp, c_i64, c_int,
                                             c_int, c_int, c_vp, c_vp, c_vp]),
     "mx_multiscale_roi_align_bwd": (c_int, [c_vp, c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp,

@@ -387,20 +387,54 @@ class PrefetchJpegLoader:
 
         th = threading.Thread(target=produce, name="mx-prefetch", daemon=True)
         th.start()
-        try:
-            while True:
-                item = q.get()
-                if item is None:
-                    break
-                if isinstance(item, BaseException):
-                    raise item
-                futs, tgs = item
+        # device stage on a loader stream: batch i+1's coefficient / target copies and IDCT launches are
+        # issued before batch i is handed out (when its host decode has finished), so they run beside
+        # step i's kernels; the training stream waits on the batch's event
+        ls = torch.cuda.Stream(device=self.dev)
+
+        def stage(item):
+            futs, tgs = item
+            with torch.cuda.stream(ls):
                 imgs = []
                 for f in futs:
                     info, host = f.result()
                     imgs.append(torch.from_numpy(host).to(self.dev) if info is None
                                 else jpeg.device_stage(info, host, self.dev))
-                yield imgs, [{k: v.to(self.dev, non_blocking=True) for k, v in t.items()} for t in tgs]
+                tg = [{k: v.to(self.dev, non_blocking=True) for k, v in t.items()} for t in tgs]
+                ev = torch.cuda.Event()
+                ev.record(ls)
+            return imgs, tg, ev
+
+        def take(block):
+            """next queue item: a staged batch, None (end), or an exception; with block=False, the
+            string "later" when the next batch is not decoded yet."""
+            if not block:
+                try:
+                    item = q.get_nowait()
+                except queue.Empty:
+                    return "later"
+                if isinstance(item, tuple) and not all(f.done() for f in item[0]):
+                    pending.append(item)
+                    return "later"
+            else:
+                item = pending.pop() if pending else q.get()
+            return stage(item) if isinstance(item, tuple) else item
+
+        pending = []
+        try:
+            nxt = take(True)
+            while nxt is not None:
+                if isinstance(nxt, BaseException):
+                    raise nxt
+                imgs, tg, ev = nxt
+                nxt = take(False)  # stage the following batch now if it is ready
+                main = torch.cuda.current_stream(self.dev)
+                main.wait_event(ev)
+                for t in imgs + [v for d in tg for v in d.values()]:
+                    t.record_stream(main)
+                yield imgs, tg
+                if isinstance(nxt, str):
+                    nxt = take(True)
         finally:
             stop.set()
             sys.setswitchinterval(old_switch)

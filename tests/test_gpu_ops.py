@@ -469,50 +469,6 @@ def test_multiscale_roi_align(dev):
         np.testing.assert_allclose(ft[l].grad.permute(0, 3, 1, 2).cpu().numpy(), r, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_multiscale_roi_align_row_kernel(dev, dtype):
-    """The row-per-wave forward (C = 256, the FPN width: whole-pixel loads, deduplicated columns) on the
-    configs[1] level maps: bit-identical to the per-RoI v8 kernel (mx_roi_fwd_set_variant 0) and, in
-    f32, to the oracle -- incl. RoIs smaller than a pixel, partly outside, and at the right / bottom
-    edges (the clamp), 1,024 RoIs mostly small (VisDrone-like, on P2)."""
-    from mx_det import _lib, ops
-    rng = np.random.default_rng(12)
-    N, C = 2, 256
-    shapes = [(200, 336), (100, 168), (50, 84), (25, 42)]
-    scales = [0.25, 0.125, 0.0625, 0.03125]
-    feats = [rng.standard_normal((N, C, h, w)).astype(np.float32) for h, w in shapes]
-    boxes = np.concatenate([_rand_boxes(rng, 700, med=24), _rand_boxes(rng, 300, med=160)])
-    edge = np.array([[1300, 780, 1344, 800], [1330, 10, 1350, 40], [5, 790, 30, 805], [-20, -30, 5, 5],
-                     [3, 3, 3.2, 3.1], [600, 400, 600.4, 400.3], [1000, 100, 1344, 800], [0, 0, 1344, 800]] * 3,
-                    np.float32)
-    boxes = np.concatenate([boxes, edge]).astype(np.float32)
-    bi = rng.integers(0, N, len(boxes)).astype(np.float32)[:, None]
-    rois = np.concatenate([bi, boxes], 1)
-    ft = [torch.from_numpy(f).to(dev).permute(0, 2, 3, 1).contiguous() for f in feats]
-    if dtype == "bf16":
-        ft = [f.bfloat16() for f in ft]
-    rt = torch.from_numpy(rois).to(dev)
-    outs = []
-    try:
-        for v in (0, 1):
-            _lib.call("mx_roi_fwd_set_variant", v)
-            with torch.no_grad():
-                outs.append(ops.multiscale_roi_align(ft, rt, scales, 2))
-    finally:
-        _lib.call("mx_roi_fwd_set_variant", 1)
-    assert torch.equal(outs[0].view(torch.int16 if dtype == "bf16" else torch.int32),
-                       outs[1].view(torch.int16 if dtype == "bf16" else torch.int32))
-    if dtype == "f32":
-        lv = _level_mapper_np(boxes)
-        ref = np.zeros((len(rois), C, 7, 7), np.float32)
-        for l in range(4):
-            sel = np.where(lv == l)[0]
-            if len(sel):
-                ref[sel] = orc.roi_align(feats[l], rois[sel], scales[l], (7, 7), 2, False)
-        got = outs[1].permute(0, 3, 1, 2).cpu().numpy()
-        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-
-
 def test_box_decode(dev):
     from mx_det import ops
     rng = np.random.default_rng(11)
