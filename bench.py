@@ -624,7 +624,8 @@ def script_main(args, world, rank, dev, imgs, tg):
     cfg.update(EPOCHS=1, AUGMENT=True, TRAIN_IMG=tmp / "coco/images/train", VAL_IMG=tmp / "coco/images/val",
                TRAIN_ANN=tmp / "coco/annotations/instances_train.json",
                VAL_ANN=tmp / "coco/annotations/instances_val.json", OUT_DIR=tmp / f"out{rank}", WEIGHTS=None,
-               TRAINABLE_LAYERS=3, TIMER={"warmup": args.warmup})
+               TRAINABLE_LAYERS=3, TIMER={"warmup": args.warmup},
+               DECODE_THREADS=int(os.environ.get("MX_DECODE_THREADS", "4")))
     train_frcnn(cfg)
     dt = cfg["TIMER"]["t1"] - cfg["TIMER"]["t0"]
     steps = cfg["TIMER"]["steps"]
@@ -648,6 +649,8 @@ def script_main(args, world, rank, dev, imgs, tg):
     rec["bench_step"] = {"workload": "bench.py augmented step, images resident in HBM", "value":
                          round(2 * args.steps * world / dt2, 3), "ms_per_step": round(1000 * dt2 / args.steps, 3)}
     rec["script_over_bench_step"] = round(rec["value"] / rec["bench_step"]["value"], 4)
+    if "loader_wait_s" in cfg["TIMER"]:
+        rec["loader_wait_ms_per_step"] = round(1000 * cfg["TIMER"]["loader_wait_s"] / steps, 3)
     _barrier(world)
     if rank == 0:
         shutil.rmtree(tmp, ignore_errors=True)

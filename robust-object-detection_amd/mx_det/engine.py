@@ -180,6 +180,8 @@ def train_frcnn(cfg):
                               pin_memory=not device_jpeg)
     if device_jpeg:
         train_loader = PrefetchJpegLoader(train_loader, dev, workers=cfg.get("DECODE_THREADS", 4))
+        if cfg.get("TIMER") is not None:
+            cfg["TIMER"]["loader"] = train_loader
     val_sampler = ShardSampler(len(val_ds), world, rank) if world > 1 else None
     val_loader = DataLoader(val_ds, batch_size=1, shuffle=False, sampler=val_sampler,
                             num_workers=cfg.get("NUM_WORKERS", 0), collate_fn=collate_fn,
@@ -237,6 +239,8 @@ def train_frcnn(cfg):
                 if world > 1:
                     dist.barrier()
                 timer["t0"] = time.perf_counter()
+                if "loader" in timer:
+                    timer["wait0"] = timer["loader"].wait_s
             if rank == 0 and ((i + 1) % 100 == 0 or (i + 1) == n_batches):
                 print(f"  [Epoch {epoch:03d}] batch {i + 1}/{n_batches}", flush=True)
         sched.step()
@@ -255,6 +259,8 @@ def train_frcnn(cfg):
         if world > 1:
             dist.barrier()
         timer["t1"], timer["steps"] = time.perf_counter(), it_global - timer["warmup"]
+        if "loader" in timer:
+            timer["loader_wait_s"] = timer["loader"].wait_s - timer.get("wait0", 0.0)
     if rank == 0:
         print("\nEvaluating on clean val set (final)...", flush=True)
     metrics = evaluate(model, val_loader, str(cfg["VAL_ANN"]), dev)
@@ -346,6 +352,7 @@ class PrefetchJpegLoader:
 
     def __init__(self, loader, dev, workers=4, depth=2):
         self.loader, self.dev, self.workers, self.depth = loader, dev, int(workers), int(depth)
+        self.wait_s = 0.0  # time the consuming thread spent waiting for host data (bench.py --mode script)
 
     def __len__(self):
         return len(self.loader)
@@ -397,7 +404,9 @@ class PrefetchJpegLoader:
             with torch.cuda.stream(ls):
                 imgs = []
                 for f in futs:
+                    t0 = time.perf_counter()
                     info, host = f.result()
+                    self.wait_s += time.perf_counter() - t0
                     imgs.append(torch.from_numpy(host).to(self.dev) if info is None
                                 else jpeg.device_stage(info, host, self.dev))
                 tg = [{k: v.to(self.dev, non_blocking=True) for k, v in t.items()} for t in tgs]
@@ -417,7 +426,9 @@ class PrefetchJpegLoader:
                     pending.append(item)
                     return "later"
             else:
+                t0 = time.perf_counter()
                 item = pending.pop() if pending else q.get()
+                self.wait_s += time.perf_counter() - t0
             return stage(item) if isinstance(item, tuple) else item
 
         pending = []
