@@ -66,13 +66,15 @@ def make_optimizer(model):
     return SGD(params, lr=0.005, momentum=0.9, weight_decay=0.0005)
 
 
-def train_step(model, opt, images, targets, augment=False, gen=None):
+def train_step(model, opt, images, targets, augment=False, gen=None, as_list=False):
     if augment:
         from mx_det import ops
         B = images.shape[0]
         r = torch.rand(2 * B, generator=gen).tolist()
         codes = [0 if r[2 * i] > 0.5 else 1 + min(int(r[2 * i + 1] * 3), 2) for i in range(B)]
         images = ops.corrupt_u8(images, codes, seed=int(torch.randint(0, 2 ** 62, (1,), generator=gen)))
+    if as_list:
+        images = list(images)
     loss_dict = model(images, targets)
     losses = sum(loss for loss in loss_dict.values())
     opt.zero_grad(set_to_none=True)
@@ -351,9 +353,11 @@ def _time_precision(precision, args, world, rank, dev, imgs, tg):
     opt = make_optimizer(model)
     gen = torch.Generator().manual_seed(1234 + rank)
 
+    as_list = os.environ.get("MX_BENCH_LIST") == "1"  # diagnostics: images as a list, as a DataLoader gives them
+
     def step(i):
         j = (2 * i) % N_IMAGES_PER_RANK
-        return train_step(ddp, opt, imgs[j:j + 2], tg[j:j + 2], args.augment, gen)
+        return train_step(ddp, opt, imgs[j:j + 2], tg[j:j + 2], args.augment, gen, as_list)
 
     for i in range(args.warmup):
         step(i)
@@ -626,7 +630,21 @@ def script_main(args, world, rank, dev, imgs, tg):
                VAL_ANN=tmp / "coco/annotations/instances_val.json", OUT_DIR=tmp / f"out{rank}", WEIGHTS=None,
                TRAINABLE_LAYERS=3, TIMER={"warmup": args.warmup},
                DECODE_THREADS=int(os.environ.get("MX_DECODE_THREADS", "4")))
-    train_frcnn(cfg)
+    prof_path = os.environ.get("MX_SCRIPT_PROFILE")  # host cProfile of the script loop (diagnostics)
+    if prof_path and rank == 0:
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        train_frcnn(cfg)
+        pr.disable()
+        buf = io.StringIO()
+        pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(45)
+        with open(prof_path, "w") as f:
+            f.write(buf.getvalue())
+    else:
+        train_frcnn(cfg)
     dt = cfg["TIMER"]["t1"] - cfg["TIMER"]["t0"]
     steps = cfg["TIMER"]["steps"]
     if world > 1:

@@ -261,70 +261,96 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
         }
   }
   __syncthreads();
-  for (int e = tid; e < PR * CPR; e += NT) {
-    int row = e / CPR, cc = (e % CPR) * 8;
-    int64_t m = m0 + h * PR + row, col0 = n0 + cc;
-    if (m >= p.M || col0 >= p.Ncol) continue;
-    m = out_row(p, m);
-    float v[8];
-    *(float4*)&v[0] = *(const float4*)&Ct[row * LD + cc];
-    *(float4*)&v[4] = *(const float4*)&Ct[row * LD + cc + 4];
-    if (vec) {
-      if (p.bias) {
+  // rows of the staged tile in groups of EU: every global operand of the group (residual, the BN
+  // backward's y / z) is loaded before any of its rows is finished, so a thread waits one memory
+  // round trip per group instead of one per row (the memory-bound 1x1 dgrads with BN-backward
+  // epilogues were latency-bound here). Per element the arithmetic and its order are unchanged.
+  constexpr int ITER = (PR * CPR + NT - 1) / NT;
+  constexpr int EU = ITER < 4 ? ITER : 4;
+  for (int k0 = 0; k0 < ITER; k0 += EU) {
+    float rr[EU][8], yy[EU][8], zz[EU][8];
+    int64_t mm[EU], cc0[EU];
+    int rw[EU];
+    bool ok[EU];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] += p.bias[col0 + t];
+    for (int u = 0; u < EU; ++u) {
+      const int e = tid + (k0 + u) * NT;
+      const int row = e / CPR, cc = (e % CPR) * 8;
+      int64_t m = m0 + h * PR + row;
+      const int64_t col0 = n0 + cc;
+      ok[u] = k0 + u < ITER && e < PR * CPR && m < p.M && col0 < p.Ncol;
+      rw[u] = row;
+      cc0[u] = col0;
+      mm[u] = ok[u] ? out_row(p, m) : 0;
+      if (ok[u] && vec) {
+        if (p.residual) ld8((const TA*)p.residual + mm[u] * p.Ncol + col0, rr[u]);
+        if (sizeof(TA) == 4 && p.out_f32 && p.bnb_part) {
+          ld8((const TA*)p.bnb_y + mm[u] * p.Ncol + col0, yy[u]);
+          ld8((const TA*)p.bnb_z + mm[u] * p.Ncol + col0, zz[u]);
+        }
       }
-      if (p.residual) {
-        float rr[8];
-        ld8((const TA*)p.residual + m * p.Ncol + col0, rr);
+    }
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] += rr[t];
-      }
+    for (int u = 0; u < EU; ++u) {
+      if (!ok[u]) continue;
+      const int row = rw[u];
+      const int64_t m = mm[u], col0 = cc0[u];
+      const int cc = (int)(col0 - n0);
+      float v[8];
+      *(float4*)&v[0] = *(const float4*)&Ct[row * LD + cc];
+      *(float4*)&v[4] = *(const float4*)&Ct[row * LD + cc + 4];
+      if (vec) {
+        if (p.bias) {
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], p.act);
-      if (p.out_f32) {
-        float* o = (float*)p.out + m * p.Ncol + col0;
-        *(float4*)o = *(float4*)&v[0];
-        *(float4*)(o + 4) = *(float4*)&v[4];
-        if (sizeof(TA) == 4 && p.bnb_part) {  // f32 activations: the stored gradient is v itself
-          float yy[8], zz[8];
-          ld8((const TA*)p.bnb_y + m * p.Ncol + col0, yy);
-          ld8((const TA*)p.bnb_z + m * p.Ncol + col0, zz);
-          const int gi = BG == 1 ? 0 : (int)((h * PR + row) / SROWS);
+          for (int t = 0; t < 8; ++t) v[t] += p.bias[col0 + t];
+        }
+        if (p.residual) {
 #pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const float g = v[t] * bnb_act_grad(yy[t], p.bnb_act);
-            bs[gi][t] += g;
-            bq[gi][t] += g * ((zz[t] - bmu[t]) * bis[t]);
+          for (int t = 0; t < 8; ++t) v[t] += rr[u][t];
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], p.act);
+        if (p.out_f32) {
+          float* o = (float*)p.out + m * p.Ncol + col0;
+          *(float4*)o = *(float4*)&v[0];
+          *(float4*)(o + 4) = *(float4*)&v[4];
+          if (sizeof(TA) == 4 && p.bnb_part) {  // f32 activations: the stored gradient is v itself
+            const int gi = BG == 1 ? 0 : (int)((h * PR + row) / SROWS);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const float g = v[t] * bnb_act_grad(yy[u][t], p.bnb_act);
+              bs[gi][t] += g;
+              bq[gi][t] += g * ((zz[u][t] - bmu[t]) * bis[t]);
+            }
+          }
+        } else {
+          uint4 w;
+          uint16_t* wh = (uint16_t*)&w;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) wh[t] = f2bf(v[t]);
+          *(uint4*)((uint16_t*)p.out + m * p.Ncol + col0) = w;
+          if (p.bnb_part) {  // the stored (bf16-rounded) gradient, as a separate reduce would read it
+            const uint4 yb = *(const uint4*)((const uint16_t*)p.bnb_y + m * p.Ncol + col0);
+            const uint4 zb = *(const uint4*)((const uint16_t*)p.bnb_z + m * p.Ncol + col0);
+            const uint16_t *yh = (const uint16_t*)&yb, *zh = (const uint16_t*)&zb;
+            const int gi = BG == 1 ? 0 : (int)((h * PR + row) / SROWS);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const float g = bf2f(wh[t]) * bnb_act_grad(bf2f(yh[t]), p.bnb_act);
+              bs[gi][t] += g;
+              bq[gi][t] += g * ((bf2f(zh[t]) - bmu[t]) * bis[t]);
+            }
           }
         }
       } else {
-        uint4 w;
-        uint16_t* wh = (uint16_t*)&w;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) wh[t] = f2bf(v[t]);
-        *(uint4*)((uint16_t*)p.out + m * p.Ncol + col0) = w;
-        if (p.bnb_part) {  // the stored (bf16-rounded) gradient, as a separate reduce would read it
-          const uint4 yy = *(const uint4*)((const uint16_t*)p.bnb_y + m * p.Ncol + col0);
-          const uint4 zz = *(const uint4*)((const uint16_t*)p.bnb_z + m * p.Ncol + col0);
-          const uint16_t *yh = (const uint16_t*)&yy, *zh = (const uint16_t*)&zz;
-          const int gi = BG == 1 ? 0 : (int)((h * PR + row) / SROWS);
-#pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const float g = bf2f(wh[t]) * bnb_act_grad(bf2f(yh[t]), p.bnb_act);
-            bs[gi][t] += g;
-            bq[gi][t] += g * ((bf2f(zh[t]) - bmu[t]) * bis[t]);
-          }
+        for (int t = 0; t < 8 && col0 + t < p.Ncol; ++t) {
+          float x = v[t];
+          if (p.bias) x += p.bias[col0 + t];
+          if (p.residual) x += ld1((const TA*)p.residual + m * p.Ncol + col0 + t);
+          x = act_f(x, p.act);
+          if (p.out_f32) ((float*)p.out)[m * p.Ncol + col0 + t] = x;
+          else ((uint16_t*)p.out)[m * p.Ncol + col0 + t] = f2bf(x);
         }
-      }
-    } else {
-      for (int t = 0; t < 8 && col0 + t < p.Ncol; ++t) {
-        float x = v[t];
-        if (p.bias) x += p.bias[col0 + t];
-        if (p.residual) x += ld1((const TA*)p.residual + m * p.Ncol + col0 + t);
-        x = act_f(x, p.act);
-        if (p.out_f32) ((float*)p.out)[m * p.Ncol + col0 + t] = x;
-        else ((uint16_t*)p.out)[m * p.Ncol + col0 + t] = f2bf(x);
       }
     }
   }
@@ -895,6 +921,19 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
       va[rr][4] += b[rr].x; va[rr][5] += b[rr].y; va[rr][6] += b[rr].z; va[rr][7] += b[rr].w;
     }
   }
+  // the rows' residual / BN-backward operands in flight together (one round trip, not one per row)
+  float rres[RPT][8], ryy[RPT][8], rzz[RPT][8];
+#pragma unroll
+  for (int rr = 0; rr < RPT; ++rr) {
+    const int64_t m = mt * BM + rl + RL * rr;
+    if (!cok || m >= p.M) continue;
+    const int64_t mo = out_row(p, m);
+    if (p.residual) ld8((const TA*)p.residual + mo * p.Ncol + col0, rres[rr]);
+    if (sizeof(TA) == 4 && p.out_f32 && p.bnb_part) {
+      ld8((const TA*)p.bnb_y + mo * p.Ncol + col0, ryy[rr]);
+      ld8((const TA*)p.bnb_z + mo * p.Ncol + col0, rzz[rr]);
+    }
+  }
 #pragma unroll
   for (int rr = 0; rr < RPT; ++rr) {
     const int64_t m = mt * BM + rl + RL * rr;
@@ -909,10 +948,8 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
     }
     const int64_t mo = out_row(p, m);
     if (p.residual) {
-      float rr[8];
-      ld8((const TA*)p.residual + mo * p.Ncol + col0, rr);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] += rr[t];
+      for (int t = 0; t < 8; ++t) v[t] += rres[rr][t];
     }
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], p.act);
@@ -921,14 +958,11 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
       *(float4*)o = *(float4*)&v[0];
       *(float4*)(o + 4) = *(float4*)&v[4];
       if (sizeof(TA) == 4 && p.bnb_part) {
-        float yy[8], zz[8];
-        ld8((const TA*)p.bnb_y + mo * p.Ncol + col0, yy);
-        ld8((const TA*)p.bnb_z + mo * p.Ncol + col0, zz);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-          const float g = v[t] * bnb_act_grad(yy[t], p.bnb_act);
+          const float g = v[t] * bnb_act_grad(ryy[rr][t], p.bnb_act);
           b2[h][t] += g;
-          c2[h][t] += g * ((zz[t] - bmu[t]) * bis[t]);
+          c2[h][t] += g * ((rzz[rr][t] - bmu[t]) * bis[t]);
         }
       }
     } else {
