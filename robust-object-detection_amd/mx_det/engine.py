@@ -239,6 +239,8 @@ def train_frcnn(cfg):
                 if world > 1:
                     dist.barrier()
                 timer["t0"] = time.perf_counter()
+                from . import _lib
+                _lib.trace_marker(1)  # rocprofv3 kernel-trace delimiters (tools/prof_steps.py)
                 if "loader" in timer:
                     timer["wait0"] = timer["loader"].wait_s
             if rank == 0 and ((i + 1) % 100 == 0 or (i + 1) == n_batches):
@@ -258,6 +260,8 @@ def train_frcnn(cfg):
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+        from . import _lib
+        _lib.trace_marker(2)
         timer["t1"], timer["steps"] = time.perf_counter(), it_global - timer["warmup"]
         if "loader" in timer:
             timer["loader_wait_s"] = timer["loader"].wait_s - timer.get("wait0", 0.0)
