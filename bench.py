@@ -629,7 +629,8 @@ def script_main(args, world, rank, dev, imgs, tg):
                TRAIN_ANN=tmp / "coco/annotations/instances_train.json",
                VAL_ANN=tmp / "coco/annotations/instances_val.json", OUT_DIR=tmp / f"out{rank}", WEIGHTS=None,
                TRAINABLE_LAYERS=3, TIMER={"warmup": args.warmup},
-               DECODE_THREADS=int(os.environ.get("MX_DECODE_THREADS", "4")))
+               DECODE_THREADS=int(os.environ.get("MX_DECODE_THREADS", "4")),
+               PRELOAD_DEVICE=os.environ.get("MX_SCRIPT_PRELOAD") == "1")
     prof_path = os.environ.get("MX_SCRIPT_PROFILE")  # host cProfile of the script loop (diagnostics)
     if prof_path and rank == 0:
         import cProfile

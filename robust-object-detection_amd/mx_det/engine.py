@@ -182,6 +182,8 @@ def train_frcnn(cfg):
         train_loader = PrefetchJpegLoader(train_loader, dev, workers=cfg.get("DECODE_THREADS", 4))
         if cfg.get("TIMER") is not None:
             cfg["TIMER"]["loader"] = train_loader
+    if cfg.get("PRELOAD_DEVICE"):  # diagnostics (bench.py --mode script): every batch decoded up front
+        train_loader = [(list(im), [dict(t) for t in tg]) for im, tg in train_loader]
     val_sampler = ShardSampler(len(val_ds), world, rank) if world > 1 else None
     val_loader = DataLoader(val_ds, batch_size=1, shuffle=False, sampler=val_sampler,
                             num_workers=cfg.get("NUM_WORKERS", 0), collate_fn=collate_fn,
