@@ -1921,8 +1921,10 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
   }
   const int pend32 = (int)pend;
   const uint32_t dy_col = (uint32_t)(k0 + ch * 8) * 4u;
-  float4 rd[2][2], rx[2][2];
-  auto load = [&]() {
+  // two register stages: a K-tile's loads are issued two tiles ahead of its LDS store, so the global
+  // latency is covered by two tiles of MFMA work instead of one (one was shorter than an L2 miss)
+  float4 rdA[2][2], rxA[2][2], rdB[2][2], rxB[2][2];
+  auto load = [&](float4 (&rd)[2][2], float4 (&rx)[2][2]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const bool pok = px_i[i] < pend32;
@@ -1948,7 +1950,7 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
       px_n[i] += dn + c2;
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const float4 (&rd)[2][2], const float4 (&rx)[2][2]) {
     char* Dh = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1979,13 +1981,7 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int64_t nk = (pend - pbeg + PXT - 1) / PXT;
-  load();
-  store(0);
-  __syncthreads();
-  for (int64_t it = 0; it < nk; ++it) {
-    const int buf = (int)(it & 1);
-    if (it + 1 < nk) load();
+  auto compute = [&](int buf) {
     const char* Dh = smem + buf * STAGE;
     bf16x8 ah[4], al[4], bh[4], bl[4];
 #pragma unroll
@@ -2006,7 +2002,23 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
       }
-    if (it + 1 < nk) store(buf ^ 1);
+  };
+  const int64_t nk = (pend - pbeg + PXT - 1) / PXT;
+  load(rdA, rxA);                // tile 0
+  if (nk > 1) load(rdB, rxB);    // tile 1
+  store(0, rdA, rxA);
+  __syncthreads();
+  for (int64_t it = 0; it < nk; it += 2) {
+    // tile it is in LDS buffer 0; B holds tile it + 1
+    if (it + 2 < nk) load(rdA, rxA);  // tile it + 2
+    compute(0);
+    if (it + 1 < nk) store(1, rdB, rxB);
+    __syncthreads();
+    if (it + 1 >= nk) break;
+    // tile it + 1 is in buffer 1; A holds tile it + 2
+    if (it + 3 < nk) load(rdB, rxB);  // tile it + 3
+    compute(1);
+    if (it + 2 < nk) store(0, rdA, rxA);
     __syncthreads();
   }
   wgrad_store(p, acc, k0, c0, wm, wn, lane, split);
