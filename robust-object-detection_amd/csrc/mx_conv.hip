@@ -261,12 +261,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
         }
   }
   __syncthreads();
+  if constexpr (sizeof(TA) == 4) {  // f32 (bf16x3) kernels
   // rows of the staged tile in groups of EU: every global operand of the group (residual, the BN
   // backward's y / z) is loaded before any of its rows is finished, so a thread waits one memory
   // round trip per group instead of one per row (the memory-bound 1x1 dgrads with BN-backward
   // epilogues were latency-bound here). Per element the arithmetic and its order are unchanged.
   constexpr int ITER = (PR * CPR + NT - 1) / NT;
-  constexpr int EU = ITER < 4 ? ITER : 4;
+  constexpr int EU = ITER < 2 ? ITER : 2;
   for (int k0 = 0; k0 < ITER; k0 += EU) {
     float rr[EU][8], yy[EU][8], zz[EU][8];
     int64_t mm[EU], cc0[EU];
@@ -353,6 +354,76 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
         }
       }
     }
+  }
+  } else {  // bf16 kernels: one row at a time (their 3-blocks-per-CU register budget has no room
+           // for a second row's operands)
+  for (int e = tid; e < PR * CPR; e += NT) {
+    int row = e / CPR, cc = (e % CPR) * 8;
+    int64_t m = m0 + h * PR + row, col0 = n0 + cc;
+    if (m >= p.M || col0 >= p.Ncol) continue;
+    m = out_row(p, m);
+    float v[8];
+    *(float4*)&v[0] = *(const float4*)&Ct[row * LD + cc];
+    *(float4*)&v[4] = *(const float4*)&Ct[row * LD + cc + 4];
+    if (vec) {
+      if (p.bias) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] += p.bias[col0 + t];
+      }
+      if (p.residual) {
+        float rr[8];
+        ld8((const TA*)p.residual + m * p.Ncol + col0, rr);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] += rr[t];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], p.act);
+      if (p.out_f32) {
+        float* o = (float*)p.out + m * p.Ncol + col0;
+        *(float4*)o = *(float4*)&v[0];
+        *(float4*)(o + 4) = *(float4*)&v[4];
+        if (sizeof(TA) == 4 && p.bnb_part) {  // f32 activations: the stored gradient is v itself
+          float yy[8], zz[8];
+          ld8((const TA*)p.bnb_y + m * p.Ncol + col0, yy);
+          ld8((const TA*)p.bnb_z + m * p.Ncol + col0, zz);
+          const int gi = BG == 1 ? 0 : (int)((h * PR + row) / SROWS);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const float g = v[t] * bnb_act_grad(yy[t], p.bnb_act);
+            bs[gi][t] += g;
+            bq[gi][t] += g * ((zz[t] - bmu[t]) * bis[t]);
+          }
+        }
+      } else {
+        uint4 w;
+        uint16_t* wh = (uint16_t*)&w;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) wh[t] = f2bf(v[t]);
+        *(uint4*)((uint16_t*)p.out + m * p.Ncol + col0) = w;
+        if (p.bnb_part) {  // the stored (bf16-rounded) gradient, as a separate reduce would read it
+          const uint4 yy = *(const uint4*)((const uint16_t*)p.bnb_y + m * p.Ncol + col0);
+          const uint4 zz = *(const uint4*)((const uint16_t*)p.bnb_z + m * p.Ncol + col0);
+          const uint16_t *yh = (const uint16_t*)&yy, *zh = (const uint16_t*)&zz;
+          const int gi = BG == 1 ? 0 : (int)((h * PR + row) / SROWS);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const float g = bf2f(wh[t]) * bnb_act_grad(bf2f(yh[t]), p.bnb_act);
+            bs[gi][t] += g;
+            bq[gi][t] += g * ((bf2f(zh[t]) - bmu[t]) * bis[t]);
+          }
+        }
+      }
+    } else {
+      for (int t = 0; t < 8 && col0 + t < p.Ncol; ++t) {
+        float x = v[t];
+        if (p.bias) x += p.bias[col0 + t];
+        if (p.residual) x += ld1((const TA*)p.residual + m * p.Ncol + col0 + t);
+        x = act_f(x, p.act);
+        if (p.out_f32) ((float*)p.out)[m * p.Ncol + col0 + t] = x;
+        else ((uint16_t*)p.out)[m * p.Ncol + col0 + t] = f2bf(x);
+      }
+    }
+  }
   }
   if (HALVES > 1) __syncthreads();
   }
