@@ -128,7 +128,7 @@ static constexpr int SROWS = 64;
 // WR = wave-rows of the block (2: 4 waves in 2x2, 4: 8 waves in 4x2; HALVES == WR then stages one
 // wave-row per pass).
 // WC = wave-columns (2: wave tiles of BN/2 columns; 1: each wave spans all BN columns).
-template <int BN, int HALVES = 1, int BMT = BM, typename TA = uint16_t, int WR = 2, int WC = 2>
+template <int BN, int HALVES = 1, int BMT = BM, typename TA = uint16_t, int WR = 2, int WC = 2, bool GROUP = false>
 __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT / (16 * WR)][BN / (16 * WC)],
                                               char* smem, int64_t m0, int64_t n0, int64_t mt, int wm, int wn,
                                               int lane, int tid, int split) {
@@ -261,7 +261,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
         }
   }
   __syncthreads();
-  if constexpr (sizeof(TA) == 4) {  // f32 (bf16x3) kernels
+  if constexpr (GROUP) {  // f32 (bf16x3) dgrad kernels
   // rows of the staged tile in groups of EU: every global operand of the group (residual, the BN
   // backward's y / z) is loaded before any of its rows is finished, so a thread waits one memory
   // round trip per group instead of one per row (the memory-bound 1x1 dgrads with BN-backward
@@ -355,8 +355,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
       }
     }
   }
-  } else {  // bf16 kernels: one row at a time (their 3-blocks-per-CU register budget has no room
-           // for a second row's operands)
+  } else {  // one row at a time: the forward (no residual / BN-backward operands) and the bf16
+           // kernels (whose 3-blocks-per-CU register budget has no room for a second row's), and
+           // fewer registers beside the side-stream wgrad
   for (int e = tid; e < PR * CPR; e += NT) {
     int row = e / CPR, cc = (e % CPR) * 8;
     int64_t m = m0 + h * PR + row, col0 = n0 + cc;
@@ -992,19 +993,6 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
       va[rr][4] += b[rr].x; va[rr][5] += b[rr].y; va[rr][6] += b[rr].z; va[rr][7] += b[rr].w;
     }
   }
-  // the rows' residual / BN-backward operands in flight together (one round trip, not one per row)
-  float rres[RPT][8], ryy[RPT][8], rzz[RPT][8];
-#pragma unroll
-  for (int rr = 0; rr < RPT; ++rr) {
-    const int64_t m = mt * BM + rl + RL * rr;
-    if (!cok || m >= p.M) continue;
-    const int64_t mo = out_row(p, m);
-    if (p.residual) ld8((const TA*)p.residual + mo * p.Ncol + col0, rres[rr]);
-    if (sizeof(TA) == 4 && p.out_f32 && p.bnb_part) {
-      ld8((const TA*)p.bnb_y + mo * p.Ncol + col0, ryy[rr]);
-      ld8((const TA*)p.bnb_z + mo * p.Ncol + col0, rzz[rr]);
-    }
-  }
 #pragma unroll
   for (int rr = 0; rr < RPT; ++rr) {
     const int64_t m = mt * BM + rl + RL * rr;
@@ -1019,8 +1007,10 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
     }
     const int64_t mo = out_row(p, m);
     if (p.residual) {
+      float rr[8];
+      ld8((const TA*)p.residual + mo * p.Ncol + col0, rr);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] += rres[rr][t];
+      for (int t = 0; t < 8; ++t) v[t] += rr[t];
     }
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], p.act);
@@ -1029,11 +1019,14 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
       *(float4*)o = *(float4*)&v[0];
       *(float4*)(o + 4) = *(float4*)&v[4];
       if (sizeof(TA) == 4 && p.bnb_part) {
+        float yy[8], zz[8];
+        ld8((const TA*)p.bnb_y + mo * p.Ncol + col0, yy);
+        ld8((const TA*)p.bnb_z + mo * p.Ncol + col0, zz);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-          const float g = v[t] * bnb_act_grad(ryy[rr][t], p.bnb_act);
+          const float g = v[t] * bnb_act_grad(yy[t], p.bnb_act);
           b2[h][t] += g;
-          c2[h][t] += g * ((rzz[rr][t] - bmu[t]) * bis[t]);
+          c2[h][t] += g * ((zz[t] - bmu[t]) * bis[t]);
         }
       }
     } else {
@@ -1169,48 +1162,6 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(WgP p, int splits) {
   for (int t = 0; t < 4; ++t) {
     const int64_t o = wgrad_dst(p, k, (int)(c4 * 4 + t));
     if (o >= 0) p.dw[o] = vv[t];
-  }
-}
-
-// Split-partial sum, one block per output channel k: every thread sums its float4 column groups over
-// the splits in split order (8 slab loads in flight per thread), the summed row [Ncol] goes to LDS, and
-// the block writes dw's row k -- Cin * RS contiguous floats in either layout -- with coalesced stores
-// (the per-column scattered 4-B stores of the KCRS transpose were half the old reduce's time).
-// Deterministic: one fixed summation order per element.
-__global__ void __launch_bounds__(256) wgrad_reduce_row_kernel(WgP p, int splits) {
-  extern __shared__ float wrow[];  // [Ncol]
-  const int64_t k = blockIdx.x;
-  const int64_t nc4 = p.Ncol >> 2, plane = p.K * p.Ncol;
-  const float* src = p.slab + k * p.Ncol;
-  for (int64_t c4 = threadIdx.x; c4 < nc4; c4 += 256) {
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int s0 = 0; s0 < splits; s0 += 8) {
-      float4 v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = s0 + j < splits ? *(const float4*)(src + (int64_t)(s0 + j) * plane + c4 * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (s0 + j < splits) {
-          a.x += v[j].x; a.y += v[j].y; a.z += v[j].z; a.w += v[j].w;
-        }
-    }
-    *(float4*)&wrow[c4 * 4] = a;
-  }
-  __syncthreads();
-  const int C = p.dC, RS = p.dRS;
-  const int64_t Cin = p.Cin, n = Cin * RS;
-  float* dst = p.dw + k * n;
-  for (int64_t o = threadIdx.x; o < n; o += 256) {
-    int64_t c, tap;
-    if (p.layout == 1) {
-      c = o / RS;
-      tap = o - c * RS;
-    } else {
-      tap = o / Cin;
-      c = o - tap * Cin;
-    }
-    dst[o] = wrow[tap * C + c];
   }
 }
 
@@ -1738,7 +1689,7 @@ __global__ void __launch_bounds__(NT, 2) conv_x3_kernel(ConvP p) {
     if (t + 1 < ntk) store(buf ^ 1);
     __syncthreads();
   }
-  conv_epilogue<BN, 2, BMT, float>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
+  conv_epilogue<BN, 2, BMT, float, 2, 2, MODE == 1>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
 }
 
 // Chunk swizzle of the f32 A half-tiles of conv_x3_buf_kernel (64-B rows = 4 chunks of 4 f32): the
@@ -1935,7 +1886,8 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
   __syncthreads();
   // wide tiles stage the whole f32 tile at once (one barrier, every wave storing); 8-wave 2x2 tiles
   // stage one wave-row per pass (their whole tile would not fit beside a second block)
-  conv_epilogue<BN, (WC == 1 ? 1 : WR), BMT, float, WR, WC>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid, split);
+  conv_epilogue<BN, (WC == 1 ? 1 : WR), BMT, float, WR, WC, MODE == 1>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid,
+                                                                       split);
 #endif
 }
 
@@ -1992,10 +1944,8 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
   }
   const int pend32 = (int)pend;
   const uint32_t dy_col = (uint32_t)(k0 + ch * 8) * 4u;
-  // two register stages: a K-tile's loads are issued two tiles ahead of its LDS store, so the global
-  // latency is covered by two tiles of MFMA work instead of one (one was shorter than an L2 miss)
-  float4 rdA[2][2], rxA[2][2], rdB[2][2], rxB[2][2];
-  auto load = [&](float4 (&rd)[2][2], float4 (&rx)[2][2]) {
+  float4 rd[2][2], rx[2][2];
+  auto load = [&]() {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const bool pok = px_i[i] < pend32;
@@ -2021,7 +1971,7 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
       px_n[i] += dn + c2;
     }
   };
-  auto store = [&](int buf, const float4 (&rd)[2][2], const float4 (&rx)[2][2]) {
+  auto store = [&](int buf) {
     char* Dh = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -2052,7 +2002,13 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](int buf) {
+  const int64_t nk = (pend - pbeg + PXT - 1) / PXT;
+  load();
+  store(0);
+  __syncthreads();
+  for (int64_t it = 0; it < nk; ++it) {
+    const int buf = (int)(it & 1);
+    if (it + 1 < nk) load();
     const char* Dh = smem + buf * STAGE;
     bf16x8 ah[4], al[4], bh[4], bl[4];
 #pragma unroll
@@ -2073,23 +2029,7 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
       }
-  };
-  const int64_t nk = (pend - pbeg + PXT - 1) / PXT;
-  load(rdA, rxA);                // tile 0
-  if (nk > 1) load(rdB, rxB);    // tile 1
-  store(0, rdA, rxA);
-  __syncthreads();
-  for (int64_t it = 0; it < nk; it += 2) {
-    // tile it is in LDS buffer 0; B holds tile it + 1
-    if (it + 2 < nk) load(rdA, rxA);  // tile it + 2
-    compute(0);
-    if (it + 1 < nk) store(1, rdB, rxB);
-    __syncthreads();
-    if (it + 1 >= nk) break;
-    // tile it + 1 is in buffer 1; A holds tile it + 2
-    if (it + 3 < nk) load(rdB, rxB);  // tile it + 3
-    compute(1);
-    if (it + 2 < nk) store(0, rdA, rxA);
+    if (it + 1 < nk) store(buf ^ 1);
     __syncthreads();
   }
   wgrad_store(p, acc, k0, c0, wm, wn, lane, split);
@@ -3539,7 +3479,7 @@ extern "C" int mx_conv2d_wgrad_ex(const mx_conv_shape* s, const uint16_t* dy, co
   MX_LAUNCH_CHECK();
   if (g.splits > 1) {
     MX_CHECK_ARG(Kout < 65536, "conv wgrad: too many output channels for the split reduce");
-    wgrad_reduce_row_kernel<<<(unsigned)Kout, 256, sizeof(float) * (size_t)p.Ncol, st>>>(p, (int)g.splits);
+    wgrad_reduce_kernel<<<dim3((unsigned)cdiv(p.Ncol / 4, 64), (unsigned)Kout), 256, 0, st>>>(p, (int)g.splits);
     MX_LAUNCH_CHECK();
   }
   return MX_OK;
@@ -3826,7 +3766,7 @@ extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const
   MX_LAUNCH_CHECK();
   if (g.splits > 1) {
     MX_CHECK_ARG(Kout < 65536, "conv wgrad x3: too many output channels for the split reduce");
-    wgrad_reduce_row_kernel<<<(unsigned)Kout, 256, sizeof(float) * (size_t)p.Ncol, st>>>(p, (int)g.splits);
+    wgrad_reduce_kernel<<<dim3((unsigned)cdiv(p.Ncol / 4, 64), (unsigned)Kout), 256, 0, st>>>(p, (int)g.splits);
     MX_LAUNCH_CHECK();
   }
   return MX_OK;
