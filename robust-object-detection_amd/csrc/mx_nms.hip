@@ -87,31 +87,57 @@ __global__ void nms_seg_kernel(const int32_t* __restrict__ head, const int32_t* 
   }
 }
 
-// one 64-thread block per (64-row block, 64-column tile relative to the row's segment start)
+// one 64-thread block per (64-row block, 64-column tile relative to the row's segment start). The
+// column tile of the block's first row's segment is staged in LDS once (one coalesced load per lane);
+// rows of another segment (a block straddling a segment start) read their columns from global.
+// colm (optional): for the row's own 64-box block of its segment, the column form of the diagonal
+// tile -- bit j - c0 set when an EARLIER box j of the block overlaps box i (the same IoU value as
+// row j's bit for i: fmaxf / fminf and the area sum are symmetric in the pair)
 __global__ void __launch_bounds__(64) nms_mask_kernel(const float4* __restrict__ sbox, const float* __restrict__ sarea,
                                                       const int32_t* __restrict__ incl, const int32_t* __restrict__ seg_start,
-                                                      int64_t n, int Wm, double thr, uint64_t* __restrict__ mask) {
-  int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  int cb = blockIdx.y;
+                                                      int64_t n, int Wm, double thr, uint64_t* __restrict__ mask,
+                                                      uint64_t* __restrict__ colm) {
+  __shared__ float4 tbox[64];
+  __shared__ float tarea[64];
+  const int tid = threadIdx.x, cb = blockIdx.y;
+  const int64_t i0 = (int64_t)blockIdx.x * 64, i = i0 + tid;
+  if (i0 >= n) return;  // whole block
+  const int sid0 = incl[i0] - 1;
+  const int64_t t0 = seg_start[sid0] + (int64_t)cb * 64, t1 = min<int64_t>(t0 + 64, seg_start[sid0 + 1]);
+  if (t0 + tid < t1) {
+    tbox[tid] = sbox[t0 + tid];
+    tarea[tid] = sarea[t0 + tid];
+  }
+  __syncthreads();
   if (i >= n) return;
-  int sid = incl[i] - 1;
-  int64_t s0 = seg_start[sid], s1 = seg_start[sid + 1];
-  int64_t c0 = s0 + (int64_t)cb * 64;
+  const int sid = incl[i] - 1;
+  const int64_t s0 = seg_start[sid], s1 = seg_start[sid + 1];
+  const int64_t c0 = s0 + (int64_t)cb * 64;
   if (c0 >= s1) return;
-  float4 bi = sbox[i];
-  float ai = sarea[i];
-  uint64_t bits = 0;
-  int64_t cend = min<int64_t>(c0 + 64, s1);
-  for (int64_t j = max<int64_t>(c0, i + 1); j < cend; ++j) {
-    float4 bj = sbox[j];
+  const bool staged = sid == sid0;
+  const bool diag = colm && cb == (int)((i - s0) >> 6);
+  const float4 bi = sbox[i];
+  const float ai = sarea[i];
+  uint64_t bits = 0, lo = 0;
+  const int jn = (int)(min<int64_t>(c0 + 64, s1) - c0);
+  const int jstart = diag ? 0 : (int)min<int64_t>(64, max<int64_t>(0, i + 1 - c0));
+  for (int jj = jstart; jj < jn; ++jj) {
+    const int64_t j = c0 + jj;
+    if (j == i) continue;
+    const float4 bj = staged ? tbox[jj] : sbox[j];
+    const float aj = staged ? tarea[jj] : sarea[j];
     float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
     float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
     float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
     float inter = w * h;
-    float ovr = inter / ((ai + sarea[j]) - inter);
-    if ((double)ovr > thr) bits |= 1ull << (j - c0);
+    float ovr = inter / ((ai + aj) - inter);
+    if ((double)ovr > thr) {
+      if (j > i) bits |= 1ull << jj;
+      else lo |= 1ull << jj;
+    }
   }
   mask[i * Wm + cb] = bits;
+  if (diag) colm[i] = lo;
 }
 
 // one wave per segment: greedy scan, 64 rows per step
@@ -275,65 +301,39 @@ __global__ void __launch_bounds__(256) nms_scan_lds_kernel(const uint64_t* __res
   }
 }
 
-// OR of a 64-bit value over the 64 lanes of the wave (DPP: pairs, quads, half-rows, rows, then the
-// row broadcasts; lane 63 ends up with the total), returned wave-uniform
-__device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
-  int x = (int)v;
-  x |= __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-  x |= __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-  x |= __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  x |= __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false);  // row_mirror
-  x |= __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-  x |= __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-  return (uint32_t)__builtin_amdgcn_readlane(x, 63);
-}
-
-// Greedy NMS inside one 64 x 64 diagonal tile: lane l holds row l's suppression bits (bit t: box l
-// suppresses box t > l); `live` = the candidates (in range, not removed by earlier blocks). The
-// greedy set G is the unique fixpoint of K -> live & ~OR{row s : s in K}: each Jacobi step fixes at
-// least one more leading position, and a repeated K is that fixpoint. A few wave-wide ORs replace
-// the walk's one dependent readlane pair per survivor; chains still unresolved after 8 steps
-// finish with the walk (the same greedy result either way).
-__device__ __forceinline__ uint64_t tile_greedy(uint64_t diag, uint64_t live, int lane) {
+// Greedy NMS inside one 64 x 64 diagonal tile from its column form: lane t holds colm (bit s: earlier
+// box s suppresses box t). Jacobi steps K -> live & ~{t : colm_t & K != 0} (one AND, one compare, one
+// ballot each) fix at least one more leading position per step, so the greedy set -- the unique
+// fixpoint -- is reached after at most 65 steps, usually a handful.
+__device__ __forceinline__ uint64_t tile_greedy_col(uint64_t colm, uint64_t live) {
   uint64_t k = live;
-  for (int it = 0; it < 8; ++it) {
-    const uint64_t c = ((k >> lane) & 1ull) ? diag : 0ull;
-    const uint64_t sup = ((uint64_t)wave_or32((uint32_t)(c >> 32)) << 32) | wave_or32((uint32_t)c);
-    const uint64_t nk = live & ~sup;
-    if (nk == k) return k;
+  for (int it = 0; it <= 64; ++it) {
+    const uint64_t nk = live & ~(uint64_t)__ballot((colm & k) != 0ull);
+    if (nk == k) break;
     k = nk;
   }
-  const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
-  uint64_t cur = ~live, kept = 0;
-  uint64_t avail = live;
-  while (avail) {
-    const int t = __builtin_ctzll(avail);
-    kept |= 1ull << t;
-    const uint64_t row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, t) << 32) |
-                         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, t);
-    cur |= row;
-    avail = ~cur & ~((2ull << t) - 1ull);
-  }
-  return kept;
+  return k;
 }
 
 // Single-wave scan (segments of up to 64*SCAN_WAVE_W boxes): one 64-lane workgroup per segment and
 // no workgroup barriers. A 64-row block's mask rows are one contiguous run of 64*Wm words; it is
 // copied whole into an LDS ring slot by LDS-DMA (16 coalesced 1 KiB buffer_load_dwordx4 ... lds, plus
-// one for the block's 64 box ids), SCAN_RING - 1 blocks ahead of the one being resolved, so the
-// dependent walk waits on L2/MALL latency once per segment instead of once per block. Lane w keeps the
-// removed bits of word w in a register; the in-tile chain is resolved by tile_greedy (Jacobi steps of
-// wave-wide ORs, the survivor walk as the fallback) and lanes w and w + 32 OR the kept rows' word w from LDS (half the rows
-// each, eight reads in flight), combined with one cross-lane permute.
+// one for the block's 64 box ids, one for its 64 column words), SCAN_RING - 1 blocks ahead of the one
+// being resolved, so the dependent chain waits on L2/MALL latency once per segment instead of once per
+// block. Lane w keeps the removed bits of word w in a register; the in-tile chain is resolved by
+// tile_greedy_col (ballot Jacobi steps on the column words) and lanes w and w + 32 OR the kept rows'
+// word w from LDS (half the rows each, eight reads in flight), combined with one cross-lane permute.
 // Same greedy result as nms_scan_kernel. Every block issues exactly SCAN_DMA VMEM instructions
 // (slots past the rows read out of range -> zero) and one flags store, so the counted waits are exact.
 static constexpr int SCAN_WAVE_W = 32;
-static constexpr int SCAN_RING = 4;
-static constexpr int SCAN_SLOT = 64 * SCAN_WAVE_W * 8 + 256;  // bytes: rows + box ids
-static constexpr int SCAN_DMA = 17;
+static constexpr int SCAN_RING = 5;
+static constexpr int SCAN_COLM = 64 * SCAN_WAVE_W * 8 + 256;   // slot offset of the column words
+static constexpr int SCAN_SLOT = SCAN_COLM + 1024;  // bytes: rows + box ids + column words (+ pad)
+static constexpr int SCAN_DMA = 18;
 
 __device__ __forceinline__ void scan_wait(int ahead) {  // DMA of the block `ahead` blocks before the newest done
-  if (ahead >= 2) wait_vmcnt<2 * SCAN_DMA>();
+  if (ahead >= 3) wait_vmcnt<3 * SCAN_DMA>();
+  else if (ahead == 2) wait_vmcnt<2 * SCAN_DMA>();
   else if (ahead == 1) wait_vmcnt<SCAN_DMA>();
   else wait_vmcnt<0>();
 }
@@ -341,13 +341,15 @@ __device__ __forceinline__ void scan_wait(int ahead) {  // DMA of the block `ahe
 __global__ void __launch_bounds__(64) nms_scan_wave_kernel(const uint64_t* __restrict__ mask,
                                                            const int32_t* __restrict__ seg_start,
                                                            const int32_t* __restrict__ nseg_p,
-                                                           const int32_t* __restrict__ svals, int Wm,
+                                                           const int32_t* __restrict__ svals,
+                                                           const uint64_t* __restrict__ colm, int Wm,
                                                            int32_t* __restrict__ flags, int32_t* __restrict__ nkeep) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smb[];  // [SCAN_RING][SCAN_SLOT]
   const int lane = threadIdx.x;
   const int nseg = *nseg_p;
   const int64_t ntot = seg_start[nseg];
   const i32x4 mrs = dma_rsrc(mask, (uint32_t)(ntot * Wm * 8)), vrs = dma_rsrc(svals, (uint32_t)(ntot * 4));
+  const i32x4 crs = dma_rsrc(colm, (uint32_t)(ntot * 8));
   const uint32_t lds0 = lds_addr(smb);
   const int nrow_inst = (Wm + 1) >> 1;  // 1 KiB per instruction: 64 rows x Wm words = Wm / 2 KiB
   for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
@@ -364,6 +366,7 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(const uint64_t* __res
       for (int i = 0; i < SCAN_DMA - 1; ++i)
         lds_dma16(mrs, dst + i * 1024, i < nrow_inst ? src + i * 1024 + lane * 16 : 0xfffffff0u, 0);
       lds_dma4(vrs, dst + 64 * SCAN_WAVE_W * 8, (uint32_t)((s0 + 64 * (int64_t)b) * 4) + lane * 4, 0);
+      lds_dma16(crs, dst + SCAN_COLM, (uint32_t)((s0 + 64 * (int64_t)b) * 8) + lane * 16, 0);  // 128 words
     };
     for (int b = 0; b < SCAN_RING - 1 && b < W; ++b) issue(b);
     uint64_t rem = 0;  // removed bits of word `lane`
@@ -374,32 +377,27 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(const uint64_t* __res
       const uint64_t* rows = (const uint64_t*)slot;
       const int32_t* ids = (const int32_t*)(slot + 64 * SCAN_WAVE_W * 8);
       const int cnt = (int)min<int64_t>(64, len - (int64_t)blk * 64);
-      const uint64_t diag = lane < cnt ? rows[lane * Wm + blk] : 0ull;
+      const uint64_t cm = ((const uint64_t*)(slot + SCAN_COLM))[lane];
       const uint64_t rm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(rem >> 32), blk) << 32) |
                           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rem, blk);
       const uint64_t valid = cnt >= 64 ? ~0ull : ((1ull << cnt) - 1);
-      const uint64_t kept = tile_greedy(diag, ~rm & valid, lane);
+      const uint64_t kept = tile_greedy_col(cm, ~rm & valid);
       // flags were zeroed by the keys kernel: every lane < cnt (>= 1 of them) stores, so each block
       // issues exactly one store instruction
       if (lane < cnt) flags[ids[lane]] = (int32_t)((kept >> lane) & 1ull);
       kept_total += __popcll(kept);
-      // word w = lane & 31 of the kept rows: lanes < 32 take rows 0..31, lanes >= 32 rows 32..63 (per-lane
-      // bit walks, 8 independent LDS reads per round), then the halves are combined across lanes
+      // word w = lane & 31 of the kept rows: lanes < 32 take rows 0..31, lanes >= 32 rows 32..63, all 32
+      // reads independent and selected by the kept bit (most rows survive at RPN densities: a bit walk's
+      // dependent ctz chain cost more than the unneeded reads), then the halves are combined across lanes
       uint64_t acc = 0;
       const int w = lane & 31;
       if (w > blk && w < W) {
-        uint32_t m = lane < 32 ? (uint32_t)kept : (uint32_t)(kept >> 32);
+        const uint32_t m = lane < 32 ? (uint32_t)kept : (uint32_t)(kept >> 32);
         const uint64_t* base = rows + (lane < 32 ? 0 : 32) * Wm + w;
-        while (m) {
-          int t[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            t[i] = m ? __builtin_ctz(m) : -1;
-            m &= m - 1;
-          }
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            if (t[i] >= 0) acc |= base[t[i] * Wm];
+        for (int t = 0; t < 32; ++t) {
+          const uint64_t v = base[t * Wm];
+          acc |= ((m >> t) & 1u) ? v : 0ull;
         }
       }
       {
@@ -553,6 +551,7 @@ __global__ void nms_group_out_kernel(const uint64_t* __restrict__ skeys, const i
 // by counting instead of binary search -- the result is always the stable (segment, score desc,
 // index) order of mx_batched_nms_grouped.
 static constexpr int PS_T = 1024, PS_NMAX = 24576, PS_GMAX = 64, PS_LMAX = 8, PS_CH = PS_NMAX / PS_T;
+static constexpr int PS_SLICES = 8;  // workgroups per image in the compaction / ranking kernels
 
 // wave-aggregated counters: cnt[key] += #lanes with that key, mx[key / L] = max(m) (key < 0: none);
 // LDS or global (agent-scope atomics) alike
@@ -740,8 +739,10 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
   __shared__ uint32_t bad;
   __shared__ int wsum[PS_T / 64], rs[PS_LMAX + 1], runseg[PS_LMAX];
   __shared__ int s_gbase, s_segbase, s_gcnt, s_trick, s_nlive, s_nseg;
-  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (g == 0)
+  // blockIdx.y = slice: every slice of an image compacts the image's entries (LDS), then ranks and
+  // writes its own share -- the dependent binary-search chains run on S CUs per image, not one
+  const int g = blockIdx.x, sl = blockIdx.y, S = gridDim.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (g == 0 && sl == 0)
     for (int k = tid; k < G * L; k += PS_T) tab2[k] = 0;  // the post pass's counters
   if (tid == 0) {
     bad = 0;
@@ -776,12 +777,14 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
   __syncthreads();
   const int gbase = s_gbase, gc = s_gcnt, trick = s_trick, nlive = s_nlive, nseg = s_nseg, segbase = s_segbase;
   // segment starts: one per non-empty level run, or one for a coordinate-trick image
-  if (trick) {
-    if (tid == 0 && gc > 0) seg_start[segbase] = gbase;
-  } else if (tid < L && tab[g * L + tid]) {
-    seg_start[segbase + runseg[tid]] = gbase + rs[tid];
+  if (sl == 0) {
+    if (trick) {
+      if (tid == 0 && gc > 0) seg_start[segbase] = gbase;
+    } else if (tid < L && tab[g * L + tid]) {
+      seg_start[segbase + runseg[tid]] = gbase + rs[tid];
+    }
   }
-  if (g == G - 1 && tid == 0) {
+  if (g == G - 1 && sl == 0 && tid == 0) {
     *nseg_out = nseg;
     seg_start[nseg] = nlive;
     if (nlive < n) seg_start[nseg + 1] = nlive;  // the tail's empty pseudo-segment
@@ -794,7 +797,7 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
   const uint32_t badm = bad;
   const float step = unord_f32(tab[G * L + g]) + 1.0f;
   // positions, 8 entries per thread per round: ranks from LDS, then all 8 gathers in flight
-  for (int q0 = 0; q0 < gc; q0 += 8 * PS_T) {
+  for (int q0 = sl * 8 * PS_T; q0 < gc; q0 += S * 8 * PS_T) {
     int pos[8], ii[8], ll[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -839,7 +842,7 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_pre_kernel(
       incl[pos[e]] = segbase + runseg[ll[e]] + 1;
     }
   }
-  for (int p = nlive + g * PS_T + tid; p < n; p += G * PS_T) incl[p] = nseg + 1;  // empty pseudo-segment
+  for (int p = nlive + (g * S + sl) * PS_T + tid; p < n; p += G * S * PS_T) incl[p] = nseg + 1;  // empty pseudo-segment
 }
 
 // one workgroup per image: survivors (flags) -> keep in (image, score desc, index) order, num_keep,
@@ -854,7 +857,7 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_post_kernel(
   __shared__ uint32_t bad;
   __shared__ int wsum[PS_T / 64], rs[PS_LMAX + 1];
   __shared__ int s_sbase, s_sc, s_total;
-  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = blockIdx.x, sl = blockIdx.y, S = gridDim.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) {
     bad = 0;
     int tot = 0;
@@ -884,20 +887,20 @@ __global__ void __launch_bounds__(PS_T) nms_sorted_post_kernel(
   ps_check_runs(key, rs, L, sc, tid, &bad);
   __syncthreads();
   const uint32_t badm = bad;
-  for (int q = tid; q < sc; q += PS_T) {
+  for (int q = sl * PS_T + tid; q < sc; q += S * PS_T) {
     const uint32_t x = key[q];
     int rank = 0;
     for (int l2 = 0; l2 < L; ++l2) rank += ps_before(key, rs[l2], rs[l2 + 1], x, q, (badm >> l2) & 1u);
     keep[sbase + rank] = idx[q];
+    if (sel && rank < post && !failed) sel[(int64_t)g * post + rank] = idx[q];
   }
   // -1: a segment exceeded max_seg (the scan's overflow flag); -2: the presorted layout contract broken
-  if (g == 0 && tid == 0) *num_keep = failed ? -2 : (*nk32 < 0 ? -1 : total);
-  for (int p = total + g * PS_T + tid; p < n; p += G * PS_T) keep[p] = 0;
-  if (sel) {
-    __syncthreads();  // this block's keep entries
-    for (int r = tid; r < post; r += PS_T) {
+  if (g == 0 && sl == 0 && tid == 0) *num_keep = failed ? -2 : (*nk32 < 0 ? -1 : total);
+  for (int p = total + (g * S + sl) * PS_T + tid; p < n; p += G * S * PS_T) keep[p] = 0;
+  if (sel) {  // ranks < min(post, count) were written above by the slice that ranked them
+    for (int r = sl * PS_T + tid; r < post; r += S * PS_T) {
       const bool ok = r < sc && !failed;
-      sel[(int64_t)g * post + r] = ok ? keep[sbase + r] : 0;
+      if (!ok) sel[(int64_t)g * post + r] = 0;
       valid[(int64_t)g * post + r] = ok ? 1 : 0;
     }
   }
@@ -912,6 +915,7 @@ struct NmsWs {
   uint32_t* gmax;
   float4 *obox, *sbox;
   float* sarea;
+  uint64_t* colm;  // column form of the diagonal mask tiles (wave scan)
   void* cub;
   size_t cub_bytes;
 };
@@ -938,6 +942,7 @@ static size_t carve(Carver& c, int64_t n, int Wm, NmsWs* w, int G = 0) {
   w->maxbits = c.take<uint32_t>(1);
   w->obox = c.take<float4>(m); w->sbox = c.take<float4>(m); w->sarea = c.take<float>(m);
   w->mask = c.take<uint64_t>((size_t)m * Wm);
+  w->colm = c.take<uint64_t>(m);
   w->cub_bytes = cub_bytes_needed(m);
   w->cub = c.take<char>(w->cub_bytes);
   return c.off;
@@ -997,12 +1002,13 @@ extern "C" int mx_batched_nms(const float* boxes, const float* scores, const int
   nms_seg_kernel<<<nb, T, 0, s>>>(w.head, w.incl, n, w.seg_start, w.nseg);
   MX_LAUNCH_CHECK();
   dim3 mg((unsigned)cdiv(n, 64), (unsigned)Wm);
-  nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask);
+  nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask,
+                                    Wm <= SCAN_WAVE_W ? w.colm : nullptr);
   MX_LAUNCH_CHECK();
   int sgrid = (int)std::min<int64_t>(n, 1024);
   if (Wm <= SCAN_WAVE_W)
     nms_scan_wave_kernel<<<sgrid, 64, (size_t)SCAN_RING * SCAN_SLOT, s>>>(w.mask, w.seg_start, w.nseg, w.v1,
-                                                                                   Wm, w.flags, w.nk);
+                                                                                   w.colm, Wm, w.flags, w.nk);
   else if (Wm <= SCAN_LDS_W)
     nms_scan_lds_kernel<<<sgrid, 256, sizeof(uint64_t) * (Wm + 64 * (size_t)Wm), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
                                                                                        Wm, w.flags, w.nk);
@@ -1054,16 +1060,18 @@ extern "C" int mx_batched_nms_grouped_sorted(const float* boxes, const float* sc
   nms_sorted_stats_kernel<<<nb, 256, 0, s>>>((const float4*)boxes, lvl, group, (int)n, (int)G, (int)L, tab, w.flags, w.nk);
   MX_LAUNCH_CHECK();
   const size_t lds = (sizeof(uint32_t) + sizeof(uint16_t)) * (size_t)n + 16;
-  nms_sorted_pre_kernel<<<(int)G, PS_T, lds, s>>>((const float4*)boxes, scores, lvl, group, (int)n, (int)G, (int)L, tab,
+  const dim3 pg((unsigned)G, (unsigned)PS_SLICES);
+  nms_sorted_pre_kernel<<<pg, PS_T, lds, s>>>((const float4*)boxes, scores, lvl, group, (int)n, (int)G, (int)L, tab,
                                                   tab2, w.sbox, w.sarea, w.v1, w.incl, w.seg_start, w.nseg, err);
   MX_LAUNCH_CHECK();
   dim3 mg((unsigned)cdiv(n, 64), (unsigned)Wm);
-  nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask);
+  nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask,
+                                    Wm <= SCAN_WAVE_W ? w.colm : nullptr);
   MX_LAUNCH_CHECK();
   const int sgrid = (int)std::min<int64_t>(n, 1024);
   if (Wm <= SCAN_WAVE_W)
     nms_scan_wave_kernel<<<sgrid, 64, (size_t)SCAN_RING * SCAN_SLOT, s>>>(w.mask, w.seg_start, w.nseg, w.v1,
-                                                                                   Wm, w.flags, w.nk);
+                                                                                   w.colm, Wm, w.flags, w.nk);
   else if (Wm <= SCAN_LDS_W)
     nms_scan_lds_kernel<<<sgrid, 256, sizeof(uint64_t) * (Wm + 64 * (size_t)Wm), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
                                                                                        Wm, w.flags, w.nk);
@@ -1072,7 +1080,7 @@ extern "C" int mx_batched_nms_grouped_sorted(const float* boxes, const float* sc
   MX_LAUNCH_CHECK();
   nms_sorted_post_stats_kernel<<<nb, 256, 0, s>>>(lvl, group, w.flags, (int)n, (int)G, (int)L, tab2);
   MX_LAUNCH_CHECK();
-  nms_sorted_post_kernel<<<(int)G, PS_T, lds, s>>>(scores, group, w.flags, (int)n, (int)G, (int)L, tab2, w.nk, err,
+  nms_sorted_post_kernel<<<pg, PS_T, lds, s>>>(scores, group, w.flags, (int)n, (int)G, (int)L, tab2, w.nk, err,
                                                    keep, num_keep, (int)post, post > 0 ? sel : nullptr,
                                                    post > 0 ? valid : nullptr);
   MX_LAUNCH_CHECK();
@@ -1124,12 +1132,13 @@ extern "C" int mx_batched_nms_grouped(const float* boxes, const float* scores, c
   nms_seg_kernel<<<nb, T, 0, s>>>(w.head, w.incl, n, w.seg_start, w.nseg);
   MX_LAUNCH_CHECK();
   dim3 mg((unsigned)cdiv(n, 64), (unsigned)Wm);
-  nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask);
+  nms_mask_kernel<<<mg, 64, 0, s>>>(w.sbox, w.sarea, w.incl, w.seg_start, n, Wm, thr, w.mask,
+                                    Wm <= SCAN_WAVE_W ? w.colm : nullptr);
   MX_LAUNCH_CHECK();
   const int sgrid = (int)std::min<int64_t>(n, 1024);
   if (Wm <= SCAN_WAVE_W)
     nms_scan_wave_kernel<<<sgrid, 64, (size_t)SCAN_RING * SCAN_SLOT, s>>>(w.mask, w.seg_start, w.nseg, w.v1,
-                                                                                   Wm, w.flags, w.nk);
+                                                                                   w.colm, Wm, w.flags, w.nk);
   else if (Wm <= SCAN_LDS_W)
     nms_scan_lds_kernel<<<sgrid, 256, sizeof(uint64_t) * (Wm + 64 * (size_t)Wm), s>>>(w.mask, w.seg_start, w.nseg, w.v1,
                                                                                        Wm, w.flags, w.nk);
