@@ -14,6 +14,7 @@ running buffers), so state_dicts load both ways; the kernels ta
 """
 import ctypes
 import os
+import threading
 import weakref
 
 import torch
@@ -778,6 +779,10 @@ class ConvAct(torch.autograd.Function):
 
 _scratch = {}
 _capture_streams = {}
+# held for the duration of every graph capture (frcnn._Graphs / _SegGraphs) and by other threads that
+# issue device work (engine.PrefetchJpegLoader's stager): HIP's global capture mode rejects stream /
+# allocation calls made from any thread while a capture is open
+capture_lock = threading.RLock()
 
 
 def capture_stream(device):

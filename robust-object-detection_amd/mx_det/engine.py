@@ -215,6 +215,7 @@ def train_frcnn(cfg):
     # is synchronised and t0 taken, at the end of training t1 and the number of timed steps
     timer = cfg.get("TIMER")
     n_batches = len(train_loader)
+    kick = getattr(train_loader, "kick", None)
     for epoch in range(1, cfg["EPOCHS"] + 1):
         if sampler is not None:
             sampler.set_epoch(epoch)
@@ -228,6 +229,8 @@ def train_frcnn(cfg):
             losses = sum(loss for loss in loss_dict.values())
             optimizer.zero_grad(set_to_none=True)
             losses.backward()
+            if kick is not None:  # the backward is queued: stage the next batch while it runs
+                kick()
             if world > 1:
                 ddp.sync_gradients()
             if it_global < warmup:  # linear warm-up of the scaled LR (epoch 1 only at the default length)
@@ -346,19 +349,54 @@ def _host_decode(b):
         return None, np.asarray(Image.open(io.BytesIO(b.tobytes())).convert("RGB")).copy()
 
 
+def _pack_targets(targets, pin=True):
+    """A batch's target dicts as ONE pinned byte buffer (each tensor 8-B aligned) + its layout: one
+    host -> HBM copy per batch instead of one per tensor (~11 us of issue each)."""
+    layout, off = [], 0
+    for t in targets:
+        ent = []
+        for k, v in t.items():
+            v = v.contiguous()
+            nb = v.numel() * v.element_size()
+            ent.append((k, v, off, nb))
+            off += (nb + 7) & ~7
+        layout.append(ent)
+    buf = torch.empty(max(off, 8), dtype=torch.uint8, pin_memory=pin)
+    for ent in layout:
+        for k, v, o, nb in ent:
+            if nb:
+                buf[o:o + nb].copy_(v.reshape(-1).view(torch.uint8))
+    return buf, [[(k, v.dtype, tuple(v.shape), o, nb) for k, v, o, nb in ent] for ent in layout]
+
+
+def _unpack_targets(dbuf, layout):
+    """Device views of the packed targets: same keys, dtypes and shapes as the loader's tensors."""
+    return [{k: dbuf[o:o + nb].view(dt).view(shape) for k, dt, shape, o, nb in ent} for ent in layout]
+
+
 class PrefetchJpegLoader:
     """The training input pipeline on the device (coco_detection_dataset.py:23 + train_frcnn_*.py's
     DataLoader): a loader of (file bytes, target) batches -> (uint8 HWC device images, device targets).
     A producer thread runs the loader (file reads, COCO target tensors), pins the targets and hands
     each image's host entropy decode to `workers` threads (the ctypes decoder releases the GIL), up to
-    `depth` batches ahead; the main thread only issues each batch's pinned -> HBM copies and the
-    device IDCT / upsampling / colour launches (mx_det.jpeg.device_stage) on the current stream, so
-    the training step never waits for host data work that had a step's time to finish. Pixels are
-    bit-identical to PIL's decode (tests/test_jpeg.py)."""
+    `depth` batches ahead; a stager thread issues each decoded batch's pinned -> HBM copies and the
+    device IDCT / upsampling / colour launches (mx_det.jpeg.device_stage) on a loader stream, one
+    batch ahead, so the training thread neither waits for host data work that had a step's time to
+    finish nor spends the GPU-idle time after its own host syncs issuing it. Pixels are bit-identical
+    to PIL's decode (tests/test_jpeg.py)."""
 
     def __init__(self, loader, dev, workers=4, depth=2):
+        import threading
         self.loader, self.dev, self.workers, self.depth = loader, dev, int(workers), int(depth)
         self.wait_s = 0.0  # time the consuming thread spent waiting for host data (bench.py --mode script)
+        self._kick = threading.Event()
+
+    def kick(self):
+        """Let the stager issue the next batch's device stage now: called by the training loop once a
+        step's backward is queued (train_frcnn), so the stage's host work overlaps the GPU's backward
+        instead of the GPU-idle start of the next step. Without kicks the consumer kicks when it runs
+        dry (staging then happens at the step start)."""
+        self._kick.set()
 
     def __len__(self):
         return len(self.loader)
@@ -390,8 +428,7 @@ class PrefetchJpegLoader:
                 with ThreadPoolExecutor(max(1, self.workers)) as pool:
                     for images, targets in self.loader:
                         futs = [pool.submit(_host_decode, b) for b in images]
-                        tgs = [{k: v.pin_memory() for k, v in t.items()} for t in targets]
-                        if not put((futs, tgs)):
+                        if not put((futs, _pack_targets(targets))):
                             return
             except BaseException as e:  # surfaced in the consuming thread
                 put(e)
@@ -400,58 +437,74 @@ class PrefetchJpegLoader:
 
         th = threading.Thread(target=produce, name="mx-prefetch", daemon=True)
         th.start()
-        # device stage on a loader stream: batch i+1's coefficient / target copies and IDCT launches are
-        # issued before batch i is handed out (when its host decode has finished), so they run beside
-        # step i's kernels; the training stream waits on the batch's event
+        # device stage on a loader stream, issued by a stager thread as soon as a batch's host decode is
+        # done: its coefficient / target copies and IDCT launches run beside the training step's kernels
+        # and their host cost falls in the training thread's blocking syncs (loss.item(), the RoI
+        # sampler's counts) instead of the GPU-idle stretch after them; the training stream waits on
+        # the batch's event. One staged batch ahead (bounded HBM for staged images).
+        from .conv import capture_lock
         ls = torch.cuda.Stream(device=self.dev)
+        staged = queue.Queue(maxsize=1)
+
+        def put_staged(item):
+            while not stop.is_set():
+                try:
+                    staged.put(item, timeout=0.1)
+                    return True
+                except queue.Full:
+                    pass
+            return False
 
         def stage(item):
-            futs, tgs = item
-            with torch.cuda.stream(ls):
-                imgs = []
-                for f in futs:
-                    t0 = time.perf_counter()
-                    info, host = f.result()
-                    self.wait_s += time.perf_counter() - t0
-                    imgs.append(torch.from_numpy(host).to(self.dev) if info is None
-                                else jpeg.device_stage(info, host, self.dev))
-                tg = [{k: v.to(self.dev, non_blocking=True) for k, v in t.items()} for t in tgs]
+            futs, (tbuf, layout) = item
+            done = [f.result() for f in futs]
+            with capture_lock, torch.cuda.device(self.dev), torch.cuda.stream(ls):
+                imgs = [torch.from_numpy(host).to(self.dev) if info is None else jpeg.device_stage(info, host, self.dev)
+                        for info, host in done]
+                tg = _unpack_targets(tbuf.to(self.dev, non_blocking=True), layout)
                 ev = torch.cuda.Event()
                 ev.record(ls)
             return imgs, tg, ev
 
-        def take(block):
-            """next queue item: a staged batch, None (end), or an exception; with block=False, the
-            string "later" when the next batch is not decoded yet."""
-            if not block:
-                try:
-                    item = q.get_nowait()
-                except queue.Empty:
-                    return "later"
-                if isinstance(item, tuple) and not all(f.done() for f in item[0]):
-                    pending.append(item)
-                    return "later"
-            else:
-                t0 = time.perf_counter()
-                item = pending.pop() if pending else q.get()
-                self.wait_s += time.perf_counter() - t0
-            return stage(item) if isinstance(item, tuple) else item
+        def stager():
+            try:
+                while not stop.is_set():
+                    try:
+                        item = q.get(timeout=0.1)
+                    except queue.Empty:
+                        continue
+                    if isinstance(item, tuple):
+                        # wait for the training loop's kick (its backward is queued: the GPU is busy
+                        # and the training thread about to block), or for the consumer to run dry
+                        while not self._kick.wait(0.1):
+                            if stop.is_set():
+                                return
+                        self._kick.clear()
+                        item = stage(item)
+                    if not put_staged(item) or item is None or isinstance(item, BaseException):
+                        return
+            except BaseException as e:  # surfaced in the consuming thread
+                put_staged(e)
 
-        pending = []
+        st = threading.Thread(target=stager, name="mx-stage", daemon=True)
+        st.start()
         try:
-            nxt = take(True)
-            while nxt is not None:
-                if isinstance(nxt, BaseException):
-                    raise nxt
-                imgs, tg, ev = nxt
-                nxt = take(False)  # stage the following batch now if it is ready
+            while True:
+                t0 = time.perf_counter()
+                if staged.empty():
+                    self.kick()
+                item = staged.get()
+                self.wait_s += time.perf_counter() - t0
+                if item is None:
+                    break
+                if isinstance(item, BaseException):
+                    raise item
+                imgs, tg, ev = item
                 main = torch.cuda.current_stream(self.dev)
                 main.wait_event(ev)
                 for t in imgs + [v for d in tg for v in d.values()]:
                     t.record_stream(main)
                 yield imgs, tg
-                if isinstance(nxt, str):
-                    nxt = take(True)
         finally:
             stop.set()
             sys.setswitchinterval(old_switch)

@@ -243,13 +243,35 @@ def test_prefetch_loader_matches_pil(dev, tmp_path):
     ann = write_coco_split(tmp_path, "train", 0, 5, H=120, W=176, mean_boxes=6)
     raw = COCODetectionDataset(str(tmp_path / "images/train"), str(ann), transforms=uint8_transform, raw=True)
     ref = COCODetectionDataset(str(tmp_path / "images/train"), str(ann), transforms=uint8_transform)
-    loader = PrefetchJpegLoader(DataLoader(raw, batch_size=2, shuffle=False, collate_fn=collate_fn), dev, workers=3)
-    seen = 0
-    for images, targets in loader:
-        for im, t in zip(images, targets):
-            r_img, r_t = ref[seen]
-            assert im.device.type == "cuda" and torch.equal(im.cpu(), r_img)
-            for k in r_t:
-                assert torch.equal(t[k].cpu(), r_t[k]), k
-            seen += 1
-    assert seen == 5
+    for kicked in (False, True):  # staging when the consumer runs dry / on the training loop's kick
+        loader = PrefetchJpegLoader(DataLoader(raw, batch_size=2, shuffle=False, collate_fn=collate_fn), dev,
+                                    workers=3)
+        seen = 0
+        for images, targets in loader:
+            for im, t in zip(images, targets):
+                r_img, r_t = ref[seen]
+                assert im.device.type == "cuda" and torch.equal(im.cpu(), r_img)
+                assert sorted(t) == sorted(r_t)
+                for k in r_t:
+                    assert t[k].dtype == r_t[k].dtype and torch.equal(t[k].cpu(), r_t[k]), k
+                seen += 1
+            if kicked:
+                loader.kick()
+        assert seen == 5
+
+
+def test_pack_targets_roundtrip():
+    """engine._pack_targets / _unpack_targets: one byte buffer per batch, views with the loader's keys,
+    dtypes, shapes and values (empty targets included)."""
+    from mx_det.engine import _pack_targets, _unpack_targets
+    t = [{"boxes": torch.rand(3, 4), "labels": torch.tensor([1, 2, 3]), "image_id": torch.tensor([7]),
+          "area": torch.rand(3), "iscrowd": torch.zeros(3, dtype=torch.int64)},
+         {"boxes": torch.zeros((0, 4)), "labels": torch.zeros((0,), dtype=torch.int64),
+          "image_id": torch.tensor([8]), "area": torch.zeros(0), "iscrowd": torch.zeros(0, dtype=torch.int64)}]
+    buf, layout = _pack_targets(t, pin=False)
+    assert buf.dtype == torch.uint8 and buf.dim() == 1
+    out = _unpack_targets(buf.clone(), layout)
+    for a, b in zip(t, out):
+        assert list(a) == list(b)
+        for k in a:
+            assert a[k].dtype == b[k].dtype and a[k].shape == b[k].shape and torch.equal(a[k], b[k]), k
