@@ -609,7 +609,8 @@ def script_main(args, world, rank, dev, imgs, tg):
     train_frcnn_augmented.py:120-216 with RandomCorruption on the device) for one epoch over an on-disk
     synthetic VisDrone-COCO set of 1333x800 JPEGs (q95, written by rank 0 first): file read, host
     entropy decode prefetched on threads, device IDCT, corruption, the train step, loss.item(). The
-    first W optimizer steps are warm-up; the K after them are timed (engine TIMER hook). For comparison
+    first W optimizer steps are warm-up; the K after them are timed (engine TIMER hook: the clock stops
+    with the last step; the once-per-epoch tail -- history line, last.pth -- is reported as epoch_end_ms). For comparison
     the same process then times the bench's own augmented step on HBM-resident images."""
     import tempfile
     from pathlib import Path
@@ -670,6 +671,8 @@ def script_main(args, world, rank, dev, imgs, tg):
     rec["script_over_bench_step"] = round(rec["value"] / rec["bench_step"]["value"], 4)
     if "loader_wait_s" in cfg["TIMER"]:
         rec["loader_wait_ms_per_step"] = round(1000 * cfg["TIMER"]["loader_wait_s"] / steps, 3)
+    # outside the clock: the once-per-epoch tail (LR step, history line, last.pth checkpoint)
+    rec["epoch_end_ms"] = round(1000 * cfg["TIMER"]["epoch_end_s"], 1)
     _barrier(world)
     if rank == 0:
         shutil.rmtree(tmp, ignore_errors=True)
