@@ -30,6 +30,14 @@ void set_error(const char* fmt, ...);
 #define MX_LAUNCH_CHECK() MX_HIP(hipGetLastError())
 
 // bf16 helpers (bit-level; round-to-nearest-even like v_cvt_pk_bf16_f32)
+// XCD-aware bijective remap of a linear block id (cdna_hip_programming.md §5 / T1): the blocks one
+// XCD receives (id % 8) get one contiguous run of work indices, in dispatch order
+__device__ __forceinline__ int64_t xcd_remap(int64_t id, int64_t nwg) {
+  if (nwg < 8) return id;
+  int64_t q = nwg / 8, r = nwg % 8, xcd = id % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
+}
+
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {
   uint32_t u = __float_as_uint(f);

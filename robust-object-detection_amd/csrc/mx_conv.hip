@@ -94,13 +94,6 @@ __device__ __forceinline__ float act_f(float v, int act) {
   return v;
 }
 
-// XCD-aware bijective remap of a linear block id (cdna_hip_programming.md §5 / T1)
-__device__ __forceinline__ int64_t xcd_remap(int64_t id, int64_t nwg) {
-  if (nwg < 8) return id;
-  int64_t q = nwg / 8, r = nwg % 8, xcd = id % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
-}
-
 // MODE 0 fwd: x[n, oh*st - pad + r, ow*st - pad + s]; MODE 1 dgrad of one stride-parity class
 // (rows = the class's (n, hh, ww) grid, taps = the class's (ri, si), pad = the class offset dh/dw):
 // dy[n, hh + dh - ri, ww + dw - si] — a dense stride-1 correlation, no wasted taps.
