@@ -126,6 +126,18 @@ class ResNet50Body(nn.Module):
         return out
 
 
+_aux_streams = {}
+
+
+def _aux_stream(device):
+    """The RPN loss chain's side stream, one per device."""
+    device = torch.device(device)
+    s = _aux_streams.get(device)
+    if s is None:
+        s = _aux_streams[device] = torch.cuda.Stream(device=device)
+    return s
+
+
 def _side_streams(knob):
     """Concurrent small levels (the FPN's P3..P6 output blocks, the RPN head's canvas chain) on side
     streams: on by default (knob "0" turns it off) and off while mc's per-launch timer is installed
@@ -557,13 +569,31 @@ class RegionProposalNetwork(nn.Module):
             return {"loss_objectness": torch.where(sm, obj, 0.0).sum() / cnt,
                     "loss_rpn_box_reg": torch.where(pm, bl, 0.0).sum() / cnt}
 
-        losses = compute_losses if defer_losses else compute_losses()
+        side = None
+        if (self.training and not defer_losses and objectness.is_cuda and getattr(be, "name", "") == "hip"
+                and _side_streams("MX_RPN_LOSS_STREAM")):
+            # the target / sampler / loss chain (~25 small launches: anchor matching, the sampler's
+            # top-k, the fused loss) on a side stream beside the proposal chain (decode, per-level
+            # top-k, NMS, selection): two latency-bound chains of small kernels overlap. Same launches,
+            # same RNG draws in the same host order; autograd runs the loss backward on this stream
+            # and syncs its gradients into the trunk graph's outputs.
+            main = torch.cuda.current_stream()
+            side = _aux_stream(objectness.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                losses = compute_losses()
+        else:
+            losses = compute_losses if defer_losses else compute_losses()
         proposals = be.box_decode(pred_deltas.detach().reshape(-1, 4), anchors.repeat(N, 1), RPN_WEIGHTS)
         proposals = proposals.view(N, A, 4)
         if self.training:  # padded (boxes, scores, valid): the RoI sampler works on the device
             boxes = self.filter_proposals_padded(proposals, objectness, images.image_sizes, num_per_level, be)
         else:
             boxes, _ = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
+        if side is not None:  # the loss values are consumed on the main stream (the loss sum)
+            for v in losses.values():
+                v.record_stream(main)
+            main.wait_stream(side)
         return boxes, losses
 
 
