@@ -593,8 +593,14 @@ class RegionProposalNetwork(nn.Module):
         if side is not None:  # the loss values are consumed on the main stream (the loss sum)
             for v in losses.values():
                 v.record_stream(main)
-            main.wait_stream(side)
+            self._loss_side = side  # joined by join_losses(): after the RoI head, not before its host sync
         return boxes, losses
+
+    def join_losses(self):
+        """Make the current stream wait for the side-stream loss chain (a no-op without one)."""
+        side = self.__dict__.pop("_loss_side", None)
+        if side is not None:
+            torch.cuda.current_stream(side.device).wait_stream(side)
 
 
 # ------------------------------------------------------------------------------------------ RoI heads
@@ -1034,6 +1040,7 @@ class FasterRCNN(nn.Module):
             if bool(host):
                 raise ValueError("All bounding boxes should have positive height and width.")
         detections, det_losses = self.roi_heads(features, proposals, il.image_sizes, targets, be)
+        self.rpn.join_losses()
         if self.training:
             losses = {}
             losses.update(det_losses)
