@@ -12,7 +12,9 @@ The parameters keep torchvision's shapes ([Cout, Cin, kh, kw] conv weights, Batc
 running buffers), so state_dicts load both ways; the kernels take KRSC bf16 copies
 (split into hi / lo planes in f32 mode) made once per step.
 """
+import contextlib
 import ctypes
+import gc
 import os
 import threading
 import weakref
@@ -783,6 +785,20 @@ _capture_streams = {}
 # issue device work (engine.PrefetchJpegLoader's stager): HIP's global capture mode rejects stream /
 # allocation calls made from any thread while a capture is open
 capture_lock = threading.RLock()
+
+
+@contextlib.contextmanager
+def capture_guard():
+    """Around every graph capture: capture_lock, and Python's cyclic GC paused -- a collection inside
+    the capture could destroy an earlier step's graph or free its tensors mid-capture."""
+    with capture_lock:
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            yield
+        finally:
+            if was:
+                gc.enable()
 
 
 def capture_stream(device):

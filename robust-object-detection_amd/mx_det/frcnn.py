@@ -1113,12 +1113,12 @@ class _Graphs:
         torch.cuda.current_stream().wait_stream(side)
         pool = torch.cuda.graph_pool_handle()
         self.fwd = torch.cuda.CUDAGraph()
-        with mc.capture_lock, torch.cuda.graph(self.fwd, pool=pool, stream=side), mc.absorb_mode():
+        with mc.capture_guard(), torch.cuda.graph(self.fwd, pool=pool, stream=side), mc.absorb_mode():
             self.static_out = fn(self.static_x)
         self.static_gout = [torch.zeros_like(o) for o in self.static_out]
         roots, groots = _absorb_roots(fn, self.static_out, self.static_gout)
         self.bwd = torch.cuda.CUDAGraph()
-        with mc.capture_lock, torch.cuda.graph(self.bwd, pool=pool, stream=side):
+        with mc.capture_guard(), torch.cuda.graph(self.bwd, pool=pool, stream=side):
             torch.autograd.backward(roots, groots)
         self.static_grads = [p.grad for p in self.params]
         self.static_xgrad = self.static_x.grad
@@ -1259,14 +1259,14 @@ class _SegGraphs:
         torch.cuda.current_stream().wait_stream(side)
         pool = torch.cuda.graph_pool_handle()
         self.fwd = torch.cuda.CUDAGraph()
-        with mc.capture_lock, torch.cuda.graph(self.fwd, pool=pool, stream=side), mc.absorb_mode():
+        with mc.capture_guard(), torch.cuda.graph(self.fwd, pool=pool, stream=side), mc.absorb_mode():
             outs, self.leaves, self.cs = self._fwd(self.static_x)
         self.static_gout = [torch.zeros_like(o) for o in outs]
         r0, g0 = _absorb_roots(self.model.rpn.head, outs, self.static_gout)
         self.bwd = []  # (segment key, graph)
         for key, roots, groots in self._bwd_plan(outs, self.static_gout, self.leaves, self.cs, (r0, g0)):
             g = torch.cuda.CUDAGraph()
-            with mc.capture_lock, torch.cuda.graph(g, pool=pool, stream=side):
+            with mc.capture_guard(), torch.cuda.graph(g, pool=pool, stream=side):
                 torch.autograd.backward(roots, groots())
             self.bwd.append((key, g))
         self.static_out = tuple(o.detach() for o in outs)
