@@ -41,6 +41,11 @@ int mx_version(void);
 const char* mx_last_error(void);
 /* Launches an empty kernel (trace_marker_kernel) on `stream`: a marker in rocprofv3 kernel traces. */
 int mx_trace_marker(int id, mx_stream_t stream);
+/* A dedicated non-blocking HIP stream on `device` (never destroyed: the process's side streams). The
+ * framework's own streams come from here, not from torch's round-robin pool of 32 streams per device:
+ * a process creating more pool streams than that (a model per test, a loader per epoch) would alias
+ * two of them -- e.g. a side stream with a graph's capture stream. */
+int mx_stream_create(int device, mx_stream_t* out);
 
 /* ---------------------------------------------------------------------------------------------
  * Anchor assignment: torchvision box_iou + Matcher (+ label/target construction), fused.

@@ -713,3 +713,16 @@ extern "C" int mx_trace_marker(int id, mx_stream_t stream) {
   MX_LAUNCH_CHECK();
   return MX_OK;
 }
+
+extern "C" int mx_stream_create(int device, mx_stream_t* out) {
+  MX_CHECK_ARG(out != nullptr, "mx_stream_create: null output");
+  int prev = 0;
+  MX_HIP(hipGetDevice(&prev));
+  MX_HIP(hipSetDevice(device));
+  hipStream_t s = nullptr;
+  const hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  MX_HIP(hipSetDevice(prev));
+  MX_HIP(e);
+  *out = (mx_stream_t)s;
+  return MX_OK;
+}

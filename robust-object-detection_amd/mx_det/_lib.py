@@ -43,6 +43,7 @@ _SIGS = {
     "mx_version": (c_int, []),
     "mx_last_error": (ctypes.c_char_p, []),
     "mx_trace_marker": (c_int, [c_int, c_vp]),
+    "mx_stream_create": (c_int, [c_int, c_vp]),
     "mx_match_workspace": (c_sz, [c_i64, c_i64]),
     "mx_match_assign": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_f, c_f, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                 c_vp, c_sz, c_vp]),

@@ -476,7 +476,6 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
 # main stream joins the side stream at the end of the backward pass (an autograd engine callback);
 # the operands stay referenced until then. Single-process only: DDP's reducer reads each gradient
 # from its AccumulateGrad hook on the main stream, so multi-rank runs keep wgrad in order.
-_side = {}
 _pending = []
 # The side-stream wgrad's dw reaches AccumulateGrad from the side stream; the backward's end-of-pass
 # callback (_join_side) makes the main stream wait for it, so torch's "AccumulateGrad node's stream does
@@ -565,9 +564,7 @@ def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False):
     ws = torch.empty(wsb, dtype=torch.uint8, device=x.device) if wsb else None
     stream = _s()
     if side:
-        st = _side.get(x.device)
-        if st is None:
-            st = _side[x.device] = torch.cuda.Stream(device=x.device)
+        st = dedicated_stream(x.device, "wgrad")
         st.wait_stream(torch.cuda.current_stream())
         stream = st.cuda_stream
     call(entry, ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws), wsb, stream)
@@ -780,7 +777,6 @@ class ConvAct(torch.autograd.Function):
 
 
 _scratch = {}
-_capture_streams = {}
 # held for the duration of every graph capture (frcnn._Graphs / _SegGraphs) and by other threads that
 # issue device work (engine.PrefetchJpegLoader's stager): HIP's global capture mode rejects stream /
 # allocation calls made from any thread while a capture is open
@@ -805,10 +801,25 @@ def capture_stream(device):
     """The stream graph captures (frcnn._Graphs / _SegGraphs) warm up AND capture on, one per device:
     the warm-up allocates this stream's reduction scratch (bn_scratch) outside any capture, so no
     workspace is ever allocated from a graph's private pool."""
+    return dedicated_stream(device, "capture")
+
+
+_dedicated = {}
+
+
+def dedicated_stream(device, name):
+    """The framework's side stream `name` on `device`: a HIP stream of its own (mx_stream_create),
+    created once. torch.cuda.Stream() hands out a round-robin pool of 32 streams per device, so a
+    process that creates more (a model per test, a loader per epoch) silently aliases two of them --
+    measured: a graph capture crashed in hipStreamEndCapture once a newer pool stream aliased the
+    capture stream's neighbours. Dedicated streams never alias each other or a pool stream."""
     device = torch.device(device)
-    s = _capture_streams.get(device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _dedicated.get((idx, name))
     if s is None:
-        s = _capture_streams[device] = torch.cuda.Stream(device=device)
+        h = ctypes.c_void_p()
+        call("mx_stream_create", idx, ctypes.addressof(h))
+        s = _dedicated[(idx, name)] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
     return s
 
 

@@ -449,7 +449,8 @@ class PrefetchJpegLoader:
         # sampler's counts) instead of the GPU-idle stretch after them; the training stream waits on
         # the batch's event. One staged batch ahead (bounded HBM for staged images).
         from .conv import capture_lock
-        ls = torch.cuda.Stream(device=self.dev)
+        from .conv import dedicated_stream
+        ls = dedicated_stream(self.dev, "loader")
         staged = queue.Queue(maxsize=1)
 
         def put_staged(item):

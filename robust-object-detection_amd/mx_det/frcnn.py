@@ -126,16 +126,9 @@ class ResNet50Body(nn.Module):
         return out
 
 
-_aux_streams = {}
-
-
 def _aux_stream(device):
     """The RPN loss chain's side stream, one per device."""
-    device = torch.device(device)
-    s = _aux_streams.get(device)
-    if s is None:
-        s = _aux_streams[device] = torch.cuda.Stream(device=device)
-    return s
+    return mc.dedicated_stream(device, "rpn_targets")
 
 
 def _side_streams(knob):
@@ -168,9 +161,7 @@ class FeaturePyramidNetwork(nn.Module):
         if feats[0].is_cuda and getattr(be, "name", "") == "hip" and _side_streams("MX_FPN_STREAMS"):
             # the small levels' 3x3 output blocks (and P6) on a side stream beside the top-down chain
             main = torch.cuda.current_stream()
-            side = self.__dict__.get("_side")
-            if side is None or side.device != feats[0].device:
-                side = self.__dict__["_side"] = torch.cuda.Stream(device=feats[0].device)
+            side = mc.dedicated_stream(feats[0].device, "fpn")
 
         def block(idx, t):
             if side is None or idx == 0:
@@ -306,9 +297,7 @@ class RPNHead(nn.Module):
             # the canvas chain (P3..P6) on a side stream beside level 0's: independent convs that fill
             # each other's tail rounds; autograd runs each backward on its forward's stream
             main = torch.cuda.current_stream()
-            side = self.__dict__.get("_side")
-            if side is None or side.device != cv.device:
-                side = self.__dict__["_side"] = torch.cuda.Stream(device=cv.device)
+            side = mc.dedicated_stream(cv.device, "rpn_head")
             side.wait_stream(main)
             cv.record_stream(side)
             with torch.cuda.stream(side):
@@ -538,10 +527,8 @@ class RegionProposalNetwork(nn.Module):
         N = feats[0].shape[0]
         A = anchors.shape[0]
 
-        def compute_losses():
-            if not self.training:
-                return {}
-            # targets, sampling and losses never wait for the GPU
+        def compute_targets():
+            # targets and sampling never wait for the GPU (no autograd: labels, targets, masks)
             if hasattr(be, "match_assign_batched"):  # every image in one launch pair, zero-padded GT
                 gtp, _, gcnt = _gt_batch(targets, anchors.device)
                 _, lab, rt, lcnt = be.match_assign_batched(gtp, gcnt, anchors, self.fg, self.bg, True, 1,
@@ -557,8 +544,12 @@ class RegionProposalNetwork(nn.Module):
                 lab = torch.stack(labels)                 # [N, A] 1 / 0 / -1
                 rt = torch.stack(reg_targets)             # [N, A, 4]
             pm, nm = self.fg_bg_sampler(lab, counts=lcnt)
+            return lab, rt, pm, nm
+
+        def loss_of(tgt):
             # torchvision: BCE mean over the sampled anchors; smooth-L1 (beta 1/9) sum over the sampled
             # positives / number sampled
+            lab, rt, pm, nm = tgt
             if hasattr(be, "rpn_loss"):  # HIP: one fused launch each way
                 lo, lb = be.rpn_loss(objectness, pred_deltas, lab, rt, pm, nm, 1.0 / 9)
                 return {"loss_objectness": lo, "loss_rpn_box_reg": lb}
@@ -569,19 +560,26 @@ class RegionProposalNetwork(nn.Module):
             return {"loss_objectness": torch.where(sm, obj, 0.0).sum() / cnt,
                     "loss_rpn_box_reg": torch.where(pm, bl, 0.0).sum() / cnt}
 
+        def compute_losses():
+            return loss_of(compute_targets()) if self.training else {}
+
         side = None
         if (self.training and not defer_losses and objectness.is_cuda and getattr(be, "name", "") == "hip"
                 and _side_streams("MX_RPN_LOSS_STREAM")):
-            # the target / sampler / loss chain (~25 small launches: anchor matching, the sampler's
-            # top-k, the fused loss) on a side stream beside the proposal chain (decode, per-level
-            # top-k, NMS, selection): two latency-bound chains of small kernels overlap. Same launches,
-            # same RNG draws in the same host order; autograd runs the loss backward on this stream
-            # and syncs its gradients into the trunk graph's outputs.
+            # the target / sampler chain (~25 small launches: anchor matching, the sampler's top-k) on a
+            # side stream beside the proposal chain (decode, per-level top-k, NMS, selection): two
+            # latency-bound chains of small kernels overlap. Same launches, same RNG draws in the same
+            # host order. The chain holds no autograd op: the fused loss (and so its backward) runs on
+            # the main stream once FasterRCNN.forward has joined the side stream after the RoI head.
+            # Its outputs, allocated on the side stream, need no record_stream: the side stream's next
+            # work (and so any reuse of their blocks) is ordered after the main stream by the
+            # wait_stream below, at the next step's start of this chain.
             main = torch.cuda.current_stream()
             side = _aux_stream(objectness.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                losses = compute_losses()
+                tgt = compute_targets()
+            losses = lambda: loss_of(tgt)  # noqa: E731 (deferred: called after join_losses)
         else:
             losses = compute_losses if defer_losses else compute_losses()
         proposals = be.box_decode(pred_deltas.detach().reshape(-1, 4), anchors.repeat(N, 1), RPN_WEIGHTS)
@@ -590,9 +588,7 @@ class RegionProposalNetwork(nn.Module):
             boxes = self.filter_proposals_padded(proposals, objectness, images.image_sizes, num_per_level, be)
         else:
             boxes, _ = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
-        if side is not None:  # the loss values are consumed on the main stream (the loss sum)
-            for v in losses.values():
-                v.record_stream(main)
+        if side is not None:
             self._loss_side = side  # joined by join_losses(): after the RoI head, not before its host sync
         return boxes, losses
 
