@@ -171,6 +171,13 @@ int mx_multiscale_roi_align_bwd(const void* grad_out, int dtype, float* const* g
  * ------------------------------------------------------------------------------------------- */
 /* One FPN level: cell anchors round([-ws,-hs,ws,hs]/2) for `size` and ratios, shifted by
  * arange*stride; order (y, x, ratio). out[gh*gw*nr, 4]. */
+/* filter_proposals after the per-level top-k (rpn.py): boxes [N*T, 4] = proposals[n][top[n][t]]
+ * clipped to (h, w) = hw[n] (clamp(min=0) then minimum, NaN-propagating as torch), grp [N*T] int32 = n
+ * when the box is at least min_size wide and high and prob >= score_thresh, else N. top [N, T] int64
+ * indices into the A proposals of the image; prob [N, T]; hw [N, 2] (h, w) f32. */
+int mx_proposal_clip_filter(const float* proposals, const int64_t* top, const float* prob, const float* hw,
+                            int64_t N, int64_t A, int64_t T, float min_size, float score_thresh, float* boxes_out,
+                            int32_t* grp_out, mx_stream_t stream);
 int mx_anchors_level(float size, const float* ratios_host, int nr, int64_t gh, int64_t gw, int64_t stride_h,
                      int64_t stride_w, float* out, mx_stream_t stream);
 /* decode_single: rel[n, ncls*4] against boxes[n,4] -> out[n, ncls*4]; weights (wx,wy,ww,wh);

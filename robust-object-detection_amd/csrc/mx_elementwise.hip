@@ -325,6 +325,42 @@ extern "C" int mx_box_decode(const float* rel, const float* boxes, int64_t n, in
   return MX_OK;
 }
 
+// filter_proposals' candidate clean-up after the per-level top-k (torchvision rpn.py filter_proposals:
+// box_ops.clip_boxes_to_image, remove_small_boxes, the score threshold), one thread per candidate:
+// box = proposals[n][top[n][t]]; x = minimum(clamp(x, min=0), w), y likewise with h (torch's NaN
+// propagation kept: a NaN coordinate stays NaN); keep = (x2-x1 >= min_size) & (y2-y1 >= min_size) &
+// (prob >= score_thresh); grp = keep ? n : N (the dead group). Replaces ~15 torch launches.
+__device__ __forceinline__ float clip_coord(float v, float hi) {
+  const float c = v < 0.f ? 0.f : v;                        // clamp(min=0): NaN stays NaN
+  return c != c ? c : (hi != hi ? hi : (hi < c ? hi : c));  // torch.minimum
+}
+
+__global__ void proposal_clip_filter_kernel(const float4* __restrict__ props, const int64_t* __restrict__ top,
+                                            const float* __restrict__ prob, const float* __restrict__ hw, int64_t N,
+                                            int64_t A, int64_t T, float min_size, float score_thresh,
+                                            float4* __restrict__ out, int32_t* __restrict__ grp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * T) return;
+  const int64_t n = i / T;
+  const float4 p = props[n * A + top[i]];
+  const float h = hw[2 * n], w = hw[2 * n + 1];
+  const float4 b = make_float4(clip_coord(p.x, w), clip_coord(p.y, h), clip_coord(p.z, w), clip_coord(p.w, h));
+  out[i] = b;
+  const bool keep = (b.z - b.x >= min_size) && (b.w - b.y >= min_size) && (prob[i] >= score_thresh);
+  grp[i] = keep ? (int32_t)n : (int32_t)N;
+}
+
+extern "C" int mx_proposal_clip_filter(const float* proposals, const int64_t* top, const float* prob, const float* hw,
+                                       int64_t N, int64_t A, int64_t T, float min_size, float score_thresh,
+                                       float* boxes_out, int32_t* grp_out, mx_stream_t stream) {
+  MX_CHECK_ARG(N >= 0 && A >= 0 && T >= 0 && N < (1ll << 31), "mx_proposal_clip_filter: bad sizes");
+  if (N * T == 0) return MX_OK;
+  proposal_clip_filter_kernel<<<(unsigned)cdiv(N * T, 256), 256, 0, (hipStream_t)stream>>>(
+      (const float4*)proposals, top, prob, hw, N, A, T, min_size, score_thresh, (float4*)boxes_out, grp_out);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
 // elements per destination row that ResizeAreaFastVec_SIMD_8u (scale 2, 128-bit vectors) handles:
 // cn 1: 8 per step, cn 3: 48 per step, cn 4: 16 per step; other channel counts: none (scalar)
 static int64_t area_fast2_vec_elems(int64_t dw, int64_t C) {

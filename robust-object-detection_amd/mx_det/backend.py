@@ -174,6 +174,9 @@ class HipBackend:
     def box_decode(self, rel, boxes, weights):
         return ops.box_decode(rel, boxes, weights)
 
+    def proposal_clip_filter(self, proposals, top, prob, hw, min_size, score_thresh):
+        return ops.proposal_clip_filter(proposals, top, prob, hw, min_size, score_thresh)
+
     def anchors_level(self, size, ratios, gh, gw, sh, sw, device):
         return ops.anchors_level(size, ratios, gh, gw, sh, sw, device)
 

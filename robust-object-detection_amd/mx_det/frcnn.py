@@ -470,37 +470,42 @@ class RegionProposalNetwork(nn.Module):
         if cached is None:  # level id per top-k slot and image index column: shape constants
             lv = torch.cat([torch.full((min(pre, n),), i, dtype=torch.int64, device=dev)
                             for i, n in enumerate(num_per_level)])
-            cached = self._hw[ckey] = (lv.unsqueeze(0).expand(N, -1), torch.arange(N, device=dev)[:, None])
-        lvl, bi = cached
+            cached = self._hw[ckey] = (lv.unsqueeze(0).expand(N, -1), torch.arange(N, device=dev)[:, None],
+                                       lv.repeat(N))
+        _, bi, lvl_flat = cached
         prob = torch.sigmoid(ob[bi, top])
-        boxes = proposals[bi, top]
         key = (tuple(map(tuple, image_sizes)), dev)
         hw = self._hw.get(key)
         if hw is None:  # (h, w) per image; built once per size set (a host->device copy waits for the GPU)
             hw = self._hw[key] = torch.tensor(image_sizes, dtype=torch.float32, device=dev)
-        x = torch.minimum(boxes[..., 0::2].clamp(min=0), hw[:, 1, None, None])
-        y = torch.minimum(boxes[..., 1::2].clamp(min=0), hw[:, 0, None, None])
-        boxes = torch.stack((x[..., 0], y[..., 0], x[..., 1], y[..., 1]), dim=-1)
-        ws, hs = boxes[..., 2] - boxes[..., 0], boxes[..., 3] - boxes[..., 1]
-        keep = (ws >= self.min_size) & (hs >= self.min_size) & (prob >= self.score_thresh)
+        if hasattr(be, "proposal_clip_filter") and os.environ.get("MX_FUSED_PROPOSALS", "1") != "0":
+            # gather + clip + small-box / score filter, one launch
+            boxes, grp = be.proposal_clip_filter(proposals, top, prob, hw, self.min_size, self.score_thresh)
+        else:
+            boxes = proposals[bi, top]
+            x = torch.minimum(boxes[..., 0::2].clamp(min=0), hw[:, 1, None, None])
+            y = torch.minimum(boxes[..., 1::2].clamp(min=0), hw[:, 0, None, None])
+            boxes = torch.stack((x[..., 0], y[..., 0], x[..., 1], y[..., 1]), dim=-1)
+            ws, hs = boxes[..., 2] - boxes[..., 0], boxes[..., 3] - boxes[..., 1]
+            keep = (ws >= self.min_size) & (hs >= self.min_size) & (prob >= self.score_thresh)
+            grp = torch.where(keep, bi, N).reshape(-1)
         # one NMS for all images, torchvision's per-image CPU dispatch rule evaluated on the device;
         # filtered-out candidates are dead entries (group N): nothing here waits for the GPU
-        T = keep.shape[1]
+        T = top.shape[1]
         n = N * T
-        grp = torch.where(keep, bi, N).reshape(-1)
         post = self.post_nms_top_n()
         if hasattr(be, "proposal_nms_select") and os.environ.get("MX_SORTED_NMS", "1") != "0":
             # the candidates are presorted (image, level, score desc: the per-level top-k order): the
             # sort-free NMS also emits the padded per-image selection
-            sel, valid = be.proposal_nms_select(boxes.reshape(-1, 4), prob.reshape(-1), lvl.reshape(-1), grp, N,
+            sel, valid = be.proposal_nms_select(boxes.reshape(-1, 4), prob.reshape(-1), lvl_flat, grp, N,
                                                 len(num_per_level), self.nms_thresh, max(pre, 1000), post)
             return boxes.reshape(-1, 4)[sel], prob.reshape(-1)[sel], valid
-        kk, nk = be.proposal_nms(boxes.reshape(-1, 4), prob.reshape(-1), lvl.reshape(-1), grp, N,
+        kk, nk = be.proposal_nms(boxes.reshape(-1, 4), prob.reshape(-1), lvl_flat, grp, N,
                                  len(num_per_level), self.nms_thresh, max(pre, 1000))
         kk, nk = kk.to(dev), nk.to(dev)
         live = torch.arange(n, device=dev) < nk
         cnt = torch.zeros(N + 1, dtype=torch.int64, device=dev)
-        cnt.scatter_add_(0, torch.where(live, grp[kk], N), live.to(torch.int64))
+        cnt.scatter_add_(0, torch.where(live, grp[kk].to(torch.int64), N), live.to(torch.int64))
         cnt = cnt[:N]
         r = torch.arange(post, device=dev)
         sel = kk[((torch.cumsum(cnt, 0) - cnt)[:, None] + r[None, :]).clamp(max=n - 1)]  # [N, post]

@@ -230,6 +230,23 @@ def batched_nms_grouped_sorted(boxes, scores, lvl, group, G, L, iou_threshold, m
     return (keep, nk) if not post else (keep, nk, sel, valid)
 
 
+def proposal_clip_filter(proposals, top, prob, hw, min_size, score_thresh):
+    """filter_proposals' clip + small-box + score filter after the per-level top-k (one launch):
+    proposals [N, A, 4] f32, top [N, T] int64, prob [N, T] f32, hw [N, 2] (h, w) f32 ->
+    (boxes [N, T, 4] clipped, grp [N*T] int32: the image index, or N for a dropped candidate)."""
+    _dev(proposals, top, prob, hw)
+    N, A = proposals.shape[0], proposals.shape[1]
+    T = top.shape[1]
+    _check(top.dtype == torch.int64 and top.shape[0] == N and prob.shape == top.shape and hw.shape == (N, 2),
+           "proposal_clip_filter: shapes")
+    p = proposals.float().contiguous()
+    boxes = torch.empty((N, T, 4), dtype=torch.float32, device=p.device)
+    grp = torch.empty(N * T, dtype=torch.int32, device=p.device)
+    call("mx_proposal_clip_filter", _p(p), _p(top.contiguous()), _p(prob.float().contiguous()),
+         _p(hw.float().contiguous()), N, A, T, float(min_size), float(score_thresh), _p(boxes), _p(grp), _stream())
+    return boxes, grp
+
+
 def level_topk(scores, num_per_level, k):
     """RegionProposalNetwork._get_top_n_idx (torchvision rpn.py): per image row of scores [N, A] and
     per level, the indices of the min(k, n_l) largest scores (value descending, ties by index) plus

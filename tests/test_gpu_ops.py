@@ -469,6 +469,36 @@ def test_multiscale_roi_align(dev):
         np.testing.assert_allclose(ft[l].grad.permute(0, 3, 1, 2).cpu().numpy(), r, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.gpu
+def test_proposal_clip_filter_matches_torch(dev):
+    """mx_proposal_clip_filter == filter_proposals' torch formulation (gather by the top-k indices,
+    clamp(min=0) + minimum against (w, h), min-size and score masks, dead group N): bit-identical boxes
+    incl. NaN / negative / out-of-image coordinates, identical groups."""
+    from mx_det import ops
+    rng = np.random.default_rng(5)
+    N, A, T = 2, 5000, 3000
+    props = rng.normal(600, 500, (N, A, 4)).astype(np.float32)
+    props[0, :50] = np.nan
+    props[1, 50:80, 2] = props[1, 50:80, 0] + 1e-4  # narrower than min_size
+    pt = torch.from_numpy(props).to(dev)
+    top = torch.from_numpy(np.stack([rng.choice(A, T, replace=False) for _ in range(N)])).to(dev)
+    top[0, :60] = torch.arange(60, device=dev)
+    prob = torch.from_numpy(rng.random((N, T)).astype(np.float32)).to(dev)
+    hw = torch.tensor([[800.0, 1333.0], [768.0, 1344.0]], device=dev)
+    for min_size, thr in ((1e-3, 0.0), (8.0, 0.3)):
+        boxes, grp = ops.proposal_clip_filter(pt, top, prob, hw, min_size, thr)
+        bi = torch.arange(N, device=dev)[:, None]
+        rb = pt[bi, top]
+        x = torch.minimum(rb[..., 0::2].clamp(min=0), hw[:, 1, None, None])
+        y = torch.minimum(rb[..., 1::2].clamp(min=0), hw[:, 0, None, None])
+        rb = torch.stack((x[..., 0], y[..., 0], x[..., 1], y[..., 1]), dim=-1)
+        keep = (rb[..., 2] - rb[..., 0] >= min_size) & (rb[..., 3] - rb[..., 1] >= min_size) & (prob >= thr)
+        rg = torch.where(keep, bi, N).reshape(-1)
+        assert torch.equal(torch.isnan(boxes), torch.isnan(rb))
+        assert torch.equal(torch.nan_to_num(boxes, nan=-7.0), torch.nan_to_num(rb, nan=-7.0))
+        assert torch.equal(grp.long(), rg)
+
+
 def test_box_decode(dev):
     from mx_det import ops
     rng = np.random.default_rng(11)
