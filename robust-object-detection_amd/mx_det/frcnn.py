@@ -997,14 +997,14 @@ class FasterRCNN(nn.Module):
         if self.training:
             if targets is None:
                 raise ValueError("In training mode, targets should be passed")
-            flags = []
+            dev_boxes = []
             for t in targets:
                 b = t["boxes"]
                 if not (isinstance(b, torch.Tensor) and b.dim() == 2 and b.shape[-1] == 4):
                     raise ValueError(f"Expected target boxes to be a tensor of shape [N, 4], got {b.shape}.")
                 if b.numel():
                     if b.is_cuda:
-                        flags.append((b[:, 2:] <= b[:, :2]).any())
+                        dev_boxes.append(b)
                     elif bool(((b[:, 2:] <= b[:, :2]).any())):
                         raise ValueError("All bounding boxes should have positive height and width.")
             # GeneralizedRCNN.forward's degenerate-box check without its per-image host round trips:
@@ -1015,22 +1015,36 @@ class FasterRCNN(nn.Module):
             # FPN and box head too) and the graphs' static buffers are updated by it. A loop that catches
             # the error and skips the batch should set MX_STRICT_TARGETS=1 (one host sync per step,
             # torchvision's order and state).
-            if flags and os.environ.get("MX_STRICT_TARGETS", "0") == "1":
-                if bool(torch.stack(flags).any()):
+            if dev_boxes and os.environ.get("MX_STRICT_TARGETS", "0") == "1":
+                if bool(torch.stack([(b[:, 2:] <= b[:, :2]).any() for b in dev_boxes]).any()):
                     raise ValueError("All bounding boxes should have positive height and width.")
-                flags = []
-            degenerate = self._flag_async(flags)
+                dev_boxes = []
         if isinstance(images, torch.Tensor) and images.dim() == 4 and images.dtype == torch.uint8:
             original = [(images.shape[1], images.shape[2])] * images.shape[0]
         else:  # float CHW (reference ToDtype output) or uint8 HWC tensors
             original = [(int(im.shape[0]), int(im.shape[1])) if im.dtype == torch.uint8 else
                         (int(im.shape[-2]), int(im.shape[-1])) for im in images]
+        boxes_in = dev_boxes if self.training else []
+        if boxes_in and os.environ.get("MX_FLAGS_LATE", "1") == "0":  # A/B switch: flags before the trunk
+            degenerate, boxes_in = self._flag_async([(b[:, 2:] <= b[:, :2]).any() for b in boxes_in]), []
+        ready = None
+        if boxes_in:  # the GT boxes are complete up to here on the main stream
+            ready = torch.cuda.Event()
+            ready.record()
         il, targets = self.transform(images, targets, be)
         trunk = self._trunk(il.tensors, be)
         if trunk is not None:  # HIP-graph replay of backbone + FPN + RPN head (static shapes)
             features, head = trunk
         else:
             features, head = self.backbone(il.tensors, be), None
+        if boxes_in:
+            # issued after the trunk (the step's first kernels are queued without waiting for ~10 flag
+            # launches' host time) on a side stream ordered only after the GT boxes, so the flag's event
+            # completes long before the check below reads it
+            side = mc.dedicated_stream(boxes_in[0].device, "flags")
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                degenerate = self._flag_async([(b[:, 2:] <= b[:, :2]).any() for b in boxes_in])
         # MX_RPN_DEFER_LOSSES=1 issues the RPN target / loss launches after the RoI sampler's host sync;
         # measured 0.5 % slower than issuing them while the trunk runs (A/B on one box), so off
         defer = os.environ.get("MX_RPN_DEFER_LOSSES", "0") != "0"
