@@ -178,6 +178,11 @@ int mx_multiscale_roi_align_bwd(const void* grad_out, int dtype, float* const* g
 int mx_proposal_clip_filter(const float* proposals, const int64_t* top, const float* prob, const float* hw,
                             int64_t N, int64_t A, int64_t T, float min_size, float score_thresh, float* boxes_out,
                             int32_t* grp_out, mx_stream_t stream);
+/* RoIHeads' sampled-RoI compaction: the K selected entries of mask [M] (bool, M = N x cm
+ * candidates, K = their count, known on the host) in ascending order -> rois [K, 5] (entry / cm as
+ * f32, then box[entry]), lab_out [K] = lab[entry] (int64), tg_out [K, 4] = tg[entry]. */
+int mx_roi_compact(const uint8_t* mask, int64_t M, int64_t K, int64_t cm, const float* box, const int64_t* lab,
+                   const float* tg, float* rois, int64_t* lab_out, float* tg_out, mx_stream_t stream);
 int mx_anchors_level(float size, const float* ratios_host, int nr, int64_t gh, int64_t gw, int64_t stride_h,
                      int64_t stride_w, float* out, mx_stream_t stream);
 /* decode_single: rel[n, ncls*4] against boxes[n,4] -> out[n, ncls*4]; weights (wx,wy,ww,wh);

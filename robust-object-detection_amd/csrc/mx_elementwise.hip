@@ -361,6 +361,55 @@ extern "C" int mx_proposal_clip_filter(const float* proposals, const int64_t* to
   return MX_OK;
 }
 
+// RoIHeads' sampled-RoI compaction (torchvision roi_heads.py select_training_samples: per image
+// torch.where(pos | neg), proposals / labels / regression targets gathered, RoI format [img, box]):
+// the selected entries of a flat mask over N x cm candidates, in ascending order, written to
+// rois [K, 5] (image index = entry / cm as f32, then the box), labels [K] and targets [K, 4]. One
+// 1024-thread workgroup: per-thread contiguous chunks, one block scan. Replaces ~12 torch launches.
+static constexpr int RC_T = 1024;
+__global__ void __launch_bounds__(RC_T) roi_compact_kernel(const uint8_t* __restrict__ mask, int64_t M, int64_t K,
+                                                           int64_t cm, const float4* __restrict__ box,
+                                                           const int64_t* __restrict__ lab, const float4* __restrict__ tg,
+                                                           float* __restrict__ rois, int64_t* __restrict__ lab_out,
+                                                           float4* __restrict__ tg_out) {
+  __shared__ int64_t wsum[RC_T / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t per = (M + RC_T - 1) / RC_T, b0 = tid * per, b1 = min<int64_t>(M, b0 + per);
+  int64_t c = 0;
+  for (int64_t i = b0; i < b1; ++i) c += mask[i] ? 1 : 0;
+  int64_t x = c;  // inclusive wave scan
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  int64_t base = 0;
+  for (int w = 0; w < wave; ++w) base += wsum[w];
+  int64_t k = base + x - c;  // exclusive prefix: this thread's first output slot
+  for (int64_t i = b0; i < b1 && k < K; ++i) {
+    if (!mask[i]) continue;
+    const float4 b = box[i];
+    float* r = rois + 5 * k;
+    r[0] = (float)(i / cm);
+    r[1] = b.x; r[2] = b.y; r[3] = b.z; r[4] = b.w;
+    lab_out[k] = lab[i];
+    tg_out[k] = tg[i];
+    ++k;
+  }
+}
+
+extern "C" int mx_roi_compact(const uint8_t* mask, int64_t M, int64_t K, int64_t cm, const float* box, const int64_t* lab,
+                              const float* tg, float* rois, int64_t* lab_out, float* tg_out, mx_stream_t stream) {
+  MX_CHECK_ARG(M >= 0 && K >= 0 && K <= M && cm >= 1, "mx_roi_compact: bad sizes M=%lld K=%lld cm=%lld",
+               (long long)M, (long long)K, (long long)cm);
+  if (K == 0) return MX_OK;
+  roi_compact_kernel<<<1, RC_T, 0, (hipStream_t)stream>>>(mask, M, K, cm, (const float4*)box, lab, (const float4*)tg,
+                                                        rois, lab_out, (float4*)tg_out);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
 // elements per destination row that ResizeAreaFastVec_SIMD_8u (scale 2, 128-bit vectors) handles:
 // cn 1: 8 per step, cn 3: 48 per step, cn 4: 16 per step; other channel counts: none (scalar)
 static int64_t area_fast2_vec_elems(int64_t dw, int64_t C) {

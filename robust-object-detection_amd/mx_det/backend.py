@@ -174,6 +174,9 @@ class HipBackend:
     def box_decode(self, rel, boxes, weights):
         return ops.box_decode(rel, boxes, weights)
 
+    def roi_compact(self, mask, total, cm, box, lab, tg):
+        return ops.roi_compact(mask, total, cm, box, lab, tg)
+
     def proposal_clip_filter(self, proposals, top, prob, hw, min_size, score_thresh):
         return ops.proposal_clip_filter(proposals, top, prob, hw, min_size, score_thresh)
 

@@ -763,10 +763,17 @@ class RoIHeads(nn.Module):
             lab_p = torch.where(valid, lab_b, -1)
             pos_m, neg_m = self.fg_bg_sampler(lab_p, be)
             sm = (pos_m | neg_m).flatten()
-            idx = _compact(sm, int(sm.sum()))             # per image ascending, as torch.where per image
+            total = int(sm.sum())                         # the stage's one host sync (sizes the RoI head)
             cm = lab_p.shape[1]
-            rois = torch.cat([(idx // cm).to(torch.float32)[:, None], box_p.reshape(-1, 4)[idx]], 1)
-            labels, tgts = [lab_p.reshape(-1)[idx]], [tg_p.reshape(-1, 4)[idx]]
+            if hasattr(be, "roi_compact") and os.environ.get("MX_FUSED_ROI_COMPACT", "1") != "0":
+                # per image ascending, as torch.where per image: one launch after the sync
+                rois, lab_k, tg_k = be.roi_compact(sm, total, cm, box_p.reshape(-1, 4), lab_p.reshape(-1),
+                                                   tg_p.reshape(-1, 4))
+                labels, tgts = [lab_k], [tg_k]
+            else:
+                idx = _compact(sm, total)
+                rois = torch.cat([(idx // cm).to(torch.float32)[:, None], box_p.reshape(-1, 4)[idx]], 1)
+                labels, tgts = [lab_p.reshape(-1)[idx]], [tg_p.reshape(-1, 4)[idx]]
         else:
             rois = torch.cat([torch.cat([torch.full((p.shape[0], 1), float(i), device=dev), p], 1)
                               for i, p in enumerate(proposals)])

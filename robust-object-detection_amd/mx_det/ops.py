@@ -247,6 +247,22 @@ def proposal_clip_filter(proposals, top, prob, hw, min_size, score_thresh):
     return boxes, grp
 
 
+def roi_compact(mask, total, cm, box, lab, tg):
+    """select_training_samples' gather after the sampler: the `total` True entries of the flat mask
+    (ascending) -> (rois [total, 5] = (entry // cm, box), labels [total] int64, targets [total, 4])."""
+    _dev(mask, box, lab, tg)
+    M = mask.numel()
+    _check(mask.dtype == torch.bool and box.shape == (M, 4) and lab.shape == (M,) and tg.shape == (M, 4),
+           "roi_compact: shapes")
+    dev = mask.device
+    rois = torch.empty((total, 5), dtype=torch.float32, device=dev)
+    lo = torch.empty(total, dtype=torch.int64, device=dev)
+    to = torch.empty((total, 4), dtype=torch.float32, device=dev)
+    call("mx_roi_compact", _p(mask.contiguous()), M, int(total), int(cm), _p(box.float().contiguous()),
+         _p(lab.to(torch.int64).contiguous()), _p(tg.float().contiguous()), _p(rois), _p(lo), _p(to), _stream())
+    return rois, lo, to
+
+
 def level_topk(scores, num_per_level, k):
     """RegionProposalNetwork._get_top_n_idx (torchvision rpn.py): per image row of scores [N, A] and
     per level, the indices of the min(k, n_l) largest scores (value descending, ties by index) plus

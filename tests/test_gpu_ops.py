@@ -499,6 +499,29 @@ def test_proposal_clip_filter_matches_torch(dev):
         assert torch.equal(grp.long(), rg)
 
 
+@pytest.mark.gpu
+def test_roi_compact_matches_torch(dev):
+    """mx_roi_compact == the torch formulation after the RoI sampler (ascending selected entries,
+    rois = (entry // cm, box), labels / targets gathered): bit-identical, incl. an empty image row
+    and a fully selected one."""
+    from mx_det import ops
+    from mx_det.frcnn import _compact
+    rng = np.random.default_rng(9)
+    N, cm = 3, 2064
+    mask = torch.from_numpy(rng.random((N, cm)) < 0.25).to(dev)
+    mask[1] = False
+    mask[2, :700] = True
+    box = torch.from_numpy(rng.normal(500, 300, (N * cm, 4)).astype(np.float32)).to(dev)
+    lab = torch.from_numpy(rng.integers(-1, 8, N * cm)).to(dev)
+    tg = torch.from_numpy(rng.normal(0, 1, (N * cm, 4)).astype(np.float32)).to(dev)
+    sm = mask.flatten()
+    total = int(sm.sum())
+    rois, lo, to = ops.roi_compact(sm, total, cm, box, lab, tg)
+    idx = _compact(sm, total)
+    ref = torch.cat([(idx // cm).to(torch.float32)[:, None], box[idx]], 1)
+    assert torch.equal(rois, ref) and torch.equal(lo, lab[idx]) and torch.equal(to, tg[idx])
+
+
 def test_box_decode(dev):
     from mx_det import ops
     rng = np.random.default_rng(11)
