@@ -178,6 +178,11 @@ int mx_multiscale_roi_align_bwd(const void* grad_out, int dtype, float* const* g
 int mx_proposal_clip_filter(const float* proposals, const int64_t* top, const float* prob, const float* hw,
                             int64_t N, int64_t A, int64_t T, float min_size, float score_thresh, float* boxes_out,
                             int32_t* grp_out, mx_stream_t stream);
+/* GeneralizedRCNN's degenerate-box check: flag[0] = any box of the m (<= 8) sets (boxes_host[j]:
+ * counts_host[j] x 4 f32 on the device, x1 y1 x2 y2) has x2 <= x1 or y2 <= y1; one launch, the flag
+ * is always written. */
+int mx_boxes_degenerate(const float* const* boxes_host, const int64_t* counts_host, int m, uint8_t* flag,
+                        mx_stream_t stream);
 /* RoIHeads' sampled-RoI compaction: the K selected entries of mask [M] (bool, M = N x cm
  * candidates, K = their count, known on the host) in ascending order -> rois [K, 5] (entry / cm as
  * f32, then box[entry]), lab_out [K] = lab[entry] (int64), tg_out [K, 4] = tg[entry]. */

@@ -361,6 +361,40 @@ extern "C" int mx_proposal_clip_filter(const float* proposals, const int64_t* to
   return MX_OK;
 }
 
+// GeneralizedRCNN.forward's degenerate-box check (generalized_rcnn.py: any box with x2 <= x1 or
+// y2 <= y1) over up to 8 images' target boxes in one single-workgroup launch: flag = 1 / 0 (always
+// written, so the flag needs no clearing launch). NaN coordinates compare false, as in torch.
+struct BoxSets {
+  const float4* p[8];
+  int64_t n[8];
+  int m;
+};
+__global__ void __launch_bounds__(1024) boxes_degenerate_kernel(BoxSets s, uint8_t* __restrict__ flag) {
+  int bad = 0;
+  for (int j = 0; j < s.m; ++j)
+    for (int64_t i = threadIdx.x; i < s.n[j]; i += blockDim.x) {
+      const float4 b = s.p[j][i];
+      bad |= (b.z <= b.x) || (b.w <= b.y);
+    }
+  bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) flag[0] = bad ? 1 : 0;
+}
+
+extern "C" int mx_boxes_degenerate(const float* const* boxes_host, const int64_t* counts_host, int m, uint8_t* flag,
+                                   mx_stream_t stream) {
+  MX_CHECK_ARG(m >= 1 && m <= 8 && flag, "mx_boxes_degenerate: 1..8 box sets");
+  BoxSets s{};
+  for (int j = 0; j < m; ++j) {
+    MX_CHECK_ARG(counts_host[j] >= 0 && (counts_host[j] == 0 || boxes_host[j]), "mx_boxes_degenerate: bad set %d", j);
+    s.p[j] = (const float4*)boxes_host[j];
+    s.n[j] = counts_host[j];
+  }
+  s.m = m;
+  boxes_degenerate_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(s, flag);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
 // RoIHeads' sampled-RoI compaction (torchvision roi_heads.py select_training_samples: per image
 // torch.where(pos | neg), proposals / labels / regression targets gathered, RoI format [img, box]):
 // the selected entries of a flat mask over N x cm candidates, in ascending order, written to

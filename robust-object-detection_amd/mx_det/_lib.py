@@ -72,6 +72,7 @@ _SIGS = {
                                             c_i64, c_int, c_int, c_int, c_int, c_vp, c_sz, c_vp]),
     "mx_anchors_level": (c_int, [c_f, c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mx_proposal_clip_filter": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_f, c_f, c_vp, c_vp, c_vp]),
+    "mx_boxes_degenerate": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp]),
     "mx_roi_compact": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_box_decode": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_f, c_vp, c_vp]),
     "mx_corrupt_u8": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_f, c_u64, c_vp, c_d, c_vp, c_vp, c_vp]),

@@ -174,6 +174,9 @@ class HipBackend:
     def box_decode(self, rel, boxes, weights):
         return ops.box_decode(rel, boxes, weights)
 
+    def boxes_degenerate(self, boxes_list):
+        return ops.boxes_degenerate(boxes_list)
+
     def roi_compact(self, mask, total, cm, box, lab, tg):
         return ops.roi_compact(mask, total, cm, box, lab, tg)
 

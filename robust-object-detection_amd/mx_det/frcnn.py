@@ -1031,27 +1031,19 @@ class FasterRCNN(nn.Module):
         else:  # float CHW (reference ToDtype output) or uint8 HWC tensors
             original = [(int(im.shape[0]), int(im.shape[1])) if im.dtype == torch.uint8 else
                         (int(im.shape[-2]), int(im.shape[-1])) for im in images]
-        boxes_in = dev_boxes if self.training else []
-        if boxes_in and os.environ.get("MX_FLAGS_LATE", "1") == "0":  # A/B switch: flags before the trunk
-            degenerate, boxes_in = self._flag_async([(b[:, 2:] <= b[:, :2]).any() for b in boxes_in]), []
-        ready = None
-        if boxes_in:  # the GT boxes are complete up to here on the main stream
-            ready = torch.cuda.Event()
-            ready.record()
+        if self.training and dev_boxes:
+            # one check launch + the pinned copy on the HIP backend (else the torch compares), issued
+            # ahead of the trunk: two launches of host time before the step's first kernels, and the
+            # event is complete long before the check below reads it
+            flags = ([be.boxes_degenerate(dev_boxes)] if hasattr(be, "boxes_degenerate") else
+                     [(b[:, 2:] <= b[:, :2]).any() for b in dev_boxes])
+            degenerate = self._flag_async(flags)
         il, targets = self.transform(images, targets, be)
         trunk = self._trunk(il.tensors, be)
         if trunk is not None:  # HIP-graph replay of backbone + FPN + RPN head (static shapes)
             features, head = trunk
         else:
             features, head = self.backbone(il.tensors, be), None
-        if boxes_in:
-            # issued after the trunk (the step's first kernels are queued without waiting for ~10 flag
-            # launches' host time) on a side stream ordered only after the GT boxes, so the flag's event
-            # completes long before the check below reads it
-            side = mc.dedicated_stream(boxes_in[0].device, "flags")
-            side.wait_event(ready)
-            with torch.cuda.stream(side):
-                degenerate = self._flag_async([(b[:, 2:] <= b[:, :2]).any() for b in boxes_in])
         # MX_RPN_DEFER_LOSSES=1 issues the RPN target / loss launches after the RoI sampler's host sync;
         # measured 0.5 % slower than issuing them while the trunk runs (A/B on one box), so off
         defer = os.environ.get("MX_RPN_DEFER_LOSSES", "0") != "0"

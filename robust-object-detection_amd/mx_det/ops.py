@@ -247,6 +247,22 @@ def proposal_clip_filter(proposals, top, prob, hw, min_size, score_thresh):
     return boxes, grp
 
 
+def boxes_degenerate(boxes_list, out=None):
+    """One device bool flag: any box (x1, y1, x2, y2) of the list's tensors with x2 <= x1 or y2 <= y1
+    (mx_boxes_degenerate, up to 8 tensors per launch)."""
+    _dev(*boxes_list)
+    dev = boxes_list[0].device
+    flags = []
+    for c in range(0, len(boxes_list), 8):
+        chunk = [b.float().contiguous() for b in boxes_list[c:c + 8]]
+        f = out if (out is not None and len(boxes_list) <= 8) else torch.empty(1, dtype=torch.bool, device=dev)
+        ptrs = (ctypes.c_void_p * len(chunk))(*[b.data_ptr() for b in chunk])
+        cnts = (ctypes.c_int64 * len(chunk))(*[b.shape[0] for b in chunk])
+        call("mx_boxes_degenerate", ptrs, cnts, len(chunk), _p(f), _stream())
+        flags.append(f)
+    return (flags[0] if len(flags) == 1 else torch.cat(flags).any()).reshape(())
+
+
 def roi_compact(mask, total, cm, box, lab, tg):
     """select_training_samples' gather after the sampler: the `total` True entries of the flat mask
     (ascending) -> (rois [total, 5] = (entry // cm, box), labels [total] int64, targets [total, 4])."""

@@ -522,6 +522,31 @@ def test_roi_compact_matches_torch(dev):
     assert torch.equal(rois, ref) and torch.equal(lo, lab[idx]) and torch.equal(to, tg[idx])
 
 
+@pytest.mark.gpu
+def test_boxes_degenerate_flag(dev):
+    """mx_boxes_degenerate == any((b[:, 2:] <= b[:, :2]).any()) over the target tensors (empty sets,
+    zero-width / -height, NaN coordinates, more than 8 sets)."""
+    from mx_det import ops
+    rng = np.random.default_rng(2)
+
+    def sets(n, bad=None):
+        out = []
+        for i in range(n):
+            b = rng.uniform(0, 500, (int(rng.integers(0, 60)), 2)).astype(np.float32)
+            b = np.concatenate([b, b + rng.uniform(1, 50, b.shape).astype(np.float32)], 1)
+            out.append(torch.from_numpy(b).to(dev))
+        if bad is not None:
+            i, kind = bad
+            b = torch.tensor([[10.0, 10.0, 10.0, 20.0]] if kind == "w" else
+                             [[10.0, 10.0, 20.0, 5.0]] if kind == "h" else [[float("nan"), 1.0, 2.0, 3.0]], device=dev)
+            out[i] = torch.cat([out[i], b])
+        return out
+    for n, bad in ((2, None), (2, (1, "w")), (3, (0, "h")), (2, (0, "nan")), (11, None), (11, (9, "w")), (1, None)):
+        bl = sets(n, bad)
+        ref = any(bool((b[:, 2:] <= b[:, :2]).any()) for b in bl)
+        assert bool(ops.boxes_degenerate(bl)) == ref, (n, bad)
+
+
 def test_box_decode(dev):
     from mx_det import ops
     rng = np.random.default_rng(11)
