@@ -32,7 +32,8 @@ def main():
     # where the device copies come from (aten::copy_ / to / contiguous call sites, 6 frames)
     for ev in prof.key_averages(group_by_stack_n=6):
         if ev.key in ("aten::copy_", "aten::clone", "aten::_to_copy", "aten::cat", "aten::index", "aten::nonzero",
-                      "aten::item", "aten::_local_scalar_dense"):
+                      "aten::item", "aten::_local_scalar_dense", "aten::mul", "aten::mul_", "aten::add_",
+                      "aten::add"):
             print(f"{ev.key} x{ev.count}")
             for fr in ev.stack[:6]:
                 print("    ", fr)
