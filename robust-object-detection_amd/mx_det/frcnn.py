@@ -416,6 +416,13 @@ class BalancedPositiveNegativeSampler:
             keys = torch.cat([torch.where(pos, r, 2.0), torch.where(neg, r, 2.0)], 0)
             _, idx = keys.topk(max(kp, kn), dim=1, largest=False)
             return (self._mark(pos, idx[:N, :kp], num_pos), self._mark(neg, idx[N:, :kn], num_neg))
+        if kp > 0 and kn > 0 and os.environ.get("MX_SAMPLER_ONE_TOPK", "1") != "0":
+            # the same stacking with mx_level_topk: both draws in one launch (value order, ties by
+            # index: the top-kp prefix of the top-max(kp, kn) rows is exactly the separate top-kp)
+            N = lab.shape[0]
+            keys = torch.cat([torch.where(pos, -r, -2.0), torch.where(neg, -r, -2.0)], 0)
+            idx = be.level_topk(keys, [L], max(kp, kn))
+            return (self._mark(pos, idx[:N, :kp], num_pos), self._mark(neg, idx[N:, :kn], num_neg))
         return self._pick(pos, r, kp, num_pos, be), self._pick(neg, r, kn, num_neg, be)
 
     @staticmethod
