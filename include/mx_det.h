@@ -121,6 +121,14 @@ int mx_batched_nms_grouped_sorted(const float* boxes, const float* scores, const
  * 1 <= nlev <= 8, min(k, level_n[l]) <= 4096. */
 int mx_level_topk(const float* scores, int64_t N, int64_t row_stride, int nlev, const int64_t* level_off,
                   const int64_t* level_n, int64_t k, int64_t* out_idx, mx_stream_t stream);
+/* mx_level_topk with a workspace of mx_level_topk_workspace(N, nlev, level_n) bytes (0: no level is
+ * long enough to slice; ws may then be NULL): a level above 24,576 elements is cut into slices whose
+ * own top-k lists (in ws) are merged by a second launch -- the same result, read by many CUs.
+ * ws == NULL: every level is one workgroup (mx_level_topk). */
+size_t mx_level_topk_workspace(int64_t N, int nlev, const int64_t* level_n);
+int mx_level_topk_ws(const float* scores, int64_t N, int64_t row_stride, int nlev, const int64_t* level_off,
+                     const int64_t* level_n, int64_t k, int64_t* out_idx, void* ws, size_t ws_bytes,
+                     mx_stream_t stream);
 size_t mx_nms_workspace(int64_t n, int64_t max_seg);
 int mx_batched_nms(const float* boxes, const float* scores, const int64_t* idxs, const int32_t* group, int64_t n,
                    int64_t max_seg, double iou_threshold, int mode, int64_t* keep, int64_t* num_keep, void* ws,

@@ -58,6 +58,8 @@ _SIGS = {
     "mx_batched_nms_grouped": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_d, c_vp, c_vp, c_vp, c_sz,
                                        c_vp]),
     "mx_level_topk": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "mx_level_topk_workspace": (c_sz, [c_i64, c_int, c_vp]),
+    "mx_level_topk_ws": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_sz, c_vp]),
     "mx_batched_nms": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_d, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_roi_align_fwd": (c_int, [c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_f, c_int, c_int, c_int,
                                  c_int, c_vp, c_vp]),

@@ -12,6 +12,7 @@ rank/shape/device; empty inputs give empty outputs.
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -294,8 +295,12 @@ def level_topk(scores, num_per_level, k):
     _check(offs[-1] + int(num_per_level[-1]) <= A, "level_topk: levels exceed the row")
     tot = sum(min(int(k), int(n)) for n in num_per_level)
     out = torch.empty((N, tot), dtype=torch.int64, device=s.device)
-    call("mx_level_topk", _p(s), N, A, L, (ctypes.c_int64 * L)(*offs),
-         (ctypes.c_int64 * L)(*[int(n) for n in num_per_level]), int(k), _p(out), _stream())
+    ln = (ctypes.c_int64 * L)(*[int(n) for n in num_per_level])
+    # long levels are sliced over many workgroups and merged (MX_TOPK_SLICED=0: one workgroup per level)
+    nb = _lib.load().mx_level_topk_workspace(N, L, ln) if os.environ.get("MX_TOPK_SLICED", "1") != "0" else 0
+    ws = _ws(nb, s.device) if nb else None
+    call("mx_level_topk_ws", _p(s), N, A, L, (ctypes.c_int64 * L)(*offs), ln, int(k), _p(out),
+         _p(ws) if ws is not None else None, int(nb), _stream())
     return out
 
 

@@ -713,7 +713,7 @@ def _level_topk_np(scores, num_per_level, k):
     return np.concatenate(out, 1)
 
 
-@pytest.mark.parametrize("case", ["train", "logits", "uniform", "ties", "edges"])
+@pytest.mark.parametrize("case", ["train", "logits", "uniform", "ties", "edges", "flat"])
 def test_level_topk(dev, case):
     """mx_level_topk == the per-level topk of RegionProposalNetwork._get_top_n_idx: exact indices vs
     the definition (value desc, index asc) and exact values vs torch.topk on the CPU. "logits" (one
@@ -735,6 +735,11 @@ def test_level_topk(dev, case):
         s = (np.round(rng.standard_normal((3, sum(levels))) * 4) / 4).astype(np.float32)
         s[1, :] = 0.5  # a row of one value: every level is one tie
         s[2, ::7] = -0.0  # -0.0 and +0.0 compare equal: ties
+    elif case == "flat":  # sliced levels whose slices tie at the threshold (merge's many-ties path)
+        levels, k = [201600, 24577, 60000], 2000
+        s = (np.round(rng.standard_normal((3, sum(levels))) * 2) / 2).astype(np.float32)
+        s[1, :] = 0.25  # one value: 9 slices x 2000 ties reach the merge
+        s[2, 100000:] = 7.0  # the top 2000 ties sit in later slices only
     else:  # tiny / empty levels, k=1, infinities, k > n
         levels, k = [5, 0, 3000, 1, 64], 1
         s = rng.standard_normal((2, sum(levels))).astype(np.float32)
@@ -754,6 +759,20 @@ def test_level_topk(dev, case):
     if case == "edges":
         got2 = ops.level_topk(st.to(dev), levels, 5000).cpu().numpy()  # k >= every n: full sorts
         assert np.array_equal(got2, _level_topk_np(s, levels, 5000))
+
+
+def test_level_topk_sliced_matches_single_workgroup(dev, monkeypatch):
+    """Slicing long levels over many workgroups (+ the merge launch) returns exactly the indices of
+    the one-workgroup-per-level path, on the RPN's training shape."""
+    from mx_det import ops
+    rng = np.random.default_rng(5)
+    levels, k = [201600, 50400, 12600, 3150, 819], 2000
+    st = torch.from_numpy((0.01 + 0.001 * rng.standard_normal((2, sum(levels)))).astype(np.float32)).to(dev)
+    monkeypatch.setenv("MX_TOPK_SLICED", "1")
+    a = ops.level_topk(st, levels, k)
+    monkeypatch.setenv("MX_TOPK_SLICED", "0")
+    b = ops.level_topk(st, levels, k)
+    assert torch.equal(a, b)
 
 
 def test_sampler_draw_via_level_topk(dev):
