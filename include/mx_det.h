@@ -411,6 +411,13 @@ int mx_conv_set_wgrad_target(int64_t blocks);
 size_t mx_conv_workspace_x3(const mx_conv_shape* s, int pass);
 int mx_conv2d_fwd_x3(const mx_conv_shape* s, const float* x, const uint16_t* w, const float* bias, const float* residual,
                      int act, float* y, float* stats, void* ws, size_t ws_bytes, mx_stream_t stream);
+/* The ResNet stem as mx_conv2d_fwd_x3 (torchvision resnet50 conv1, reached from
+ * train_frcnn_baseline.py:171 through the detector's backbone): R = S = 7, K = 64, the same packed w
+ * [2][64][7][7][C] and outputs (y = act(conv + bias), optional BN statistics partials, no residual),
+ * with only channels 0..3 of x and w read -- the caller's real input channels are <= 4 (RGB padded
+ * to C = 8 with zeros). One MFMA K-step per filter row: 224 products per output instead of 416. */
+int mx_conv2d_stem_x3(const mx_conv_shape* s, const float* x, const uint16_t* w, const float* bias, int act, float* y,
+                      float* stats, mx_stream_t stream);
 int mx_conv2d_dgrad_x3(const mx_conv_shape* s, const float* dy, const uint16_t* wt, const float* residual, float* dx,
                        const float* y, const float* z, const float* mean, const float* invstd, int act, float* part,
                        int64_t part_mb, void* ws, size_t ws_bytes, mx_stream_t stream);
@@ -478,6 +485,12 @@ int mx_bn_finalize_ex(const float* stats, int64_t mblocks, int64_t K, int64_t co
 /* apply: x of xdtype, residual and y of ydtype (bf16 -> bf16, f32 -> bf16, f32 -> f32). */
 int mx_bn_apply(const void* x, int xdtype, int64_t M, int64_t K, const float* scale, const float* shift,
                 const void* residual, int act, void* y, int ydtype, mx_stream_t stream);
+/* mx_bn_apply (f32, no residual) followed by mx_maxpool_fwd (k, stride, pad; no argmax) in one pass,
+ * bit-identical to the two: y [N, Ho, Wo, C] = maxpool(act(z * scale + shift)). The ResNet stem's
+ * bn1 -> relu -> maxpool (torchvision resnet.py _forward_impl, reached from train_frcnn_baseline.py:171)
+ * when no gradient flows through them (frozen stem). */
+int mx_bn_act_maxpool(const float* z, int64_t N, int64_t H, int64_t W, int64_t C, const float* scale, const float* shift,
+                      int act, int k, int stride, int pad, float* y, mx_stream_t stream);
 /* Hot-path backward: reduce_ex = one launch of per-row-block partials (no float atomics) whose last
  * block per 64-channel chunk does the f64 column reduce, writing sums[2][K] = (sum g, sum g*xhat) =
  * (dbeta, dgamma) and coef[3][K], the per-channel affine form dx = coef0*g + coef1*x + coef2;

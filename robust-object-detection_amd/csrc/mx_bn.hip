@@ -590,6 +590,49 @@ __global__ void __launch_bounds__(256) roi_loss_bwd_kernel(const float* __restri
   }
 }
 
+// BatchNorm apply + activation + max pooling in one pass (the ResNet stem's bn1 -> relu -> maxpool when
+// no gradient flows through them): every window element is transformed exactly as bn_apply_kernel
+// does (no residual) and reduced exactly as maxpool_fwd_kernel does (first valid element, then
+// greater or NaN), so the result is bit-identical to the two kernels -- without writing and
+// re-reading the full-resolution activation. One thread per (output pixel, 8 channels).
+__global__ void __launch_bounds__(256) bn_act_maxpool_kernel(const float* __restrict__ z, int64_t N, int64_t H,
+                                                             int64_t W, int64_t C, int64_t Ho, int64_t Wo, int k,
+                                                             int st, int pd, const float* __restrict__ scale,
+                                                             const float* __restrict__ shift, int act,
+                                                             float* __restrict__ y) {
+  const int64_t C8 = C / 8;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * Ho * Wo * C8) return;
+  const int64_t c8 = e % C8, t = e / C8;
+  const int64_t ow = t % Wo, oh = (t / Wo) % Ho, n = t / (Wo * Ho);
+  float sc[8], sh[8], best[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    sc[q] = scale[c8 * 8 + q];
+    sh[q] = shift[c8 * 8 + q];
+    best[q] = -INFINITY;
+  }
+  const float zero = 0.f;
+  bool have = false;
+  for (int r = 0; r < k; ++r) {
+    const int64_t ih = oh * st - pd + r;
+    if (ih < 0 || ih >= H) continue;
+    for (int s = 0; s < k; ++s) {
+      const int64_t iw = ow * st - pd + s;
+      if (iw < 0 || iw >= W) continue;
+      float vv[8];
+      ld8(z + ((n * H + ih) * W + iw) * C + c8 * 8, vv);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float v = actf(vv[q] * sc[q] + sh[q] + zero, act);
+        if (v > best[q] || !have || v != v) best[q] = v;
+      }
+      have = true;
+    }
+  }
+  st8(y + t * C + c8 * 8, best);
+}
+
 }  // namespace mx
 
 using namespace mx;
@@ -871,6 +914,21 @@ extern "C" int mx_roi_loss_bwd(const float* logits, int64_t ldl, int C, const fl
   MX_CHECK_ARG(R > 0 && C > 0 && grad && grad_logits && grad_reg, "roi_loss bwd: bad arguments");
   roi_loss_bwd_kernel<<<(unsigned)cdiv(R, 256), 256, 0, (hipStream_t)stream>>>(logits, ldl, C, reg, ldr, labels, targets,
                                                                                R, beta, grad, grad_logits, grad_reg);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" int mx_bn_act_maxpool(const float* z, int64_t N, int64_t H, int64_t W, int64_t C, const float* scale,
+                                 const float* shift, int act, int k, int stride, int pad, float* y, mx_stream_t stream) {
+  MX_CHECK_ARG(z && scale && shift && y, "bn_act_maxpool: null operand");
+  MX_CHECK_ARG(N >= 0 && H > 0 && W > 0 && C > 0 && C % 8 == 0, "bn_act_maxpool: bad shape (C %% 8 == 0)");
+  MX_CHECK_ARG(k > 0 && stride > 0 && pad >= 0 && pad * 2 <= k, "bn_act_maxpool: bad pooling window");
+  MX_CHECK_ARG(act >= 0 && act <= 2, "bn_act_maxpool: act %d", act);
+  const int64_t Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  const int64_t n = N * Ho * Wo * (C / 8);
+  if (n == 0) return MX_OK;
+  bn_act_maxpool_kernel<<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(z, N, H, W, C, Ho, Wo, k, stride, pad,
+                                                                                   scale, shift, act, y);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

@@ -2748,6 +2748,160 @@ __global__ void krsc_to_dgrad_kernel(const uint16_t* __restrict__ w, PackP p) {
   p.wt[p.off[q] + ((c * p.Rc[q] + r / p.st_h) * p.Sc[q] + sx / p.st_w) * p.Kpad + k] = w[i];
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// ResNet stem (torchvision resnet50 conv1 -> bn1 -> ReLU), bf16x3: a 7x7 conv of an NHWC f32 image whose
+// first 4 channels (RGB + one zero pad) are read, to 64 channels. The generic x3 kernels walk
+// K = 7*7*8 = 392 (two-thirds zero products, padded to 416); here one MFMA K-step of 32 is one filter
+// row r: 8 taps (s = 0..6 and a zero s = 7) x 4 channels, so 7 K-steps (224) cover the 147 real
+// products. The MFMA's A operand is the weights (rows = output channels; the packed hi / lo planes are
+// rearranged into fragment-ready [plane][r][k][s*4 + c] rows in LDS once per block), B the pixels:
+// lane (g, c16) of a 16-pixel tile loads taps 2g, 2g+1 of pixel c16 as two float4 (channels 0..3)
+// and splits them into hi / lo in registers -- no LDS staging of the image. A wave owns 64 output
+// pixels (STEM_T tiles of 16, one BatchNorm statistics row) for all 64 channels: per-channel
+// (sum, sum of squares) partials of the train-mode BatchNorm, or bias + activation, in the epilogue;
+// the accumulator layout (4 consecutive channels of one pixel per lane) gives float4 stores. Blocks
+// loop over contiguous pixel ranges (XCD-aware), so the weight rearrangement is paid ~2 x CUs times.
+static constexpr int STEM_T = 4, STEM_K = 64, STEM_R = 7;
+struct StemP {
+  const float* x;       // [N][H][W][C] f32, channels 0..3 read
+  const uint16_t* w;    // [2][64][7][7][C] bf16 hi / lo planes (mx_conv2d_fwd_x3's packing)
+  const float* bias;    // [64] or null
+  float* y;             // [N][Ho][Wo][64]
+  float* stats;         // null, or [2][mblocks][64] BatchNorm partials (sum; sum of squares)
+  int64_t M, mblocks;   // M = N * Ho * Wo
+  int64_t tiles_per_block;
+  int H, W, C, Ho, Wo, st_h, st_w, pad_h, pad_w, act;
+  int xbytes;           // bytes of x: the buffer loads' range (out-of-range offsets read zeros)
+};
+
+__global__ void __launch_bounds__(256, 2) conv_stem_x3_kernel(StemP p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __shared__ __attribute__((aligned(16))) uint16_t wl[2 * STEM_R * STEM_K * 32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = p.H, W = p.W, C = p.C;
+  {
+    // (plane, r, k, s) quads of 4 channels: 8-B loads of the packed planes, zeros at s = 7
+    const int64_t plane = (int64_t)STEM_K * 49 * C;
+    for (int i = tid; i < 2 * STEM_R * STEM_K * 8; i += 256) {
+      const int sx = i & 7, k = (i >> 3) & 63, r = (i >> 9) % STEM_R, pl = i / (8 * 64 * STEM_R);
+      uint2 v = make_uint2(0u, 0u);
+      if (sx < 7) v = *(const uint2*)(p.w + pl * plane + ((int64_t)k * 49 + r * 7 + sx) * C);
+      *(uint2*)(wl + ((pl * STEM_R + r) * STEM_K + k) * 32 + sx * 4) = v;
+    }
+  }
+  __syncthreads();
+  const int64_t blk = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int g = lane >> 4, c16 = lane & 15;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+  const int64_t ntiles = (p.M + 16 * STEM_T - 1) / (16 * STEM_T);
+  const int64_t tbeg = blk * p.tiles_per_block, tend = min<int64_t>(ntiles, tbeg + p.tiles_per_block);
+  for (int64_t tile = tbeg + wave; tile < tend; tile += 4) {
+    const int64_t m0 = tile * (16 * STEM_T);
+    int rowb[STEM_T], ih0[STEM_T], iw0[STEM_T];
+#pragma unroll
+    for (int t = 0; t < STEM_T; ++t) {
+      const int64_t m = m0 + t * 16 + c16;
+      if (m < p.M) {
+        const int ow = (int)(m % p.Wo);
+        const int64_t q = m / p.Wo;
+        const int oh = (int)(q % p.Ho), n = (int)(q / p.Ho);
+        rowb[t] = n * H;
+        ih0[t] = oh * p.st_h - p.pad_h;
+        iw0[t] = ow * p.st_w - p.pad_w + 2 * g;
+      } else {
+        rowb[t] = 0;
+        ih0[t] = -(1 << 20);  // every row invalid
+        iw0[t] = 0;
+      }
+    }
+    f32x4 acc[STEM_T][4];
+#pragma unroll
+    for (int t = 0; t < STEM_T; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < STEM_R; ++r) {
+      float4 ra[STEM_T], rb[STEM_T];
+#pragma unroll
+      for (int t = 0; t < STEM_T; ++t) {
+        const int ih = ih0[t] + r;
+        const bool rok = (unsigned)ih < (unsigned)H;
+        const uint32_t e0 = ((uint32_t)(rowb[t] + ih) * (uint32_t)W + (uint32_t)iw0[t]) * (uint32_t)C;
+        const bool ok0 = rok && (unsigned)iw0[t] < (unsigned)W;
+        const bool ok1 = rok && g < 3 && (unsigned)(iw0[t] + 1) < (unsigned)W;
+        ra[t] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok0 ? e0 * 4u : kOOB, 0, 0));
+        rb[t] = __builtin_bit_cast(float4,
+                                   __builtin_amdgcn_raw_buffer_load_b128(xr, ok1 ? (e0 + (uint32_t)C) * 4u : kOOB, 0, 0));
+      }
+      bf16x8 ah[4], al[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = r * STEM_K + 16 * j + c16;
+        ah[j] = *(const bf16x8*)(wl + row * 32 + g * 8);
+        al[j] = *(const bf16x8*)(wl + (STEM_R * STEM_K + row) * 32 + g * 8);
+      }
+#pragma unroll
+      for (int t = 0; t < STEM_T; ++t) {
+        uint4 h, l;
+        split8(ra[t], rb[t], h, l);
+        const bf16x8 bh = __builtin_bit_cast(bf16x8, h), bl = __builtin_bit_cast(bf16x8, l);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[j], bh, acc[t][j], 0, 0, 0);
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bl, acc[t][j], 0, 0, 0);
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bh, acc[t][j], 0, 0, 0);
+        }
+      }
+    }
+    if (p.stats) {  // this wave's 64 pixels are statistics row m0 / 64
+      const int64_t srow = m0 / SROWS;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < STEM_T; ++t) {
+          const bool ok = m0 + t * 16 + c16 < p.M;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float v = ok ? acc[t][j][i] : 0.f;
+            s[i] += v;
+            q[i] += v * v;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            s[i] += __shfl_xor(s[i], o);
+            q[i] += __shfl_xor(q[i], o);
+          }
+        if (c16 == 0) {
+          const int ch = 16 * j + 4 * g;
+          *(float4*)(p.stats + srow * STEM_K + ch) = make_float4(s[0], s[1], s[2], s[3]);
+          *(float4*)(p.stats + (p.mblocks + srow) * STEM_K + ch) = make_float4(q[0], q[1], q[2], q[3]);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < STEM_T; ++t) {
+      const int64_t m = m0 + t * 16 + c16;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ch = 16 * j + 4 * g;
+        const float4 b = p.bias ? *(const float4*)(p.bias + ch) : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 v = make_float4(acc[t][j][0] + b.x, acc[t][j][1] + b.y, acc[t][j][2] + b.z, acc[t][j][3] + b.w);
+        if (p.act == 1) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        *(float4*)(p.y + m * STEM_K + ch) = v;
+      }
+    }
+  }
+#endif
+}
+
 }  // namespace mx
 
 using namespace mx;
@@ -3762,5 +3916,31 @@ extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const
     wgrad_reduce_kernel<<<dim3((unsigned)cdiv(p.Ncol / 4, 64), (unsigned)Kout), 256, 0, st>>>(p, (int)g.splits);
     MX_LAUNCH_CHECK();
   }
+  return MX_OK;
+}
+
+extern "C" int mx_conv2d_stem_x3(const mx_conv_shape* s, const float* x, const uint16_t* w, const float* bias,
+                                 int act, float* y, float* stats, mx_stream_t stream) {
+  int rc = conv_check(s);
+  if (rc) return rc;
+  MX_CHECK_ARG(s->R == 7 && s->S == 7 && s->K == STEM_K, "conv stem x3: a 7x7 conv to 64 channels is required");
+  MX_CHECK_ARG(s->C >= 4 && s->C % 4 == 0, "conv stem x3: input channel stride C=%lld must be a multiple of 4",
+               (long long)s->C);
+  MX_CHECK_ARG(act == 0 || act == 1, "conv stem x3: act 0 (none) or 1 (relu)");
+  MX_CHECK_ARG(x && w && y, "conv stem x3: null operand");
+  MX_CHECK_ARG(s->N * s->H * s->W * s->C * 4 < (1ll << 31), "conv stem x3: input must stay below 2 GiB");
+  StemP p{};
+  p.x = x; p.w = w; p.bias = bias; p.y = y; p.stats = stats;
+  p.M = s->N * s->Ho * s->Wo;
+  p.mblocks = cdiv(p.M, SROWS);
+  p.H = (int)s->H; p.W = (int)s->W; p.C = (int)s->C; p.Ho = (int)s->Ho; p.Wo = (int)s->Wo;
+  p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w; p.act = act;
+  p.xbytes = (int)(s->N * s->H * s->W * s->C * 4);
+  const int64_t ntiles = cdiv(p.M, 16 * STEM_T);
+  const int64_t slots = 2 * (int64_t)num_cus();
+  p.tiles_per_block = std::max<int64_t>(4, cdiv(cdiv(ntiles, slots), 4) * 4);
+  const int64_t blocks = cdiv(ntiles, p.tiles_per_block);
+  conv_stem_x3_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(p);
+  MX_LAUNCH_CHECK();
   return MX_OK;
 }

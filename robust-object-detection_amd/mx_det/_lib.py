@@ -152,6 +152,8 @@ _SIGS = {
     "mx_sgd_pack_build": (c_int, [c_vp, c_i64, c_vp, c_vp, ctypes.c_size_t, c_vp, c_vp]),
     "mx_sgd_pack_step": (c_int, [c_vp, c_vp, c_i64, c_i64, ctypes.c_size_t, c_f, c_f, c_f, c_f, c_int, c_vp]),
     "mx_bn_apply": (c_int, [c_vp, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
+    "mx_bn_act_maxpool": (c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp,
+                                  c_vp]),
     "mx_bn_bwd_reduce": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
     "mx_bn_bwd_apply": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_bn_bwd_workspace": (ctypes.c_size_t, [c_i64, c_i64]),
@@ -159,6 +161,7 @@ _SIGS = {
                                     ctypes.c_size_t, c_vp, c_vp, c_vp]),
     "mx_bn_bwd_apply_ex": (c_int, [c_vp, c_vp, c_vp, c_int, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
     "mx_conv_workspace_x3": (c_sz, [ctypes.POINTER(ConvShape), c_int]),
+    "mx_conv2d_stem_x3": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
     "mx_conv2d_fwd_x3": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_sz,
                                  c_vp]),
     "mx_conv2d_dgrad_x3": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,

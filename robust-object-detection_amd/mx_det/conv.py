@@ -207,9 +207,11 @@ def _tuned(key, cands, apply, run, default):
         apply(default)
 
 
-def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dtype=None, stats=False):
+def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dtype=None, stats=False, cin=None):
     """x NHWC, wk KRSC bf16 -> y NHWC; optional BN stat partials. bf16 x: wk [K,R,S,C], output
-    out_dtype (default bf16). f32 x (bf16x3): wk [2,K,R,S,C] hi / lo planes, output and residual f32."""
+    out_dtype (default bf16). f32 x (bf16x3): wk [2,K,R,S,C] hi / lo planes, output and residual f32.
+    cin: the weight's real input channels (<= C); a 7x7 conv to 64 channels of a <= 4-channel input
+    (the ResNet stem) runs mx_conv2d_stem_x3 (MX_STEM_KERNEL=0: the generic x3 kernels)."""
     x3 = is_x3(x)
     assert wk.dtype == torch.bfloat16 and x.is_contiguous() and wk.is_contiguous()
     if x3:
@@ -231,6 +233,14 @@ def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dty
         residual = residual.contiguous()
         assert residual.dtype == (torch.float32 if x3 else torch.bfloat16), residual.dtype
     t0 = _timer.start() if _timer else None
+    if (x3 and cin is not None and cin <= 4 and K == 64 and R == 7 and S == 7 and residual is None
+            and act in (ACT_NONE, ACT_RELU) and os.environ.get("MX_STEM_KERNEL", "1") != "0"):
+        call("mx_conv2d_stem_x3", ctypes.byref(sh), _p(x), _p(wk), _p(bias), int(act), _p(y), _p(st), _s())
+        if _timer:
+            _timer.stop("x3_fwd64", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * cin, t0,
+                        _tag(sh.N, sh.H, sh.W, C, K, R, S, stride),
+                        x.numel() * x.element_size() + wk.numel() * 2 + y.numel() * y.element_size())
+        return (y, st) if stats else y
 
     def run():
         if x3:
@@ -848,6 +858,38 @@ def bn_scratch(nbytes, device):
     return t
 
 
+def bn_train_finalize(st, K, M, gamma, beta, eps, momentum, rmean, rvar):
+    """Train-mode BatchNorm from the conv's statistics partials st [2, mb, K]: batch mean / invstd, the
+    apply's per-channel scale / shift, and the running-stat update in place (mx_bn_finalize_ex)."""
+    mean = torch.empty(K, dtype=torch.float32, device=st.device)
+    invstd, scale, shift = torch.empty_like(mean), torch.empty_like(mean), torch.empty_like(mean)
+    fws = bn_scratch(_lib.load().mx_bn_finalize_workspace(st.shape[1], K), st.device)
+    call("mx_bn_finalize_ex", _p(st), st.shape[1], K, M, _p(gamma.detach()), _p(beta.detach()), float(eps),
+         float(momentum), _p(rmean), _p(rvar), _p(mean), _p(invstd), _p(scale), _p(shift), _p(fws), fws.numel(), _s())
+    return mean, invstd, scale, shift
+
+
+def conv_bn_act_maxpool(x, conv, bn, act, k, st, pd):
+    """Forward-only conv -> train-mode BatchNorm -> act -> max pool, for a block no gradient flows
+    through (the frozen ResNet stem: conv1 / bn1 parameters frozen, image input): the conv writes the
+    BN statistics partials (mx_conv2d_stem_x3 for the 7x7 stem), and the BN apply runs inside the pool
+    (mx_bn_act_maxpool), so the full-resolution activation is written once (the conv output) and
+    never re-written. Same running-stat update and result as conv_bn + maxpool."""
+    assert is_x3(x) and bn.training
+    if bn.num_batches_tracked is not None and id(bn) not in _nbt_batched:
+        bn.num_batches_tracked.add_(1)
+    w = conv.weight
+    wk, _ = operands(w, x.shape[3], conv.stride, conv.padding, _ceil8(w.shape[0]), False, split=True)
+    z, stt = conv_fwd(x.contiguous(), wk, conv.stride, conv.padding, stats=True, cin=w.shape[1])
+    N, H, W, K = z.shape
+    _, _, scale, shift = bn_train_finalize(stt, K, N * H * W, bn.weight, bn.bias, bn.eps, bn.momentum,
+                                           bn.running_mean, bn.running_var)
+    Ho, Wo = (H + 2 * pd - k) // st + 1, (W + 2 * pd - k) // st + 1
+    y = torch.empty((N, Ho, Wo, K), dtype=torch.float32, device=z.device)
+    call("mx_bn_act_maxpool", _p(z), N, H, W, K, _p(scale), _p(shift), int(act), k, st, pd, _p(y), _s())
+    return y
+
+
 class ConvBNAct(torch.autograd.Function):
     """y = act(BN_train(conv(x, w)) (+ residual)). Updates running stats in place."""
 
@@ -858,16 +900,10 @@ class ConvBNAct(torch.autograd.Function):
         ctx.link, ctx.role = link if link is not None else (None, None)
         ctx.bnb_own, ctx.bnb_feed = bnb_own, bnb_feed
         wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(w.shape[0]), need_dx, split=is_x3(x))
-        z, st = conv_fwd(x, wk, stride, pad, stats=True)
+        z, st = conv_fwd(x, wk, stride, pad, stats=True, cin=w.shape[1])
         K = w.shape[0]
         M = z.numel() // K
-        mean = torch.empty(K, dtype=torch.float32, device=x.device)
-        invstd, scale, shift = torch.empty_like(mean), torch.empty_like(mean), torch.empty_like(mean)
-        fwb = _lib.load().mx_bn_finalize_workspace(st.shape[1], K)
-        fws = bn_scratch(fwb, x.device)
-        call("mx_bn_finalize_ex", _p(st), st.shape[1], K, M, _p(gamma.detach()), _p(beta.detach()), float(eps),
-             float(momentum), _p(rmean), _p(rvar), _p(mean), _p(invstd), _p(scale), _p(shift), _p(fws), fws.numel(),
-             _s())
+        mean, invstd, scale, shift = bn_train_finalize(st, K, M, gamma, beta, eps, momentum, rmean, rvar)
         y = torch.empty_like(z)
         res = residual.contiguous() if residual is not None else None
         t0 = _timer.start() if _timer else None
@@ -1054,4 +1090,5 @@ def fold_bn(conv, bn):
 def eval_conv_bn(x, conv, bn, act, residual=None):
     w, b = fold_bn(conv, bn)
     wk, _ = pack_weight(w, x.shape[3], conv.stride, conv.padding, split=is_x3(x))
-    return conv_fwd(x.contiguous(), wk, conv.stride, conv.padding, bias=b, residual=residual, act=act)
+    return conv_fwd(x.contiguous(), wk, conv.stride, conv.padding, bias=b, residual=residual, act=act,
+                    cin=conv.weight.shape[1])

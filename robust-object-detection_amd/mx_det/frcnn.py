@@ -101,6 +101,13 @@ class ResNet50Body(nn.Module):
     LAYERS = ("layer1", "layer2", "layer3", "layer4")
 
     def stem(self, x, be):
+        if (getattr(be, "name", "") == "hip" and x.is_cuda and x.dtype == torch.float32 and self.bn1.training
+                and os.environ.get("MX_STEM_FUSED", "1") != "0" and not (torch.is_grad_enabled() and (
+                    x.requires_grad or any(p.requires_grad for p in self.conv1.parameters())
+                    or any(p.requires_grad for p in self.bn1.parameters())))):
+            # frozen stem (torchvision trainable_layers <= 4): no gradient flows through conv1 / bn1 /
+            # relu / maxpool, so the BN apply runs inside the pool (mc.conv_bn_act_maxpool)
+            return mc.conv_bn_act_maxpool(x, self.conv1, self.bn1, ACT_RELU, 3, 2, 1)
         x = be.conv_bn(x, self.conv1, self.bn1, ACT_RELU)
         return be.maxpool(x, 3, 2, 1)
 

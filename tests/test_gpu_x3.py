@@ -109,6 +109,68 @@ def test_x3_fwd(dev, N, H, W, C, K, k, st, pd):
     torch.testing.assert_close(s[1], (z * z).sum(0), rtol=0, atol=1e-5 * (z * z).sum(0).max().item())
 
 
+@pytest.mark.parametrize("N,H,W,cin,st,pd,act", [
+    (2, 33, 41, 3, 2, 3, 1),     # odd sizes: a pixel tail below one 64-pixel statistics row
+    (1, 64, 96, 3, 2, 3, 0),
+    (2, 120, 200, 3, 2, 3, 1),   # several tiles per block
+    (1, 23, 19, 4, 1, 2, 1),     # 4 real channels, stride 1, pad 2
+])
+def test_x3_stem_kernel(dev, N, H, W, cin, st, pd, act, monkeypatch):
+    """mx_conv2d_stem_x3 (the 7x7 -> 64 ResNet stem, one MFMA K-step per filter row) against float64
+    torch with the x3 bar, its BN statistics partials against the f64 sums, and against the generic
+    x3 kernels (MX_STEM_KERNEL=0) on the same packed operands."""
+    from mx_det import conv as mc
+    g = torch.Generator().manual_seed(N * 100 + H)
+    x = torch.zeros(N, H, W, 8)
+    x[..., :cin] = torch.randn(N, H, W, cin, generator=g)
+    w = torch.randn(64, cin, 7, 7, generator=g) * 0.05
+    b = torch.randn(64, generator=g)
+    xn = x[..., :cin].permute(0, 3, 1, 2)
+    ref = F.conv2d(xn.double(), w.double(), b.double(), st, pd).permute(0, 2, 3, 1)
+    reft = F.conv2d(tf32(xn).double(), tf32(w).double(), b.double(), st, pd).permute(0, 2, 3, 1)
+    z = (ref - b.double()).reshape(-1, 64)
+    if act:
+        ref, reft = ref.clamp_min(0), reft.clamp_min(0)
+    wk, _ = mc.pack_weight(w.to(dev), 8, (st, st), (pd, pd), split=True)
+    xd = x.to(dev)
+    monkeypatch.setenv("MX_STEM_KERNEL", "1")
+    y, stats = mc.conv_fwd(xd, wk, (st, st), (pd, pd), bias=b.to(dev), act=act, stats=True, cin=cin)
+    _check(y, ref, reft)
+    s = stats.cpu().double().sum(1)
+    torch.testing.assert_close(s[0], z.sum(0), rtol=0, atol=1e-5 * z.abs().sum(0).max().item())
+    torch.testing.assert_close(s[1], (z * z).sum(0), rtol=0, atol=1e-5 * (z * z).sum(0).max().item())
+    monkeypatch.setenv("MX_STEM_KERNEL", "0")
+    y0 = mc.conv_fwd(xd, wk, (st, st), (pd, pd), bias=b.to(dev), act=act, cin=cin)
+    assert rel(y, y0) < 1e-6
+
+
+def test_stem_fused_bn_pool_matches_unfused(dev):
+    """The frozen stem's conv -> train BN -> relu -> maxpool with the BN apply inside the pool
+    (conv_bn_act_maxpool) returns bit-identically what conv_bn + maxpool return, and updates the
+    running statistics identically."""
+    import copy
+    from mx_det import conv as mc
+    from mx_det.backend import _MaxPool
+    torch.manual_seed(3)
+    conv = mc.Conv2d(3, 64, 7, 2, 3, bias=False).to(dev)
+    bn = mc.BatchNorm2d(64).to(dev)
+    with torch.no_grad():
+        conv.weight.normal_(0, 0.05)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    for p in list(conv.parameters()) + list(bn.parameters()):
+        p.requires_grad_(False)
+    bn2 = copy.deepcopy(bn)
+    x = torch.zeros(2, 70, 90, 8, device=dev)
+    x[..., :3] = torch.randn(2, 70, 90, 3, device=dev)
+    y1 = mc.conv_bn_act_maxpool(x, conv, bn, mc.ACT_RELU, 3, 2, 1)
+    y2 = _MaxPool.apply(mc.conv_bn(x, conv, bn2, mc.ACT_RELU), 3, 2, 1)
+    assert y1.shape == y2.shape == (2, 18, 23, 64)
+    assert torch.equal(y1, y2)
+    assert torch.equal(bn.running_mean, bn2.running_mean) and torch.equal(bn.running_var, bn2.running_var)
+    assert int(bn.num_batches_tracked) == int(bn2.num_batches_tracked) == 1
+
+
 def test_x3_fwd_residual_leaky(dev):
     from mx_det import conv as mc
     g = torch.Generator().manual_seed(1)
