@@ -2802,10 +2802,9 @@ __global__ void __launch_bounds__(256, 2) conv_stem_x3_kernel(StemP p) {
 #pragma unroll
     for (int t = 0; t < STEM_T; ++t) {
       const int64_t m = m0 + t * 16 + c16;
-      if (m < p.M) {
-        const int ow = (int)(m % p.Wo);
-        const int64_t q = m / p.Wo;
-        const int oh = (int)(q % p.Ho), n = (int)(q / p.Ho);
+      if (m < p.M) {  // M < 2^31 (conv_check): 32-bit index math
+        const int mi = (int)m, q = mi / p.Wo, ow = mi - q * p.Wo;
+        const int n = q / p.Ho, oh = q - n * p.Ho;
         rowb[t] = n * H;
         ih0[t] = oh * p.st_h - p.pad_h;
         iw0[t] = ow * p.st_w - p.pad_w + 2 * g;
@@ -3938,7 +3937,7 @@ extern "C" int mx_conv2d_stem_x3(const mx_conv_shape* s, const float* x, const u
   p.xbytes = (int)(s->N * s->H * s->W * s->C * 4);
   const int64_t ntiles = cdiv(p.M, 16 * STEM_T);
   const int64_t slots = 2 * (int64_t)num_cus();
-  p.tiles_per_block = std::max<int64_t>(4, cdiv(cdiv(ntiles, slots), 4) * 4);
+  p.tiles_per_block = std::max<int64_t>(4, cdiv(ntiles, slots));  // ~2 blocks per CU, equal shares
   const int64_t blocks = cdiv(ntiles, p.tiles_per_block);
   conv_stem_x3_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(p);
   MX_LAUNCH_CHECK();
