@@ -2796,6 +2796,11 @@ __global__ void __launch_bounds__(256, 2) conv_stem_x3_kernel(StemP p) {
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
   const int64_t ntiles = (p.M + 16 * STEM_T - 1) / (16 * STEM_T);
   const int64_t tbeg = blk * p.tiles_per_block, tend = min<int64_t>(ntiles, tbeg + p.tiles_per_block);
+  float4 bias4[4];  // this lane's 4 channels of each 16-channel column tile (loaded once: no vmcnt wait
+                    // between the epilogue's stores)
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    bias4[j] = p.bias ? *(const float4*)(p.bias + 16 * j + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
   for (int64_t tile = tbeg + wave; tile < tend; tile += 4) {
     const int64_t m0 = tile * (16 * STEM_T);
     int rowb[STEM_T], ih0[STEM_T], iw0[STEM_T];
@@ -2819,9 +2824,10 @@ __global__ void __launch_bounds__(256, 2) conv_stem_x3_kernel(StemP p) {
     for (int t = 0; t < STEM_T; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < STEM_R; ++r) {
-      float4 ra[STEM_T], rb[STEM_T];
+    // filter row r + 1's image loads are issued before row r's MFMAs (two register stages; the
+    // scheduling barriers keep the compiler from sinking them next to their first use)
+    float4 ra[2][STEM_T], rb[2][STEM_T];
+    auto issue = [&](const int r, float4 (&xa)[STEM_T], float4 (&xb)[STEM_T]) {
 #pragma unroll
       for (int t = 0; t < STEM_T; ++t) {
         const int ih = ih0[t] + r;
@@ -2829,10 +2835,17 @@ __global__ void __launch_bounds__(256, 2) conv_stem_x3_kernel(StemP p) {
         const uint32_t e0 = ((uint32_t)(rowb[t] + ih) * (uint32_t)W + (uint32_t)iw0[t]) * (uint32_t)C;
         const bool ok0 = rok && (unsigned)iw0[t] < (unsigned)W;
         const bool ok1 = rok && g < 3 && (unsigned)(iw0[t] + 1) < (unsigned)W;
-        ra[t] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok0 ? e0 * 4u : kOOB, 0, 0));
-        rb[t] = __builtin_bit_cast(float4,
+        xa[t] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok0 ? e0 * 4u : kOOB, 0, 0));
+        xb[t] = __builtin_bit_cast(float4,
                                    __builtin_amdgcn_raw_buffer_load_b128(xr, ok1 ? (e0 + (uint32_t)C) * 4u : kOOB, 0, 0));
       }
+    };
+    issue(0, ra[0], rb[0]);
+#pragma unroll
+    for (int r = 0; r < STEM_R; ++r) {
+      const int b = r & 1;
+      if (r + 1 < STEM_R) issue(r + 1, ra[b ^ 1], rb[b ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
       bf16x8 ah[4], al[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -2843,7 +2856,7 @@ __global__ void __launch_bounds__(256, 2) conv_stem_x3_kernel(StemP p) {
 #pragma unroll
       for (int t = 0; t < STEM_T; ++t) {
         uint4 h, l;
-        split8(ra[t], rb[t], h, l);
+        split8(ra[b][t], rb[b][t], h, l);
         const bf16x8 bh = __builtin_bit_cast(bf16x8, h), bl = __builtin_bit_cast(bf16x8, l);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -2852,6 +2865,7 @@ __global__ void __launch_bounds__(256, 2) conv_stem_x3_kernel(StemP p) {
           acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bh, acc[t][j], 0, 0, 0);
         }
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (p.stats) {  // this wave's 64 pixels are statistics row m0 / 64
       const int64_t srow = m0 / SROWS;
@@ -2889,7 +2903,7 @@ __global__ void __launch_bounds__(256, 2) conv_stem_x3_kernel(StemP p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int ch = 16 * j + 4 * g;
-        const float4 b = p.bias ? *(const float4*)(p.bias + ch) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 b = bias4[j];
         float4 v = make_float4(acc[t][j][0] + b.x, acc[t][j][1] + b.y, acc[t][j][2] + b.z, acc[t][j][3] + b.w);
         if (p.act == 1) {
           v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
