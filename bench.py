@@ -85,13 +85,53 @@ def train_step(model, opt, images, targets, augment=False, gen=None, as_list=Fal
     return float(losses.item())
 
 
+def host_threads():
+    """CPU threads the CPU-baseline legs run on: the host cores this job may use, whatever the launcher
+    did to OMP_NUM_THREADS. torch.distributed.run sets OMP_NUM_THREADS=1 in every rank when it was unset
+    (so at N>1 torch.get_num_threads() would be 1); _launch_ranks passes the parent's setting on as
+    MX_HOST_THREADS. Order: MX_CPU_THREADS (explicit), MX_HOST_THREADS (the launching shell's
+    OMP_NUM_THREADS), OMP_NUM_THREADS unless it is torchrun's default of 1 at N>1, else the CPUs this
+    process may run on (sched_getaffinity)."""
+    for k in ("MX_CPU_THREADS", "MX_HOST_THREADS"):
+        v = os.environ.get(k, "")
+        if v.isdigit() and int(v) > 0:
+            return int(v)
+    v = os.environ.get("OMP_NUM_THREADS", "")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if v.isdigit() and int(v) > 0 and not (int(v) == 1 and world > 1):
+        return int(v)
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        return max(1, os.cpu_count() or 1)
+
+
+class _threads:
+    """torch.set_num_threads(n) for the block, restored afterwards."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __enter__(self):
+        self.old = torch.get_num_threads()
+        torch.set_num_threads(self.n)
+        return torch.get_num_threads()
+
+    def __exit__(self, *a):
+        torch.set_num_threads(self.old)
+
+
 def cpu_baseline(gpu_model, seconds_hint=30.0):
     """The oracle CPU restatement (oracle/cpu_backend.py: torch-CPU fp32 dense ops + C torchvision ops)
-    timed on this host's cores for ONE train step of the same workload (bs=2, 1333x800)."""
+    timed on this host's cores (host_threads()) for ONE train step of the same workload (bs=2, 1333x800)."""
+    with _threads(host_threads()) as cores:
+        return _cpu_baseline(gpu_model, seconds_hint, cores)
+
+
+def _cpu_baseline(gpu_model, seconds_hint, cores):
     from oracle.cpu_backend import CpuBackend
     from mx_det.data import synth_batch
     torch.manual_seed(0)
-    cores = torch.get_num_threads()
     m = build_model("cpu", backend=CpuBackend())
     m.load_state_dict({k: v.detach().cpu() for k, v in gpu_model.state_dict().items()})
     m.train()
@@ -345,7 +385,7 @@ def _time_precision(precision, args, world, rank, dev, imgs, tg):
     torch.manual_seed(42)
     model = build_model(dev, precision=precision).train()
     ddp = model
-    if world > 1:
+    if dist.is_initialized():  # world > 1, or MX_BENCH_DP=1 (a one-rank nccl group)
         # DDP semantics (rank-0 init, per-GPU BN, averaged gradients) with the HIP graphs kept on:
         # gradients are all-reduced over RCCL after the backward (mx_det.dp.DataParallel)
         from mx_det.dp import DataParallel
@@ -427,9 +467,13 @@ def _time_eval(precision, args, world, rank, dev, imgs, restored):
 
 def cpu_eval_baseline(gpu_model, gpu_unet, img, seconds_hint=30.0):
     """The oracle CPU restatement (CpuBackend model + oracle/unet_ref.py U-Net) timed on one image of
-    the same eval workload, from the GPU models' weights."""
+    the same eval workload, from the GPU models' weights, on host_threads() threads."""
+    with _threads(host_threads()) as cores:
+        return _cpu_eval_baseline(gpu_model, gpu_unet, img, seconds_hint, cores)
+
+
+def _cpu_eval_baseline(gpu_model, gpu_unet, img, seconds_hint, cores):
     from oracle.cpu_backend import CpuBackend
-    cores = torch.get_num_threads()
     m = build_model("cpu", backend=CpuBackend())
     m.load_state_dict({k: v.detach().cpu() for k, v in gpu_model.state_dict().items()})
     m.eval()
@@ -713,16 +757,23 @@ def visdrone_main(args, world, rank, dev):
         print(json.dumps(rec), flush=True)
 
 
-def _launch_ranks(n):
-    """torch.distributed.run --nproc-per-node n over 127.0.0.1 re-running this script with the same
-    arguments; returns the launcher's exit code."""
+def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    return port
+
+
+def _launch_ranks(n):
+    """torch.distributed.run --nproc-per-node n over 127.0.0.1 re-running this script with the same
+    arguments; returns the launcher's exit code."""
+    port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():  # torchrun would keep it; recorded for host_threads()
+        env.setdefault("MX_HOST_THREADS", os.environ["OMP_NUM_THREADS"])
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL / CUDA IPC)
     return subprocess.call(cmd, env=env)
 
@@ -765,11 +816,18 @@ def main():
     rehearse = os.environ.get("MX_BENCH_REHEARSE") == "1"
     if rehearse:
         local = 0
+    # MX_BENCH_DP=1 at one rank: a world-size-1 nccl group and the DataParallel wrapper, i.e. the N>1
+    # code path (RCCL init with device_id, hook-issued async all-reduces beside the graph replays)
+    one_rank_dp = world == 1 and os.environ.get("MX_BENCH_DP") == "1"
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or one_rank_dp:
         if rehearse:
             dist.init_process_group("gloo")
+        elif one_rank_dp:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
         else:
             dist.init_process_group("nccl", device_id=dev)
 
@@ -786,7 +844,7 @@ def main():
             script_main(args, world, rank, dev, imgs, tg)
         else:
             eval_main(args, world, rank, dev, imgs)
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
             dist.destroy_process_group()
         return
@@ -811,7 +869,8 @@ def main():
         "config": {"workload": "configs[1]: FRCNN R50-FPN v2 baseline train step" + (" + 50% on-GPU corruption"
                                                                                    if args.augment else ""),
                    "global_batch": 2 * world, "per_gpu_batch": 2, "image": "1333x800 (padded 1344x800)",
-                   "parallelism": f"dp{world}", "trainable_backbone_layers": 3},
+                   "parallelism": f"dp{world}" + (" (nccl group, DataParallel)" if world == 1 and dist.is_initialized()
+                                                   else ""), "trainable_backbone_layers": 3},
     }
     peak = {"f32": X3_PEAK_TFLOPS, "bf16": BF16_PEAK_TFLOPS}
     # the measurement legs run a train step through the data-parallel wrapper, whose gradient
@@ -873,7 +932,7 @@ def main():
         rec["cpu_baseline"] = cpu_baseline(cpu_model)
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -167,9 +167,11 @@ class HipBackend:
 
     def proposal_nms_select(self, boxes, scores, lvl, group, G, L, thr, max_seg, post):
         """filter_proposals' NMS on its presorted candidates plus the padded per-image selection:
-        (sel [G, post], valid [G, post]) (mx_batched_nms_grouped_sorted)."""
-        _, _, sel, valid = ops.batched_nms_grouped_sorted(boxes, scores, lvl, group, G, L, thr, max_seg, post)
-        return sel, valid
+        (sel [G, post], valid [G, post], num_keep [1] int64) (mx_batched_nms_grouped_sorted). num_keep < 0
+        flags a failure the selection cannot show (-2: candidates not in the presorted layout, -1: a
+        segment over max_seg): the caller checks it (frcnn RegionProposalNetwork.check_nms)."""
+        _, nk, sel, valid = ops.batched_nms_grouped_sorted(boxes, scores, lvl, group, G, L, thr, max_seg, post)
+        return sel, valid, nk
 
     def box_decode(self, rel, boxes, weights):
         return ops.box_decode(rel, boxes, weights)

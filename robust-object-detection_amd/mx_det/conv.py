@@ -538,6 +538,28 @@ def side_wgrad_enabled(ctx):
     return _dp or not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
 
 
+def grad_dest(ctx):
+    """The data-parallel bucket slot (mx_det.dp.DataParallel: `_mx_grad_slot` on the parameter) of this
+    conv's weight gradient, as a fresh view for the wgrad kernel to write into -- or None. AccumulateGrad
+    adopts the returned tensor as `.grad` (autograd holds its only reference), so the gradient is born in
+    the all-reduce buffer. Only a weight used ONCE in the graph whose `.grad` is None qualifies (a shared
+    weight's calls would all write the same slot before autograd sums them); a view of a parameter (FC6's
+    [1024, 256, 7, 7] over the Linear weight) maps to its base's slot. Call before side_wgrad_enabled
+    (which consumes ctx.uses)."""
+    uses = ctx.uses
+    if uses is None or uses.n != 1:
+        return None
+    w = ctx.wref()
+    if w is None:
+        return None
+    p = w if w.is_leaf else w._base
+    slot = getattr(p, "_mx_grad_slot", None) if p is not None else None
+    if slot is None or not p.is_leaf or p.grad is not None or not w.is_contiguous() or w.numel() != p.numel():
+        return None
+    flat, off = slot
+    return flat.narrow(0, off, p.numel()).view(w.shape)
+
+
 def _join_side():
     cur = torch.cuda.current_stream()
     for ev, _keep in _pending:
@@ -545,11 +567,11 @@ def _join_side():
     _pending.clear()
 
 
-def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False):
+def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False, out=None):
     """dy NHWC [N,Ho,Wo,K], x NHWC (both bf16, or both f32 -> bf16x3 kernels) -> dW f32
     [kout, cin, R, S] (torch weight layout; the zero-padded channels K > kout, C > cin are dropped).
     side=True (inside a backward pass only): launched on the side stream, joined at the end of the
-    backward."""
+    backward. out: a preallocated f32 [kout, cin, R, S] destination (grad_dest)."""
     sh = shape(x, K, R, S, stride, pad)
     kout = kout or K
     cin = cin or x.shape[3]
@@ -557,7 +579,11 @@ def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False):
     assert dy.dtype == x.dtype, (dy.dtype, x.dtype)
     wsfn = "mx_conv_workspace_x3" if x3 else "mx_conv_workspace"
     entry = "mx_conv2d_wgrad_x3" if x3 else "mx_conv2d_wgrad_ex"
-    dw = torch.empty((kout, cin, R, S), dtype=torch.float32, device=x.device)
+    if out is not None:
+        assert out.shape == (kout, cin, R, S) and out.dtype == torch.float32 and out.is_contiguous(), out.shape
+        dw = out
+    else:
+        dw = torch.empty((kout, cin, R, S), dtype=torch.float32, device=x.device)
     dyc = dy.contiguous()
     t0 = _timer.start() if _timer else None
     key = ("wgrad", x.dtype, sh.N, sh.H, sh.W, x.shape[3], K, R, S, tuple(stride), tuple(pad))
@@ -782,7 +808,9 @@ class ConvAct(torch.autograd.Function):
             if ctx.chain is not None:
                 dx = ctx.chain.hand(dx)
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1], side=side_wgrad_enabled(ctx))
+            dst = grad_dest(ctx)
+            dw = conv_wgrad(gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1], side=side_wgrad_enabled(ctx),
+                            out=dst)
         return dx, dw, db, None, None, None, None
 
 
@@ -965,7 +993,8 @@ class ConvBNAct(torch.autograd.Function):
             if chain is not None:
                 dx = chain.hand(dx)
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(dz, x, K, R, S, stride, pad, cin=wshape[1], side=side_wgrad_enabled(ctx))
+            dst = grad_dest(ctx)
+            dw = conv_wgrad(dz, x, K, R, S, stride, pad, cin=wshape[1], side=side_wgrad_enabled(ctx), out=dst)
         dgamma = sums[1] if ctx.needs_input_grad[2] else None
         dbeta = sums[0] if ctx.needs_input_grad[3] else None
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None

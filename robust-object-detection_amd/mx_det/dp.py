@@ -25,12 +25,30 @@ order whichever of its units replayed graphs. Anything not started by a hook (ea
 in ~`bucket_mb` buckets. Over xGMI a ring all-reduce of the 172 MB of f32 gradients costs
 ~2·(N-1)/N·172 MB / bus bandwidth; with the overlap only the last segment's (layer2, 5 MB) is
 exposed.
+
+Persistent buckets: every group (and every remaining bucket) owns ONE flat f32 gradient buffer for
+the wrapper's lifetime, and each trainable parameter a fixed slot in it (`p._mx_grad_slot`). The conv
+weight gradients -- all but ~1 % of the 43M trainable values -- are written by their wgrad kernels
+straight into their slot (conv.grad_dest: the conv backward hands AccumulateGrad a view of the slot,
+which it adopts as `.grad`; inside the captured backward graphs the slot is the graph's own gradient
+buffer), so the all-reduce runs on the gradients in place: no flatten copy in, no unflatten copy out.
+A gradient that arrives elsewhere (BatchNorm affine, biases, the RPN head's weights summed over five
+levels, a parameter unused on this rank) is copied into its slot (one multi-tensor launch per group)
+and the parameter's `.grad` becomes the slot view. Over RCCL the average is `ReduceOp.AVG` (ncclAvg:
+no separate 1/N pass); gloo has no AVG, so it sums and scales.
 """
 import torch
 import torch.distributed as dist
-from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
 
-from . import conv as _conv
+
+def _slot_view(flat, off, p):
+    return flat.narrow(0, off, p.numel()).view(p.shape)
+
+
+def _in_slot(g, flat, off, p):
+    """True when gradient g already IS parameter p's slot of the bucket `flat` (same memory, dense)."""
+    return (g is not None and g.data_ptr() == flat.data_ptr() + 4 * off and g.dtype == torch.float32
+            and g.is_contiguous() and g.numel() == p.numel())
 
 
 class DataParallel:
@@ -42,7 +60,7 @@ class DataParallel:
             for t in list(model.parameters()) + list(model.buffers()):
                 dist.broadcast(t.data, 0, group=group)
         self.params = [p for p in model.parameters() if p.requires_grad]
-        self._work = {}  # key -> (work, flat, grads) started from a graph hand-off hook
+        self._work = {}  # key -> (work, key) started from a graph hand-off hook
         # the RoI head's gradients are complete as soon as its backward graph has replayed, before
         # the trunk's (most of the step's backward): their all-reduce starts right then and overlaps
         # the trunk backward (hook fired by frcnn._Graphs; without it they join the normal buckets)
@@ -79,8 +97,26 @@ class DataParallel:
         if cur:
             self.buckets.append(cur)
         self.bucket_mb = bucket_mb
+        # persistent flat buffer per group / bucket, a fixed slot per parameter (module docstring)
+        self.flats = {}
+        for key, ps in self.groups + [(("bucket", i), b) for i, b in enumerate(self.buckets)]:
+            if any(p.dtype != torch.float32 for p in ps) or len({p.device for p in ps}) != 1:
+                raise RuntimeError("DataParallel: trainable parameters must be f32 on one device per group")
+            flat = torch.zeros(sum(p.numel() for p in ps), dtype=torch.float32, device=ps[0].device)
+            slots, off = [], 0
+            for p in ps:
+                p.__dict__["_mx_grad_slot"] = (flat, off)
+                slots.append((p, off))
+                off += p.numel()
+            self.flats[key] = (flat, slots)
+        self.op, self.scale = dist.ReduceOp.SUM, 1.0 / self.world
+        if dist.get_backend(group) == "nccl":  # RCCL: ncclAvg, the 1/N folded into the reduction
+            self.op, self.scale = dist.ReduceOp.AVG, None
+        self.copied = 0  # gradients copied into their slot in the last synced step (diagnostics)
+        self._copied = 0
         for m in model.modules():  # graphs and side-stream wgrad stay enabled under this wrapper
             m.__dict__["_mx_dp"] = True
+        from . import conv as _conv
         _conv.set_data_parallel(True)
 
     def __call__(self, *args, **kwargs):
@@ -95,22 +131,32 @@ class DataParallel:
         return self
 
     @torch.no_grad()
-    def _start(self, params):
-        grads = []
-        for p in params:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-            grads.append(p.grad)
-        flat = _flatten_dense_tensors(grads)
-        return dist.all_reduce(flat, group=self.group, async_op=True), flat, grads
+    def _start(self, key):
+        """Gather group `key`'s gradients into its flat buffer (only those not already written into
+        their slot) and start its all-reduce."""
+        flat, slots = self.flats[key]
+        src, dst, zero = [], [], []
+        for p, off in slots:
+            g = p.grad
+            if g is None:
+                zero.append(_slot_view(flat, off, p))
+            elif not _in_slot(g, flat, off, p):
+                src.append(g)
+                dst.append(_slot_view(flat, off, p))
+        if zero:
+            torch._foreach_zero_(zero)
+        if src:
+            torch._foreach_copy_(dst, src)
+        self._copied += len(src)
+        return dist.all_reduce(flat, op=self.op, group=self.group, async_op=True), key
 
     def _issue_through(self, key):
         """Start, in canonical order, every group up to and including `key` not yet started."""
         if key not in dict(self.groups):
             return
-        for k, params in self.groups:
+        for k, _ in self.groups:
             if k not in self._work:
-                self._work[k] = self._start(params)
+                self._work[k] = self._start(k)
                 self.issued.append(k)
             if k == key:
                 return
@@ -129,17 +175,22 @@ class DataParallel:
         """Average the trainable gradients over all ranks (call after backward, before step). A
         parameter without a gradient on this rank contributes zeros (and gets the average).
         Every rank issues the all-reduces in the same canonical order (module docstring), whichever
-        of them its hooks started."""
+        of them its hooks started. Afterwards every trainable `.grad` is its bucket slot."""
         if self.groups:
             self._issue_through(self.groups[-1][0])  # whatever no hook started, in canonical order
         started = self._work
         self._work = {}
         pending = [started[k] for k, _ in self.groups]
-        for b in self.buckets:
-            pending.append(self._start(b))
+        for i in range(len(self.buckets)):
+            pending.append(self._start(("bucket", i)))
             self.issued.append("bucket")
-        for work, flat, grads in pending:
+        for work, key in pending:
             work.wait()
-            flat.mul_(1.0 / self.world)
-            torch._foreach_copy_(grads, _unflatten_dense_tensors(flat, grads))
+            flat, slots = self.flats[key]
+            if self.scale is not None:
+                flat.mul_(self.scale)
+            for p, off in slots:
+                if not _in_slot(p.grad, flat, off, p):
+                    p.grad = _slot_view(flat, off, p)
         self.last_issued, self.issued = self.issued, []
+        self.copied, self._copied = self._copied, 0

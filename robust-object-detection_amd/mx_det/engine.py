@@ -215,6 +215,23 @@ def train_frcnn(cfg):
     # is synchronised and t0 taken, at the end of training t1 and the number of timed steps
     timer = cfg.get("TIMER")
     n_batches = len(train_loader)
+
+    def _start_clock():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        timer["t0"] = time.perf_counter()
+        from . import _lib
+        _lib.trace_marker(1)  # rocprofv3 kernel-trace delimiters (tools/prof_steps.py)
+        if "loader" in timer:
+            timer["wait0"] = timer["loader"].wait_s
+
+    if timer is not None:
+        if not 0 <= timer["warmup"] < n_batches * cfg["EPOCHS"]:
+            raise ValueError(f"TIMER warmup {timer['warmup']} must be below the {n_batches * cfg['EPOCHS']} "
+                             "training steps")
+        if timer["warmup"] == 0:
+            _start_clock()
     kick = getattr(train_loader, "kick", None)
     for epoch in range(1, cfg["EPOCHS"] + 1):
         if sampler is not None:
@@ -239,15 +256,8 @@ def train_frcnn(cfg):
             it_global += 1
             optimizer.step()
             epoch_loss += float(losses.item())
-            if timer is not None and it_global == timer["warmup"]:
-                torch.cuda.synchronize()
-                if world > 1:
-                    dist.barrier()
-                timer["t0"] = time.perf_counter()
-                from . import _lib
-                _lib.trace_marker(1)  # rocprofv3 kernel-trace delimiters (tools/prof_steps.py)
-                if "loader" in timer:
-                    timer["wait0"] = timer["loader"].wait_s
+            if timer is not None and timer["warmup"] > 0 and it_global == timer["warmup"]:
+                _start_clock()
             if rank == 0 and ((i + 1) % 100 == 0 or (i + 1) == n_batches):
                 print(f"  [Epoch {epoch:03d}] batch {i + 1}/{n_batches}", flush=True)
         if timer is not None and epoch == cfg["EPOCHS"]:
@@ -367,7 +377,12 @@ def _pack_targets(targets, pin=True):
             ent.append((k, v, off, nb))
             off += (nb + 7) & ~7
         layout.append(ent)
-    buf = torch.empty(max(off, 8), dtype=torch.uint8, pin_memory=pin)
+    if pin:
+        from .conv import capture_lock
+        with capture_lock:  # a pinned allocation beside an open graph capture would invalidate it
+            buf = torch.empty(max(off, 8), dtype=torch.uint8, pin_memory=True)
+    else:
+        buf = torch.empty(max(off, 8), dtype=torch.uint8)
     for ent in layout:
         for k, v, o, nb in ent:
             if nb:

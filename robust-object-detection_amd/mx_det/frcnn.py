@@ -511,12 +511,14 @@ class RegionProposalNetwork(nn.Module):
         if hasattr(be, "proposal_nms_select") and os.environ.get("MX_SORTED_NMS", "1") != "0":
             # the candidates are presorted (image, level, score desc: the per-level top-k order): the
             # sort-free NMS also emits the padded per-image selection
-            sel, valid = be.proposal_nms_select(boxes.reshape(-1, 4), prob.reshape(-1), lvl_flat, grp, N,
-                                                len(num_per_level), self.nms_thresh, max(pre, 1000), post)
+            sel, valid, nk = be.proposal_nms_select(boxes.reshape(-1, 4), prob.reshape(-1), lvl_flat, grp, N,
+                                                    len(num_per_level), self.nms_thresh, max(pre, 1000), post)
+            self._watch_nms(nk)
             return boxes.reshape(-1, 4)[sel], prob.reshape(-1)[sel], valid
         kk, nk = be.proposal_nms(boxes.reshape(-1, 4), prob.reshape(-1), lvl_flat, grp, N,
                                  len(num_per_level), self.nms_thresh, max(pre, 1000))
         kk, nk = kk.to(dev), nk.to(dev)
+        self._watch_nms(nk)
         live = torch.arange(n, device=dev) < nk
         cnt = torch.zeros(N + 1, dtype=torch.int64, device=dev)
         cnt.scatter_add_(0, torch.where(live, grp[kk].to(torch.int64), N), live.to(torch.int64))
@@ -525,6 +527,43 @@ class RegionProposalNetwork(nn.Module):
         sel = kk[((torch.cumsum(cnt, 0) - cnt)[:, None] + r[None, :]).clamp(max=n - 1)]  # [N, post]
         valid = r[None, :] < cnt[:, None]                 # survivors are a prefix of each row
         return boxes.reshape(-1, 4)[sel], prob.reshape(-1)[sel], valid
+
+    def _watch_nms(self, nk):
+        """The proposal NMS reports what its selection cannot show as num_keep < 0 (-2: candidates not in
+        the presorted (image, level) layout, mx_batched_nms_grouped_sorted; -1: an (image, level) segment
+        over max_seg): copied to pinned memory without waiting, checked by check_nms() once a later host
+        sync has passed -- the step never trains on a silently empty selection."""
+        if nk.is_cuda and torch.cuda.is_current_stream_capturing():
+            return  # a captured proposal chain (tests/test_gpu_graphs.py) has no host sync to check at
+        if not nk.is_cuda:
+            if int(nk.reshape(-1)[0]) < 0:
+                self._nk_pending = (nk.reshape(()).clone(), None)
+            return
+        host = self.__dict__.get("_nk_host")
+        if host is None:
+            with mc.capture_lock:  # pinned allocation: never beside an open graph capture
+                host = self.__dict__["_nk_host"] = torch.empty((), dtype=torch.int64, pin_memory=True)
+        host.copy_(nk.reshape(-1)[0], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._nk_pending = (host, ev)
+
+    def check_nms(self):
+        """Raise if the last proposal NMS reported a failure (see _watch_nms). Called after the RoI head,
+        whose host sync has already waited for the NMS, so the event wait is free."""
+        pend = self.__dict__.pop("_nk_pending", None)
+        if pend is None:
+            return
+        host, ev = pend
+        if ev is not None:
+            ev.synchronize()
+        v = int(host)
+        if v == -2:
+            raise RuntimeError("proposal NMS: candidates are not in the presorted (image, level, score) layout "
+                               "mx_batched_nms_grouped_sorted requires (num_keep = -2); MX_SORTED_NMS=0 selects "
+                               "the general grouped NMS")
+        if v < 0:
+            raise RuntimeError(f"proposal NMS: an (image, level) segment exceeds max_seg (num_keep = {v})")
 
     def filter_proposals(self, proposals, objectness, image_sizes, num_per_level, be):
         """torchvision's filter_proposals: per image, the kept proposal boxes and scores (lists; one
@@ -598,6 +637,9 @@ class RegionProposalNetwork(nn.Module):
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 tgt = compute_targets()
+            # recorded right away: if the proposal chain below raises, FasterRCNN.forward's finally
+            # still joins the side stream (join_losses)
+            self._loss_side = side
             losses = lambda: loss_of(tgt)  # noqa: E731 (deferred: called after join_losses)
         else:
             losses = compute_losses if defer_losses else compute_losses()
@@ -607,9 +649,7 @@ class RegionProposalNetwork(nn.Module):
             boxes = self.filter_proposals_padded(proposals, objectness, images.image_sizes, num_per_level, be)
         else:
             boxes, _ = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
-        if side is not None:
-            self._loss_side = side  # joined by join_losses(): after the RoI head, not before its host sync
-        return boxes, losses
+        return boxes, losses  # the side stream is joined by join_losses(): after the RoI head
 
     def join_losses(self):
         """Make the current stream wait for the side-stream loss chain (a no-op without one)."""
@@ -1061,14 +1101,15 @@ class FasterRCNN(nn.Module):
         # MX_RPN_DEFER_LOSSES=1 issues the RPN target / loss launches after the RoI sampler's host sync;
         # measured 0.5 % slower than issuing them while the trunk runs (A/B on one box), so off
         defer = os.environ.get("MX_RPN_DEFER_LOSSES", "0") != "0"
-        proposals, rpn_losses = self.rpn(il, features, targets, be, head=head, defer_losses=defer)
         try:
+            proposals, rpn_losses = self.rpn(il, features, targets, be, head=head, defer_losses=defer)
             if degenerate is not None:
                 host, ev = degenerate
                 ev.synchronize()
                 if bool(host):
                     raise ValueError("All bounding boxes should have positive height and width.")
             detections, det_losses = self.roi_heads(features, proposals, il.image_sizes, targets, be)
+            self.rpn.check_nms()
         finally:  # also when the step raises: no side-stream work is left unjoined behind it
             self.rpn.join_losses()
         if self.training:

@@ -56,8 +56,12 @@ def decode_coefs(data, info=None, out=None):
 def host_stage(data):
     """The host half of decode(): marker parse + entropy decode straight into pinned memory ->
     (info, pinned int16 tensor), ready for an asynchronous copy (device_stage). Thread-safe."""
+    from .conv import capture_lock
     info = parse(data)
-    host = torch.empty(info.coef_total, dtype=torch.int16, pin_memory=True)
+    # pinned allocations (cudaHostAlloc on a cache miss) are prohibited while another thread has a graph
+    # capture open in global mode: the training thread's captures (frcnn._Graphs) hold capture_lock
+    with capture_lock:
+        host = torch.empty(info.coef_total, dtype=torch.int16, pin_memory=True)
     return decode_coefs(data, info, out=host)
 
 

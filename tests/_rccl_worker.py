@@ -1,0 +1,109 @@
+"""Rank body of tests/test_gpu_rccl.py: the data-parallel path over the `nccl` backend (RCCL on ROCm) in a
+fresh process -- a world-size-1 group on cuda:0, which runs every RCCL call configs[2]'s 8-GPU run makes
+(init with device_id, the rank-0 broadcasts, async all-reduces issued from the graph hand-off hooks on
+RCCL's stream beside the HIP-graph replays, ReduceOp.AVG, waits) with nothing to exchange.
+
+Three augmented steps (train_frcnn_augmented.py:159-177: on-GPU RandomCorruption, forward, loss sum,
+backward) through mx_det.dp.DataParallel with the segmented trunk graphs, beside an unwrapped copy of
+the model that runs the same segmented graphs (a no-op hand-off hook selects them), so both execute the
+same kernels in the same order: losses and gradients must agree to 1e-6 (they are expected bitwise).
+Also records the hook / issue order and how many gradients were copied into their bucket slot (the
+rest were written there by their wgrad kernels). Writes one JSON result to argv[1]."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "robust-object-detection_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def _keys(seed):
+    g = torch.Generator().manual_seed(seed)
+    return lambda shape, device: torch.rand(shape, generator=g).to(device)
+
+
+def _model(dev):
+    from mx_det import frcnn
+    torch.manual_seed(0)
+    m = frcnn.fasterrcnn_resnet50_fpn_v2(weights=None)
+    m.roi_heads.box_predictor = frcnn.FastRCNNPredictor(m.roi_heads.box_predictor.cls_score.in_features, 7)
+    frcnn.set_trainable_layers(m.backbone.body, 3)
+    return m.to(dev).train()
+
+
+def main():
+    out = sys.argv[1]
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    res = {"backend": dist.get_backend(), "steps": 0, "worst_grad": 0.0, "worst_loss": 0.0, "order": [],
+           "issued": [], "copied": [], "slot_grads": 0, "trainable": 0}
+    from mx_det import ops, frcnn
+    from mx_det.data import synth_batch
+    from mx_det.dp import DataParallel
+    ref = _model(dev)
+    ref.__dict__["_mx_seg_ready"] = lambda key, ps: None  # same segmented trunk graphs, no exchange
+    m = _model(dev)
+    m.load_state_dict(ref.state_dict())
+    dp = DataParallel(m)
+    res["reduce_op"] = str(dp.op)
+    hook = m.__dict__["_mx_seg_ready"]
+    m.__dict__["_mx_seg_ready"] = lambda key, ps: (res["order"].append(key), hook(key, ps))
+    imgs, tg = synth_batch(40, 6, H=512, W=672, device=dev)
+    for step in range(3):
+        i, t = imgs[2 * step:2 * step + 2], tg[2 * step:2 * step + 2]
+        i = ops.corrupt_u8(i, [(step + k) % 4 for k in range(2)], seed=step)
+        for mod in (ref, m):
+            mod.rpn.fg_bg_sampler.rand = _keys(7 + step)
+            mod.roi_heads.fg_bg_sampler.rand = _keys(8 + step)
+        lr = ref(i, t)
+        ld = dp(i, t)
+        for p in list(ref.parameters()) + list(m.parameters()):
+            p.grad = None
+        sum(lr.values()).backward()
+        sum(ld.values()).backward()
+        before = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+        born = 0  # gradients written straight into their bucket slot by the backward (no copy)
+        for p in m.parameters():
+            if p.requires_grad and p.grad is not None:
+                flat, off = p._mx_grad_slot
+                born += int(p.grad.data_ptr() == flat.data_ptr() + 4 * off)
+        res["slot_grads"] = born
+        dp.sync_gradients()
+        torch.cuda.synchronize()
+        res["issued"].append(list(dp.last_issued))
+        res["copied"].append(dp.copied)
+        for k in lr:
+            a, b = float(ld[k]), float(lr[k])
+            res["worst_loss"] = max(res["worst_loss"], abs(a - b) / max(abs(b), 1e-30))
+        for (n, p), q in zip(m.named_parameters(), ref.parameters()):
+            if not p.requires_grad:
+                continue
+            flat, off = p._mx_grad_slot
+            assert p.grad.data_ptr() == flat.data_ptr() + 4 * off, n  # every .grad is its slot after sync
+            e = ((p.grad - q.grad).norm() / q.grad.norm().clamp_min(1e-30)).item()
+            if e > res["worst_grad"]:
+                res["worst_grad"], res["worst_param"] = e, n
+            # a one-rank average is the identity
+            assert torch.equal(p.grad, before[n]), n
+        res["trainable"] = sum(p.requires_grad for p in m.parameters())
+        with torch.no_grad():  # one identical update on both copies: the replays see new, equal weights
+            for p, q in zip(m.parameters(), ref.parameters()):
+                if p.requires_grad:
+                    d = 1e-3 * q.grad
+                    p.sub_(d)
+                    q.sub_(d)
+        res["steps"] += 1
+        print(f"step {step} worst_grad {res['worst_grad']:.3e} copied {dp.copied}", flush=True)
+    res["trunk_seg_graphs"] = sum(isinstance(g, frcnn._SegGraphs) for g in m.__dict__.get("_mx_graphs", {}).values())
+    res["head_graphs"] = len(m.roi_heads.__dict__.get("_mx_graphs", {}))
+    with open(out, "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

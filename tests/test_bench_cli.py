@@ -41,3 +41,39 @@ def test_gpus_n_spawns_launcher(monkeypatch):
     assert "--master-addr=127.0.0.1" in cmd and cmd[-6:] == ["--gpus", "8", "--steps", "3", "--warmup", "1"]
     assert cmd[cmd.index("--nnodes=1") + 4].endswith("bench.py")
     assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_cpu_baseline_threads_ignore_torchrun_default(monkeypatch):
+    """torch.distributed.run sets OMP_NUM_THREADS=1 in every rank when the variable was unset,
+    so a CPU baseline reading torch.get_num_threads() at N>1 timed ONE thread. bench.host_threads()
+    picks the host's cores itself."""
+    import bench
+    for k in ("MX_CPU_THREADS", "MX_HOST_THREADS", "OMP_NUM_THREADS", "WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    ncpu = len(os.sched_getaffinity(0))
+    assert bench.host_threads() == ncpu
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")  # torchrun's default: not a request
+    assert bench.host_threads() == ncpu
+    monkeypatch.setenv("MX_HOST_THREADS", "16")  # the launching shell's setting, passed on by _launch_ranks
+    assert bench.host_threads() == 16
+    monkeypatch.setenv("MX_CPU_THREADS", "6")
+    assert bench.host_threads() == 6
+    monkeypatch.delenv("MX_CPU_THREADS")
+    monkeypatch.delenv("MX_HOST_THREADS")
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench.host_threads() == 3
+    with bench._threads(2) as n:
+        assert n == 2
+    assert bench.torch.get_num_threads() != 2 or ncpu == 2
+
+
+def test_launcher_passes_the_shell_thread_count(monkeypatch):
+    import bench
+    seen = {}
+    monkeypatch.setattr(bench.subprocess, "call", lambda cmd, env=None: seen.update(env=env) or 0)
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    monkeypatch.delenv("MX_HOST_THREADS", raising=False)
+    bench._launch_ranks(2)
+    assert seen["env"]["MX_HOST_THREADS"] == "16"

@@ -107,7 +107,9 @@ def test_dp_issue_order_is_canonical_whatever_the_hooks():
         dp.groups = [(k, [k]) for k in keys]
         dp.buckets = [["rest"]]
         dp._work, dp.issued, dp.last_issued, dp.world = {}, [], [], 1
-        dp._start = lambda params: (_Done(), torch.zeros(1), [torch.zeros(1)])
+        dp.flats = {k: (torch.zeros(1), []) for k in keys + [("bucket", 0)]}
+        dp.scale, dp._copied = None, 0
+        dp._start = lambda key: (_Done(), key)
         return dp
 
     class _Done:

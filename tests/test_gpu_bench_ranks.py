@@ -19,7 +19,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.mark.timeout(560)
 def test_bench_two_ranks_default_flags():
-    env = dict(os.environ, MX_BENCH_REHEARSE="1", HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="8")
+    # the launching shell's OMP_NUM_THREADS (16 on the GPU boxes) is left as it is: the CPU baseline must
+    # pick its thread count itself (bench.host_threads), not inherit torchrun's per-rank default of 1
+    env = dict(os.environ, MX_BENCH_REHEARSE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
@@ -35,4 +37,5 @@ def test_bench_two_ranks_default_flags():
         assert key in rec, key
     assert rec["roofline"]["frac"] > 0 and "roi_align_fwd" in rec["hbm_ops"]
     assert rec["cpu_baseline"]["value"] > 0 and rec["cpu_baseline"]["kind"] == "port"
+    assert rec["cpu_baseline"]["cores"] > 1, rec["cpu_baseline"]
     assert "roofline" in rec["bf16_variant"]

@@ -115,6 +115,7 @@ def test_x3_fwd(dev, N, H, W, C, K, k, st, pd):
     (2, 120, 200, 3, 2, 3, 1),   # several tiles per block
     (1, 23, 19, 4, 1, 2, 1),     # 4 real channels, stride 1, pad 2
     (2, 64, 128, 3, 2, 3, 1),    # Ho % 4 == 0, Wo % 16 == 0: 4 x 16 patch tiles
+    (2, 800, 1344, 3, 2, 3, 1),  # the headline stem: configs[1]'s padded 2 x 800 x 1344 batch -> 400 x 672
 ])
 def test_x3_stem_kernel(dev, N, H, W, cin, st, pd, act, monkeypatch):
     """mx_conv2d_stem_x3 (the 7x7 -> 64 ResNet stem, one MFMA K-step per filter row) against float64
