@@ -42,6 +42,8 @@ for s in $STEPS; do
         || { echo "prof_steps failed"; tail -5 "$OUT/step_kernels.log"; }
       tr=$(find "$OUT/prof" -name '*kernel_trace.csv' | head -n 1)
       [ -n "$tr" ] && python3 tools/step_gaps.py "$tr" 20 > "$OUT/step_gaps.log" 2>&1
+      [ -n "$tr" ] && python3 tools/step_concurrency.py "$tr" 10 > "$OUT/step_concurrency.log" 2>&1
+      [ -n "$tr" ] && gzip -c "$tr" > "$OUT/kernel_trace.csv.gz"
       rm -rf "$OUT/prof"
       tail -1 "$OUT/prof.log" ;;
     pmc)
