@@ -560,6 +560,52 @@ def grad_dest(ctx):
     return flat.narrow(0, off, p.numel()).view(w.shape)
 
 
+def wgrad_stream(device):
+    """The side stream of the weight gradients forked from the CURRENT stream: one per issuing stream
+    (the backward runs a node on its forward's stream: the main / capture stream, the FPN and RPN-head
+    branch streams). A side stream is in-order, so one shared by every branch made a wgrad whose fork
+    event fires late (an FPN branch's, inside the captured backward graph) hold back every later wgrad
+    of the main chain: they ran as a serial tail after the dgrad chain (profiles/r05c, 1.9 ms)."""
+    if os.environ.get("MX_WGRAD_PER_STREAM", "1") == "0":
+        return dedicated_stream(device, "wgrad")
+    cur = torch.cuda.current_stream(device)
+    name = _wgrad_names.get(cur.cuda_stream)
+    if name is None:
+        name = _wgrad_names[cur.cuda_stream] = "wgrad" if not _wgrad_names else f"wgrad{len(_wgrad_names)}"
+    return dedicated_stream(device, name)
+
+
+_wgrad_names = {}
+
+
+def _wgrad_plan(ctx, dy, x, K, R, S, stride, pad, kout=None, cin=None):
+    """A conv backward's weight gradient, decided BEFORE its dgrad is launched: (job, side, fork) for
+    wgrad_launch after the dgrad, or None when the weight needs no gradient. A side-stream wgrad is
+    prepared (wgrad_prepare: every allocation and copy) and forked from an event recorded here, ahead
+    of the dgrad (its operands dy and x are final), so (a) it runs beside the dgrad, and (b) inside a
+    captured backward graph the node feeding both gets the dgrad as its FIRST dependent, which keeps
+    the dgrad chain -- the backward's critical path -- on one hardware queue of the HIP graph executor
+    instead of hopping to another at every conv (each hop ~10 us of idle GPU:
+    profiles/r05b_step_concurrency.txt). MX_WGRAD_FORK_EARLY=0: prepared and forked after the dgrad."""
+    if not ctx.needs_input_grad[1]:
+        return None
+    dst = grad_dest(ctx)
+    side = side_wgrad_enabled(ctx)
+    if side and os.environ.get("MX_WGRAD_FORK_EARLY", "1") != "0":
+        job = wgrad_prepare(dy, x, K, R, S, stride, pad, kout, cin, dst)
+        fork = torch.cuda.Event()
+        fork.record()
+        return job, side, fork
+    return (dy, x, K, R, S, stride, pad, kout, cin, dst), side, None
+
+
+def _wgrad_run(plan):
+    job, side, fork = plan
+    if not isinstance(job, _WgradJob):
+        job = wgrad_prepare(*job)
+    return wgrad_launch(job, side, fork)
+
+
 def _join_side():
     cur = torch.cuda.current_stream()
     for ev, _keep in _pending:
@@ -567,44 +613,69 @@ def _join_side():
     _pending.clear()
 
 
-def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False, out=None):
-    """dy NHWC [N,Ho,Wo,K], x NHWC (both bf16, or both f32 -> bf16x3 kernels) -> dW f32
-    [kout, cin, R, S] (torch weight layout; the zero-padded channels K > kout, C > cin are dropped).
-    side=True (inside a backward pass only): launched on the side stream, joined at the end of the
-    backward. out: a preallocated f32 [kout, cin, R, S] destination (grad_dest)."""
-    sh = shape(x, K, R, S, stride, pad)
-    kout = kout or K
-    cin = cin or x.shape[3]
-    x3 = is_x3(x)
+class _WgradJob:
+    """A weight gradient's launch prepared ahead of time (wgrad_prepare): shape, operands, output and
+    split workspace allocated and the tuner's pick applied, so the launch itself allocates nothing."""
+    __slots__ = ("sh", "x3", "entry", "dw", "dyc", "x", "ws", "wsb", "cfg", "kout", "cin", "K", "R", "S", "stride",
+                 "t0")
+
+
+def wgrad_prepare(dy, x, K, R, S, stride, pad, kout=None, cin=None, out=None):
+    """Everything of conv_wgrad before the launch: on the current stream (allocations, dy.contiguous(),
+    the tuner's first trial of the shape). A side-stream launch forked BEFORE the dgrad (_wgrad_plan)
+    needs these done first: a workspace allocated after the dgrad could reuse the dgrad's just-freed
+    split-K slab while the dgrad's reduce still reads it."""
+    j = _WgradJob()
+    sh = j.sh = shape(x, K, R, S, stride, pad)
+    j.kout = kout = kout or K
+    j.cin = cin = cin or x.shape[3]
+    j.K, j.R, j.S, j.stride = K, R, S, stride
+    j.x3 = x3 = is_x3(x)
     assert dy.dtype == x.dtype, (dy.dtype, x.dtype)
     wsfn = "mx_conv_workspace_x3" if x3 else "mx_conv_workspace"
-    entry = "mx_conv2d_wgrad_x3" if x3 else "mx_conv2d_wgrad_ex"
+    j.entry = entry = "mx_conv2d_wgrad_x3" if x3 else "mx_conv2d_wgrad_ex"
     if out is not None:
         assert out.shape == (kout, cin, R, S) and out.dtype == torch.float32 and out.is_contiguous(), out.shape
         dw = out
     else:
         dw = torch.empty((kout, cin, R, S), dtype=torch.float32, device=x.device)
-    dyc = dy.contiguous()
-    t0 = _timer.start() if _timer else None
+    j.dw = dw
+    j.x = x
+    j.dyc = dyc = dy.contiguous()
+    j.t0 = _timer.start() if _timer else None
     key = ("wgrad", x.dtype, sh.N, sh.H, sh.W, x.shape[3], K, R, S, tuple(stride), tuple(pad))
     if key not in _tune_cache and _tune_on() and _timer is None and not torch.cuda.is_current_stream_capturing():
-        def trial():  # timed on the current stream; the real launch below may go to the side stream
+        def trial():  # timed on the current stream; the real launch may go to the side stream
             wsb_ = getattr(_lib.load(), wsfn)(ctypes.byref(sh), 2)
             ws_ = torch.empty(wsb_, dtype=torch.uint8, device=x.device) if wsb_ else None
             call(entry, ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws_), wsb_, _s())
         _tuned(key, _WG_CANDS_X3 if x3 else _WG_CANDS, _apply_wg, trial, _WG_DEFAULT)
-    tune = _tune_on()
-    if tune:
-        _apply_wg(_tune_cache.get(key, _WG_DEFAULT))
-    wsb = getattr(_lib.load(), wsfn)(ctypes.byref(sh), 2)
-    ws = torch.empty(wsb, dtype=torch.uint8, device=x.device) if wsb else None
+    j.cfg = _tune_cache.get(key, _WG_DEFAULT) if _tune_on() else None
+    if j.cfg is not None:
+        _apply_wg(j.cfg)
+    j.wsb = getattr(_lib.load(), wsfn)(ctypes.byref(sh), 2)
+    j.ws = torch.empty(j.wsb, dtype=torch.uint8, device=x.device) if j.wsb else None
+    if j.cfg is not None:
+        _apply_wg(_WG_DEFAULT)
+    return j
+
+
+def wgrad_launch(j, side=False, fork=None):
+    """Launch a prepared weight gradient (wgrad_prepare) on the current stream, or with side=True on
+    the side stream, after `fork` (an event recorded on the current stream) or, without one, after
+    everything issued so far on the current stream. Returns dW."""
     stream = _s()
     if side:
-        st = dedicated_stream(x.device, "wgrad")
-        st.wait_stream(torch.cuda.current_stream())
+        st = wgrad_stream(j.x.device)
+        if fork is not None:  # recorded by _wgrad_plan before the dgrad
+            st.wait_event(fork)
+        else:
+            st.wait_stream(torch.cuda.current_stream())
         stream = st.cuda_stream
-    call(entry, ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws), wsb, stream)
-    if tune:
+    if j.cfg is not None:
+        _apply_wg(j.cfg)
+    call(j.entry, ctypes.byref(j.sh), _p(j.dyc), _p(j.x), _p(j.dw), j.kout, j.cin, 1, _p(j.ws), j.wsb, stream)
+    if j.cfg is not None:
         _apply_wg(_WG_DEFAULT)
     if side:
         ev = torch.cuda.Event()
@@ -613,12 +684,23 @@ def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False, out
             torch.autograd.Variable._execution_engine.queue_callback(_join_side)
         # dw itself is NOT held: AccumulateGrad adopts the tensor only while autograd holds the sole
         # reference (an extra one makes it clone dw on the main stream, before the side kernel ran)
-        _pending.append((ev, (dyc, x, ws)))
+        _pending.append((ev, (j.dyc, j.x, j.ws)))
+    dw, sh, x, dyc, K, R, S, stride, t0 = j.dw, j.sh, j.x, j.dyc, j.K, j.R, j.S, j.stride, j.t0
+    x3 = j.x3
+    j.dw = None
     if _timer:
         _timer.stop(("x3_" if x3 else "") + "wgrad", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * x.shape[3], t0,
                     _tag(sh.N, sh.H, sh.W, x.shape[3], K, R, S, stride),
                     dyc.numel() * dyc.element_size() + x.numel() * x.element_size() + dw.numel() * 4)
     return dw
+
+
+def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False, out=None):
+    """dy NHWC [N,Ho,Wo,K], x NHWC (both bf16, or both f32 -> bf16x3 kernels) -> dW f32
+    [kout, cin, R, S] (torch weight layout; the zero-padded channels K > kout, C > cin are dropped).
+    side=True (inside a backward pass only): launched on the side stream, joined at the end of the
+    backward. out: a preallocated f32 [kout, cin, R, S] destination (grad_dest)."""
+    return wgrad_launch(wgrad_prepare(dy, x, K, R, S, stride, pad, kout, cin, out), side)
 
 
 def act_bias_bwd(gy, y, act, K8, need_db, g_dtype=torch.bfloat16):
@@ -791,6 +873,7 @@ class ConvAct(torch.autograd.Function):
         dx = dw = db = None
         K8 = (K + 7) // 8 * 8
         gk, db = act_bias_bwd(gy, y, act, K8, has_b and ctx.needs_input_grad[2], g_dtype=x.dtype)
+        wg = _wgrad_plan(ctx, gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1])  # before the dgrad
         if ctx.needs_input_grad[0]:
             if _is_dense(x.shape, R, S, stride, pad):  # 1x1-GEMM form: dX[N, R*S*C] = dY[N, K8] wt
                 N, H, W, C = x.shape
@@ -807,10 +890,8 @@ class ConvAct(torch.autograd.Function):
                 dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad, residual=_chain_res(ctx.chain, extra))
             if ctx.chain is not None:
                 dx = ctx.chain.hand(dx)
-        if ctx.needs_input_grad[1]:
-            dst = grad_dest(ctx)
-            dw = conv_wgrad(gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1], side=side_wgrad_enabled(ctx),
-                            out=dst)
+        if wg is not None:
+            dw = _wgrad_run(wg)
         return dx, dw, db, None, None, None, None
 
 
@@ -977,6 +1058,7 @@ class ConvBNAct(torch.autograd.Function):
         if _timer:
             _timer.stop("bn_bwd_apply", M * K * z.element_size() * (4 + (1 if has_res else 0)), t0, f"{M}x{K}")
         dx = dw = None
+        wg = _wgrad_plan(ctx, dz, x, K, R, S, stride, pad, cin=wshape[1])  # before the dgrad
         link = ctx.link
         if ctx.role == "sink" and dres is not None:
             link.dres, dres = dres, None  # handed to the block's first conv: added in its dgrad epilogue
@@ -992,9 +1074,8 @@ class ConvBNAct(torch.autograd.Function):
             dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad, residual=_chain_res(chain, res), bnb=bnb)
             if chain is not None:
                 dx = chain.hand(dx)
-        if ctx.needs_input_grad[1]:
-            dst = grad_dest(ctx)
-            dw = conv_wgrad(dz, x, K, R, S, stride, pad, cin=wshape[1], side=side_wgrad_enabled(ctx), out=dst)
+        if wg is not None:
+            dw = _wgrad_run(wg)
         dgamma = sums[1] if ctx.needs_input_grad[2] else None
         dbeta = sums[0] if ctx.needs_input_grad[3] else None
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None

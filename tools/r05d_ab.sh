@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out/r05d
+timeout -k 10 400 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_model.py tests/test_gpu_dp.py tests/test_gpu_guards.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r05d/tests.log 2>&1 || { echo tests failed; tail -30 gpurun_out/r05d/tests.log; exit 1; }
+tail -2 gpurun_out/r05d/tests.log
+bash tools/ab_env.sh r05d MX_WGRAD_PER_STREAM 0 1 3 30 || exit 1
+bash tools/gpu_check.sh r05d prof
