@@ -284,6 +284,30 @@ def time_cold(fn, reps=10, scrub_mb=4096):
     return sum(a.elapsed_time(b) for a, b in ev) / reps * 1e3
 
 
+def time_warm(fn, reps=10):
+    """Device time of fn() replayed back to back (operands warm in L2 / Infinity Cache, as when the
+    producer ran just before), mean in microseconds between the first and last event."""
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3
+
+
+def _roi_set(rois, feats, scales, k_min):
+    """Which RoI set hbm_ops timed: count and per-level split (LevelMapper, as the kernels do)."""
+    w, h = rois[:, 3] - rois[:, 1], rois[:, 4] - rois[:, 2]
+    lvl = torch.floor(4 + torch.log2(torch.sqrt((w * h).clamp_min(1e-12)) / 224) + 1e-6).clamp(k_min, k_min + len(feats) - 1)
+    return {"rois": int(rois.shape[0]), "per_level": {f"P{int(k)}": int((lvl == k).sum()) for k in
+                                                      range(k_min, k_min + len(feats))},
+            "source": "the sampled RoIs of one eager train step right after the timed steps (same synthetic "
+                      "batch cycle as the timed region)"}
+
+
 def hbm_ops_roofline(model, opt, imgs, tg, reps=10):
     """RoIAlign forward / backward and the proposal NMS on the inputs of a real train step, timed with
     HIP events on their launch stream (torch's current stream) with cold caches and no host gaps
@@ -330,13 +354,17 @@ def hbm_ops_roofline(model, opt, imgs, tg, reps=10):
         K, C, es = rois.shape[0], feats[0].shape[3], feats[0].element_size()
         with torch.no_grad():
             us = timed(lambda: ops.multiscale_roi_align(feats, rois, scales, k_min))
+            us_warm = time_warm(lambda: ops.multiscale_roi_align(feats, rois, scales, k_min), reps)
         byts = K * 49 * C * es + _roi_footprint_bytes(feats, rois, scales, k_min, C, es)
         gbs = byts / (us * 1e-6) / 1e9
+        res["roi_set"] = _roi_set(rois, feats, scales, k_min)
         res["roi_align_fwd"] = {"kernel": "roi_align_fwd_v8_kernel", "rois": K, "channels": C,
                                 "dtype": str(feats[0].dtype).replace("torch.", ""), "avg_launch_us": round(us, 2),
+                                "warm_launch_us": round(us_warm, 2),
                                 "algorithmic_mb": round(byts / 1e6, 2), "achieved": round(gbs, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                "timing": "cold caches (4 GiB scrub before each rep), GPU time only"}
+                                "timing": "avg_launch_us: cold caches (4 GiB scrub before each rep), GPU time only; "
+                                          "warm_launch_us: back-to-back replays (operands in L2 / Infinity Cache)"}
         # backward (deterministic gather): every f32 level-map element written once + gout read once;
         # the op's own call (the autograd node's body), timed without autograd bookkeeping
         fs = [f.clone().requires_grad_(True) for f in feats]
@@ -346,12 +374,14 @@ def hbm_ops_roofline(model, opt, imgs, tg, reps=10):
         r_saved, lv_saved = out.grad_fn.saved_tensors
         shapes = [tuple(f.shape) for f in feats]
         us = timed(lambda: ops.multiscale_roi_align_backward(g, r_saved, lv_saved, shapes, list(scales)))
+        us_warm = time_warm(lambda: ops.multiscale_roi_align_backward(g, r_saved, lv_saved, shapes, list(scales)), reps)
         maps = sum(f.numel() for f in feats) * 4
         byts = maps + g.numel() * g.element_size()
         gbs = byts / (us * 1e-6) / 1e9
         res["roi_align_bwd"] = {"kernel": "roi_bwd_gather_kernel (+ roi_bwd_prep_kernel)" if det else
                                 "roi_align_bwd_kernel (atomics) + zero fill", "deterministic": det, "rois": K,
-                                "channels": C, "avg_call_us": round(us, 2), "level_map_mb": round(maps / 1e6, 2),
+                                "channels": C, "avg_call_us": round(us, 2), "warm_call_us": round(us_warm, 2),
+                                "level_map_mb": round(maps / 1e6, 2),
                                 "algorithmic_mb": round(byts / 1e6, 2), "achieved": round(gbs, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
     if "nms_sel" in cap:  # the sort-free form on filter_proposals' presorted candidates (default)

@@ -561,37 +561,28 @@ def grad_dest(ctx):
 
 
 def wgrad_stream(device):
-    """The side stream of the weight gradients forked from the CURRENT stream: one per issuing stream
-    (the backward runs a node on its forward's stream: the main / capture stream, the FPN and RPN-head
-    branch streams). A side stream is in-order, so one shared by every branch made a wgrad whose fork
-    event fires late (an FPN branch's, inside the captured backward graph) hold back every later wgrad
-    of the main chain: they ran as a serial tail after the dgrad chain (profiles/r05c, 1.9 ms)."""
-    if os.environ.get("MX_WGRAD_PER_STREAM", "1") == "0":
-        return dedicated_stream(device, "wgrad")
-    cur = torch.cuda.current_stream(device)
-    name = _wgrad_names.get(cur.cuda_stream)
-    if name is None:
-        name = _wgrad_names[cur.cuda_stream] = "wgrad" if not _wgrad_names else f"wgrad{len(_wgrad_names)}"
-    return dedicated_stream(device, name)
-
-
-_wgrad_names = {}
+    """The side stream of the weight gradients. (One per issuing stream measured neutral, r05d.)"""
+    return dedicated_stream(device, "wgrad")
 
 
 def _wgrad_plan(ctx, dy, x, K, R, S, stride, pad, kout=None, cin=None):
-    """A conv backward's weight gradient, decided BEFORE its dgrad is launched: (job, side, fork) for
-    wgrad_launch after the dgrad, or None when the weight needs no gradient. A side-stream wgrad is
-    prepared (wgrad_prepare: every allocation and copy) and forked from an event recorded here, ahead
-    of the dgrad (its operands dy and x are final), so (a) it runs beside the dgrad, and (b) inside a
-    captured backward graph the node feeding both gets the dgrad as its FIRST dependent, which keeps
-    the dgrad chain -- the backward's critical path -- on one hardware queue of the HIP graph executor
-    instead of hopping to another at every conv (each hop ~10 us of idle GPU:
-    profiles/r05b_step_concurrency.txt). MX_WGRAD_FORK_EARLY=0: prepared and forked after the dgrad."""
+    """A conv backward's weight gradient, decided before its dgrad is launched: (job or its arguments,
+    side, fork event) for _wgrad_run after the dgrad, or None when the weight needs no gradient.
+
+    Side-stream wgrads and the HIP graph executor (profiles r05b-r05f): a captured backward graph is
+    cut into in-order node lists along first dependents; each list runs on one hardware queue, and a
+    wait between lists costs ~10 us of idle GPU. MX_WGRAD_FORK selects where a side wgrad forks:
+      "early" (default) -- from an event recorded here, before the dgrad (the wgrad is prepared first:
+                 every allocation and copy on the current stream). The dgrad stays the first dependent,
+                 so the dgrad chain -- the backward's critical path -- keeps one queue;
+      "late"  -- after its dgrad: the wgrad is the dgrad's first dependent and the chain starts a new
+                 list at every conv (A/B 91.0 vs 94.2 img/s for early, r05c). Grouping several wgrads
+                 behind one fork measured slower still (90.3 at 3 per fork, 69 at 6: r05f), removed."""
     if not ctx.needs_input_grad[1]:
         return None
     dst = grad_dest(ctx)
     side = side_wgrad_enabled(ctx)
-    if side and os.environ.get("MX_WGRAD_FORK_EARLY", "1") != "0":
+    if side and os.environ.get("MX_WGRAD_FORK", "early") != "late":
         job = wgrad_prepare(dy, x, K, R, S, stride, pad, kout, cin, dst)
         fork = torch.cuda.Event()
         fork.record()

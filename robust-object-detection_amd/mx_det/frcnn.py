@@ -513,11 +513,13 @@ class RegionProposalNetwork(nn.Module):
             # sort-free NMS also emits the padded per-image selection
             sel, valid, nk = be.proposal_nms_select(boxes.reshape(-1, 4), prob.reshape(-1), lvl_flat, grp, N,
                                                     len(num_per_level), self.nms_thresh, max(pre, 1000), post)
+            self._nk_last = nk
             self._watch_nms(nk)
             return boxes.reshape(-1, 4)[sel], prob.reshape(-1)[sel], valid
         kk, nk = be.proposal_nms(boxes.reshape(-1, 4), prob.reshape(-1), lvl_flat, grp, N,
                                  len(num_per_level), self.nms_thresh, max(pre, 1000))
         kk, nk = kk.to(dev), nk.to(dev)
+        self._nk_last = nk
         self._watch_nms(nk)
         live = torch.arange(n, device=dev) < nk
         cnt = torch.zeros(N + 1, dtype=torch.int64, device=dev)
@@ -588,9 +590,7 @@ class RegionProposalNetwork(nn.Module):
         def compute_targets():
             # targets and sampling never wait for the GPU (no autograd: labels, targets, masks)
             if hasattr(be, "match_assign_batched"):  # every image in one launch pair, zero-padded GT
-                gtp, _, gcnt = _gt_batch(targets, anchors.device)
-                _, lab, rt, lcnt = be.match_assign_batched(gtp, gcnt, anchors, self.fg, self.bg, True, 1,
-                                                           weights=RPN_WEIGHTS, with_counts=True)
+                return self.targets_of(anchors, _gt_batch(targets, anchors.device), be)
             else:
                 lcnt = None
                 labels, reg_targets = [], []
@@ -650,6 +650,22 @@ class RegionProposalNetwork(nn.Module):
         else:
             boxes, _ = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
         return boxes, losses  # the side stream is joined by join_losses(): after the RoI head
+
+    def targets_of(self, anchors, gt, be):
+        """assign_targets_to_anchors + fg_bg_sampler on the device: (labels [N, A], regression targets
+        [N, A, 4], positive mask, negative mask) from the zero-padded GT batch gt = (boxes, labels,
+        counts) (_gt_batch). Never waits for the GPU."""
+        gtp, _, gcnt = gt
+        _, lab, rt, lcnt = be.match_assign_batched(gtp, gcnt, anchors, self.fg, self.bg, True, 1,
+                                                   weights=RPN_WEIGHTS, with_counts=True)
+        pm, nm = self.fg_bg_sampler(lab, counts=lcnt)
+        return lab, rt, pm, nm
+
+    def loss_of(self, objectness, pred_deltas, tgt, be):
+        """The RPN losses from targets_of's output (HIP: one fused launch each way)."""
+        lab, rt, pm, nm = tgt
+        lo, lb = be.rpn_loss(objectness, pred_deltas, lab, rt, pm, nm, 1.0 / 9)
+        return {"loss_objectness": lo, "loss_rpn_box_reg": lb}
 
     def join_losses(self):
         """Make the current stream wait for the side-stream loss chain (a no-op without one)."""
@@ -785,10 +801,40 @@ class RoIHeads(nn.Module):
         scales = [2.0 ** round(math.log2(float(f.shape[1]) / float(max_h))) for f in feats]
         return scales, int(-math.log2(scales[0]))
 
-    def forward(self, features, proposals, image_sizes, targets=None, be=None):
+    def sample(self, proposals, gt, be):
+        """The RoI sampler's device part (training): candidates per image = its kept proposals (a valid
+        prefix of `post` slots, score order) then its GT boxes (torchvision: cat([proposals, gt])),
+        padded to [N, post + Gmax] with label -1 on padding, matched and sampled. -> (boxes [N, L, 4],
+        labels [N, L], regression targets [N, L, 4], sampled mask [N*L], number sampled (device
+        scalar)). Never waits for the GPU (HIP backend)."""
+        pb, _, pvalid = proposals
+        dev = pb.device
+        # GT slots padded to _gt_batch's width (a multiple of 32) on every backend, so the sampler
+        # draws keys over the same [N, post + gm] rows whichever path builds them
+        gtp, glp, gcnt = gt
+        gm = gtp.shape[1]
+        gslot = torch.arange(gm, device=dev)
+        box_p = torch.cat([pb, gtp], 1)               # [N, post + gm, 4]
+        valid = torch.cat([pvalid, gslot[None, :] < gcnt[:, None]], 1)
+        _, lab_b, tg_p = be.match_assign_batched(gtp, gcnt, box_p, self.fg, self.bg, False, 2,
+                                                 gt_labels=glp, weights=ROI_WEIGHTS)
+        lab_p = torch.where(valid, lab_b, -1)
+        pos_m, neg_m = self.fg_bg_sampler(lab_p, be)
+        sm = (pos_m | neg_m).flatten()
+        return box_p, lab_p, tg_p, sm, sm.sum()
+
+    def forward(self, features, proposals, image_sizes, targets=None, be=None, sampled=None):
+        """sampled: the sample() outputs with the sampled count already on the host (FasterRCNN's
+        captured proposal stage), in place of matching and sampling here."""
         feats = [features[k] for k in self.featmap_names]
         dev = feats[0].device
-        if self.training:
+        if self.training and sampled is not None:
+            box_p, lab_p, tg_p, sm, total = sampled
+            cm = lab_p.shape[1]
+            rois, lab_k, tg_k = be.roi_compact(sm, total, cm, box_p.reshape(-1, 4), lab_p.reshape(-1),
+                                               tg_p.reshape(-1, 4))
+            labels, tgts = [lab_k], [tg_k]
+        elif self.training:
             # candidates per image = its kept proposals (a valid prefix of `post` slots, score order)
             # then its GT boxes (torchvision: cat([proposals, gt])), padded to [N, post + Gmax] with
             # label -1 on padding, matched and sampled on the device; the one host sync of this stage
@@ -1037,6 +1083,43 @@ class FasterRCNN(nn.Module):
         head = self.rpn.head
         return feats, head.split(list(outs[nf:]), head.layout(outs[:nf]), be)
 
+    def _stage(self, il, features, head, targets, be):
+        """The training step's proposal stage -- the RPN's anchor matching and sampler, box decode,
+        filter_proposals (per-level top-k, clip / filter, NMS, selection) and the RoI sampler's matching
+        and draw -- as one captured HIP graph per (input shape, GT width) (_StageGraph): ~130 small
+        launches issued from Python took ~1.4 ms of mostly host-bound time per step (r05b trace). It
+        holds no autograd op (the losses' inputs are its outputs). Returns ((labels, targets, pos, neg),
+        padded proposals, RoI sample) or None (eager path: eval, MX_GRAPHS=0 / MX_STAGE_GRAPH=0, non-HIP
+        backends, an injected sampler key stream, an eager trunk).
+
+        OFF by default (MX_STAGE_GRAPH=1 enables it): on ROCm 7.2 the first replay after the capture
+        is correct, but a replay after the step's backward faulted the GPU with an illegal address
+        (tools/stage_diag.py, gpurun_out/r05g: forward + backward ok, the next replay faults) -- cause
+        not found; the stage holds torch.rand and torch.topk (rocprim scan) launches besides the
+        framework's own kernels."""
+        if not (self.training and head is not None and getattr(be, "name", "") == "hip" and _graphs_enabled(self)
+                and os.environ.get("MX_STAGE_GRAPH", "0") == "1" and hasattr(be, "proposal_nms_select")
+                and self.rpn.fg_bg_sampler.rand is None and self.roi_heads.fg_bg_sampler.rand is None
+                and not torch.cuda.is_current_stream_capturing()):
+            return None
+        objectness, pred_deltas, num_per_level = head
+        if not objectness.is_cuda:
+            return None
+        feats = list(features.values())
+        grid = [(f.shape[1], f.shape[2]) for f in feats]
+        anchors = self.rpn.anchor_generator(il.tensors.shape[1:3], grid, feats[0].device, be)
+        gt = _gt_batch(targets, objectness.device)
+        key = (tuple(objectness.shape), tuple(gt[0].shape), tuple(map(tuple, il.image_sizes)), tuple(num_per_level),
+               tuple(il.tensors.shape))
+        cache = self.__dict__.setdefault("_mx_stage_graphs", {})
+        g = cache.get(key)
+        if g is None:
+            if len(cache) >= 8:
+                return None
+            g = cache[key] = _StageGraph(self, be, objectness, pred_deltas, gt, anchors, il.image_sizes,
+                                         list(num_per_level))
+        return g(objectness, pred_deltas, gt)
+
     def _flag_async(self, flags):
         """(pinned host bool, event) of any(flags) copied without waiting, or None."""
         if not flags:
@@ -1101,14 +1184,28 @@ class FasterRCNN(nn.Module):
         # MX_RPN_DEFER_LOSSES=1 issues the RPN target / loss launches after the RoI sampler's host sync;
         # measured 0.5 % slower than issuing them while the trunk runs (A/B on one box), so off
         defer = os.environ.get("MX_RPN_DEFER_LOSSES", "0") != "0"
+        stage = self._stage(il, features, head, targets, be) if not defer else None
         try:
-            proposals, rpn_losses = self.rpn(il, features, targets, be, head=head, defer_losses=defer)
+            if stage is not None:  # HIP-graph replay of the proposal stage (no autograd inside)
+                objectness, pred_deltas = head[0], head[1]
+                tgt, proposals, sampled = stage
+                rpn_losses = self.rpn.loss_of(objectness, pred_deltas, tgt, be)
+            else:
+                proposals, rpn_losses = self.rpn(il, features, targets, be, head=head, defer_losses=defer)
+                sampled = None
             if degenerate is not None:
                 host, ev = degenerate
                 ev.synchronize()
                 if bool(host):
                     raise ValueError("All bounding boxes should have positive height and width.")
-            detections, det_losses = self.roi_heads(features, proposals, il.image_sizes, targets, be)
+            if stage is not None:
+                box_p, lab_p, tg_p, sm, stat = sampled
+                total, nk = stat.tolist()  # the stage's one host sync: sampled RoI count + NMS status
+                if nk < 0:
+                    self.rpn._nk_pending = (torch.tensor(nk), None)
+                    self.rpn.check_nms()
+                sampled = (box_p, lab_p, tg_p, sm, int(total))
+            detections, det_losses = self.roi_heads(features, proposals, il.image_sizes, targets, be, sampled=sampled)
             self.rpn.check_nms()
         finally:  # also when the step raises: no side-stream work is left unjoined behind it
             self.rpn.join_losses()
@@ -1136,6 +1233,58 @@ def _graphs_enabled(mod=None):
     # under torch DDP the gradient all-reduce hooks live on the parameters' AccumulateGrad nodes,
     # which the replayed backward graph bypasses: such runs keep the trunk eager
     return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+
+class _StageGraph:
+    """FasterRCNN._stage's captured graph: static inputs (objectness, deltas -- detached copies -- and the
+    padded GT batch) -> static outputs, captured after two eager warm-ups on the capture stream (every
+    per-shape constant and workspace exists before the capture; the sampler keys come from the default
+    device generator, which advances per replay as in eager execution). The outputs are overwritten by
+    the next replay: this step consumes them (RoI compaction, the RPN loss and its backward) first."""
+
+    def __init__(self, model, be, obj, dl, gt, anchors, image_sizes, num_per_level):
+        self.model, self.be = model, be
+        self.anchors, self.image_sizes, self.npl = anchors, [tuple(s) for s in image_sizes], num_per_level
+        self.static = [obj.detach().clone(), dl.detach().clone()] + [t.clone() for t in gt]
+        dev = obj.device
+        side = mc.capture_stream(dev)
+        side.wait_stream(torch.cuda.current_stream())
+        # the warm-ups' sampler draws are not the step's: the device generator is put back, so the first
+        # replay draws exactly what the eager stage would have (graph and eager runs stay comparable)
+        rng = torch.cuda.get_rng_state(dev)
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self._run()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize(dev)
+        torch.cuda.set_rng_state(rng, dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with mc.capture_guard(), torch.cuda.graph(self.graph, stream=side):
+            self.out = self._run()
+        torch.cuda.set_rng_state(rng, dev)
+        self.model.rpn.__dict__.pop("_nk_pending", None)  # the warm-ups' NMS watch: checked via `stat`
+
+    def _run(self):
+        m, be = self.model, self.be
+        obj, dl, gtp, glp, gcnt = self.static
+        N, A = obj.shape
+        gt = (gtp, glp, gcnt)
+        tgt = m.rpn.targets_of(self.anchors, gt, be)
+        props = be.box_decode(dl.reshape(-1, 4), self.anchors.repeat(N, 1), RPN_WEIGHTS).view(N, A, 4)
+        proposals = m.rpn.filter_proposals_padded(props, obj, self.image_sizes, self.npl, be)
+        nk = m.rpn._nk_last
+        box_p, lab_p, tg_p, sm, total = m.roi_heads.sample(proposals, gt, be)
+        stat = torch.stack([total.reshape(()).to(torch.int64), nk.reshape(-1)[0].to(torch.int64)])
+        return tgt, proposals, (box_p, lab_p, tg_p, sm, stat)
+
+    def __call__(self, obj, dl, gt):
+        s = self.static
+        s[0].copy_(obj.detach())
+        s[1].copy_(dl.detach())
+        for a, b in zip(s[2:], gt):
+            a.copy_(b)
+        self.graph.replay()
+        return self.out
 
 
 class _Trunk(nn.Module):
