@@ -1429,6 +1429,11 @@ class _GraphFn(torch.autograd.Function):
 def _capture_trunk(model, be, x):
     if model.__dict__.get("_mx_seg_ready") is not None:  # data-parallel: per-segment gradient hand-off
         return _SegGraphs(model, be, x)
+    if os.environ.get("MX_SEG_GRAPHS", "0") == "1":
+        # one backward graph per segment on one GPU too: the HIP graph executor submits a graph's node
+        # lists one after another, so a segment's side-stream wgrads start before the next segment's
+        # dgrad chain is submitted instead of after the whole trunk's (MX_WGRAD_FORK=early)
+        return _SegGraphs(model, be, x)
     trunk = _Trunk(model, be)
     return _Graphs(trunk, trunk.parameters(), model, x)
 
