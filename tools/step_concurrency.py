@@ -75,13 +75,13 @@ for i in range(1, len(iv)):
 ktime = defaultdict(float)
 for s, e, n in iv:
     ktime[cat(n)] += (e - s) / 1e3
-print(f"{steps} steps: span {span / steps:.3f} ms/step, busy {busy / 1e3 / steps:.3f}, idle {(span - busy / 1e3) / steps:.3f}, "
-      f">=2 kernels {conc / 1e3 / steps:.3f} ms/step")
+print(f"{steps} steps: span {span / steps:.3f} us/step, busy {busy / 1e3 / steps:.3f}, idle {(span - busy / 1e3) / steps:.3f}, "
+      f">=2 kernels {conc / 1e3 / steps:.3f} us/step")
 for k in ("<5us", "5-20us", ">=20us"):
-    print(f"  idle gaps {k:7s}: {gaps[k] / steps:8.3f} ms/step in {gcount[k] / steps:6.1f} gaps/step")
-print("kernel time by category (ms/step, summed over streams):")
+    print(f"  idle gaps {k:7s}: {gaps[k] / steps:8.3f} us/step in {gcount[k] / steps:6.1f} gaps/step")
+print("kernel time by category (us/step, summed over streams):")
 for k, v in sorted(ktime.items(), key=lambda kv: -kv[1]):
     print(f"  {k:15s} {v / steps:8.3f}")
-print("largest idle pairs (gaps >= 5 us), ms/step:")
+print("largest idle pairs (gaps >= 5 us), us/step:")
 for (a, b), (c, t) in sorted(pairs.items(), key=lambda kv: -kv[1][1])[:30]:
     print(f"  {t / steps:7.3f} ({c / steps:5.1f}/step)  {a:48s} -> {b}")
