@@ -376,6 +376,14 @@ def _gt_batch(targets, dev):
 _gt_batch.cache = None
 
 
+def _gt_event(stream):
+    """An event on `stream` after the step's padded GT batch (_gt_batch, built there when not cached):
+    the RoI sampler reads the cached batch on the main stream."""
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    return ev
+
+
 def _compact(mask, total):
     """Indices of the True entries of a flat bool mask, ascending, when their number is already
     known on the host (torch.nonzero without its device->host sync)."""
@@ -636,7 +644,13 @@ class RegionProposalNetwork(nn.Module):
             side = _aux_stream(objectness.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
+                gt_ready = None
+                if hasattr(be, "match_assign_batched"):
+                    _gt_batch(targets, objectness.device)  # built (or found cached) first
+                    gt_ready = _gt_event(side)
                 tgt = compute_targets()
+            if gt_ready is not None:  # _gt_batch's cached batch, built on the side stream, is read by the
+                main.wait_event(gt_ready)  # RoI sampler on this stream
             # recorded right away: if the proposal chain below raises, FasterRCNN.forward's finally
             # still joins the side stream (join_losses)
             self._loss_side = side
