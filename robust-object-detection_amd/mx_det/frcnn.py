@@ -649,8 +649,10 @@ class RegionProposalNetwork(nn.Module):
                     _gt_batch(targets, objectness.device)  # built (or found cached) first
                     gt_ready = _gt_event(side)
                 tgt = compute_targets()
-            if gt_ready is not None:  # _gt_batch's cached batch, built on the side stream, is read by the
-                main.wait_event(gt_ready)  # RoI sampler on this stream
+            # _gt_batch's cached batch, built on the side stream, is read by the RoI sampler on the main
+            # stream: FasterRCNN.forward waits for this event right before the RoI heads (not here, where
+            # the proposal chain, which does not read it, would wait too)
+            self._gt_ready = gt_ready
             # recorded right away: if the proposal chain below raises, FasterRCNN.forward's finally
             # still joins the side stream (join_losses)
             self._loss_side = side
@@ -1219,6 +1221,9 @@ class FasterRCNN(nn.Module):
                     self.rpn._nk_pending = (torch.tensor(nk), None)
                     self.rpn.check_nms()
                 sampled = (box_p, lab_p, tg_p, sm, int(total))
+            gt_ready = self.rpn.__dict__.pop("_gt_ready", None)
+            if gt_ready is not None:  # the RoI sampler reads the GT batch the RPN's side stream built
+                torch.cuda.current_stream().wait_event(gt_ready)
             detections, det_losses = self.roi_heads(features, proposals, il.image_sizes, targets, be, sampled=sampled)
             self.rpn.check_nms()
         finally:  # also when the step raises: no side-stream work is left unjoined behind it
