@@ -1449,10 +1449,9 @@ def _capture_trunk(model, be, x):
     if model.__dict__.get("_mx_seg_ready") is not None:  # data-parallel: per-segment gradient hand-off
         return _SegGraphs(model, be, x)
     if os.environ.get("MX_SEG_GRAPHS", "0") == "1":
-        # one backward graph per segment on one GPU too: the HIP graph executor submits a graph's node
-        # lists one after another, so a segment's side-stream wgrads start before the next segment's
-        # dgrad chain is submitted instead of after the whole trunk's (MX_WGRAD_FORK=early)
-        return _SegGraphs(model, be, x)
+        # the segments' backwards in ONE graph, each segment's side wgrads deferred behind its dgrad
+        # chain so that they run beside the next segments (conv.defer_side_wgrads)
+        return _SegGraphs(model, be, x, one_graph=True)
     trunk = _Trunk(model, be)
     return _Graphs(trunk, trunk.parameters(), model, x)
 
@@ -1472,7 +1471,7 @@ class _SegGraphs:
 
     SEGS = ("fpn+rpn_head", "layer4", "layer3", "layer2", "stem+layer1")
 
-    def __init__(self, model, be, x):
+    def __init__(self, model, be, x, one_graph=False):
         self.model, self.be = model, be
         body = model.backbone.body
         self.seg_params = {"stem+layer1": list(body.conv1.parameters()) + list(body.bn1.parameters()) +
@@ -1505,12 +1504,44 @@ class _SegGraphs:
             outs, self.leaves, self.cs = self._fwd(self.static_x)
         self.static_gout = [torch.zeros_like(o) for o in outs]
         r0, g0 = _absorb_roots(self.model.rpn.head, outs, self.static_gout)
-        self.bwd = []  # (segment key, graph)
-        for key, roots, groots in self._bwd_plan(outs, self.static_gout, self.leaves, self.cs, (r0, g0)):
+        # [(segment keys, backward graph)] in replay order; one_graph (single GPU, no hand-off hooks):
+        # every segment in one graph, each segment's side-stream wgrads collected while its backward is
+        # captured (conv.defer_side_wgrads) and launched right after its dgrad chain on a stream of the
+        # segment's own. The HIP graph executor cuts a graph into in-order node lists along first
+        # dependents and submits them one after another: segment k's wgrads are the first dependents of
+        # its last dgrad-chain node, so they extend segment k's list and run beside segment k+1's chain
+        # (the next list) -- instead of one side list submitted after the whole trunk's dgrad chain
+        # (MX_WGRAD_DEFER=0: the in-graph early fork of conv._wgrad_plan).
+        self.bwd, self.jobs = [], []
+        plan = self._bwd_plan(outs, self.static_gout, self.leaves, self.cs, (r0, g0))
+        if one_graph:
+            defer = os.environ.get("MX_WGRAD_DEFER", "1") != "0"
+            forks = []
             g = torch.cuda.CUDAGraph()
             with mc.capture_guard(), torch.cuda.graph(g, pool=pool, stream=side):
-                torch.autograd.backward(roots, groots())
-            self.bwd.append((key, g))
+                for key, roots, groots in plan:
+                    jobs = []
+                    with mc.defer_side_wgrads(jobs if defer else None):
+                        torch.autograd.backward(roots, groots())
+                    if jobs:
+                        ws = mc.dedicated_stream(x.device, "wgrad_seg%d" % len(forks))
+                        ws.wait_stream(side)
+                        with torch.cuda.stream(ws):
+                            for j in jobs:
+                                mc.wgrad_launch_deferred(j)
+                        forks.append(ws)
+                        # operands and workspaces stay referenced: no later allocation of this capture
+                        # (or of a later graph in the pool) may reuse them while the wgrads run
+                        self.jobs.extend(jobs)
+                for ws in forks:
+                    side.wait_stream(ws)
+            self.bwd.append((tuple(k for k, _, _ in plan), g))
+        else:
+            for key, roots, groots in plan:
+                g = torch.cuda.CUDAGraph()
+                with mc.capture_guard(), torch.cuda.graph(g, pool=pool, stream=side):
+                    torch.autograd.backward(roots, groots())
+                self.bwd.append(((key,), g))
         self.static_out = tuple(o.detach() for o in outs)
         self.static_grads = {k: [p.grad for p in v] for k, v in self.seg_params.items()}
         # the boundary-leaf gradients pass between the backward graphs: keep them referenced
@@ -1571,23 +1602,25 @@ class _SegGraphFn(torch.autograd.Function):
     def backward(ctx, *gouts):
         tg = ctx.tg
         _load_gouts(tg, gouts)
-        for key, _ in tg.bwd:  # see _GraphFn.backward
-            for p, g in zip(tg.seg_params[key], tg.static_grads[key]):
-                if g is not None and p.grad is g:
-                    p.grad = g.clone()
+        for keys, _ in tg.bwd:  # see _GraphFn.backward
+            for key in keys:
+                for p, g in zip(tg.seg_params[key], tg.static_grads[key]):
+                    if g is not None and p.grad is g:
+                        p.grad = g.clone()
         hook = tg.model.__dict__.get("_mx_seg_ready")
-        for key, graph in tg.bwd:
+        for keys, graph in tg.bwd:
             graph.replay()
-            ps, gs = tg.seg_params[key], tg.static_grads[key]
-            for p, g in zip(ps, gs):
-                if g is None:
-                    continue
-                if p.grad is None:
-                    p.grad = g
-                else:
-                    p.grad.add_(g)
-            if hook is not None and ps:
-                hook(key, ps)
+            for key in keys:
+                ps, gs = tg.seg_params[key], tg.static_grads[key]
+                for p, g in zip(ps, gs):
+                    if g is None:
+                        continue
+                    if p.grad is None:
+                        p.grad = g
+                    else:
+                        p.grad.add_(g)
+                if hook is not None and ps:
+                    hook(key, ps)
         return None, None, None
 
 
