@@ -133,6 +133,19 @@ class ResNet50Body(nn.Module):
         return out
 
 
+_helper_pool = None
+
+
+def _helper():
+    """One helper thread for host work issued beside a blocking graph launch (RegionProposalNetwork.
+    start_targets)."""
+    global _helper_pool
+    if _helper_pool is None:
+        import concurrent.futures
+        _helper_pool = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="mx_rpn_targets")
+    return _helper_pool
+
+
 def _aux_stream(device):
     """The RPN loss chain's side stream, one per device."""
     return mc.dedicated_stream(device, "rpn_targets")
@@ -376,6 +389,14 @@ def _gt_batch(targets, dev):
 _gt_batch.cache = None
 
 
+def _gt_event(stream):
+    """An event on `stream` after the step's padded GT batch (_gt_batch, built there when not cached):
+    the RoI sampler reads the cached batch on the main stream."""
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    return ev
+
+
 def _compact(mask, total):
     """Indices of the True entries of a flat bool mask, ascending, when their number is already
     known on the host (torch.nonzero without its device->host sync)."""
@@ -574,15 +595,17 @@ class RegionProposalNetwork(nn.Module):
         counts = valid.sum(1).tolist()
         return [pb[i, :c] for i, c in enumerate(counts)], [ps[i, :c] for i, c in enumerate(counts)]
 
-    def forward(self, images, features, targets=None, be=None, head=None, defer_losses=False):
+    def forward(self, images, features, targets=None, be=None, head=None, defer_losses=False, early=None):
         """torchvision RegionProposalNetwork.forward -> (proposals, losses). defer_losses=True returns a
         callable in place of the losses dict: the caller issues the shape-independent target / sampler
         / loss launches later (FasterRCNN.forward: right after the RoI sampler's host sync, so the GPU
-        works on them while the host issues the RoI head instead of idling)."""
+        works on them while the host issues the RoI head instead of idling). early: the targets
+        already issued on the side stream by start_targets (FasterRCNN.forward, beside the trunk)."""
         feats = list(features.values())
         # objectness [N, A], pred_deltas [N, A, 4], anchors per level
         objectness, pred_deltas, num_per_level = head if head is not None else self.head(feats, be)
         grid = [(f.shape[1], f.shape[2]) for f in feats]
+        self.__dict__.setdefault("_grids", {})[tuple(images.tensors.shape)] = grid
         anchors = self.anchor_generator(images.tensors.shape[1:3], grid, feats[0].device, be)
         N = feats[0].shape[0]
         A = anchors.shape[0]
@@ -622,7 +645,10 @@ class RegionProposalNetwork(nn.Module):
             return loss_of(compute_targets()) if self.training else {}
 
         side = None
-        if (self.training and not defer_losses and objectness.is_cuda and getattr(be, "name", "") == "hip"
+        if early is not None:  # issued beside the trunk (start_targets); joined by join_losses()
+            tgt = early
+            losses = lambda: loss_of(tgt)  # noqa: E731
+        elif (self.training and not defer_losses and objectness.is_cuda and getattr(be, "name", "") == "hip"
                 and _side_streams("MX_RPN_LOSS_STREAM")):
             # the target / sampler chain (~25 small launches: anchor matching, the sampler's top-k) on a
             # side stream beside the proposal chain (decode, per-level top-k, NMS, selection): two
@@ -636,7 +662,13 @@ class RegionProposalNetwork(nn.Module):
             side = _aux_stream(objectness.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
+                gt_ready = None
+                if hasattr(be, "match_assign_batched"):
+                    _gt_batch(targets, objectness.device)  # built (or found cached) first
+                    gt_ready = _gt_event(side)
                 tgt = compute_targets()
+            if gt_ready is not None:  # _gt_batch's cached batch, built on the side stream, is read by the
+                main.wait_event(gt_ready)  # RoI sampler on this stream
             # recorded right away: if the proposal chain below raises, FasterRCNN.forward's finally
             # still joins the side stream (join_losses)
             self._loss_side = side
@@ -650,6 +682,37 @@ class RegionProposalNetwork(nn.Module):
         else:
             boxes, _ = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
         return boxes, losses  # the side stream is joined by join_losses(): after the RoI head
+
+    def start_targets(self, images, targets, be):
+        """The RPN's target / sampler chain issued by a helper thread on the side stream while the calling
+        thread replays the trunk's forward graph (FasterRCNN.forward): the chain needs only the anchors
+        and the ground truth, and hipGraphLaunch holds its thread for about the graph's GPU time (the
+        launch blocks on the full hardware queue), so issuing the chain's ~40 launches afterwards cost
+        ~0.8 ms of GPU idle per step (profiles/r05c). Same launches, same RNG draws in the same order
+        (nothing between them draws). Returns a future of the targets, or None when the trunk will not
+        replay a graph for this shape (first step of a shape: the grid sizes come from an earlier
+        step), on a non-HIP backend or with MX_RPN_TARGETS_THREAD=0. join_losses() waits for it."""
+        x = images.tensors
+        grid = self.__dict__.get("_grids", {}).get(tuple(x.shape))
+        if (grid is None or not self.training or not x.is_cuda or getattr(be, "name", "") != "hip"
+                or not hasattr(be, "match_assign_batched") or not _side_streams("MX_RPN_LOSS_STREAM")
+                or os.environ.get("MX_RPN_TARGETS_THREAD", "1") == "0" or torch.cuda.is_current_stream_capturing()):
+            return None
+        dev = x.device
+        anchors = self.anchor_generator(x.shape[1:3], grid, dev, be)
+        main = torch.cuda.current_stream(dev)
+        side = _aux_stream(dev)
+        side.wait_stream(main)  # the ground truth was resized on the main stream
+
+        def job():
+            with mc.capture_lock, torch.cuda.device(dev), torch.cuda.stream(side), torch.no_grad():
+                gt = _gt_batch(targets, dev)
+                return self.targets_of(anchors, gt, be), _gt_event(side)
+
+        fut = _helper().submit(job)
+        self._loss_side = side
+        self._tgt_future = fut
+        return fut
 
     def targets_of(self, anchors, gt, be):
         """assign_targets_to_anchors + fg_bg_sampler on the device: (labels [N, A], regression targets
@@ -668,7 +731,11 @@ class RegionProposalNetwork(nn.Module):
         return {"loss_objectness": lo, "loss_rpn_box_reg": lb}
 
     def join_losses(self):
-        """Make the current stream wait for the side-stream loss chain (a no-op without one)."""
+        """Make the current stream wait for the side-stream loss chain (a no-op without one); first the
+        helper thread's issue of it (start_targets), if any."""
+        fut = self.__dict__.pop("_tgt_future", None)
+        if fut is not None:
+            fut.result()
         side = self.__dict__.pop("_loss_side", None)
         if side is not None:
             torch.cuda.current_stream(side.device).wait_stream(side)
@@ -1176,22 +1243,31 @@ class FasterRCNN(nn.Module):
                      [(b[:, 2:] <= b[:, :2]).any() for b in dev_boxes])
             degenerate = self._flag_async(flags)
         il, targets = self.transform(images, targets, be)
-        trunk = self._trunk(il.tensors, be)
-        if trunk is not None:  # HIP-graph replay of backbone + FPN + RPN head (static shapes)
-            features, head = trunk
-        else:
-            features, head = self.backbone(il.tensors, be), None
         # MX_RPN_DEFER_LOSSES=1 issues the RPN target / loss launches after the RoI sampler's host sync;
         # measured 0.5 % slower than issuing them while the trunk runs (A/B on one box), so off
         defer = os.environ.get("MX_RPN_DEFER_LOSSES", "0") != "0"
-        stage = self._stage(il, features, head, targets, be) if not defer else None
+        early = None
+        if (not defer and self.training and il.tensors.is_cuda
+                and self.__dict__.get("_mx_graphs", {}).get((tuple(il.tensors.shape), il.tensors.dtype)) is not None
+                and os.environ.get("MX_STAGE_GRAPH", "0") != "1"):
+            early = self.rpn.start_targets(il, targets, be)  # its launches beside the trunk's graph launch
         try:
+            trunk = self._trunk(il.tensors, be)
+            if trunk is not None:  # HIP-graph replay of backbone + FPN + RPN head (static shapes)
+                features, head = trunk
+            else:
+                features, head = self.backbone(il.tensors, be), None
+            if early is not None:
+                early, gt_ready = self.rpn.__dict__.pop("_tgt_future").result()
+                torch.cuda.current_stream().wait_event(gt_ready)  # the RoI sampler reads the same GT batch
+            stage = self._stage(il, features, head, targets, be) if not defer else None
             if stage is not None:  # HIP-graph replay of the proposal stage (no autograd inside)
                 objectness, pred_deltas = head[0], head[1]
                 tgt, proposals, sampled = stage
                 rpn_losses = self.rpn.loss_of(objectness, pred_deltas, tgt, be)
             else:
-                proposals, rpn_losses = self.rpn(il, features, targets, be, head=head, defer_losses=defer)
+                proposals, rpn_losses = self.rpn(il, features, targets, be, head=head, defer_losses=defer,
+                                                 early=early)
                 sampled = None
             if degenerate is not None:
                 host, ev = degenerate
