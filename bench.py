@@ -826,6 +826,8 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-augment-variant", action="store_true")
     ap.add_argument("--no-eval-variant", action="store_true", help="skip the eval / eval_restored legs of the train run")
+    ap.add_argument("--no-dp-variant", action="store_true",
+                    help="skip the one-rank nccl DataParallel leg of the train run (N=1 only)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -940,6 +942,30 @@ def main():
                                               "the same train step", "dtype": DTYPE_TEXT[head],
                                   "value": round(images / dt3, 3), "ms_per_step": round(1000 * dt3 / args.steps, 3)}
         del m3
+    if world == 1 and not dist.is_initialized() and not args.no_dp_variant:
+        # configs[2]'s code path at one GPU: a one-rank nccl (RCCL) group and mx_det.dp.DataParallel --
+        # segmented backward graphs, hook-issued async all-reduces, the NMS flag read -- on the headline
+        # workload and precision, timed the same way; its ms/step over the headline's is the per-rank
+        # overhead the N-GPU run pays on top of the exchange itself
+        try:
+            del ddp, opt
+        except NameError:
+            pass
+        torch.cuda.empty_cache()
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ["MASTER_PORT"] = str(_free_port())
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        try:
+            m5, ddp, opt, dt5 = _time_precision(head, args, world, rank, dev, imgs, tg)
+            ddp.close()
+        finally:
+            dist.destroy_process_group()
+        rec["dp_variant"] = {"workload": "configs[1] step through mx_det.dp.DataParallel in a one-rank nccl (RCCL) "
+                                         "group (the N-GPU code path)", "dtype": DTYPE_TEXT[head],
+                             "parallelism": "dp1 (nccl group, DataParallel)", "value": round(images / dt5, 3),
+                             "ms_per_step": round(1000 * dt5 / args.steps, 3),
+                             "ratio_to_headline": round(dt5 / dt, 4)}
+        del m5, ddp, opt
     if not args.no_eval_variant:
         # the metric's "+ eval" half, in the same driver run: eval_all.py:97-143 per-image eval forward
         # and configs[3] (eval_restored.py: U-Net restore fused in front), headline precision, each rank

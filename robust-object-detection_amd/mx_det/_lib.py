@@ -197,6 +197,9 @@ def load():
             fn.restype = res
             fn.argtypes = args
         _lib = lib
+        tail = os.environ.get("MX_CONV_TAIL")  # split-K tail of the bf16x3 conv grid (default on)
+        if tail is not None and hasattr(lib, "mx_conv_set_tail"):
+            call("mx_conv_set_tail", 1 if tail != "0" else 0)
     return _lib
 
 

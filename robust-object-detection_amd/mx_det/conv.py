@@ -20,6 +20,7 @@ import threading
 import weakref
 
 import torch
+from torch.utils.weak import WeakIdKeyDictionary
 
 from . import _lib
 from ._lib import call
@@ -514,6 +515,10 @@ _uses = weakref.WeakValueDictionary()
 
 
 def _count_use(w):
+    """Count a forward use of weight w; a view (FC6's 4-D view of the Linear weight) counts against
+    its base parameter, so two views of one parameter in one graph are two uses of it (grad_dest)."""
+    if not w.is_leaf and w._base is not None:
+        w = w._base
     c = _uses.get(id(w))
     if c is None:
         c = _uses[id(w)] = _Uses()
@@ -538,13 +543,19 @@ def side_wgrad_enabled(ctx):
     return _dp or not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
 
 
+# parameter -> (flat bucket, offset): the gradient slots of mx_det.dp.DataParallel (set there, dropped
+# by its close()); weak keys, so nothing here keeps a parameter or pickles a bucket with it
+grad_slots = WeakIdKeyDictionary()
+
+
 def grad_dest(ctx):
-    """The data-parallel bucket slot (mx_det.dp.DataParallel: `_mx_grad_slot` on the parameter) of this
-    conv's weight gradient, as a fresh view for the wgrad kernel to write into -- or None. AccumulateGrad
+    """The data-parallel bucket slot (mx_det.dp.DataParallel: `grad_slots[parameter]`) of this conv's
+    weight gradient, as a fresh view for the wgrad kernel to write into -- or None. AccumulateGrad
     adopts the returned tensor as `.grad` (autograd holds its only reference), so the gradient is born in
     the all-reduce buffer. Only a weight used ONCE in the graph whose `.grad` is None qualifies (a shared
     weight's calls would all write the same slot before autograd sums them); a view of a parameter (FC6's
-    [1024, 256, 7, 7] over the Linear weight) maps to its base's slot. Call before side_wgrad_enabled
+    [1024, 256, 7, 7] over the Linear weight) maps to its base's slot, and its uses are counted on the
+    base (_count_use), so two views of one parameter disqualify both. Call before side_wgrad_enabled
     (which consumes ctx.uses)."""
     uses = ctx.uses
     if uses is None or uses.n != 1:
@@ -553,7 +564,7 @@ def grad_dest(ctx):
     if w is None:
         return None
     p = w if w.is_leaf else w._base
-    slot = getattr(p, "_mx_grad_slot", None) if p is not None else None
+    slot = grad_slots.get(p) if p is not None else None
     if slot is None or not p.is_leaf or p.grad is not None or not w.is_contiguous() or w.numel() != p.numel():
         return None
     flat, off = slot

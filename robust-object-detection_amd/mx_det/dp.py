@@ -27,7 +27,8 @@ in ~`bucket_mb` buckets. Over xGMI a ring all-reduce of the 172 MB of f32 gradie
 exposed.
 
 Persistent buckets: every group (and every remaining bucket) owns ONE flat f32 gradient buffer for
-the wrapper's lifetime, and each trainable parameter a fixed slot in it (`p._mx_grad_slot`). The conv
+the wrapper's lifetime, and each trainable parameter a fixed slot in it (`conv.grad_slots`, a weak
+id-keyed map owned by this wrapper and cleared by `close()`; nothing is stored on the parameter). The conv
 weight gradients -- all but ~1 % of the 43M trainable values -- are written by their wgrad kernels
 straight into their slot (conv.grad_dest: the conv backward hands AccumulateGrad a view of the slot,
 which it adopts as `.grad`; inside the captured backward graphs the slot is the graph's own gradient
@@ -36,6 +37,13 @@ A gradient that arrives elsewhere (BatchNorm affine, biases, the RPN head's weig
 levels, a parameter unused on this rank) is copied into its slot (one multi-tensor launch per group)
 and the parameter's `.grad` becomes the slot view. Over RCCL the average is `ReduceOp.AVG` (ncclAvg:
 no separate 1/N pass); gloo has no AVG, so it sums and scales.
+
+Failing together: a rank whose proposal NMS reports a failure (RegionProposalNetwork.check_nms,
+num_keep < 0) must not raise alone -- the other ranks would block in the next all-reduce until the
+RCCL timeout. Under this wrapper the RPN records the failure instead (`_mx_defer_nms_error`); the
+first all-reduce of every step carries one extra float, this rank's failure flag, and
+`sync_gradients()` reads the reduced flag (a wait on that first collective only, long finished by
+then) and raises on every rank before the optimizer step, with the local message where there is one.
 """
 import torch
 import torch.distributed as dist
@@ -97,18 +105,28 @@ class DataParallel:
         if cur:
             self.buckets.append(cur)
         self.bucket_mb = bucket_mb
-        # persistent flat buffer per group / bucket, a fixed slot per parameter (module docstring)
+        # persistent flat buffer per group / bucket, a fixed slot per parameter (module docstring); the
+        # first collective of the step (canonical order) carries the NMS failure flag after its slots
+        from . import conv as _conv
+        self._slots = _conv.grad_slots
+        units = self.groups + [(("bucket", i), b) for i, b in enumerate(self.buckets)]
+        self.flag_key = units[0][0] if units else None
         self.flats = {}
-        for key, ps in self.groups + [(("bucket", i), b) for i, b in enumerate(self.buckets)]:
+        for key, ps in units:
             if any(p.dtype != torch.float32 for p in ps) or len({p.device for p in ps}) != 1:
                 raise RuntimeError("DataParallel: trainable parameters must be f32 on one device per group")
-            flat = torch.zeros(sum(p.numel() for p in ps), dtype=torch.float32, device=ps[0].device)
+            n = sum(p.numel() for p in ps)
+            flat = torch.zeros(n + (key == self.flag_key), dtype=torch.float32, device=ps[0].device)
             slots, off = [], 0
             for p in ps:
-                p.__dict__["_mx_grad_slot"] = (flat, off)
+                self._slots[p] = (flat, off)
                 slots.append((p, off))
                 off += p.numel()
             self.flats[key] = (flat, slots)
+        self._flag_host = None
+        self.rpn = getattr(model, "rpn", None)
+        if self.rpn is not None:
+            self.rpn.__dict__["_mx_defer_nms_error"] = True
         self.op, self.scale = dist.ReduceOp.SUM, 1.0 / self.world
         if dist.get_backend(group) == "nccl":  # RCCL: ncclAvg, the 1/N folded into the reduction
             self.op, self.scale = dist.ReduceOp.AVG, None
@@ -116,8 +134,19 @@ class DataParallel:
         self._copied = 0
         for m in model.modules():  # graphs and side-stream wgrad stay enabled under this wrapper
             m.__dict__["_mx_dp"] = True
-        from . import conv as _conv
         _conv.set_data_parallel(True)
+
+    def close(self):
+        """Drop this wrapper's gradient slots (conv.grad_slots) and hooks; `.grad`s keep their views."""
+        for flat, slots in self.flats.values():
+            for p, _ in slots:
+                cur = self._slots.get(p)
+                if cur is not None and cur[0] is flat:
+                    del self._slots[p]
+        for m, k in ((getattr(self.model, "roi_heads", None), "_mx_grads_ready"), (self.model, "_mx_seg_ready"),
+                     (self.rpn, "_mx_defer_nms_error")):
+            if m is not None:
+                m.__dict__.pop(k, None)
 
     def __call__(self, *args, **kwargs):
         return self.model(*args, **kwargs)
@@ -148,6 +177,8 @@ class DataParallel:
         if src:
             torch._foreach_copy_(dst, src)
         self._copied += len(src)
+        if key == self.flag_key:  # this rank's proposal-NMS failure flag rides in the first collective
+            flat[-1].fill_(1.0 if self.rpn is not None and self.rpn.__dict__.get("_nms_error") else 0.0)
         return dist.all_reduce(flat, op=self.op, group=self.group, async_op=True), key
 
     def _issue_through(self, key):
@@ -184,6 +215,8 @@ class DataParallel:
         for i in range(len(self.buckets)):
             pending.append(self._start(("bucket", i)))
             self.issued.append("bucket")
+        if pending:
+            self._check_flag(*pending[0])
         for work, key in pending:
             work.wait()
             flat, slots = self.flats[key]
@@ -194,3 +227,28 @@ class DataParallel:
                     p.grad = _slot_view(flat, off, p)
         self.last_issued, self.issued = self.issued, []
         self.copied, self._copied = self._copied, 0
+
+    def _check_flag(self, work, key):
+        """Read the reduced NMS failure flag of the step's first collective (module docstring) and
+        raise on every rank if any rank failed. The read waits for that collective only (on a stream
+        of its own), not for the rest of the backward."""
+        flat, _ = self.flats[key]
+        local = self.rpn.__dict__.pop("_nms_error", None) if self.rpn is not None else None
+        if flat.is_cuda:
+            if self._flag_host is None:
+                self._flag_host = torch.zeros((), dtype=torch.float32, pin_memory=True)
+                from . import conv as _conv
+                self._flag_stream = _conv.dedicated_stream(flat.device, "dp_flag")
+            with torch.cuda.stream(self._flag_stream):
+                work.wait()
+                self._flag_host.copy_(flat[-1], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            ev.synchronize()
+            bad = float(self._flag_host)
+        else:
+            work.wait()
+            bad = float(flat[-1])
+        if bad != 0.0:
+            raise RuntimeError("DataParallel: the proposal NMS failed on at least one rank this step; no rank "
+                               "applies it" + (f" (this rank: {local})" if local else ""))

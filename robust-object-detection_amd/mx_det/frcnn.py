@@ -133,6 +133,19 @@ class ResNet50Body(nn.Module):
         return out
 
 
+_helper_pool = None
+
+
+def _helper():
+    """One helper thread for host work issued beside a blocking graph launch (RegionProposalNetwork.
+    start_targets)."""
+    global _helper_pool
+    if _helper_pool is None:
+        import concurrent.futures
+        _helper_pool = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="mx_rpn_targets")
+    return _helper_pool
+
+
 def _aux_stream(device):
     """The RPN loss chain's side stream, one per device."""
     return mc.dedicated_stream(device, "rpn_targets")
@@ -521,13 +534,11 @@ class RegionProposalNetwork(nn.Module):
             # sort-free NMS also emits the padded per-image selection
             sel, valid, nk = be.proposal_nms_select(boxes.reshape(-1, 4), prob.reshape(-1), lvl_flat, grp, N,
                                                     len(num_per_level), self.nms_thresh, max(pre, 1000), post)
-            self._nk_last = nk
             self._watch_nms(nk)
             return boxes.reshape(-1, 4)[sel], prob.reshape(-1)[sel], valid
         kk, nk = be.proposal_nms(boxes.reshape(-1, 4), prob.reshape(-1), lvl_flat, grp, N,
                                  len(num_per_level), self.nms_thresh, max(pre, 1000))
         kk, nk = kk.to(dev), nk.to(dev)
-        self._nk_last = nk
         self._watch_nms(nk)
         live = torch.arange(n, device=dev) < nk
         cnt = torch.zeros(N + 1, dtype=torch.int64, device=dev)
@@ -568,6 +579,11 @@ class RegionProposalNetwork(nn.Module):
         if ev is not None:
             ev.synchronize()
         v = int(host)
+        if v < 0 and self.__dict__.get("_mx_defer_nms_error"):
+            # mx_det.dp.DataParallel: recorded, raised on every rank by sync_gradients (a lone raise here
+            # would leave the other ranks blocked in the next all-reduce)
+            self._nms_error = f"proposal NMS num_keep = {v}"
+            return
         if v == -2:
             raise RuntimeError("proposal NMS: candidates are not in the presorted (image, level, score) layout "
                                "mx_batched_nms_grouped_sorted requires (num_keep = -2); MX_SORTED_NMS=0 selects "
@@ -582,15 +598,17 @@ class RegionProposalNetwork(nn.Module):
         counts = valid.sum(1).tolist()
         return [pb[i, :c] for i, c in enumerate(counts)], [ps[i, :c] for i, c in enumerate(counts)]
 
-    def forward(self, images, features, targets=None, be=None, head=None, defer_losses=False):
+    def forward(self, images, features, targets=None, be=None, head=None, defer_losses=False, early=None):
         """torchvision RegionProposalNetwork.forward -> (proposals, losses). defer_losses=True returns a
         callable in place of the losses dict: the caller issues the shape-independent target / sampler
         / loss launches later (FasterRCNN.forward: right after the RoI sampler's host sync, so the GPU
-        works on them while the host issues the RoI head instead of idling)."""
+        works on them while the host issues the RoI head instead of idling). early: the targets
+        already issued on the side stream by start_targets (FasterRCNN.forward, beside the trunk)."""
         feats = list(features.values())
         # objectness [N, A], pred_deltas [N, A, 4], anchors per level
         objectness, pred_deltas, num_per_level = head if head is not None else self.head(feats, be)
         grid = [(f.shape[1], f.shape[2]) for f in feats]
+        self.__dict__.setdefault("_grids", {})[tuple(images.tensors.shape)] = grid
         anchors = self.anchor_generator(images.tensors.shape[1:3], grid, feats[0].device, be)
         N = feats[0].shape[0]
         A = anchors.shape[0]
@@ -630,7 +648,10 @@ class RegionProposalNetwork(nn.Module):
             return loss_of(compute_targets()) if self.training else {}
 
         side = None
-        if (self.training and not defer_losses and objectness.is_cuda and getattr(be, "name", "") == "hip"
+        if early is not None:  # issued beside the trunk (start_targets); joined by join_losses()
+            tgt = early
+            losses = lambda: loss_of(tgt)  # noqa: E731
+        elif (self.training and not defer_losses and objectness.is_cuda and getattr(be, "name", "") == "hip"
                 and _side_streams("MX_RPN_LOSS_STREAM")):
             # the target / sampler chain (~25 small launches: anchor matching, the sampler's top-k) on a
             # side stream beside the proposal chain (decode, per-level top-k, NMS, selection): two
@@ -667,6 +688,37 @@ class RegionProposalNetwork(nn.Module):
             boxes, _ = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
         return boxes, losses  # the side stream is joined by join_losses(): after the RoI head
 
+    def start_targets(self, images, targets, be):
+        """The RPN's target / sampler chain issued by a helper thread on the side stream while the calling
+        thread replays the trunk's forward graph (FasterRCNN.forward): the chain needs only the anchors
+        and the ground truth, and hipGraphLaunch holds its thread for about the graph's GPU time (the
+        launch blocks on the full hardware queue), so issuing the chain's ~40 launches afterwards cost
+        ~0.8 ms of GPU idle per step (profiles/r05c). Same launches, same RNG draws in the same order
+        (nothing between them draws). Returns a future of the targets, or None when the trunk will not
+        replay a graph for this shape (first step of a shape: the grid sizes come from an earlier
+        step), on a non-HIP backend or with MX_RPN_TARGETS_THREAD=0. join_losses() waits for it."""
+        x = images.tensors
+        grid = self.__dict__.get("_grids", {}).get(tuple(x.shape))
+        if (grid is None or not self.training or not x.is_cuda or getattr(be, "name", "") != "hip"
+                or not hasattr(be, "match_assign_batched") or not _side_streams("MX_RPN_LOSS_STREAM")
+                or os.environ.get("MX_RPN_TARGETS_THREAD", "1") == "0" or torch.cuda.is_current_stream_capturing()):
+            return None
+        dev = x.device
+        anchors = self.anchor_generator(x.shape[1:3], grid, dev, be)
+        main = torch.cuda.current_stream(dev)
+        side = _aux_stream(dev)
+        side.wait_stream(main)  # the ground truth was resized on the main stream
+
+        def job():
+            with mc.capture_lock, torch.cuda.device(dev), torch.cuda.stream(side), torch.no_grad():
+                gt = _gt_batch(targets, dev)
+                return self.targets_of(anchors, gt, be), _gt_event(side)
+
+        fut = _helper().submit(job)
+        self._loss_side = side
+        self._tgt_future = fut
+        return fut
+
     def targets_of(self, anchors, gt, be):
         """assign_targets_to_anchors + fg_bg_sampler on the device: (labels [N, A], regression targets
         [N, A, 4], positive mask, negative mask) from the zero-padded GT batch gt = (boxes, labels,
@@ -684,7 +736,11 @@ class RegionProposalNetwork(nn.Module):
         return {"loss_objectness": lo, "loss_rpn_box_reg": lb}
 
     def join_losses(self):
-        """Make the current stream wait for the side-stream loss chain (a no-op without one)."""
+        """Make the current stream wait for the side-stream loss chain (a no-op without one); first the
+        helper thread's issue of it (start_targets), if any."""
+        fut = self.__dict__.pop("_tgt_future", None)
+        if fut is not None:
+            fut.result()
         side = self.__dict__.pop("_loss_side", None)
         if side is not None:
             torch.cuda.current_stream(side.device).wait_stream(side)
@@ -817,40 +873,10 @@ class RoIHeads(nn.Module):
         scales = [2.0 ** round(math.log2(float(f.shape[1]) / float(max_h))) for f in feats]
         return scales, int(-math.log2(scales[0]))
 
-    def sample(self, proposals, gt, be):
-        """The RoI sampler's device part (training): candidates per image = its kept proposals (a valid
-        prefix of `post` slots, score order) then its GT boxes (torchvision: cat([proposals, gt])),
-        padded to [N, post + Gmax] with label -1 on padding, matched and sampled. -> (boxes [N, L, 4],
-        labels [N, L], regression targets [N, L, 4], sampled mask [N*L], number sampled (device
-        scalar)). Never waits for the GPU (HIP backend)."""
-        pb, _, pvalid = proposals
-        dev = pb.device
-        # GT slots padded to _gt_batch's width (a multiple of 32) on every backend, so the sampler
-        # draws keys over the same [N, post + gm] rows whichever path builds them
-        gtp, glp, gcnt = gt
-        gm = gtp.shape[1]
-        gslot = torch.arange(gm, device=dev)
-        box_p = torch.cat([pb, gtp], 1)               # [N, post + gm, 4]
-        valid = torch.cat([pvalid, gslot[None, :] < gcnt[:, None]], 1)
-        _, lab_b, tg_p = be.match_assign_batched(gtp, gcnt, box_p, self.fg, self.bg, False, 2,
-                                                 gt_labels=glp, weights=ROI_WEIGHTS)
-        lab_p = torch.where(valid, lab_b, -1)
-        pos_m, neg_m = self.fg_bg_sampler(lab_p, be)
-        sm = (pos_m | neg_m).flatten()
-        return box_p, lab_p, tg_p, sm, sm.sum()
-
-    def forward(self, features, proposals, image_sizes, targets=None, be=None, sampled=None):
-        """sampled: the sample() outputs with the sampled count already on the host (FasterRCNN's
-        captured proposal stage), in place of matching and sampling here."""
+    def forward(self, features, proposals, image_sizes, targets=None, be=None):
         feats = [features[k] for k in self.featmap_names]
         dev = feats[0].device
-        if self.training and sampled is not None:
-            box_p, lab_p, tg_p, sm, total = sampled
-            cm = lab_p.shape[1]
-            rois, lab_k, tg_k = be.roi_compact(sm, total, cm, box_p.reshape(-1, 4), lab_p.reshape(-1),
-                                               tg_p.reshape(-1, 4))
-            labels, tgts = [lab_k], [tg_k]
-        elif self.training:
+        if self.training:
             # candidates per image = its kept proposals (a valid prefix of `post` slots, score order)
             # then its GT boxes (torchvision: cat([proposals, gt])), padded to [N, post + Gmax] with
             # label -1 on padding, matched and sampled on the device; the one host sync of this stage
@@ -1099,43 +1125,6 @@ class FasterRCNN(nn.Module):
         head = self.rpn.head
         return feats, head.split(list(outs[nf:]), head.layout(outs[:nf]), be)
 
-    def _stage(self, il, features, head, targets, be):
-        """The training step's proposal stage -- the RPN's anchor matching and sampler, box decode,
-        filter_proposals (per-level top-k, clip / filter, NMS, selection) and the RoI sampler's matching
-        and draw -- as one captured HIP graph per (input shape, GT width) (_StageGraph): ~130 small
-        launches issued from Python took ~1.4 ms of mostly host-bound time per step (r05b trace). It
-        holds no autograd op (the losses' inputs are its outputs). Returns ((labels, targets, pos, neg),
-        padded proposals, RoI sample) or None (eager path: eval, MX_GRAPHS=0 / MX_STAGE_GRAPH=0, non-HIP
-        backends, an injected sampler key stream, an eager trunk).
-
-        OFF by default (MX_STAGE_GRAPH=1 enables it): on ROCm 7.2 the first replay after the capture
-        is correct, but a replay after the step's backward faulted the GPU with an illegal address
-        (tools/stage_diag.py, gpurun_out/r05g: forward + backward ok, the next replay faults) -- cause
-        not found; the stage holds torch.rand and torch.topk (rocprim scan) launches besides the
-        framework's own kernels."""
-        if not (self.training and head is not None and getattr(be, "name", "") == "hip" and _graphs_enabled(self)
-                and os.environ.get("MX_STAGE_GRAPH", "0") == "1" and hasattr(be, "proposal_nms_select")
-                and self.rpn.fg_bg_sampler.rand is None and self.roi_heads.fg_bg_sampler.rand is None
-                and not torch.cuda.is_current_stream_capturing()):
-            return None
-        objectness, pred_deltas, num_per_level = head
-        if not objectness.is_cuda:
-            return None
-        feats = list(features.values())
-        grid = [(f.shape[1], f.shape[2]) for f in feats]
-        anchors = self.rpn.anchor_generator(il.tensors.shape[1:3], grid, feats[0].device, be)
-        gt = _gt_batch(targets, objectness.device)
-        key = (tuple(objectness.shape), tuple(gt[0].shape), tuple(map(tuple, il.image_sizes)), tuple(num_per_level),
-               tuple(il.tensors.shape))
-        cache = self.__dict__.setdefault("_mx_stage_graphs", {})
-        g = cache.get(key)
-        if g is None:
-            if len(cache) >= 8:
-                return None
-            g = cache[key] = _StageGraph(self, be, objectness, pred_deltas, gt, anchors, il.image_sizes,
-                                         list(num_per_level))
-        return g(objectness, pred_deltas, gt)
-
     def _flag_async(self, flags):
         """(pinned host bool, event) of any(flags) copied without waiting, or None."""
         if not flags:
@@ -1192,39 +1181,32 @@ class FasterRCNN(nn.Module):
                      [(b[:, 2:] <= b[:, :2]).any() for b in dev_boxes])
             degenerate = self._flag_async(flags)
         il, targets = self.transform(images, targets, be)
-        trunk = self._trunk(il.tensors, be)
-        if trunk is not None:  # HIP-graph replay of backbone + FPN + RPN head (static shapes)
-            features, head = trunk
-        else:
-            features, head = self.backbone(il.tensors, be), None
         # MX_RPN_DEFER_LOSSES=1 issues the RPN target / loss launches after the RoI sampler's host sync;
         # measured 0.5 % slower than issuing them while the trunk runs (A/B on one box), so off
         defer = os.environ.get("MX_RPN_DEFER_LOSSES", "0") != "0"
-        stage = self._stage(il, features, head, targets, be) if not defer else None
+        early = None
+        if (not defer and self.training and il.tensors.is_cuda
+                and self.__dict__.get("_mx_graphs", {}).get((tuple(il.tensors.shape), il.tensors.dtype)) is not None):
+            early = self.rpn.start_targets(il, targets, be)  # its launches beside the trunk's graph launch
         try:
-            if stage is not None:  # HIP-graph replay of the proposal stage (no autograd inside)
-                objectness, pred_deltas = head[0], head[1]
-                tgt, proposals, sampled = stage
-                rpn_losses = self.rpn.loss_of(objectness, pred_deltas, tgt, be)
+            trunk = self._trunk(il.tensors, be)
+            if trunk is not None:  # HIP-graph replay of backbone + FPN + RPN head (static shapes)
+                features, head = trunk
             else:
-                proposals, rpn_losses = self.rpn(il, features, targets, be, head=head, defer_losses=defer)
-                sampled = None
+                features, head = self.backbone(il.tensors, be), None
+            if early is not None:  # the helper thread issued the target chain during the trunk launch
+                early, self.rpn._gt_ready = self.rpn.__dict__.pop("_tgt_future").result()
+            proposals, rpn_losses = self.rpn(il, features, targets, be, head=head, defer_losses=defer,
+                                             early=early)
             if degenerate is not None:
                 host, ev = degenerate
                 ev.synchronize()
                 if bool(host):
                     raise ValueError("All bounding boxes should have positive height and width.")
-            if stage is not None:
-                box_p, lab_p, tg_p, sm, stat = sampled
-                total, nk = stat.tolist()  # the stage's one host sync: sampled RoI count + NMS status
-                if nk < 0:
-                    self.rpn._nk_pending = (torch.tensor(nk), None)
-                    self.rpn.check_nms()
-                sampled = (box_p, lab_p, tg_p, sm, int(total))
             gt_ready = self.rpn.__dict__.pop("_gt_ready", None)
             if gt_ready is not None:  # the RoI sampler reads the GT batch the RPN's side stream built
                 torch.cuda.current_stream().wait_event(gt_ready)
-            detections, det_losses = self.roi_heads(features, proposals, il.image_sizes, targets, be, sampled=sampled)
+            detections, det_losses = self.roi_heads(features, proposals, il.image_sizes, targets, be)
             self.rpn.check_nms()
         finally:  # also when the step raises: no side-stream work is left unjoined behind it
             self.rpn.join_losses()
@@ -1252,58 +1234,6 @@ def _graphs_enabled(mod=None):
     # under torch DDP the gradient all-reduce hooks live on the parameters' AccumulateGrad nodes,
     # which the replayed backward graph bypasses: such runs keep the trunk eager
     return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
-
-
-class _StageGraph:
-    """FasterRCNN._stage's captured graph: static inputs (objectness, deltas -- detached copies -- and the
-    padded GT batch) -> static outputs, captured after two eager warm-ups on the capture stream (every
-    per-shape constant and workspace exists before the capture; the sampler keys come from the default
-    device generator, which advances per replay as in eager execution). The outputs are overwritten by
-    the next replay: this step consumes them (RoI compaction, the RPN loss and its backward) first."""
-
-    def __init__(self, model, be, obj, dl, gt, anchors, image_sizes, num_per_level):
-        self.model, self.be = model, be
-        self.anchors, self.image_sizes, self.npl = anchors, [tuple(s) for s in image_sizes], num_per_level
-        self.static = [obj.detach().clone(), dl.detach().clone()] + [t.clone() for t in gt]
-        dev = obj.device
-        side = mc.capture_stream(dev)
-        side.wait_stream(torch.cuda.current_stream())
-        # the warm-ups' sampler draws are not the step's: the device generator is put back, so the first
-        # replay draws exactly what the eager stage would have (graph and eager runs stay comparable)
-        rng = torch.cuda.get_rng_state(dev)
-        with torch.cuda.stream(side):
-            for _ in range(2):
-                self._run()
-        torch.cuda.current_stream().wait_stream(side)
-        torch.cuda.synchronize(dev)
-        torch.cuda.set_rng_state(rng, dev)
-        self.graph = torch.cuda.CUDAGraph()
-        with mc.capture_guard(), torch.cuda.graph(self.graph, stream=side):
-            self.out = self._run()
-        torch.cuda.set_rng_state(rng, dev)
-        self.model.rpn.__dict__.pop("_nk_pending", None)  # the warm-ups' NMS watch: checked via `stat`
-
-    def _run(self):
-        m, be = self.model, self.be
-        obj, dl, gtp, glp, gcnt = self.static
-        N, A = obj.shape
-        gt = (gtp, glp, gcnt)
-        tgt = m.rpn.targets_of(self.anchors, gt, be)
-        props = be.box_decode(dl.reshape(-1, 4), self.anchors.repeat(N, 1), RPN_WEIGHTS).view(N, A, 4)
-        proposals = m.rpn.filter_proposals_padded(props, obj, self.image_sizes, self.npl, be)
-        nk = m.rpn._nk_last
-        box_p, lab_p, tg_p, sm, total = m.roi_heads.sample(proposals, gt, be)
-        stat = torch.stack([total.reshape(()).to(torch.int64), nk.reshape(-1)[0].to(torch.int64)])
-        return tgt, proposals, (box_p, lab_p, tg_p, sm, stat)
-
-    def __call__(self, obj, dl, gt):
-        s = self.static
-        s[0].copy_(obj.detach())
-        s[1].copy_(dl.detach())
-        for a, b in zip(s[2:], gt):
-            a.copy_(b)
-        self.graph.replay()
-        return self.out
 
 
 class _Trunk(nn.Module):

@@ -44,6 +44,7 @@ def main():
     from mx_det import ops, frcnn
     from mx_det.data import synth_batch
     from mx_det.dp import DataParallel
+    from mx_det import conv as mc
     ref = _model(dev)
     ref.__dict__["_mx_seg_ready"] = lambda key, ps: None  # same segmented trunk graphs, no exchange
     m = _model(dev)
@@ -69,7 +70,7 @@ def main():
         born = 0  # gradients written straight into their bucket slot by the backward (no copy)
         for p in m.parameters():
             if p.requires_grad and p.grad is not None:
-                flat, off = p._mx_grad_slot
+                flat, off = mc.grad_slots[p]
                 born += int(p.grad.data_ptr() == flat.data_ptr() + 4 * off)
         res["slot_grads"] = born
         dp.sync_gradients()
@@ -82,7 +83,7 @@ def main():
         for (n, p), q in zip(m.named_parameters(), ref.parameters()):
             if not p.requires_grad:
                 continue
-            flat, off = p._mx_grad_slot
+            flat, off = mc.grad_slots[p]
             assert p.grad.data_ptr() == flat.data_ptr() + 4 * off, n  # every .grad is its slot after sync
             e = ((p.grad - q.grad).norm() / q.grad.norm().clamp_min(1e-30)).item()
             if e > res["worst_grad"]:

@@ -109,6 +109,7 @@ def test_dp_issue_order_is_canonical_whatever_the_hooks():
         dp._work, dp.issued, dp.last_issued, dp.world = {}, [], [], 1
         dp.flats = {k: (torch.zeros(1), []) for k in keys + [("bucket", 0)]}
         dp.scale, dp._copied = None, 0
+        dp.rpn, dp._flag_host = None, None
         dp._start = lambda key: (_Done(), key)
         return dp
 
@@ -129,3 +130,81 @@ def test_dp_issue_order_is_canonical_whatever_the_hooks():
         fire(dp)
         dp.sync_gradients()
         assert dp.last_issued == canonical, (name, dp.last_issued)
+
+
+class _TinyRpn(torch.nn.Module):
+    pass
+
+
+class _Tiny(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.lin = torch.nn.Linear(8, 4)
+        self.rpn = _TinyRpn()
+
+    def forward(self, x):
+        return self.lin(x).square().sum()
+
+
+def _nms_flag_worker(rank, world, port, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "robust-object-detection_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mx_det import conv as mc
+    from mx_det.dp import DataParallel
+    torch.manual_seed(rank)
+    m = _Tiny()
+    dp = DataParallel(m)
+    res = {}
+    for step in range(2):  # step 0: every rank fine; step 1: rank 1's proposal NMS failed
+        if step == 1 and rank == 1:
+            m.rpn._nms_error = "proposal NMS num_keep = -2"
+        dp(torch.randn(3, 8)).backward()
+        try:
+            dp.sync_gradients()
+            res[step] = "ok"
+        except RuntimeError as e:
+            res[step] = str(e)
+        for p in m.parameters():
+            p.grad = None
+    res["slots"] = sum(p in mc.grad_slots for p in m.parameters())
+    res["no_attr"] = not any("_mx_grad_slot" in p.__dict__ for p in m.parameters())
+    dp.close()
+    res["closed"] = sum(p in mc.grad_slots for p in m.parameters())
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_dp_nms_failure_raises_on_every_rank():
+    """a rank whose proposal NMS fails must not raise alone (the others would block in the
+    next all-reduce). Under DataParallel the failure rides in the first collective's flag and every
+    rank raises from sync_gradients; the gradient slots live in conv.grad_slots (nothing on the
+    parameter) and close() drops them."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_nms_flag_worker, args=(world, _port(), out), nprocs=world, join=True)
+    for r in range(world):
+        res = out[r]
+        assert res[0] == "ok", res
+        assert "proposal NMS failed" in res[1], res
+        assert ("num_keep = -2" in res[1]) == (r == 1), res
+        assert res["slots"] == 2 and res["no_attr"] and res["closed"] == 0, res
+
+
+def test_check_nms_records_under_data_parallel():
+    """RegionProposalNetwork.check_nms raises on a failed NMS status, except under DataParallel
+    (`_mx_defer_nms_error`), where it records the failure for sync_gradients."""
+    import pytest
+    from mx_det import frcnn
+    m = frcnn.fasterrcnn_resnet50_fpn_v2(weights=None)
+    rpn = m.rpn
+    rpn._nk_pending = (torch.tensor(-2), None)
+    with pytest.raises(RuntimeError, match="presorted"):
+        rpn.check_nms()
+    rpn.__dict__["_mx_defer_nms_error"] = True
+    rpn._nk_pending = (torch.tensor(-1), None)
+    rpn.check_nms()
+    assert rpn._nms_error == "proposal NMS num_keep = -1"

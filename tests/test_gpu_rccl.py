@@ -66,3 +66,18 @@ def test_bench_line_under_nccl_group():
     assert rec["n_gpus"] == 1 and rec["value"] > 0
     assert rec["config"]["parallelism"] == "dp1 (nccl group, DataParallel)"
     assert "roofline" in rec and "hbm_ops" in rec
+
+
+@pytest.mark.timeout(360)
+def test_bench_line_carries_dp_variant():
+    """The default N=1 line times the headline step a second time through DataParallel in a one-rank
+    nccl group (dp_variant: the N-GPU code path's per-rank cost), then leaves the group."""
+    env = _env()
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--steps", "2", "--warmup", "2", "--precision", "f32",
+                        "--no-eval-variant", "--no-augment-variant", "--no-cpu-baseline", "--no-roofline"],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    rec = json.loads(p.stdout.strip().splitlines()[-1])
+    assert rec["config"]["parallelism"] == "dp1"
+    dv = rec["dp_variant"]
+    assert dv["parallelism"] == "dp1 (nccl group, DataParallel)" and dv["value"] > 0 and dv["ratio_to_headline"] > 0

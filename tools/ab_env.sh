@@ -8,7 +8,7 @@ mkdir -p $OUT
 export PYTHONUNBUFFERED=1
 for i in $(seq 1 $R); do
   for v in $A $B; do
-    env $VAR=$v timeout -k 10 300 python -u bench.py --precision f32 --no-augment-variant --no-eval-variant \
+    env $VAR=$v timeout -k 10 300 python -u bench.py --precision f32 --no-augment-variant --no-eval-variant --no-dp-variant \
       --no-cpu-baseline --no-roofline --steps $S --warmup 5 > $OUT/ab_${v}_$i.log 2>&1 || { echo "$v $i failed"; tail -5 $OUT/ab_${v}_$i.log; exit 1; }
     echo "$VAR=$v $i $(tail -1 $OUT/ab_${v}_$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
   done

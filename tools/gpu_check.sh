@@ -35,7 +35,7 @@ for s in $STEPS; do
       tail -1 "$OUT/bench.log" ;;
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o prof -- \
-        python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/prof.log" 2>&1 \
+        python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-dp-variant > "$OUT/prof.log" 2>&1 \
         || { echo "prof failed rc=$?"; tail -30 "$OUT/prof.log"; exit 1; }
       for f in $(find "$OUT/prof" -name '*_stats.csv'); do cp "$f" "$OUT/"; done
       python3 tools/prof_steps.py "$OUT/prof" --steps 10 --out "$OUT/step_kernels.csv" > "$OUT/step_kernels.log" 2>&1 \

@@ -28,7 +28,7 @@ for s in "$@"; do
         --no-roofline > "$OUT/rehearse.log" 2>&1 || { echo "rehearse failed"; tail -30 "$OUT/rehearse.log"; exit 1; }
       tail -1 "$OUT/rehearse.log" ;;
     hbm)
-      timeout -k 10 300 python -u bench.py --precision f32 --no-augment-variant --no-eval-variant --no-cpu-baseline \
+      timeout -k 10 300 python -u bench.py --precision f32 --no-augment-variant --no-eval-variant --no-dp-variant --no-cpu-baseline \
         --steps 10 --warmup 3 > "$OUT/hbm.log" 2>&1 || { echo "hbm bench failed"; tail -30 "$OUT/hbm.log"; exit 1; }
       tail -1 "$OUT/hbm.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], json.dumps(d.get('hbm_ops')))" ;;
     script)

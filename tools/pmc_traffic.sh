@@ -14,7 +14,7 @@ for prec in $PRECS; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d $OUT/$prec/$c -o p -- \
       python3 bench.py --steps 2 --warmup 1 --precision $prec --no-cpu-baseline --no-roofline --no-augment-variant \
-      --no-eval-variant > $OUT/$prec-$c.log 2>&1 || { echo "pmc $prec $c failed"; tail -5 $OUT/$prec-$c.log; exit 1; }
+      --no-eval-variant --no-dp-variant > $OUT/$prec-$c.log 2>&1 || { echo "pmc $prec $c failed"; tail -5 $OUT/$prec-$c.log; exit 1; }
   done
   python3 tools/traffic_summary.py $OUT/$prec > $OUT/traffic_$prec.json && rm -rf $OUT/$prec || exit 1
 done
