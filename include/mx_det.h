@@ -395,14 +395,6 @@ int mx_conv_set_korder(int order);
 /* Timing experiments only: 1 = the bf16x3 buffer kernels skip their epilogue (outputs undefined). */
 int mx_conv_set_debug(int v);
 int mx_conv_set_wgrad_target(int64_t blocks);
-/* Split-K tail of the bf16x3 buffer conv kernel (1, default): when the grid's last round of tiles would
-   leave most CUs idle, those tiles split K and the reduce kernel finishes their rows. 0: off. */
-int mx_conv_set_tail(int on);
-/* Host-only queries of the bf16x3 fwd / dgrad GEMM layout (no device work): out[7] = {bmt, bn, tiles,
-   splits, tail_tile, m_base, tail_splits} for an M x Ncol x Kdim GEMM under the current settings, and
-   out[3] = {tile, split, partial} of block gid in the tail layout. */
-int mx_conv_x3_geometry(int64_t M, int64_t Ncol, int64_t Kdim, int64_t* out);
-int mx_conv_tail_map(int64_t tail_tile, int splits, int64_t gid, int64_t* out);
 
 /* ---------------------------------------------------------------------------------------------
  * Precision-faithful convolution (bf16x3): the reference trains and evaluates its convs in fp32

@@ -50,11 +50,6 @@ struct ConvP {
   float* slab;
   int splits;
   int64_t kt_per_split;
-  // split-K tail (bf16x3 buffer kernel): tiles [0, tail_tile) run unsplit with the fused epilogue; the
-  // tiles from tail_tile on (whole block rows: the GEMM rows from m_base on) run `splits` ways into
-  // slab[split][M - m_base][Ncol] and the reduce kernel finishes rows [m_base, M). 0 / 0: every tile
-  // splits when slab is set (plain split-K)
-  int64_t tail_tile, m_base;
   // dgrad parity class: GEMM row m = (n, hh, ww) of the class grid stores to dx row
   // (n, st_h*hh + ph, st_w*ww + pw) of the full [N][H][W] grid
   int remap, rst_h, rst_w, rph, rpw;
@@ -91,22 +86,6 @@ __device__ __forceinline__ int64_t out_row(const ConvP& p, int64_t m) {
   if (!p.remap) return m;
   const int64_t ww = m % p.OW, t = m / p.OW, hh = t % p.OH, n = t / p.OH;
   return (n * p.rH + hh * p.rst_h + p.rph) * p.rW + ww * p.rst_w + p.rpw;
-}
-
-// Block -> (tile, split) of the split-K tail layout (ConvP::tail_tile): the first tail_tile blocks are
-// whole tiles, the rest `splits` consecutive blocks per tile. tail_tile = 0 is plain split-K.
-__host__ __device__ __forceinline__ void tail_map(int64_t tail_tile, int splits, int64_t gid, int64_t& bid, int& split,
-                                                  bool& partial) {
-  if (gid < tail_tile) {
-    bid = gid;
-    split = 0;
-    partial = false;
-  } else {
-    const int64_t g = gid - tail_tile;
-    bid = tail_tile + g / splits;
-    split = (int)(g % splits);
-    partial = true;
-  }
 }
 
 __device__ __forceinline__ float act_f(float v, int act) {
@@ -151,10 +130,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
   static_assert(HALVES == 1 || HALVES == WR, "staging: the whole tile at once, or one wave-row per pass");
   static_assert(WM == SROWS || (SROWS % WM == 0 && WR * WM >= SROWS), "wave-rows of 64, 32 or 16 rows");
   (void)mt;
-  if (p.slab && split >= 0) {  // split-K partial: f32 tile to the slab, epilogue deferred to the reduce kernel
+  if (p.slab) {  // split-K partial: f32 tile to the slab, epilogue deferred to the reduce kernel
     constexpr int LD = BN + 4;
     float* Ct = (float*)smem;
-    float* dst = p.slab + (int64_t)split * (p.M - p.m_base) * p.Ncol;  // the plane holds rows [m_base, M)
+    float* dst = p.slab + (int64_t)split * p.M * p.Ncol;
     constexpr int CPR = BN / 4;
 #pragma unroll
     for (int h = 0; h < HALVES; ++h) {
@@ -172,7 +151,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvP& p, f32x4 (&acc)[BMT /
       for (int e = tid; e < PR * CPR; e += NT) {
         int row = e / CPR, cc = (e % CPR) * 4;
         int64_t m = m0 + h * PR + row, col0 = n0 + cc;
-        if (m < p.M && col0 < p.Ncol) *(float4*)(dst + (m - p.m_base) * p.Ncol + col0) = *(const float4*)&Ct[row * LD + cc];
+        if (m < p.M && col0 < p.Ncol) *(float4*)(dst + m * p.Ncol + col0) = *(const float4*)&Ct[row * LD + cc];
       }
       if (HALVES > 1) __syncthreads();
     }
@@ -976,7 +955,7 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
   constexpr int RL = 256 / CG, RPT = BM / RL, CW = 8 * CG;
   __shared__ float red[2][RL][CW + 1];
   const int tid = threadIdx.x, cl = tid % CG, rl = tid / CG;
-  const int64_t mt = p.m_base / BM + blockIdx.x, col0 = (int64_t)blockIdx.y * CW + cl * 8;
+  const int64_t mt = blockIdx.x, col0 = (int64_t)blockIdx.y * CW + cl * 8;
   const bool cok = col0 < p.Ncol;
   float s2[2][8] = {}, q2[2][8] = {};
   float b2[2][8] = {}, c2[2][8] = {}, bmu[8], bis[8];  // BN-backward partials (p.bnb_part)
@@ -984,7 +963,7 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) { bmu[t] = p.bnb_mean[col0 + t]; bis[t] = p.bnb_invstd[col0 + t]; }
   }
-  const int64_t stride = (p.M - p.m_base) * p.Ncol;  // slab planes hold rows [m_base, M)
+  const int64_t stride = p.M * p.Ncol;
   // the rows' loads of one split plane are issued together (2*RPT x 16 B in flight per thread); the
   // per-element summation order over the splits is sequential
   float va[RPT][8] = {};
@@ -994,7 +973,7 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvP p) {
     for (int rr = 0; rr < RPT; ++rr) {
       const int64_t m = mt * BM + rl + RL * rr;
       if (cok && m < p.M) {
-        const float* src = p.slab + k * stride + (m - p.m_base) * p.Ncol + col0;
+        const float* src = p.slab + k * stride + m * p.Ncol + col0;
         a[rr] = *(const float4*)src;
         b[rr] = *(const float4*)(src + 4);
       } else {
@@ -1740,11 +1719,8 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
   const int wm = wave / WC, wn = wave % WC;
   const int64_t ntiles_n = (p.Ncol + BN - 1) / BN;
   const int64_t gid = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
-  int64_t bid;
-  int split;
-  bool partial;
-  tail_map(p.tail_tile, p.splits, gid, bid, split, partial);
-  partial = partial && p.slab != nullptr;
+  const int split = (int)(gid % p.splits);
+  const int64_t bid = gid / p.splits;
   const int64_t mt = bid / ntiles_n, nt = bid % ntiles_n;
   const int64_t m0 = mt * BMT, n0 = nt * BN;
   const int lrow = lane >> 2, pc = lane & 3;  // landing row within the instruction, physical chunk
@@ -1785,8 +1761,8 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
   const i32x4 blrsrc = dma_rsrc(p.wt + p.wt_plane, (uint32_t)(p.wt_elems * 2));
   const uint32_t lds0 = lds_addr(smem);
   const int64_t nk = p.Kdim / 32;
-  const int64_t kbeg = partial ? (int64_t)split * p.kt_per_split : 0;
-  const int64_t ntk = partial ? min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg : nk;
+  const int64_t kbeg = (int64_t)split * p.kt_per_split;
+  const int64_t ntk = min<int64_t>(nk, kbeg + p.kt_per_split) - kbeg;
   // wave-uniform K position of the next tile to issue: tap (cr, cq), channel cc
   const int korder = __builtin_amdgcn_readfirstlane(p.korder);
   KPos kp;
@@ -1904,7 +1880,7 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
   // wide tiles stage the whole f32 tile at once (one barrier, every wave storing); 8-wave 2x2 tiles
   // stage one wave-row per pass (their whole tile would not fit beside a second block)
   conv_epilogue<BN, (WC == 1 ? 1 : WR), BMT, float, WR, WC, MODE == 1>(p, acc, smem, m0, n0, mt, wm, wn, lane, tid,
-                                                                       partial ? split : -1);
+                                                                       split);
 #endif
 }
 
@@ -2967,10 +2943,6 @@ struct Geo {
   int64_t M, Ncol, Kdim, tiles, nk;
   int splits, bmt, bn;
   bool narrow;
-  // split-K tail of the bf16x3 buffer kernel (make_geo_x3): tiles from tail_tile on split tail_splits
-  // ways, GEMM rows from m_base on finished by the reduce kernel; tail_splits 1 = none
-  int64_t tail_tile, m_base;
-  int tail_splits;
 };
 static int num_cus();
 static int g_force_bmt = 0, g_force_bn = 0;  // mx_conv_set_tile (0 = automatic)
@@ -3688,43 +3660,6 @@ extern "C" int mx_conv2d_wgrad(const mx_conv_shape* s, const uint16_t* dy, const
 // ================================================================================================
 // bf16x3 (f32 activation) entry points: same GEMM decompositions as the bf16 path (fwd, dgrad per
 // stride-parity class, wgrad split over pixels), f32 activations / gradients, split weights.
-static int g_conv_tail = 1;  // mx_conv_set_tail
-extern "C" int mx_conv_set_tail(int on) {
-  MX_CHECK_ARG(on == 0 || on == 1, "mx_conv_set_tail: 0 (off) or 1 (split-K tail of the bf16x3 buffer kernel)");
-  g_conv_tail = on;
-  return MX_OK;
-}
-// blocks per CU of the 128-row bf16x3 buffer-kernel instance launch_igemm_x3 picks for this tile width
-static int x3_occ128(int bn) {
-  if (bn == 64) return g_buf_stages == 3 ? 3 : 2;
-  if (g_buf_stages == 5 || g_buf_stages == 3) return 1;
-  return 2;
-}
-// Split-K tail: a grid of T tiles on `slots` resident blocks runs floor(T / slots) full rounds and a
-// last round of T % slots tiles on a mostly idle chip (the P2 3x3: 2,100 tiles, 512 slots, a fifth
-// round at 10 % occupancy). When that round is at most a quarter full, its tiles (rounded up to whole
-// block rows) split K S ways -- S blocks of 1/S the work each fill the idle slots -- and the reduce
-// kernel finishes their rows (slab planes of the tail rows only).
-static void x3_tail(Geo& g) {
-  g.tail_tile = 0;
-  g.m_base = 0;
-  g.tail_splits = 1;
-  if (!g_conv_tail || g.splits != 1 || g.bmt != 128 || g.nk < 16) return;
-  const int64_t slots = (int64_t)num_cus() * x3_occ128(g.bn);
-  const int64_t ntn = cdiv(g.Ncol, g.bn), rem = g.tiles % slots;
-  if (g.tiles <= slots || rem == 0 || 4 * rem > slots) return;
-  const int64_t tail = cdiv(rem, ntn) * ntn;  // whole block rows
-  const int64_t S = std::min<int64_t>(std::min<int64_t>(8, g.nk / 8), std::max<int64_t>(2, slots / tail));
-  if (S < 2 || tail >= g.tiles) return;
-  g.tail_splits = (int)S;
-  g.tail_tile = g.tiles - tail;
-  g.m_base = (g.tail_tile / ntn) * 128;
-}
-static size_t x3_ws(const Geo& g) {
-  size_t need = g.splits > 1 ? sizeof(float) * (size_t)g.splits * g.M * g.Ncol : 0;
-  if (g.tail_splits > 1) need = std::max(need, sizeof(float) * (size_t)g.tail_splits * (g.M - g.m_base) * g.Ncol);
-  return need;
-}
 static Geo make_geo_x3(int64_t M, int64_t Ncol, int64_t Kdim) {
   Geo g;
   g.M = M; g.Ncol = Ncol; g.Kdim = Kdim;
@@ -3755,30 +3690,7 @@ static Geo make_geo_x3(int64_t M, int64_t Ncol, int64_t Kdim) {
     g.splits = (int)std::max<int64_t>(1, sp);
   }
   if (g_max_splits && g.splits > g_max_splits) g.splits = g_max_splits;
-  x3_tail(g);
   return g;
-}
-
-// Host-side queries of the tail layout (tests/test_conv_tail.py checks the block -> (tile, K range)
-// cover on the CPU): out = {bmt, bn, tiles, splits, tail_tile, m_base, tail_splits}.
-extern "C" int mx_conv_x3_geometry(int64_t M, int64_t Ncol, int64_t Kdim, int64_t* out) {
-  MX_CHECK_ARG(out && M > 0 && Ncol > 0 && Kdim > 0, "mx_conv_x3_geometry: bad arguments");
-  const Geo g = make_geo_x3(M, Ncol, Kdim);
-  const int64_t v[7] = {g.bmt, g.bn, g.tiles, g.splits, g.tail_tile, g.m_base, g.tail_splits};
-  for (int i = 0; i < 7; ++i) out[i] = v[i];
-  return MX_OK;
-}
-// out = {tile, split, partial} of block gid (the kernel's tail_map)
-extern "C" int mx_conv_tail_map(int64_t tail_tile, int splits, int64_t gid, int64_t* out) {
-  MX_CHECK_ARG(out && splits >= 1 && gid >= 0 && tail_tile >= 0, "mx_conv_tail_map: bad arguments");
-  int64_t bid;
-  int split;
-  bool partial;
-  tail_map(tail_tile, splits, gid, bid, split, partial);
-  out[0] = bid;
-  out[1] = split;
-  out[2] = partial;
-  return MX_OK;
 }
 
 template <int BN, int MODE, int BMT>
@@ -3803,7 +3715,6 @@ static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, h
   if (g.bmt == 256 && !buf) {  // 256-row tiles exist only as the buffer kernel
     g.bmt = 128;
     g.tiles = cdiv(g.M, 128) * cdiv(g.Ncol, g.bn);
-    g.tail_splits = 1;
   }
   int64_t blocks = g.tiles;
   MX_CHECK_ARG(g.Kdim < (1ll << 30) && p.IH < (1ll << 26) && p.IW < (1ll << 26) && p.IC < (1ll << 30),
@@ -3820,16 +3731,6 @@ static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, h
     p.splits = (int)cdiv(nk, p.kt_per_split);
     p.slab = (float*)ws;
     blocks *= p.splits;
-  } else if (buf && g.tail_splits > 1) {
-    const size_t need = x3_ws(g);
-    MX_CHECK_ARG(ws && ws_bytes >= need, "conv: split-K tail workspace of %zu bytes required (mx_conv_workspace_x3)",
-                 need);
-    p.kt_per_split = cdiv(nk, (int64_t)g.tail_splits);
-    p.splits = (int)cdiv(nk, p.kt_per_split);
-    p.slab = (float*)ws;
-    p.tail_tile = g.tail_tile;
-    p.m_base = g.m_base;
-    blocks = g.tail_tile + (g.tiles - g.tail_tile) * p.splits;
   }
   MX_CHECK_ARG(blocks < (1ll << 31), "conv: grid too large");
   if (buf) {
@@ -3866,13 +3767,12 @@ static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, h
     else launch_x3<128, MODE, 128>(p, blocks, st);
   }
   MX_LAUNCH_CHECK();
-  if (p.slab) {  // rows [m_base, M): all of them for plain split-K, the tail's for the split-K tail
-    const int64_t rblocks = cdiv(g.M - p.m_base, BM);
-    if (rblocks * cdiv(g.Ncol, 64) >= 2 * (int64_t)num_cus()) {
-      dim3 rg((unsigned)rblocks, (unsigned)cdiv(g.Ncol, 64));
+  if (p.slab) {
+    if (cdiv(g.M, BM) * cdiv(g.Ncol, 64) >= 2 * (int64_t)num_cus()) {
+      dim3 rg((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.Ncol, 64));
       conv_splitk_reduce_kernel<8, float><<<rg, 256, 0, st>>>(p);
     } else {
-      dim3 rg((unsigned)rblocks, (unsigned)cdiv(g.Ncol, 16));
+      dim3 rg((unsigned)cdiv(g.M, BM), (unsigned)cdiv(g.Ncol, 16));
       conv_splitk_reduce_kernel<2, float><<<rg, 256, 0, st>>>(p);
     }
     MX_LAUNCH_CHECK();
@@ -3908,7 +3808,10 @@ extern "C" size_t mx_conv_workspace_x3(const mx_conv_shape* s, int pass) {
     const WGeo g = wgrad_geo_x3(&sd);
     return g.splits > 1 ? sizeof(float) * (size_t)g.splits * sd.K * sd.R * sd.S * sd.C : 0;
   }
-  if (pass == 0) return x3_ws(make_geo_x3(s->N * s->Ho * s->Wo, s->K, s->R * s->S * s->C));
+  if (pass == 0) {
+    const Geo g = make_geo_x3(s->N * s->Ho * s->Wo, s->K, s->R * s->S * s->C);
+    return g.splits > 1 ? sizeof(float) * (size_t)g.splits * g.M * g.Ncol : 0;
+  }
   if (s->stride_h < 1 || s->stride_h > 2 || s->stride_w < 1 || s->stride_w > 2) return 0;
   DClass cl[4];
   int64_t off[4];
@@ -3916,7 +3819,8 @@ extern "C" size_t mx_conv_workspace_x3(const mx_conv_shape* s, int pass) {
   const int n = dgrad_classes(s, s->C, s->K, cl, off, br, bs);
   size_t mx = 0;
   for (int i = 0; i < n; ++i) {
-    mx = std::max(mx, x3_ws(make_geo_x3(s->N * cl[i].Hc * cl[i].Wc, s->C, (int64_t)cl[i].Rc * cl[i].Sc * s->K)));
+    const Geo g = make_geo_x3(s->N * cl[i].Hc * cl[i].Wc, s->C, (int64_t)cl[i].Rc * cl[i].Sc * s->K);
+    if (g.splits > 1) mx = std::max(mx, sizeof(float) * (size_t)g.splits * g.M * g.Ncol);
   }
   return mx;
 }

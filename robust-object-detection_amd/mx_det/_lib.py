@@ -110,9 +110,6 @@ _SIGS = {
     "mx_conv_set_wgrad_variant": (c_int, [c_int]),
     "mx_conv_get_wgrad_variant": (c_int, []),
     "mx_conv_set_wgrad_target": (c_int, [c_i64]),
-    "mx_conv_set_tail": (c_int, [c_int]),
-    "mx_conv_x3_geometry": (c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_i64)]),
-    "mx_conv_tail_map": (c_int, [c_i64, c_int, c_i64, ctypes.POINTER(c_i64)]),
     "mx_conv2d_wgrad_ex": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp,
                                    ctypes.c_size_t, c_vp]),
     "mx_conv_transpose_weight": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
@@ -197,9 +194,6 @@ def load():
             fn.restype = res
             fn.argtypes = args
         _lib = lib
-        tail = os.environ.get("MX_CONV_TAIL")  # split-K tail of the bf16x3 conv grid (default on)
-        if tail is not None and hasattr(lib, "mx_conv_set_tail"):
-            call("mx_conv_set_tail", 1 if tail != "0" else 0)
     return _lib
 
 

@@ -593,8 +593,6 @@ def _wgrad_plan(ctx, dy, x, K, R, S, stride, pad, kout=None, cin=None):
         return None
     dst = grad_dest(ctx)
     side = side_wgrad_enabled(ctx)
-    if side and _defer is not None:  # a segmented backward capture (defer_side_wgrads)
-        return wgrad_prepare(dy, x, K, R, S, stride, pad, kout, cin, dst), "defer", None
     if side and os.environ.get("MX_WGRAD_FORK", "early") != "late":
         job = wgrad_prepare(dy, x, K, R, S, stride, pad, kout, cin, dst)
         fork = torch.cuda.Event()
@@ -605,45 +603,9 @@ def _wgrad_plan(ctx, dy, x, K, R, S, stride, pad, kout=None, cin=None):
 
 def _wgrad_run(plan):
     job, side, fork = plan
-    if side == "defer":
-        dw = job.dw
-        job.dw = None  # AccumulateGrad adopts dw only while autograd holds its sole reference
-        job.dwp = dw.data_ptr()
-        _defer.append(job)
-        return dw
     if not isinstance(job, _WgradJob):
         job = wgrad_prepare(*job)
     return wgrad_launch(job, side, fork)
-
-
-# Deferred side wgrads (frcnn._SegGraphs one_graph): while a segment's backward is captured, every
-# side-eligible weight gradient is prepared (operands, output and workspace allocated in the capture's
-# pool) and collected here instead of launched; the capture then launches the collected wgrads on the
-# wgrad stream after the segment's whole dgrad chain (wgrad_launch_deferred). Within one captured
-# graph the HIP graph executor submits a side list only after the main list it forks from
-# (profiles/r05c: layer4..2's wgrads ran as a ~2 ms tail after the trunk's dgrad chain).
-_defer = None
-
-
-@contextlib.contextmanager
-def defer_side_wgrads(jobs):
-    """Collect this backward's side-stream weight gradients into `jobs` (a list; None: launch them)."""
-    global _defer
-    prev, _defer = _defer, jobs
-    try:
-        yield
-    finally:
-        _defer = prev
-
-
-def wgrad_launch_deferred(j):
-    """Launch a weight gradient collected by defer_side_wgrads on the current stream (its output is
-    the tensor autograd adopted as .grad, addressed by pointer: dw must stay referenced elsewhere)."""
-    if j.cfg is not None:
-        _apply_wg(j.cfg)
-    call(j.entry, ctypes.byref(j.sh), _p(j.dyc), _p(j.x), j.dwp, j.kout, j.cin, 1, _p(j.ws), j.wsb, _s())
-    if j.cfg is not None:
-        _apply_wg(_WG_DEFAULT)
 
 
 def _join_side():
@@ -656,8 +618,8 @@ def _join_side():
 class _WgradJob:
     """A weight gradient's launch prepared ahead of time (wgrad_prepare): shape, operands, output and
     split workspace allocated and the tuner's pick applied, so the launch itself allocates nothing."""
-    __slots__ = ("sh", "x3", "entry", "dw", "dwp", "dyc", "x", "ws", "wsb", "cfg", "kout", "cin", "K", "R", "S",
-                 "stride", "t0")
+    __slots__ = ("sh", "x3", "entry", "dw", "dyc", "x", "ws", "wsb", "cfg", "kout", "cin", "K", "R", "S", "stride",
+                 "t0")
 
 
 def wgrad_prepare(dy, x, K, R, S, stride, pad, kout=None, cin=None, out=None):

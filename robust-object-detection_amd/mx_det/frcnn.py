@@ -133,19 +133,6 @@ class ResNet50Body(nn.Module):
         return out
 
 
-_helper_pool = None
-
-
-def _helper():
-    """One helper thread for host work issued beside a blocking graph launch (RegionProposalNetwork.
-    start_targets)."""
-    global _helper_pool
-    if _helper_pool is None:
-        import concurrent.futures
-        _helper_pool = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="mx_rpn_targets")
-    return _helper_pool
-
-
 def _aux_stream(device):
     """The RPN loss chain's side stream, one per device."""
     return mc.dedicated_stream(device, "rpn_targets")
@@ -598,17 +585,15 @@ class RegionProposalNetwork(nn.Module):
         counts = valid.sum(1).tolist()
         return [pb[i, :c] for i, c in enumerate(counts)], [ps[i, :c] for i, c in enumerate(counts)]
 
-    def forward(self, images, features, targets=None, be=None, head=None, defer_losses=False, early=None):
+    def forward(self, images, features, targets=None, be=None, head=None, defer_losses=False):
         """torchvision RegionProposalNetwork.forward -> (proposals, losses). defer_losses=True returns a
         callable in place of the losses dict: the caller issues the shape-independent target / sampler
         / loss launches later (FasterRCNN.forward: right after the RoI sampler's host sync, so the GPU
-        works on them while the host issues the RoI head instead of idling). early: the targets
-        already issued on the side stream by start_targets (FasterRCNN.forward, beside the trunk)."""
+        works on them while the host issues the RoI head instead of idling)."""
         feats = list(features.values())
         # objectness [N, A], pred_deltas [N, A, 4], anchors per level
         objectness, pred_deltas, num_per_level = head if head is not None else self.head(feats, be)
         grid = [(f.shape[1], f.shape[2]) for f in feats]
-        self.__dict__.setdefault("_grids", {})[tuple(images.tensors.shape)] = grid
         anchors = self.anchor_generator(images.tensors.shape[1:3], grid, feats[0].device, be)
         N = feats[0].shape[0]
         A = anchors.shape[0]
@@ -648,10 +633,7 @@ class RegionProposalNetwork(nn.Module):
             return loss_of(compute_targets()) if self.training else {}
 
         side = None
-        if early is not None:  # issued beside the trunk (start_targets); joined by join_losses()
-            tgt = early
-            losses = lambda: loss_of(tgt)  # noqa: E731
-        elif (self.training and not defer_losses and objectness.is_cuda and getattr(be, "name", "") == "hip"
+        if (self.training and not defer_losses and objectness.is_cuda and getattr(be, "name", "") == "hip"
                 and _side_streams("MX_RPN_LOSS_STREAM")):
             # the target / sampler chain (~25 small launches: anchor matching, the sampler's top-k) on a
             # side stream beside the proposal chain (decode, per-level top-k, NMS, selection): two
@@ -688,37 +670,6 @@ class RegionProposalNetwork(nn.Module):
             boxes, _ = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
         return boxes, losses  # the side stream is joined by join_losses(): after the RoI head
 
-    def start_targets(self, images, targets, be):
-        """The RPN's target / sampler chain issued by a helper thread on the side stream while the calling
-        thread replays the trunk's forward graph (FasterRCNN.forward): the chain needs only the anchors
-        and the ground truth, and hipGraphLaunch holds its thread for about the graph's GPU time (the
-        launch blocks on the full hardware queue), so issuing the chain's ~40 launches afterwards cost
-        ~0.8 ms of GPU idle per step (profiles/r05c). Same launches, same RNG draws in the same order
-        (nothing between them draws). Returns a future of the targets, or None when the trunk will not
-        replay a graph for this shape (first step of a shape: the grid sizes come from an earlier
-        step), on a non-HIP backend or with MX_RPN_TARGETS_THREAD=0. join_losses() waits for it."""
-        x = images.tensors
-        grid = self.__dict__.get("_grids", {}).get(tuple(x.shape))
-        if (grid is None or not self.training or not x.is_cuda or getattr(be, "name", "") != "hip"
-                or not hasattr(be, "match_assign_batched") or not _side_streams("MX_RPN_LOSS_STREAM")
-                or os.environ.get("MX_RPN_TARGETS_THREAD", "1") == "0" or torch.cuda.is_current_stream_capturing()):
-            return None
-        dev = x.device
-        anchors = self.anchor_generator(x.shape[1:3], grid, dev, be)
-        main = torch.cuda.current_stream(dev)
-        side = _aux_stream(dev)
-        side.wait_stream(main)  # the ground truth was resized on the main stream
-
-        def job():
-            with mc.capture_lock, torch.cuda.device(dev), torch.cuda.stream(side), torch.no_grad():
-                gt = _gt_batch(targets, dev)
-                return self.targets_of(anchors, gt, be), _gt_event(side)
-
-        fut = _helper().submit(job)
-        self._loss_side = side
-        self._tgt_future = fut
-        return fut
-
     def targets_of(self, anchors, gt, be):
         """assign_targets_to_anchors + fg_bg_sampler on the device: (labels [N, A], regression targets
         [N, A, 4], positive mask, negative mask) from the zero-padded GT batch gt = (boxes, labels,
@@ -729,18 +680,8 @@ class RegionProposalNetwork(nn.Module):
         pm, nm = self.fg_bg_sampler(lab, counts=lcnt)
         return lab, rt, pm, nm
 
-    def loss_of(self, objectness, pred_deltas, tgt, be):
-        """The RPN losses from targets_of's output (HIP: one fused launch each way)."""
-        lab, rt, pm, nm = tgt
-        lo, lb = be.rpn_loss(objectness, pred_deltas, lab, rt, pm, nm, 1.0 / 9)
-        return {"loss_objectness": lo, "loss_rpn_box_reg": lb}
-
     def join_losses(self):
-        """Make the current stream wait for the side-stream loss chain (a no-op without one); first the
-        helper thread's issue of it (start_targets), if any."""
-        fut = self.__dict__.pop("_tgt_future", None)
-        if fut is not None:
-            fut.result()
+        """Make the current stream wait for the side-stream loss chain (a no-op without one)."""
         side = self.__dict__.pop("_loss_side", None)
         if side is not None:
             torch.cuda.current_stream(side.device).wait_stream(side)
@@ -1184,20 +1125,13 @@ class FasterRCNN(nn.Module):
         # MX_RPN_DEFER_LOSSES=1 issues the RPN target / loss launches after the RoI sampler's host sync;
         # measured 0.5 % slower than issuing them while the trunk runs (A/B on one box), so off
         defer = os.environ.get("MX_RPN_DEFER_LOSSES", "0") != "0"
-        early = None
-        if (not defer and self.training and il.tensors.is_cuda
-                and self.__dict__.get("_mx_graphs", {}).get((tuple(il.tensors.shape), il.tensors.dtype)) is not None):
-            early = self.rpn.start_targets(il, targets, be)  # its launches beside the trunk's graph launch
         try:
             trunk = self._trunk(il.tensors, be)
             if trunk is not None:  # HIP-graph replay of backbone + FPN + RPN head (static shapes)
                 features, head = trunk
             else:
                 features, head = self.backbone(il.tensors, be), None
-            if early is not None:  # the helper thread issued the target chain during the trunk launch
-                early, self.rpn._gt_ready = self.rpn.__dict__.pop("_tgt_future").result()
-            proposals, rpn_losses = self.rpn(il, features, targets, be, head=head, defer_losses=defer,
-                                             early=early)
+            proposals, rpn_losses = self.rpn(il, features, targets, be, head=head, defer_losses=defer)
             if degenerate is not None:
                 host, ev = degenerate
                 ev.synchronize()
@@ -1379,9 +1313,10 @@ def _capture_trunk(model, be, x):
     if model.__dict__.get("_mx_seg_ready") is not None:  # data-parallel: per-segment gradient hand-off
         return _SegGraphs(model, be, x)
     if os.environ.get("MX_SEG_GRAPHS", "0") == "1":
-        # the segments' backwards in ONE graph, each segment's side wgrads deferred behind its dgrad
-        # chain so that they run beside the next segments (conv.defer_side_wgrads)
-        return _SegGraphs(model, be, x, one_graph=True)
+        # one backward graph per segment on one GPU too: the HIP graph executor submits a graph's node
+        # lists one after another, so a segment's side-stream wgrads start before the next segment's
+        # dgrad chain is submitted instead of after the whole trunk's (MX_WGRAD_FORK=early)
+        return _SegGraphs(model, be, x)
     trunk = _Trunk(model, be)
     return _Graphs(trunk, trunk.parameters(), model, x)
 
@@ -1401,7 +1336,7 @@ class _SegGraphs:
 
     SEGS = ("fpn+rpn_head", "layer4", "layer3", "layer2", "stem+layer1")
 
-    def __init__(self, model, be, x, one_graph=False):
+    def __init__(self, model, be, x):
         self.model, self.be = model, be
         body = model.backbone.body
         self.seg_params = {"stem+layer1": list(body.conv1.parameters()) + list(body.bn1.parameters()) +
@@ -1434,44 +1369,12 @@ class _SegGraphs:
             outs, self.leaves, self.cs = self._fwd(self.static_x)
         self.static_gout = [torch.zeros_like(o) for o in outs]
         r0, g0 = _absorb_roots(self.model.rpn.head, outs, self.static_gout)
-        # [(segment keys, backward graph)] in replay order; one_graph (single GPU, no hand-off hooks):
-        # every segment in one graph, each segment's side-stream wgrads collected while its backward is
-        # captured (conv.defer_side_wgrads) and launched right after its dgrad chain on a stream of the
-        # segment's own. The HIP graph executor cuts a graph into in-order node lists along first
-        # dependents and submits them one after another: segment k's wgrads are the first dependents of
-        # its last dgrad-chain node, so they extend segment k's list and run beside segment k+1's chain
-        # (the next list) -- instead of one side list submitted after the whole trunk's dgrad chain
-        # (MX_WGRAD_DEFER=0: the in-graph early fork of conv._wgrad_plan).
-        self.bwd, self.jobs = [], []
-        plan = self._bwd_plan(outs, self.static_gout, self.leaves, self.cs, (r0, g0))
-        if one_graph:
-            defer = os.environ.get("MX_WGRAD_DEFER", "1") != "0"
-            forks = []
+        self.bwd = []  # (segment key, graph)
+        for key, roots, groots in self._bwd_plan(outs, self.static_gout, self.leaves, self.cs, (r0, g0)):
             g = torch.cuda.CUDAGraph()
             with mc.capture_guard(), torch.cuda.graph(g, pool=pool, stream=side):
-                for key, roots, groots in plan:
-                    jobs = []
-                    with mc.defer_side_wgrads(jobs if defer else None):
-                        torch.autograd.backward(roots, groots())
-                    if jobs:
-                        ws = mc.dedicated_stream(x.device, "wgrad_seg%d" % len(forks))
-                        ws.wait_stream(side)
-                        with torch.cuda.stream(ws):
-                            for j in jobs:
-                                mc.wgrad_launch_deferred(j)
-                        forks.append(ws)
-                        # operands and workspaces stay referenced: no later allocation of this capture
-                        # (or of a later graph in the pool) may reuse them while the wgrads run
-                        self.jobs.extend(jobs)
-                for ws in forks:
-                    side.wait_stream(ws)
-            self.bwd.append((tuple(k for k, _, _ in plan), g))
-        else:
-            for key, roots, groots in plan:
-                g = torch.cuda.CUDAGraph()
-                with mc.capture_guard(), torch.cuda.graph(g, pool=pool, stream=side):
-                    torch.autograd.backward(roots, groots())
-                self.bwd.append(((key,), g))
+                torch.autograd.backward(roots, groots())
+            self.bwd.append((key, g))
         self.static_out = tuple(o.detach() for o in outs)
         self.static_grads = {k: [p.grad for p in v] for k, v in self.seg_params.items()}
         # the boundary-leaf gradients pass between the backward graphs: keep them referenced
@@ -1532,25 +1435,23 @@ class _SegGraphFn(torch.autograd.Function):
     def backward(ctx, *gouts):
         tg = ctx.tg
         _load_gouts(tg, gouts)
-        for keys, _ in tg.bwd:  # see _GraphFn.backward
-            for key in keys:
-                for p, g in zip(tg.seg_params[key], tg.static_grads[key]):
-                    if g is not None and p.grad is g:
-                        p.grad = g.clone()
+        for key, _ in tg.bwd:  # see _GraphFn.backward
+            for p, g in zip(tg.seg_params[key], tg.static_grads[key]):
+                if g is not None and p.grad is g:
+                    p.grad = g.clone()
         hook = tg.model.__dict__.get("_mx_seg_ready")
-        for keys, graph in tg.bwd:
+        for key, graph in tg.bwd:
             graph.replay()
-            for key in keys:
-                ps, gs = tg.seg_params[key], tg.static_grads[key]
-                for p, g in zip(ps, gs):
-                    if g is None:
-                        continue
-                    if p.grad is None:
-                        p.grad = g
-                    else:
-                        p.grad.add_(g)
-                if hook is not None and ps:
-                    hook(key, ps)
+            ps, gs = tg.seg_params[key], tg.static_grads[key]
+            for p, g in zip(ps, gs):
+                if g is None:
+                    continue
+                if p.grad is None:
+                    p.grad = g
+                else:
+                    p.grad.add_(g)
+            if hook is not None and ps:
+                hook(key, ps)
         return None, None, None
 
 

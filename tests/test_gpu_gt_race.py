@@ -4,9 +4,7 @@ the main stream. FasterRCNN.forward makes the main stream wait for the batch's e
 RoI heads (frcnn.py, `_gt_ready`). Here the side stream is held back by a ~10 ms spin kernel issued
 in front of the batch's construction: with the wait in place the RoI sample, the losses and every
 trainable gradient stay bitwise equal to the undelayed step; without it the main stream would read
-the batch before it is written (zero-filled or stale slots and counts). Both issue forms are covered:
-the chain issued after the trunk on the calling thread (MX_RPN_TARGETS_THREAD=0) and by the helper
-thread during the trunk's graph launch (=1)."""
+the batch before it is written (zero-filled or stale slots and counts)."""
 import pytest
 import torch
 
@@ -24,10 +22,9 @@ def _model(dev):
     return m.to(dev).train()
 
 
-def _run(dev, monkeypatch, thread, delay):
+def _run(dev, monkeypatch, delay):
     from mx_det import frcnn
     from mx_det.data import synth_batch
-    monkeypatch.setenv("MX_RPN_TARGETS_THREAD", thread)
     orig = frcnn._gt_batch
     main = torch.cuda.current_stream(dev)
     delayed = []
@@ -47,7 +44,7 @@ def _run(dev, monkeypatch, thread, delay):
     imgs, tg = synth_batch(17, 6, H=448, W=640, device=dev)
     out = []
     try:
-        for step in range(3):  # capture, then replays (the helper thread needs a replayed trunk)
+        for step in range(3):  # capture, then graph replays
             torch.cuda.manual_seed(200 + step)
             losses = m(imgs[2 * step:2 * step + 2], tg[2 * step:2 * step + 2])
             for p in m.parameters():
@@ -62,10 +59,9 @@ def _run(dev, monkeypatch, thread, delay):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("thread", ["0", "1"])
-def test_gt_batch_side_stream_delay_is_waited_for(dev, monkeypatch, thread):
-    ref, n0 = _run(dev, monkeypatch, thread, False)
-    got, n1 = _run(dev, monkeypatch, thread, True)
+def test_gt_batch_side_stream_delay_is_waited_for(dev, monkeypatch):
+    ref, n0 = _run(dev, monkeypatch, False)
+    got, n1 = _run(dev, monkeypatch, True)
     assert n0 == 0 and n1 >= 3, (n0, n1)  # every step's batch was built behind the spin
     for step, ((la, ga), (lb, gb)) in enumerate(zip(got, ref)):
         assert la == lb, (step, la, lb)

@@ -424,54 +424,3 @@ def test_x3_dgrad_residual_stride2(dev, k, st, pd, tile, monkeypatch):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
     finally:
         call("mx_conv_set_tile", 0, 0)
-
-
-@pytest.mark.timeout(300)
-def test_x3_tail_split(dev, monkeypatch):
-    """Split-K tail (mx_conv_set_tail, on by default): the P2 3x3 forward (2,100 tiles on 512 slots:
-    the last 52 tiles split K 8 ways, finished by the reduce kernel) and its dgrad with a residual and
-    BN-backward partials, against the same launches with the tail off. The unsplit tiles' rows (below
-    m_base) and their BatchNorm statistics / partial rows are bitwise equal; the tail's rows differ
-    only by the split summation order (1e-6 relative); both stay at the x3 bar against float64."""
-    import ctypes
-    from mx_det import _lib, conv as mc
-    from mx_det._lib import call
-    monkeypatch.setenv("MX_CONV_TUNE", "0")  # the library's default tile for both runs
-    out = (ctypes.c_int64 * 7)()
-    N, H, W, C, K = 2, 200, 336, 256, 256
-    assert _lib.load().mx_conv_x3_geometry(N * H * W, K, 9 * C, out) == 0
-    m_base, splits = out[5], out[6]
-    assert splits > 1 and 0 < m_base < N * H * W, list(out)
-    g = torch.Generator().manual_seed(11)
-    x = torch.randn(N, H, W, C, generator=g)
-    w = torch.randn(K, C, 3, 3, generator=g) * 0.05
-    b = torch.randn(K, generator=g)
-    dy = torch.randn(N, H, W, K, generator=g)
-    res = torch.randn(N, H, W, C, generator=g)
-    z = torch.randn(N, H, W, C, generator=g) * 2 + 0.3
-    mean = z.reshape(-1, C).mean(0)
-    invstd = 1.0 / torch.sqrt(z.reshape(-1, C).var(0, unbiased=False) + 1e-5)
-    y = F.relu(z * 0.7 + 0.1)
-    wk, wt = mc.pack_weight(w.to(dev), C, (1, 1), (1, 1), dgrad=True, split=True)
-
-    def run():
-        yy, st = mc.conv_fwd(x.to(dev), wk, (1, 1), (1, 1), bias=b.to(dev), stats=True)
-        link = mc.BNBLink()
-        link.y, link.z, link.mean, link.invstd, link.act = y.to(dev), z.to(dev), mean.to(dev), invstd.to(dev), 1
-        dx = mc.conv_dgrad(dy.to(dev), wt, (N, H, W, C), 3, 3, (1, 1), (1, 1), residual=res.to(dev), bnb=link)
-        torch.cuda.synchronize()
-        return yy.reshape(-1, K).cpu(), st.cpu(), dx.reshape(-1, C).cpu(), link.part.cpu()
-
-    y1, s1, d1, p1 = run()
-    call("mx_conv_set_tail", 0)
-    try:
-        y0, s0, d0, p0 = run()
-    finally:
-        call("mx_conv_set_tail", 1)
-    r = m_base // 64  # 64-row statistics rows below the tail
-    assert torch.equal(y1[:m_base], y0[:m_base]) and torch.equal(d1[:m_base], d0[:m_base])
-    assert torch.equal(s1[:, :r], s0[:, :r]) and torch.equal(p1[:, :r], p0[:, :r])
-    assert rel(y1[m_base:], y0[m_base:]) < 1e-6 and rel(d1[m_base:], d0[m_base:]) < 1e-6
-    assert rel(s1[:, r:], s0[:, r:]) < 1e-5 and rel(p1[:, r:], p0[:, r:]) < 1e-5
-    ref = F.conv2d(x.permute(0, 3, 1, 2).double(), w.double(), b.double(), 1, 1).permute(0, 2, 3, 1).reshape(-1, K)
-    assert rel(y1, ref) < 1e-5
