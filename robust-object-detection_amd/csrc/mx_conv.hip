@@ -1888,6 +1888,11 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
 // into hi / lo while staged (register loads, 32-pixel K-tiles, pixel-major bf16 LDS tiles with the
 // swz_w swizzle), fragments read transposed with ds_read_b64_tr_b16 as in conv_wgrad_buf_kernel;
 // 128 x 128 (k, col) block tiles, the pixel axis split into slab partials (wgrad_reduce_kernel).
+// IL (mx_conv_set_wgrad_variant(6)): the next K-tile's hi / lo split and LDS stores are interleaved with
+// the second half of this K-tile's MFMAs (sched_group_barrier) instead of following all of them; the
+// loads and stores are unconditional (past the split they read zeros into the unused buffer), so the
+// loop body is one basic block the scheduler can interleave.
+template <bool IL>
 __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
 #if defined(__HIP_DEVICE_COMPILE__)
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2001,7 +2006,7 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
   __syncthreads();
   for (int64_t it = 0; it < nk; ++it) {
     const int buf = (int)(it & 1);
-    if (it + 1 < nk) load();
+    if (IL || it + 1 < nk) load();
     const char* Dh = smem + buf * STAGE;
     bf16x8 ah[4], al[4], bh[4], bl[4];
 #pragma unroll
@@ -2022,7 +2027,170 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_x3_kernel(WgP p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
       }
-    if (it + 1 < nk) store(buf ^ 1);
+    if (IL) {
+      store(buf ^ 1);
+      // schedule of one K-tile: the next tile's 8 loads, the 32 fragment reads beside the first 12
+      // MFMAs, then the remaining 36 MFMAs each with ~3 of the split VALU and every third with one of
+      // the 8 LDS stores
+      __builtin_amdgcn_sched_group_barrier(0x020, 8, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+      for (int q = 0; q < 12; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 36; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        if (q % 3 == 2) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      }
+    } else if (it + 1 < nk) {
+      store(buf ^ 1);
+    }
+    __syncthreads();
+  }
+  wgrad_store(p, acc, k0, c0, wm, wn, lane, split);
+#endif
+}
+
+// Pre-split operand planes for conv_wgrad_x3d_kernel: f32 src[n] -> bf16 hi[n], lo[n] (split8, the same
+// hi / lo values the register-staged kernels make). 8 elements per thread; n % 8 == 0.
+__global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ src, int64_t n8,
+                                                           uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const float4 a = ((const float4*)src)[2 * i], b = ((const float4*)src)[2 * i + 1];
+  uint4 h, l;
+  split8(a, b, h, l);
+  ((uint4*)hi)[i] = h;
+  ((uint4*)lo)[i] = l;
+}
+
+// bf16x3 wgrad on pre-split operands (mx_conv_set_wgrad_variant(7)): dy and x arrive as bf16 hi / lo
+// planes (split_planes_kernel), so each K-tile's four LDS planes [32 px][128] (dy hi, dy lo, x hi, x
+// lo; 256-B rows, swz_w swizzle) are filled by LDS-DMA (buffer_load_dwordx4 ... lds: no register
+// staging, no split VALU, no ds_write) one K-tile ahead of the MFMAs; fragments, MFMA order and the
+// epilogue are those of conv_wgrad_x3_kernel, so the result is bitwise the same. Wave w fills rows
+// [8w, 8w + 8) of every plane, 4 rows per DMA instruction; the swizzle is applied on the source chunk.
+// p.dy / p.x: the hi planes; the lo planes follow at +P*K / +N*H*W*C elements.
+__global__ void __launch_bounds__(NT, 2) conv_wgrad_x3d_kernel(WgP p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int PXT = 32, OPB = PXT * 256, STAGE = 4 * OPB;  // planes: dy hi, dy lo, x hi, x lo
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t ntn = (p.Ncol + 127) / 128;
+  const int64_t ntiles = ((p.K + 127) / 128) * ntn;
+  const int64_t work = xcd_remap(blockIdx.x, (int64_t)gridDim.x);
+  const int64_t split = work / ntiles, tile = work % ntiles;
+  const int64_t mt = tile / ntn, nt = tile % ntn;
+  const int64_t k0 = mt * 128, c0 = nt * 128;
+  const int64_t pbeg = split * p.kchunk;
+  const int64_t pend = min<int64_t>(p.P, pbeg + p.kchunk);
+  if (pbeg >= pend) return;
+  const int64_t dyel = p.P * p.K, xel = p.N * p.H * p.W * p.C;
+  const i32x4 dyh = dma_rsrc(p.dy, (uint32_t)(dyel * 2)), dyl = dma_rsrc(p.dy + dyel, (uint32_t)(dyel * 2));
+  const i32x4 xh = dma_rsrc(p.x, (uint32_t)(xel * 2)), xl = dma_rsrc(p.x + xel, (uint32_t)(xel * 2));
+  const int OW = (int)p.OW, OH = (int)p.OH, H = (int)p.H, W = (int)p.W, C = (int)p.C;
+  // this lane's two landing rows (j = 0, 1) and the logical chunk its 16 B come from
+  const int dw = PXT % OW, dh = (PXT / OW) % OH, dn = PXT / (OW * OH);
+  int px_n[2], px_oh[2], px_ow[2], px_i[2], ihb[2], iwb[2], xcol[2];
+  uint32_t dcol[2];
+  bool kok[2], cok[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = wave * 8 + j * 4 + (lane >> 4);
+    const int lc = swz_w(row, lane & 15);
+    const int64_t pi = pbeg + row;
+    px_i[j] = (int)pi;
+    const int64_t t = pi / OW;
+    px_ow[j] = (int)(pi - t * OW);
+    px_oh[j] = (int)(t % OH);
+    px_n[j] = (int)(t / OH);
+    kok[j] = k0 + lc * 8 < p.K;
+    dcol[j] = (uint32_t)(k0 + lc * 8) * 2u;
+    const int64_t col = c0 + lc * 8;
+    cok[j] = col < p.Ncol;
+    const int tap = cok[j] ? (int)(col / C) : 0;
+    xcol[j] = cok[j] ? (int)(col - (int64_t)tap * C) : 0;
+    const int r = tap / p.S, sq = tap - (tap / p.S) * p.S;
+    ihb[j] = -p.pad_h + r;
+    iwb[j] = -p.pad_w + sq;
+  }
+  const int pend32 = (int)pend;
+  const uint32_t lds0 = lds_addr(smem);
+  auto issue = [&](int buf) {
+    const uint32_t D = lds0 + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool pok = px_i[j] < pend32;
+      const uint32_t od = (pok && kok[j]) ? __umul24((uint32_t)px_i[j], (uint32_t)(p.K * 2)) + dcol[j] : kOOB;
+      const int ih = __mul24(px_oh[j], p.st_h) + ihb[j], iw = __mul24(px_ow[j], p.st_w) + iwb[j];
+      const bool xok = pok && cok[j] && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const uint32_t ox = xok ? (uint32_t)__mul24(__mul24(px_n[j], H) + ih, W) + (uint32_t)iw : 0u;
+      const uint32_t oxb = xok ? __umul24(ox, (uint32_t)(C * 2)) + (uint32_t)xcol[j] * 2u : kOOB;
+      const uint32_t dst = D + (wave * 8 + j * 4) * 256;
+      lds_dma16(dyh, dst, od, 0u);
+      lds_dma16(dyl, dst + OPB, od, 0u);
+      lds_dma16(xh, dst + 2 * OPB, oxb, 0u);
+      lds_dma16(xl, dst + 3 * OPB, oxb, 0u);
+      px_i[j] += PXT;
+      int ow = px_ow[j] + dw;
+      const int c1 = ow >= OW ? 1 : 0;
+      ow -= c1 * OW;
+      int oh = px_oh[j] + dh + c1;
+      const int c2 = oh >= OH ? 1 : 0;
+      oh -= c2 * OH;
+      px_ow[j] = ow;
+      px_oh[j] = oh;
+      px_n[j] += dn + c2;
+    }
+  };
+  auto tr_read = [&](const char* T, int prow0, int colbase) -> s16x4 {
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int row = prow0 + 8 * g + q;
+    const int colx = colbase + 4 * pp;
+    const int chunk = colx >> 3, within = (colx & 7) * 2;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(T + row * 256 + (swz_w(row, chunk) << 4) + within));
+  };
+  auto frag = [&](const char* T, int colbase) -> bf16x8 {
+    const s16x4 lo = tr_read(T, 0, colbase), hi = tr_read(T, 4, colbase);
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nk = (pend - pbeg + PXT - 1) / PXT;
+  issue(0);
+  wait_vmcnt<0>();
+  __syncthreads();
+  for (int64_t it = 0; it < nk; ++it) {
+    const int buf = (int)(it & 1);
+    issue(buf ^ 1);  // the next K-tile (rows past the split read zeros; the last one lands unused)
+    const char* Dh = smem + buf * STAGE;
+    bf16x8 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ah[i] = frag(Dh, wm * 64 + i * 16);
+      al[i] = frag(Dh + OPB, wm * 64 + i * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bh[j] = frag(Dh + 2 * OPB, wn * 64 + j * 16);
+      bl[j] = frag(Dh + 3 * OPB, wn * 64 + j * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+    wait_vmcnt<0>();  // this wave's DMA of the next K-tile has landed; the barrier publishes everyone's
     __syncthreads();
   }
   wgrad_store(p, acc, k0, c0, wm, wn, lane, split);
@@ -3216,8 +3384,10 @@ extern "C" int mx_conv_get_variant(void) { return g_conv_variant; }
 // 3 (default) buffer descriptors (conv_wgrad_buf_kernel; maps under 32 output pixels take 0)
 static int g_wgrad_variant = 3;
 extern "C" int mx_conv_set_wgrad_variant(int v) {
-  MX_CHECK_ARG(v >= 0 && v <= 5, "mx_conv_set_wgrad_variant: 0 px32, 1 px64, 2 direct-to-LDS, 3 buffer descriptors, "
-                                "4 = 3 for bf16 / the 128 x 256 wide block for bf16x3");
+  MX_CHECK_ARG(v >= 0 && v <= 7, "mx_conv_set_wgrad_variant: 0 px32, 1 px64, 2 direct-to-LDS, 3 buffer descriptors, "
+                                "4 = 3 for bf16 / the 128 x 256 wide block for bf16x3, 5 the 256 x 256 bf16x3 block, "
+                                "6 = 3 for bf16 / the interleaved-schedule bf16x3 kernel, 7 = 3 for bf16 / the bf16x3 "
+                                "kernel on pre-split operand planes (LDS-DMA)");
   g_wgrad_variant = v;
   return MX_OK;
 }
@@ -3800,13 +3970,22 @@ static WGeo wgrad_geo_x3(const mx_conv_shape* s) {
   return g;
 }
 
+// variant 7 (conv_wgrad_x3d_kernel): bf16 hi / lo planes of dy and x after the split slab
+static int wgrad_x3_dma() { return g_wgrad_variant == 7; }
+static size_t wgrad_x3_slab(const mx_conv_shape* sd, const WGeo& g) {
+  return g.splits > 1 ? (sizeof(float) * (size_t)g.splits * sd->K * sd->R * sd->S * sd->C + 255) / 256 * 256 : 0;
+}
+static size_t wgrad_x3_planes(const mx_conv_shape* sd) {
+  return 2 * sizeof(uint16_t) * (size_t)(sd->N * sd->Ho * sd->Wo * sd->K + sd->N * sd->H * sd->W * sd->C);
+}
+
 extern "C" size_t mx_conv_workspace_x3(const mx_conv_shape* s, int pass) {
   if (!s || pass < 0 || pass > 2) return 0;
   if (pass == 2) {
     bool dense;
     const mx_conv_shape sd = wgrad_shape(s, &dense);
     const WGeo g = wgrad_geo_x3(&sd);
-    return g.splits > 1 ? sizeof(float) * (size_t)g.splits * sd.K * sd.R * sd.S * sd.C : 0;
+    return wgrad_x3_slab(&sd, g) + (wgrad_x3_dma() ? wgrad_x3_planes(&sd) : 0);
   }
   if (pass == 0) {
     const Geo g = make_geo_x3(s->N * s->Ho * s->Wo, s->K, s->R * s->S * s->C);
@@ -3907,11 +4086,23 @@ extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const
   p.dC = dC; p.dRS = dRS;
   const WGeo g = wgrad_geo_x3(s);
   p.kchunk = g.kchunk;
-  if (g.splits > 1) {
-    const size_t need = sizeof(float) * (size_t)g.splits * p.K * p.Ncol;
-    MX_CHECK_ARG(ws && ws_bytes >= need, "conv wgrad x3: split workspace of %zu bytes required (mx_conv_workspace_x3)",
+  const bool dma = wgrad_x3_dma();
+  const size_t slab = wgrad_x3_slab(s, g), need = slab + (dma ? wgrad_x3_planes(s) : 0);
+  if (need) {
+    MX_CHECK_ARG(ws && ws_bytes >= need, "conv wgrad x3: workspace of %zu bytes required (mx_conv_workspace_x3)",
                  need);
-    p.slab = (float*)ws;
+  }
+  if (g.splits > 1) p.slab = (float*)ws;
+  if (dma) {  // the operands as bf16 hi / lo planes, read by LDS-DMA
+    const int64_t dyel = p.P * p.K, xel = p.N * p.H * p.W * p.C;
+    uint16_t* dyp = (uint16_t*)((char*)ws + slab);
+    uint16_t* xp = dyp + 2 * dyel;
+    split_planes_kernel<<<(unsigned)cdiv(dyel / 8, 256), 256, 0, st>>>(dy, dyel / 8, dyp, dyp + dyel);
+    MX_LAUNCH_CHECK();
+    split_planes_kernel<<<(unsigned)cdiv(xel / 8, 256), 256, 0, st>>>(x, xel / 8, xp, xp + xel);
+    MX_LAUNCH_CHECK();
+    p.dy = dyp;
+    p.x = xp;
   }
   MX_CHECK_ARG(g.tiles * g.splits < (1ll << 31), "conv wgrad x3: grid too large");
   MX_CHECK_ARG(p.P * p.K * 4 < (1ll << 31) && p.N * p.H * p.W * p.C * 4 < (1ll << 31) && p.P + 64 < (1ll << 23) &&
@@ -3921,8 +4112,12 @@ extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const
     conv_wgrad_x3ww_kernel<<<(unsigned)(g.tiles * g.splits), 256, 2 * 8 * 32 * 256, st>>>(p);
   else if (wgrad_x3_wide())
     conv_wgrad_x3w_kernel<<<(unsigned)(g.tiles * g.splits), 512, 2 * 6 * 32 * 256, st>>>(p);
+  else if (dma)
+    conv_wgrad_x3d_kernel<<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);
+  else if (g_wgrad_variant == 6)
+    conv_wgrad_x3_kernel<true><<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);
   else
-    conv_wgrad_x3_kernel<<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);
+    conv_wgrad_x3_kernel<false><<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);
   MX_LAUNCH_CHECK();
   if (g.splits > 1) {
     MX_CHECK_ARG(Kout < 65536, "conv wgrad x3: too many output channels for the split reduce");

@@ -387,11 +387,13 @@ def test_x3_bottleneck_bn_partials_from_dgrad_epilogue(dev, monkeypatch):
             assert rel(res["1"][1][n], res["0"][1][n]) < 1e-4, n
 
 
-@pytest.mark.parametrize("variant", [4, 5])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7])
 @pytest.mark.parametrize("case", [CASES[i] for i in (0, 2, 4, 7, 8, 9, 11)])
 def test_x3_wgrad_wide_tiles(dev, monkeypatch, variant, case):
-    """The wide wgrad tiles forced for every shape (4: 128 x 256 at 8 waves; 5: 256 x 256 at one wave
-    per SIMD, accumulators in AGPRs): K / column counts below or not a multiple of the tile, split and
+    """The wgrad kernel variants forced for every shape (4: 128 x 256 at 8 waves; 5: 256 x 256 at one
+    wave per SIMD, accumulators in AGPRs; 6: the 128 x 128 kernel with the interleaved schedule and
+    unconditional loads / stores; 7: the 128 x 128 kernel fed by LDS-DMA from pre-split hi / lo
+    planes): K / column counts below or not a multiple of the tile, split and
     unsplit pixel axes, strided gathers -- the same bar as the default kernel."""
     from mx_det._lib import call
     monkeypatch.setenv("MX_CONV_TUNE", "0")
@@ -424,3 +426,27 @@ def test_x3_dgrad_residual_stride2(dev, k, st, pd, tile, monkeypatch):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
     finally:
         call("mx_conv_set_tile", 0, 0)
+
+
+@pytest.mark.parametrize("case", [CASES[i] for i in (0, 1, 2, 4, 7, 8, 9, 11)] + [HEADLINE[0], HEADLINE[1]])
+def test_x3_wgrad_presplit_is_bitwise_default(dev, monkeypatch, case):
+    """The LDS-DMA wgrad on pre-split operand planes (variant 7) makes the same hi / lo values
+    (split_planes_kernel = the staging kernel's split8), the same fragments and the same MFMA order as
+    the register-staged kernel (3): dW is bitwise equal, split pixel axes and strided gathers included."""
+    from mx_det import conv as mc
+    from mx_det._lib import call
+    monkeypatch.setenv("MX_CONV_TUNE", "0")
+    N, H, W, C, K, k, st, pd = case
+    g = torch.Generator().manual_seed(3 + C + K)
+    x = torch.randn(N, H, W, C, generator=g).to(dev)
+    Ho, Wo = mc.out_hw(H, W, k, k, (st, st), (pd, pd))
+    dy = torch.randn(N, Ho, Wo, K, generator=g).to(dev)
+    out = {}
+    for v in (3, 7):
+        call("mx_conv_set_wgrad_variant", v)
+        try:
+            out[v] = mc.conv_wgrad(dy, x, K, k, k, (st, st), (pd, pd))
+            torch.cuda.synchronize()
+        finally:
+            call("mx_conv_set_wgrad_variant", 3)
+    assert torch.equal(out[3], out[7])
