@@ -129,7 +129,11 @@ _FD_CANDS_X3 = ((0, 0, 0, 0), (0, 0, 1, 0), (0, 0, 2, 0), (64, 128, 0, 0), (128,
                 (0, 0, 0, 5), (64, 64, 0, 5))
 if __import__("os").environ.get("MX_X3_ALTW", "1") == "0":  # A/B switch for the newest candidate
     _FD_CANDS_X3 = tuple(c for c in _FD_CANDS_X3 if c[3] != 5)
-_WG_CANDS_X3 = ((3, 0), (3, 256), (3, 768), (3, 1024), (4, 0), (4, 512), (5, 0), (5, 512))
+# wgrad variant 7: LDS-DMA on pre-split hi / lo planes (19 % faster kernel on the P2 3x3, but the split
+# pass costs ~70 us there: wins only on the largest shapes)
+_WG_CANDS_X3 = ((3, 0), (3, 256), (3, 768), (3, 1024), (4, 0), (4, 512), (5, 0), (5, 512), (7, 0))
+if __import__("os").environ.get("MX_X3_DMAW", "1") == "0":  # A/B switch for the newest candidate
+    _WG_CANDS_X3 = tuple(c for c in _WG_CANDS_X3 if c[0] != 7)
 _tune_cache = {}
 
 

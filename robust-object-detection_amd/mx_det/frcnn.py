@@ -1323,18 +1323,25 @@ def _capture_trunk(model, be, x):
 
 class _SegGraphs:
     """The trunk (backbone + FPN + RPN head) as ONE forward graph and a chain of backward graphs, one
-    per segment in backward order: FPN + RPN head, layer4, layer3, layer2, stem + layer1. The forward
-    detaches each layer output into a leaf that both the next layer and the FPN consume; each
-    backward graph back-propagates one segment from its output leaf's gradient (written by the graphs
-    replayed before it), so when a segment's graph has been issued its parameters' gradients are
-    final and `model._mx_seg_ready(key, params, grads)` can start their all-reduce on RCCL's stream
-    while the remaining segments' backward graphs run (mx_det.dp.DataParallel; SURVEY.md §8e: bucketed
-    all-reduce overlapped with the backward). Same kernels as the one-graph trunk; the only change is
-    that the gradient reaching a layer output is summed over its consumers (FPN lateral, next layer)
-    in a different order. Buffers and captures follow _Graphs (shared private pool, replays in capture
-    order)."""
+    per segment in backward order, so that when a segment's graph has been issued its parameters'
+    gradients are final and `model._mx_seg_ready(key, params)` can start their all-reduce on RCCL's
+    stream while the remaining segments' backward graphs run (mx_det.dp.DataParallel; SURVEY.md §8e:
+    bucketed all-reduce overlapped with the backward).
 
-    SEGS = ("fpn+rpn_head", "layer4", "layer3", "layer2", "stem+layer1")
+    Segment boundaries sit at stage outputs C2..C5 (MX_DP_BOUNDS, digits 2-5; default "23"): at a
+    boundary the forward detaches the stage output into a leaf that the next stage and the FPN lateral
+    both consume, and the segment below it back-propagates from that leaf's gradient (written by the
+    graphs replayed before it). Without a boundary the next stage and the FPN consume the output
+    itself and the backward flows through in one autograd pass. "2345" gives five segments (FPN + RPN
+    head, layer4, layer3, layer2, stem + layer1); "23" gives FPN + RPN head + layer4 + layer3 (106 MB
+    of gradients, all-reduced while layer2's backward runs), layer2, stem + layer1. Every boundary
+    costs a join: a segment's graph completes with its side-stream weight gradients, and the next
+    segment's dgrad chain waits for them (one-GPU A/B: profiles/r06_ab.txt). Same kernels as the
+    one-graph trunk; at a boundary the gradient reaching the stage output is summed over its consumers
+    in a different order. Buffers and captures follow _Graphs (shared private pool, replays in
+    capture order)."""
+
+    LAYER_KEYS = ("stem+layer1", "layer2", "layer3", "layer4")  # producers of C2, C3, C4, C5
 
     def __init__(self, model, be, x):
         self.model, self.be = model, be
@@ -1345,10 +1352,14 @@ class _SegGraphs:
                            "layer4": list(body.layer4.parameters()),
                            "fpn+rpn_head": list(model.backbone.fpn.parameters()) + list(model.rpn.head.parameters())}
         self.seg_params = {k: [p for p in v if p.requires_grad] for k, v in self.seg_params.items()}
-        # leaf k (C2..C5) needs a gradient iff some segment upstream of it trains
-        up = ["stem+layer1", "layer2", "layer3", "layer4"]
+        spec = os.environ.get("MX_DP_BOUNDS", "23")
+        if not spec or any(c not in "2345" for c in spec):
+            raise ValueError(f"MX_DP_BOUNDS={spec!r}: digits 2-5 (stage outputs C2..C5 that end a segment)")
+        self.bounds = {int(c) - 2 for c in spec}  # leaf index k <-> C(k+2)
+        # C(k+2) needs a gradient iff some stage below it trains
+        up = list(self.LAYER_KEYS)
         self.need = [any(self.seg_params[u] for u in up[:k + 1]) for k in range(4)]
-        self.params = [p for k in self.SEGS for p in self.seg_params[k]]
+        self.params = [p for k in ("fpn+rpn_head",) + self.LAYER_KEYS for p in self.seg_params[k]]
         saved = {k: v.clone() for k, v in model.state_dict().items()
                  if k.endswith(("running_mean", "running_var", "num_batches_tracked"))}
         grads = [p.grad for p in self.params]
@@ -1357,29 +1368,29 @@ class _SegGraphs:
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(2):
-                outs, leaves, cs = self._fwd(self.static_x)
-                self._bwd_all(outs, [torch.ones_like(o) for o in outs], leaves, cs)
-                del outs, leaves, cs
+                outs, ins, cs = self._fwd(self.static_x)
+                self._bwd_all(outs, [torch.ones_like(o) for o in outs], ins, cs)
+                del outs, ins, cs
                 for p in self.params:
                     p.grad = None
         torch.cuda.current_stream().wait_stream(side)
         pool = torch.cuda.graph_pool_handle()
         self.fwd = torch.cuda.CUDAGraph()
         with mc.capture_guard(), torch.cuda.graph(self.fwd, pool=pool, stream=side), mc.absorb_mode():
-            outs, self.leaves, self.cs = self._fwd(self.static_x)
+            outs, self.ins, self.cs = self._fwd(self.static_x)
         self.static_gout = [torch.zeros_like(o) for o in outs]
         r0, g0 = _absorb_roots(self.model.rpn.head, outs, self.static_gout)
-        self.bwd = []  # (segment key, graph)
-        for key, roots, groots in self._bwd_plan(outs, self.static_gout, self.leaves, self.cs, (r0, g0)):
+        self.bwd = []  # (segment keys, graph)
+        for keys, roots, groots in self._bwd_plan(outs, self.static_gout, self.ins, self.cs, (r0, g0)):
             g = torch.cuda.CUDAGraph()
             with mc.capture_guard(), torch.cuda.graph(g, pool=pool, stream=side):
                 torch.autograd.backward(roots, groots())
-            self.bwd.append((key, g))
+            self.bwd.append((keys, g))
         self.static_out = tuple(o.detach() for o in outs)
         self.static_grads = {k: [p.grad for p in v] for k, v in self.seg_params.items()}
         # the boundary-leaf gradients pass between the backward graphs: keep them referenced
-        self.keep = [l.grad for l in self.leaves] + [o for o in outs]
-        self.leaves, self.cs = None, None
+        self.keep = [self.ins[k].grad for k in sorted(self.bounds)] + [o for o in outs]
+        self.ins, self.cs = None, None
         for p, g in zip(self.params, grads):
             p.grad = g
         with torch.no_grad():
@@ -1390,33 +1401,43 @@ class _SegGraphs:
         self.on_ready = None
 
     def _fwd(self, x):
+        """-> (trunk outputs, ins, cs): cs[k] = C(k+2) as produced, ins[k] = what the next stage and the
+        FPN lateral consume (a detached leaf at a boundary, else cs[k] itself)."""
         body, be = self.model.backbone.body, self.be
         c = body.run_layer("layer1", body.stem(x, be), be)
-        leaves, cs = [], [c]
-        for k, name in enumerate(("layer2", "layer3", "layer4")):
-            leaf = c.detach().requires_grad_(self.need[k])
-            if k > 0 and self.need[k] and mc.absorbing():
-                mc.chain_over(leaf)  # C3 / C4 leaves: next stage's conv1 + downsample and the FPN lateral
-            leaves.append(leaf)
-            c = body.run_layer(name, leaf, be)
-            cs.append(c)
-        leaves.append(c.detach().requires_grad_(self.need[3]))
-        feats = self.model.backbone.fpn(OrderedDict((str(i), l) for i, l in enumerate(leaves)), be)
-        return tuple(feats.values()) + tuple(self.model.rpn.head.raw(list(feats.values()), be)), leaves, cs
+        ins, cs = [], [c]
+        for k, name in enumerate(("layer2", "layer3", "layer4", None)):
+            t = c.detach().requires_grad_(self.need[k]) if k in self.bounds else c
+            if k in (1, 2) and self.need[k] and mc.absorbing():
+                mc.chain_over(t)  # C3 / C4: next stage's conv1 + downsample and the FPN lateral
+            ins.append(t)
+            if name is not None:
+                c = body.run_layer(name, t, be)
+                cs.append(c)
+        feats = self.model.backbone.fpn(OrderedDict((str(i), l) for i, l in enumerate(ins)), be)
+        return tuple(feats.values()) + tuple(self.model.rpn.head.raw(list(feats.values()), be)), ins, cs
 
-    def _bwd_plan(self, outs, gouts, leaves, cs, first=None):
-        """[(segment key, roots, () -> root gradients)] in backward order; a layer segment runs only
-        when its output leaf carries a gradient (read lazily: the leaf's .grad exists once the
-        segments before it have run). first: the FPN + RPN-head roots after gradient absorption."""
+    def _bwd_plan(self, outs, gouts, ins, cs, first=None):
+        """[(segment keys, roots, () -> root gradients)] in backward order. The first segment starts at
+        the trunk outputs (FPN + RPN head) and takes every stage above the highest boundary; each
+        boundary C(k+2) starts a segment at cs[k] with its leaf's gradient (read lazily: the leaf's
+        .grad exists once the segments above have run), down to the next boundary. A segment that
+        would hold no gradient (frozen stages) is left out. first: the FPN + RPN-head roots after
+        gradient absorption."""
         r0, g0 = first if first is not None else (outs, gouts)
-        plan = [("fpn+rpn_head", r0, lambda: g0)]
-        for k, key in zip((3, 2, 1, 0), ("layer4", "layer3", "layer2", "stem+layer1")):
-            if self.need[k]:
-                plan.append((key, [cs[k]], (lambda lf: (lambda: [lf.grad]))(leaves[k])))
-        return plan
+        plan = [(["fpn+rpn_head"], r0, lambda: g0)]
+        for k in (3, 2, 1, 0):  # C5 .. C2 and their producers layer4 .. stem+layer1
+            key = self.LAYER_KEYS[k]
+            if k in self.bounds:
+                if not self.need[k]:
+                    break  # nothing below trains
+                plan.append(([key], [cs[k]], (lambda lf: (lambda: [lf.grad]))(ins[k])))
+            else:
+                plan[-1][0].append(key)
+        return [(tuple(keys), roots, groots) for keys, roots, groots in plan]
 
-    def _bwd_all(self, outs, gouts, leaves, cs):
-        for _, roots, groots in self._bwd_plan(outs, gouts, leaves, cs):
+    def _bwd_all(self, outs, gouts, ins, cs):
+        for _, roots, groots in self._bwd_plan(outs, gouts, ins, cs):
             torch.autograd.backward(roots, groots())
 
     def __call__(self, x):
@@ -1435,23 +1456,26 @@ class _SegGraphFn(torch.autograd.Function):
     def backward(ctx, *gouts):
         tg = ctx.tg
         _load_gouts(tg, gouts)
-        for key, _ in tg.bwd:  # see _GraphFn.backward
-            for p, g in zip(tg.seg_params[key], tg.static_grads[key]):
-                if g is not None and p.grad is g:
-                    p.grad = g.clone()
+        for keys, _ in tg.bwd:  # see _GraphFn.backward
+            for key in keys:
+                for p, g in zip(tg.seg_params[key], tg.static_grads[key]):
+                    if g is not None and p.grad is g:
+                        p.grad = g.clone()
         hook = tg.model.__dict__.get("_mx_seg_ready")
-        for key, graph in tg.bwd:
+        for keys, graph in tg.bwd:
             graph.replay()
-            ps, gs = tg.seg_params[key], tg.static_grads[key]
-            for p, g in zip(ps, gs):
-                if g is None:
-                    continue
-                if p.grad is None:
-                    p.grad = g
-                else:
-                    p.grad.add_(g)
-            if hook is not None and ps:
-                hook(key, ps)
+            ps = []
+            for key in keys:
+                for p, g in zip(tg.seg_params[key], tg.static_grads[key]):
+                    if g is None:
+                        continue
+                    ps.append(p)
+                    if p.grad is None:
+                        p.grad = g
+                    else:
+                        p.grad.add_(g)
+            if hook is not None and ps:  # every group up to the segment's last trained key is final
+                hook([k for k in keys if tg.seg_params[k]][-1], ps)
         return None, None, None
 
 

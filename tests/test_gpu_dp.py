@@ -47,15 +47,23 @@ def pg():
     conv.set_data_parallel(False)
 
 
-def test_segmented_trunk_graphs_match_one_graph(dev, pg):
+@pytest.mark.parametrize("bounds,order", [("23", ["layer3", "layer2"]),
+                                          ("2345", ["fpn+rpn_head", "layer4", "layer3", "layer2"]),
+                                          ("5", ["fpn+rpn_head", "layer2"]), ("4", ["layer4", "layer2"])])
+def test_segmented_trunk_graphs_match_one_graph(dev, pg, monkeypatch, bounds, order):
+    """Segment boundaries MX_DP_BOUNDS (frcnn._SegGraphs): the hook fires once per segment with its
+    last key; "5" puts the FPN alone, then layer4 + layer3 + layer2 in one pass; "4": FPN + layer4,
+    then layer3 + layer2."""
     from mx_det import frcnn
     from mx_det.data import synth_batch
     from mx_det.dp import DataParallel
+    monkeypatch.setenv("MX_DP_BOUNDS", bounds)
+    expect = order
     ref = _model(dev)
     m = _model(dev)
     m.load_state_dict(ref.state_dict())
     dp = DataParallel(m)
-    order = []
+    order = []  # hook log (the parameter is `expect`)
     hook = m.__dict__["_mx_seg_ready"]
     m.__dict__["_mx_seg_ready"] = lambda key, ps: (order.append(key), hook(key, ps))
     imgs, tg = synth_batch(40, 6, H=512, W=672, device=dev)
@@ -82,7 +90,7 @@ def test_segmented_trunk_graphs_match_one_graph(dev, pg):
                     d = 1e-3 * q.grad
                     p.sub_(d)
                     q.sub_(d)
-        assert order == ["fpn+rpn_head", "layer4", "layer3", "layer2"], order
+        assert order == expect, order
         order.clear()
     g = next(iter(m.__dict__["_mx_graphs"].values()))
     assert isinstance(g, frcnn._SegGraphs)
