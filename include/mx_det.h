@@ -424,6 +424,24 @@ int mx_conv2d_dgrad_x3(const mx_conv_shape* s, const float* dy, const uint16_t* 
 int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const float* x, float* dw, int64_t Kout, int64_t Cin,
                        int layout, void* ws, size_t ws_bytes, mx_stream_t stream);
 
+/* Pre-split operands (x3p): an f32 tensor of n elements (n % 8 == 0) as its bf16x3 planes, planes[0..n) = hi,
+ * planes[n..2n) = lo -- the same split the x3 kernels make in registers, so the x3p entries below are
+ * bitwise equal to their x3 forms. A conv whose input (fwd) or output gradient (dgrad, wgrad) arrives as
+ * planes reads it by LDS-DMA straight into the MFMA fragments' layout: no split VALU, no register
+ * staging. fwd_x3p / dgrad_x3p need C % 32 == 0 (fwd) / K % 32 == 0 (dgrad) and R*S <= 64 (the buffer
+ * kernel) and take the x3 workspaces; wgrad_x3p takes both dy and x as planes and the workspace of
+ * mx_conv_workspace_x3p(s, 2) (its split slab only). Same arguments otherwise. */
+int mx_split_planes(const float* src, int64_t n, uint16_t* planes, mx_stream_t stream);
+size_t mx_conv_workspace_x3p(const mx_conv_shape* s, int pass);
+int mx_conv2d_fwd_x3p(const mx_conv_shape* s, const uint16_t* xp, const uint16_t* w, const float* bias,
+                      const float* residual, int act, float* y, float* stats, void* ws, size_t ws_bytes,
+                      mx_stream_t stream);
+int mx_conv2d_dgrad_x3p(const mx_conv_shape* s, const uint16_t* dyp, const uint16_t* wt, const float* residual,
+                        float* dx, const float* y, const float* z, const float* mean, const float* invstd, int act,
+                        float* part, int64_t part_mb, void* ws, size_t ws_bytes, mx_stream_t stream);
+int mx_conv2d_wgrad_x3p(const mx_conv_shape* s, const uint16_t* dyp, const uint16_t* xp, float* dw, int64_t Kout,
+                        int64_t Cin, int layout, void* ws, size_t ws_bytes, mx_stream_t stream);
+
 /* NHWC pooling / resampling (dtype MX_BF16 or MX_F32 storage, C % 8 == 0).
  * maxpool: F.max_pool2d (ResNet stem k3 s2 p1 — torchvision resnet50 reached at
  *   train_frcnn_baseline.py:139; U-Net MaxPool2d(2), restoration_net.py:39); argmax (nullable,

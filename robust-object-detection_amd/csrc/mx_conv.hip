@@ -65,6 +65,7 @@ struct ConvP {
   // tap window of one chunk, so the re-reads across taps stay in L2
   int korder;
   int dbg_skip_epi;  // timing experiments only (mx_conv_set_debug): skip the bf16x3 buffer kernel's epilogue
+  int aplanes;       // bf16x3 buffer kernel: A arrives as bf16 hi / lo planes (src = hi, lo at src + src_elems)
   // dgrad feeding a train-mode BatchNorm backward (mx_conv2d_dgrad_bnb): per 64-row block column
   // sums of g = bf16(dx) * act'(y) and g * (z - mean) * invstd -> bnb_part [2][mblocks64][Ncol]
   const void* bnb_y;
@@ -1704,7 +1705,10 @@ __device__ __forceinline__ int x3_swz(int row) {
 // WC = 1 (wide wave tiles: WR waves stacked along M, each spanning all BN columns): every A row is
 // split by exactly one wave (WC = 2 splits each row in both wave-columns), half the split VALU per
 // MFMA, at twice the B fragment reads per wave.
-template <int BN, int MODE, int STAGES, int OCC, int BMT, int WR = 2, int WC = 2>
+// AP (mx_conv2d_*_x3p): A arrives pre-split as bf16 hi / lo planes (mx_split_planes, the same split8 values)
+// and lands like the weight planes -- a hi and a lo plane of 64-B rows (32 channels) -- so its fragments
+// are read directly, without the split VALU; bitwise the same products.
+template <int BN, int MODE, int STAGES, int OCC, int BMT, int WR = 2, int WC = 2, bool AP = false>
 __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p) {
 #if defined(__HIP_DEVICE_COMPILE__)
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1724,7 +1728,7 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
   const int64_t mt = bid / ntiles_n, nt = bid % ntiles_n;
   const int64_t m0 = mt * BMT, n0 = nt * BN;
   const int lrow = lane >> 2, pc = lane & 3;  // landing row within the instruction, physical chunk
-  const int qa = pc ^ x3_swz(lrow), qb = pc ^ tile_swz<4>(lrow);  // logical chunks fetched
+  const int qa = AP ? (pc ^ tile_swz<4>(lrow)) : (pc ^ x3_swz(lrow)), qb = pc ^ tile_swz<4>(lrow);  // logical chunks
   const int IH = (int)p.IH, IW = (int)p.IW, IC = (int)p.IC, R = p.R, S = p.S;
   uint32_t a_voff[AI];
   uint64_t a_mask[AI];
@@ -1740,14 +1744,14 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
       const int n = (int)(t / p.OH);
       const int h0 = MODE == 0 ? oh * p.st_h - p.pad_h : oh + p.pad_h - (R - 1);
       const int w0 = MODE == 0 ? ow * p.st_w - p.pad_w : ow + p.pad_w - (S - 1);
-      off = ((n * IH + h0) * IW + w0) * IC + qa * 4;
+      off = ((n * IH + h0) * IW + w0) * IC + qa * (AP ? 8 : 4);
       for (int r = 0; r < R; ++r)
         for (int q = 0; q < S; ++q) {
           const int rr = MODE == 0 ? r : R - 1 - r, qq = MODE == 0 ? q : S - 1 - q;
           if ((unsigned)(h0 + rr) < (unsigned)IH && (unsigned)(w0 + qq) < (unsigned)IW) mask |= 1ull << (r * S + q);
         }
     }
-    a_voff[i] = (uint32_t)off * 4u;
+    a_voff[i] = (uint32_t)off * (AP ? 2u : 4u);
     a_mask[i] = mask;
   }
   uint32_t b_voff[BI];
@@ -1756,7 +1760,8 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
     const int64_t n = n0 + wave * BR + i * RPI + lrow;
     b_voff[i] = n < p.Ncol ? (uint32_t)((n * p.Kdim + qb * 8) * 2) : kOOB;
   }
-  const i32x4 arsrc = dma_rsrc(p.src, (uint32_t)(p.src_elems * 4));
+  const i32x4 arsrc = dma_rsrc(p.src, (uint32_t)(p.src_elems * (AP ? 2 : 4)));
+  const i32x4 alrsrc = AP ? dma_rsrc(p.src + p.src_elems, (uint32_t)(p.src_elems * 2)) : arsrc;
   const i32x4 bhrsrc = dma_rsrc(p.wt, (uint32_t)(p.wt_elems * 2));
   const i32x4 blrsrc = dma_rsrc(p.wt + p.wt_plane, (uint32_t)(p.wt_elems * 2));
   const uint32_t lds0 = lds_addr(smem);
@@ -1776,7 +1781,7 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
     const uint32_t B = A + 2 * AH;
     const int cr = kp.cr, cq = kp.cq, cc = kp.cc;
     const int rr = MODE == 0 ? cr : R - 1 - cr, qq = MODE == 0 ? cq : S - 1 - cq;
-    const uint32_t a_soff = (uint32_t)(((rr * IW + qq) * IC + cc) * 4);
+    const uint32_t a_soff = (uint32_t)(((rr * IW + qq) * IC + cc) * (AP ? 2 : 4));
     const int tap = cr * S + cq;
     const uint32_t b_soff = (uint32_t)__builtin_amdgcn_readfirstlane((int)((tap * IC + cc) * 2));
     if (!(dbg & 8)) {
@@ -1785,8 +1790,13 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
       const bool ok = (a_mask[i] >> tap) & 1ull;
       const uint32_t v = a_voff[i] + a_soff;
       const uint32_t dst = A + (wave * AR + i * RPI) * RB;
-      lds_dma16(arsrc, dst, ok ? v : kOOB, 0u);
-      lds_dma16(arsrc, dst + AH, ok ? v + 64u : kOOB, 0u);
+      if constexpr (AP) {  // hi and lo planes: 64-B rows of 32 bf16 channels each
+        lds_dma16(arsrc, dst, ok ? v : kOOB, 0u);
+        lds_dma16(alrsrc, dst + AH, ok ? v : kOOB, 0u);
+      } else {             // two 16-channel f32 half-tiles
+        lds_dma16(arsrc, dst, ok ? v : kOOB, 0u);
+        lds_dma16(arsrc, dst + AH, ok ? v + 64u : kOOB, 0u);
+      }
     }
     }
     if (!(dbg & 4)) {
@@ -1832,6 +1842,12 @@ __global__ void __launch_bounds__(64 * WR * WC, OCC) conv_x3_buf_kernel(ConvP p)
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
       const int row = wm * WM + i * 16 + (lane & 15);
+      if constexpr (AP) {  // pre-split: read like the weight planes
+        const int off = row * RB + ((g ^ tile_swz<4>(row)) << 4);
+        ah[i] = *(const bf16x8*)(A + off);
+        al[i] = *(const bf16x8*)(A + AH + off);
+        continue;
+      }
       const int f = x3_swz(row);
       const float4 u = *(const float4*)(Ag + row * RB + ((q0 ^ f) << 4));
       const float4 w = *(const float4*)(Ag + row * RB + (((q0 + 1) ^ f) << 4));
@@ -3874,13 +3890,19 @@ template <int BN, int MODE, int STAGES, int OCC, int BMT, int WR = 2, int WC = 2
 static void launch_x3_buf(const ConvP& p, int64_t blocks, hipStream_t st) {
   const size_t ring = (size_t)STAGES * 2 * (BMT + BN) * 64;
   const size_t epi = (size_t)(WC == 1 ? BMT : BMT / WR) * (BN + 4) * 4;
-  conv_x3_buf_kernel<BN, MODE, STAGES, OCC, BMT, WR, WC><<<(unsigned)blocks, 64 * WR * WC, std::max(ring, epi), st>>>(p);
+  if (p.aplanes)
+    conv_x3_buf_kernel<BN, MODE, STAGES, OCC, BMT, WR, WC, true>
+        <<<(unsigned)blocks, 64 * WR * WC, std::max(ring, epi), st>>>(p);
+  else
+    conv_x3_buf_kernel<BN, MODE, STAGES, OCC, BMT, WR, WC, false>
+        <<<(unsigned)blocks, 64 * WR * WC, std::max(ring, epi), st>>>(p);
 }
 
 template <int MODE>
 static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, hipStream_t st) {
   const bool buf = g_conv_loader >= 1 && p.IC % 32 == 0 && p.R * p.S <= 64 && p.Kdim % 32 == 0 && p.src_elems > 0 &&
                    p.src_elems * 4 < (1ll << 31) && p.wt_elems > 0 && p.wt_plane + p.wt_elems < (1ll << 30);
+  MX_CHECK_ARG(buf || !p.aplanes, "conv x3p: pre-split A planes need the buffer kernel (channels %% 32 == 0, R*S <= 64)");
   Geo g = g0;
   if (g.bmt == 256 && !buf) {  // 256-row tiles exist only as the buffer kernel
     g.bmt = 128;
@@ -3955,10 +3977,11 @@ static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, h
 static int wgrad_x3_wide() { return g_wgrad_variant == 4; }
 // 5: 256 x 256 tile, one wave per SIMD (conv_wgrad_x3ww_kernel; a tuner candidate)
 static int wgrad_x3_ww() { return g_wgrad_variant == 5; }
-static WGeo wgrad_geo_x3(const mx_conv_shape* s) {
+// std128: the 128 x 128 geometry whatever the variant (the pre-split x3p entry, one kernel)
+static WGeo wgrad_geo_x3(const mx_conv_shape* s, bool std128 = false) {
   WGeo g;
   const int64_t P = s->N * s->Ho * s->Wo, Ncol = s->R * s->S * s->C;
-  const bool wide = wgrad_x3_wide(), ww = wgrad_x3_ww();
+  const bool wide = !std128 && wgrad_x3_wide(), ww = !std128 && wgrad_x3_ww();
   g.tiles = ww ? cdiv(s->K, 256) * cdiv(Ncol, 256) : cdiv(s->K, 128) * cdiv(Ncol, wide ? 256 : 128);
   g.pxt = 32;
   const int64_t slots = g_wgrad_target ? g_wgrad_target : (int64_t)num_cus() * ((wide || ww) ? 1 : 2);
@@ -3977,6 +4000,15 @@ static size_t wgrad_x3_slab(const mx_conv_shape* sd, const WGeo& g) {
 }
 static size_t wgrad_x3_planes(const mx_conv_shape* sd) {
   return 2 * sizeof(uint16_t) * (size_t)(sd->N * sd->Ho * sd->Wo * sd->K + sd->N * sd->H * sd->W * sd->C);
+}
+
+// pre-split (x3p) entry points: the wgrad needs only its split slab
+extern "C" size_t mx_conv_workspace_x3p(const mx_conv_shape* s, int pass) {
+  if (!s || pass < 0 || pass > 2) return 0;
+  if (pass < 2) return mx_conv_workspace_x3(s, pass);
+  bool dense;
+  const mx_conv_shape sd = wgrad_shape(s, &dense);
+  return wgrad_x3_slab(&sd, wgrad_geo_x3(&sd, true));
 }
 
 extern "C" size_t mx_conv_workspace_x3(const mx_conv_shape* s, int pass) {
@@ -4004,16 +4036,16 @@ extern "C" size_t mx_conv_workspace_x3(const mx_conv_shape* s, int pass) {
   return mx;
 }
 
-extern "C" int mx_conv2d_fwd_x3(const mx_conv_shape* s, const float* x, const uint16_t* w, const float* bias,
-                                const float* residual, int act, float* y, float* stats, void* ws, size_t ws_bytes,
-                                mx_stream_t stream) {
+static int conv_fwd_x3(const mx_conv_shape* s, const void* x, int aplanes, const uint16_t* w, const float* bias,
+                       const float* residual, int act, float* y, float* stats, void* ws, size_t ws_bytes,
+                       mx_stream_t stream) {
   int rc = conv_check(s);
   if (rc) return rc;
   MX_CHECK_ARG(s->C % 8 == 0, "conv fwd x3: C=%lld must be a multiple of 8 (pad the input channels)", (long long)s->C);
   MX_CHECK_ARG(s->K % 8 == 0 || !residual, "conv fwd x3: residual needs K %% 8 == 0");
   MX_CHECK_ARG(x && w && y, "conv fwd x3: null operand");
   ConvP p{};
-  p.src = (const uint16_t*)(const void*)x; p.wt = w;
+  p.src = (const uint16_t*)x; p.wt = w; p.aplanes = aplanes;
   p.M = s->N * s->Ho * s->Wo; p.Ncol = s->K; p.Kdim = s->R * s->S * s->C;
   p.OH = s->Ho; p.OW = s->Wo; p.IH = s->H; p.IW = s->W; p.IC = s->C;
   p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
@@ -4023,9 +4055,22 @@ extern "C" int mx_conv2d_fwd_x3(const mx_conv_shape* s, const float* x, const ui
   return launch_igemm_x3<0>(p, make_geo_x3(p.M, p.Ncol, p.Kdim), ws, ws_bytes, (hipStream_t)stream);
 }
 
-extern "C" int mx_conv2d_dgrad_x3(const mx_conv_shape* s, const float* dy, const uint16_t* wt, const float* residual,
-                                  float* dx, const float* y, const float* z, const float* mean, const float* invstd,
-                                  int act, float* part, int64_t part_mb, void* ws, size_t ws_bytes, mx_stream_t stream) {
+extern "C" int mx_conv2d_fwd_x3(const mx_conv_shape* s, const float* x, const uint16_t* w, const float* bias,
+                                const float* residual, int act, float* y, float* stats, void* ws, size_t ws_bytes,
+                                mx_stream_t stream) {
+  return conv_fwd_x3(s, x, 0, w, bias, residual, act, y, stats, ws, ws_bytes, stream);
+}
+
+extern "C" int mx_conv2d_fwd_x3p(const mx_conv_shape* s, const uint16_t* xp, const uint16_t* w, const float* bias,
+                                 const float* residual, int act, float* y, float* stats, void* ws, size_t ws_bytes,
+                                 mx_stream_t stream) {
+  return conv_fwd_x3(s, xp, 1, w, bias, residual, act, y, stats, ws, ws_bytes, stream);
+}
+
+static int conv_dgrad_x3(const mx_conv_shape* s, const void* dy, int aplanes, const uint16_t* wt,
+                         const float* residual, float* dx, const float* y, const float* z, const float* mean,
+                         const float* invstd, int act, float* part, int64_t part_mb, void* ws, size_t ws_bytes,
+                         mx_stream_t stream) {
   int rc = conv_check(s);
   if (rc) return rc;
   MX_CHECK_ARG(s->K % 8 == 0 && s->C % 8 == 0, "conv dgrad x3: K and C must be multiples of 8");
@@ -4046,7 +4091,7 @@ extern "C" int mx_conv2d_dgrad_x3(const mx_conv_shape* s, const float* dy, const
     const DClass& c = cl[i];
     if (c.Hc * c.Wc == 0) continue;
     ConvP p{};
-    p.src = (const uint16_t*)(const void*)dy; p.wt = wt + c.off; p.wt_plane = plane;
+    p.src = (const uint16_t*)dy; p.wt = wt + c.off; p.wt_plane = plane; p.aplanes = aplanes;
     p.M = s->N * c.Hc * c.Wc; p.Ncol = s->C; p.Kdim = (int64_t)c.Rc * c.Sc * s->K;
     p.OH = c.Hc; p.OW = c.Wc; p.IH = s->Ho; p.IW = s->Wo; p.IC = s->K;
     p.R = std::max(c.Rc, 1); p.S = std::max(c.Sc, 1); p.st_h = 1; p.st_w = 1; p.pad_h = c.dh; p.pad_w = c.dw;
@@ -4064,8 +4109,43 @@ extern "C" int mx_conv2d_dgrad_x3(const mx_conv_shape* s, const float* dy, const
   return MX_OK;
 }
 
+extern "C" int mx_conv2d_dgrad_x3(const mx_conv_shape* s, const float* dy, const uint16_t* wt, const float* residual,
+                                  float* dx, const float* y, const float* z, const float* mean, const float* invstd,
+                                  int act, float* part, int64_t part_mb, void* ws, size_t ws_bytes, mx_stream_t stream) {
+  return conv_dgrad_x3(s, dy, 0, wt, residual, dx, y, z, mean, invstd, act, part, part_mb, ws, ws_bytes, stream);
+}
+
+extern "C" int mx_conv2d_dgrad_x3p(const mx_conv_shape* s, const uint16_t* dyp, const uint16_t* wt,
+                                   const float* residual, float* dx, const float* y, const float* z, const float* mean,
+                                   const float* invstd, int act, float* part, int64_t part_mb, void* ws,
+                                   size_t ws_bytes, mx_stream_t stream) {
+  return conv_dgrad_x3(s, dyp, 1, wt, residual, dx, y, z, mean, invstd, act, part, part_mb, ws, ws_bytes, stream);
+}
+
+extern "C" int mx_split_planes(const float* src, int64_t n, uint16_t* planes, mx_stream_t stream) {
+  MX_CHECK_ARG(src && planes && n >= 0 && n % 8 == 0, "mx_split_planes: n must be a multiple of 8");
+  if (n == 0) return MX_OK;
+  split_planes_kernel<<<(unsigned)cdiv(n / 8, 256), 256, 0, (hipStream_t)stream>>>(src, n / 8, planes, planes + n);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+static int conv_wgrad_x3(const mx_conv_shape* s, const void* dy, const void* x, int planes, float* dw, int64_t Kout,
+                         int64_t Cin, int layout, void* ws, size_t ws_bytes, mx_stream_t stream);
 extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const float* x, float* dw, int64_t Kout,
                                   int64_t Cin, int layout, void* ws, size_t ws_bytes, mx_stream_t stream) {
+  return conv_wgrad_x3(s, dy, x, 0, dw, Kout, Cin, layout, ws, ws_bytes, stream);
+}
+// dy / x already as bf16 hi / lo planes (mx_split_planes): the LDS-DMA kernel without its split passes;
+// workspace = the split slab only (mx_conv_workspace_x3p)
+extern "C" int mx_conv2d_wgrad_x3p(const mx_conv_shape* s, const uint16_t* dyp, const uint16_t* xp, float* dw,
+                                   int64_t Kout, int64_t Cin, int layout, void* ws, size_t ws_bytes, mx_stream_t stream) {
+  return conv_wgrad_x3(s, dyp, xp, 1, dw, Kout, Cin, layout, ws, ws_bytes, stream);
+}
+static int conv_wgrad_x3(const mx_conv_shape* s, const void* dy_, const void* x_, int planes, float* dw, int64_t Kout,
+                         int64_t Cin, int layout, void* ws, size_t ws_bytes, mx_stream_t stream) {
+  const float* dy = (const float*)dy_;
+  const float* x = (const float*)x_;
   int rc = conv_check(s);
   if (rc) return rc;
   MX_CHECK_ARG(s->K % 8 == 0 && s->C % 8 == 0, "conv wgrad x3: K and C must be multiples of 8");
@@ -4078,22 +4158,22 @@ extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const
   const mx_conv_shape sd = wgrad_shape(s, &dense);
   s = &sd;
   WgP p{};
-  p.dy = (const uint16_t*)(const void*)dy; p.x = (const uint16_t*)(const void*)x; p.dw = dw;
+  p.dy = (const uint16_t*)dy_; p.x = (const uint16_t*)x_; p.dw = dw;
   p.P = s->N * s->Ho * s->Wo; p.K = s->K; p.Ncol = s->R * s->S * s->C;
   p.OH = s->Ho; p.OW = s->Wo; p.H = s->H; p.W = s->W; p.C = s->C; p.N = s->N;
   p.R = (int)s->R; p.S = (int)s->S; p.st_h = s->stride_h; p.st_w = s->stride_w; p.pad_h = s->pad_h; p.pad_w = s->pad_w;
   p.Kout = Kout; p.Cin = Cin; p.layout = layout;
   p.dC = dC; p.dRS = dRS;
-  const WGeo g = wgrad_geo_x3(s);
+  const WGeo g = wgrad_geo_x3(s, planes != 0);
   p.kchunk = g.kchunk;
-  const bool dma = wgrad_x3_dma();
-  const size_t slab = wgrad_x3_slab(s, g), need = slab + (dma ? wgrad_x3_planes(s) : 0);
+  const bool dma = planes || wgrad_x3_dma(), split = dma && !planes;
+  const size_t slab = wgrad_x3_slab(s, g), need = slab + (split ? wgrad_x3_planes(s) : 0);
   if (need) {
     MX_CHECK_ARG(ws && ws_bytes >= need, "conv wgrad x3: workspace of %zu bytes required (mx_conv_workspace_x3)",
                  need);
   }
   if (g.splits > 1) p.slab = (float*)ws;
-  if (dma) {  // the operands as bf16 hi / lo planes, read by LDS-DMA
+  if (split) {  // the operands as bf16 hi / lo planes, read by LDS-DMA
     const int64_t dyel = p.P * p.K, xel = p.N * p.H * p.W * p.C;
     uint16_t* dyp = (uint16_t*)((char*)ws + slab);
     uint16_t* xp = dyp + 2 * dyel;
@@ -4108,12 +4188,12 @@ extern "C" int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const
   MX_CHECK_ARG(p.P * p.K * 4 < (1ll << 31) && p.N * p.H * p.W * p.C * 4 < (1ll << 31) && p.P + 64 < (1ll << 23) &&
                    p.N * p.H * p.W < (1ll << 23) && p.K * 4 < (1ll << 24) && p.C * 4 < (1ll << 24),
                "conv wgrad x3: dy / x must each stay below 2 GiB and 8M pixels (32-bit / 24-bit offset math)");
-  if (wgrad_x3_ww())
+  if (dma)
+    conv_wgrad_x3d_kernel<<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);
+  else if (wgrad_x3_ww())
     conv_wgrad_x3ww_kernel<<<(unsigned)(g.tiles * g.splits), 256, 2 * 8 * 32 * 256, st>>>(p);
   else if (wgrad_x3_wide())
     conv_wgrad_x3w_kernel<<<(unsigned)(g.tiles * g.splits), 512, 2 * 6 * 32 * 256, st>>>(p);
-  else if (dma)
-    conv_wgrad_x3d_kernel<<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);
   else if (g_wgrad_variant == 6)
     conv_wgrad_x3_kernel<true><<<(unsigned)(g.tiles * g.splits), NT, 2 * 4 * 32 * 256, st>>>(p);
   else

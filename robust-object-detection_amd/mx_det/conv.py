@@ -212,11 +212,13 @@ def _tuned(key, cands, apply, run, default):
         apply(default)
 
 
-def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dtype=None, stats=False, cin=None):
+def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dtype=None, stats=False, cin=None,
+             xp=None):
     """x NHWC, wk KRSC bf16 -> y NHWC; optional BN stat partials. bf16 x: wk [K,R,S,C], output
     out_dtype (default bf16). f32 x (bf16x3): wk [2,K,R,S,C] hi / lo planes, output and residual f32.
     cin: the weight's real input channels (<= C); a 7x7 conv to 64 channels of a <= 4-channel input
-    (the ResNet stem) runs mx_conv2d_stem_x3 (MX_STEM_KERNEL=0: the generic x3 kernels)."""
+    (the ResNet stem) runs mx_conv2d_stem_x3 (MX_STEM_KERNEL=0: the generic x3 kernels). xp: x's
+    split_planes (f32 x, C % 32 == 0): mx_conv2d_fwd_x3p reads them instead of splitting x."""
     x3 = is_x3(x)
     assert wk.dtype == torch.bfloat16 and x.is_contiguous() and wk.is_contiguous()
     if x3:
@@ -251,7 +253,8 @@ def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dty
         if x3:
             wsb = _lib.load().mx_conv_workspace_x3(ctypes.byref(sh), 0)
             ws = torch.empty(wsb, dtype=torch.uint8, device=x.device) if wsb else None
-            call("mx_conv2d_fwd_x3", ctypes.byref(sh), _p(x), _p(wk), _p(bias), _p(residual), int(act), _p(y), _p(st),
+            call("mx_conv2d_fwd_x3p" if xp is not None else "mx_conv2d_fwd_x3", ctypes.byref(sh),
+                 _p(xp if xp is not None else x), _p(wk), _p(bias), _p(residual), int(act), _p(y), _p(st),
                  _p(ws), wsb, _s())
             return
         wsb = _lib.load().mx_conv_workspace(ctypes.byref(sh), 0)
@@ -259,7 +262,8 @@ def conv_fwd(x, wk, stride, pad, bias=None, residual=None, act=ACT_NONE, out_dty
         call("mx_conv2d_fwd_ex", ctypes.byref(sh), _p(x), _p(wk), _p(bias), _p(residual), int(act), _p(y),
              1 if out_dtype == torch.bfloat16 else 0, _p(st), _p(ws), wsb, _s())
 
-    key = ("fwd", x.dtype, sh.N, sh.H, sh.W, C, K, R, S, tuple(stride), tuple(pad), residual is not None, out_dtype)
+    key = ("fwd", x.dtype, sh.N, sh.H, sh.W, C, K, R, S, tuple(stride), tuple(pad), residual is not None, out_dtype,
+           xp is not None)
     _tuned(key, _FD_CANDS_X3 if x3 else _FD_CANDS, _apply_fd, run, _FD_DEFAULT)
     if _timer:
         kind = ("x3_" if x3 else "") + ("fwd128" if K > 64 else "fwd64")
@@ -432,15 +436,51 @@ def operands(w, cin_pad, stride, pad, kpad, dgrad, dense=False, split=False):
     return pack_weight(w, cin_pad, stride, pad, kpad=kpad, dgrad=dgrad, split=split)
 
 
+def split_planes(t):
+    """f32 tensor -> its bf16x3 planes [2, *shape] (hi, lo: the split the x3 kernels make in registers;
+    mx_split_planes). The x3p conv entries read them by LDS-DMA (no split VALU); bitwise the same."""
+    t = t.contiguous()
+    pl = torch.empty((2,) + tuple(t.shape), dtype=torch.bfloat16, device=t.device)
+    call("mx_split_planes", _p(t), t.numel(), _p(pl), _s())
+    return pl
+
+
+def planes_for(n_elems, chans, krs):
+    """Whether a conv operand of n_elems f32 values is split into planes once (split_planes) for the
+    x3p kernels: its channel count a multiple of 32 (the buffer kernel's K-tile), and enough MFMA work
+    per element to pay the split pass (8 B of HBM traffic per element): MX_X3_PLANES=0 turns it off,
+    MX_X3_PLANES_KRS (default 1152: a 3x3 conv to 128 channels) is the minimum output channels x taps
+    of the conv reading it, MX_X3_PLANES_MIN (default 4M) the minimum element count."""
+    if os.environ.get("MX_X3_PLANES", "1") == "0" or chans % 32:
+        return False
+    return (krs >= int(os.environ.get("MX_X3_PLANES_KRS", "1152"))
+            and n_elems >= int(os.environ.get("MX_X3_PLANES_MIN", str(4 << 20))))
+
+
+def _x_planes(x, K, R, S, dense):
+    """x's split_planes when the conv's forward (and its wgrad) should read planes, else None."""
+    if not is_x3(x) or dense or R * S > 64 or not planes_for(x.numel(), x.shape[3], K * R * S):
+        return None
+    return split_planes(x)
+
+
+def _dy_planes(dy, C, R, S, dense):
+    """dy's split_planes for the dgrad (and, with x's planes, the wgrad), or None."""
+    if not is_x3(dy) or dense or R * S > 64 or not planes_for(dy.numel(), dy.shape[-1], C * R * S):
+        return None
+    return split_planes(dy)
+
+
 def _is_dense(x_shape, R, S, stride, pad):
     """A conv whose single output pixel sees the whole input (valid RxS conv on an RxS map)."""
     return (x_shape[1], x_shape[2]) == (R, S) and tuple(pad) == (0, 0) and R * S > 1
 
 
-def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
+def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None, dyp=None):
     """dy NHWC [N,Ho,Wo,K] (K = the wt's padded output channels), wt from pack_weight(dgrad=True)
     -> dx NHWC [N,H,W,C] of dy's dtype (+ residual, a tensor of dx's shape and dtype added in the
-    epilogue, at every pixel once under either stride). f32 dy: bf16x3 kernels on the split wt."""
+    epilogue, at every pixel once under either stride). f32 dy: bf16x3 kernels on the split wt; dyp: dy's
+    split_planes (K % 32 == 0), read by mx_conv2d_dgrad_x3p instead of splitting dy."""
     N, H, W, C = x_shape
     K = dy.shape[3]
     x3 = is_x3(dy)
@@ -461,7 +501,8 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
             wsb = _lib.load().mx_conv_workspace_x3(ctypes.byref(sh), 1)
             ws = torch.empty(wsb, dtype=torch.uint8, device=dy.device) if wsb else None
             b = bnb if part is not None else None
-            call("mx_conv2d_dgrad_x3", ctypes.byref(sh), _p(dyc), _p(wt), _p(residual), _p(dx),
+            call("mx_conv2d_dgrad_x3p" if dyp is not None else "mx_conv2d_dgrad_x3", ctypes.byref(sh),
+                 _p(dyp if dyp is not None else dyc), _p(wt), _p(residual), _p(dx),
                  _p(b.y) if b else None, _p(b.z) if b else None, _p(b.mean) if b else None,
                  _p(b.invstd) if b else None, int(b.act) if b else 0, _p(part), mb, _p(ws), wsb, _s())
             return
@@ -473,7 +514,8 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None):
         else:
             call("mx_conv2d_dgrad_ex", ctypes.byref(sh), _p(dyc), _p(wt), _p(residual), _p(dx), _p(ws), wsb, _s())
 
-    key = ("dgrad", dy.dtype, N, H, W, C, K, R, S, tuple(stride), tuple(pad), residual is not None, part is not None)
+    key = ("dgrad", dy.dtype, N, H, W, C, K, R, S, tuple(stride), tuple(pad), residual is not None, part is not None,
+           dyp is not None)
     _tuned(key, _FD_CANDS_X3 if x3 else _FD_CANDS, _apply_fd, run, _FD_DEFAULT)
     if part is not None:
         bnb.part = part
@@ -580,7 +622,7 @@ def wgrad_stream(device):
     return dedicated_stream(device, "wgrad")
 
 
-def _wgrad_plan(ctx, dy, x, K, R, S, stride, pad, kout=None, cin=None):
+def _wgrad_plan(ctx, dy, x, K, R, S, stride, pad, kout=None, cin=None, dyp=None, xp=None):
     """A conv backward's weight gradient, decided before its dgrad is launched: (job or its arguments,
     side, fork event) for _wgrad_run after the dgrad, or None when the weight needs no gradient.
 
@@ -598,11 +640,11 @@ def _wgrad_plan(ctx, dy, x, K, R, S, stride, pad, kout=None, cin=None):
     dst = grad_dest(ctx)
     side = side_wgrad_enabled(ctx)
     if side and os.environ.get("MX_WGRAD_FORK", "early") != "late":
-        job = wgrad_prepare(dy, x, K, R, S, stride, pad, kout, cin, dst)
+        job = wgrad_prepare(dy, x, K, R, S, stride, pad, kout, cin, dst, dyp, xp)
         fork = torch.cuda.Event()
         fork.record()
         return job, side, fork
-    return (dy, x, K, R, S, stride, pad, kout, cin, dst), side, None
+    return (dy, x, K, R, S, stride, pad, kout, cin, dst, dyp, xp), side, None
 
 
 def _wgrad_run(plan):
@@ -623,23 +665,32 @@ class _WgradJob:
     """A weight gradient's launch prepared ahead of time (wgrad_prepare): shape, operands, output and
     split workspace allocated and the tuner's pick applied, so the launch itself allocates nothing."""
     __slots__ = ("sh", "x3", "entry", "dw", "dyc", "x", "ws", "wsb", "cfg", "kout", "cin", "K", "R", "S", "stride",
-                 "t0")
+                 "t0", "C", "nbytes")
 
 
-def wgrad_prepare(dy, x, K, R, S, stride, pad, kout=None, cin=None, out=None):
+_WG_CANDS_X3P = ((3, 0), (3, 256), (3, 768), (3, 1024))  # the pre-split kernel: block targets only
+
+
+def wgrad_prepare(dy, x, K, R, S, stride, pad, kout=None, cin=None, out=None, dyp=None, xp=None):
     """Everything of conv_wgrad before the launch: on the current stream (allocations, dy.contiguous(),
     the tuner's first trial of the shape). A side-stream launch forked BEFORE the dgrad (_wgrad_plan)
     needs these done first: a workspace allocated after the dgrad could reuse the dgrad's just-freed
-    split-K slab while the dgrad's reduce still reads it."""
+    split-K slab while the dgrad's reduce still reads it. dyp / xp: both operands' split_planes
+    (mx_conv2d_wgrad_x3p, the LDS-DMA kernel) -- used only when both are given."""
     j = _WgradJob()
     sh = j.sh = shape(x, K, R, S, stride, pad)
     j.kout = kout = kout or K
+    j.C = x.shape[3]
     j.cin = cin = cin or x.shape[3]
     j.K, j.R, j.S, j.stride = K, R, S, stride
     j.x3 = x3 = is_x3(x)
+    j.nbytes = dy.numel() * dy.element_size() + x.numel() * x.element_size()
     assert dy.dtype == x.dtype, (dy.dtype, x.dtype)
-    wsfn = "mx_conv_workspace_x3" if x3 else "mx_conv_workspace"
-    j.entry = entry = "mx_conv2d_wgrad_x3" if x3 else "mx_conv2d_wgrad_ex"
+    pl = x3 and dyp is not None and xp is not None
+    wsfn = "mx_conv_workspace_x3p" if pl else "mx_conv_workspace_x3" if x3 else "mx_conv_workspace"
+    j.entry = entry = "mx_conv2d_wgrad_x3p" if pl else "mx_conv2d_wgrad_x3" if x3 else "mx_conv2d_wgrad_ex"
+    if pl:
+        dy, x = dyp, xp  # the operands the launch reads
     if out is not None:
         assert out.shape == (kout, cin, R, S) and out.dtype == torch.float32 and out.is_contiguous(), out.shape
         dw = out
@@ -649,13 +700,13 @@ def wgrad_prepare(dy, x, K, R, S, stride, pad, kout=None, cin=None, out=None):
     j.x = x
     j.dyc = dyc = dy.contiguous()
     j.t0 = _timer.start() if _timer else None
-    key = ("wgrad", x.dtype, sh.N, sh.H, sh.W, x.shape[3], K, R, S, tuple(stride), tuple(pad))
+    key = ("wgrad", x.dtype, sh.N, sh.H, sh.W, j.C, K, R, S, tuple(stride), tuple(pad), pl)
     if key not in _tune_cache and _tune_on() and _timer is None and not torch.cuda.is_current_stream_capturing():
         def trial():  # timed on the current stream; the real launch may go to the side stream
             wsb_ = getattr(_lib.load(), wsfn)(ctypes.byref(sh), 2)
             ws_ = torch.empty(wsb_, dtype=torch.uint8, device=x.device) if wsb_ else None
             call(entry, ctypes.byref(sh), _p(dyc), _p(x), _p(dw), kout, cin, 1, _p(ws_), wsb_, _s())
-        _tuned(key, _WG_CANDS_X3 if x3 else _WG_CANDS, _apply_wg, trial, _WG_DEFAULT)
+        _tuned(key, _WG_CANDS_X3P if pl else _WG_CANDS_X3 if x3 else _WG_CANDS, _apply_wg, trial, _WG_DEFAULT)
     j.cfg = _tune_cache.get(key, _WG_DEFAULT) if _tune_on() else None
     if j.cfg is not None:
         _apply_wg(j.cfg)
@@ -691,13 +742,12 @@ def wgrad_launch(j, side=False, fork=None):
         # dw itself is NOT held: AccumulateGrad adopts the tensor only while autograd holds the sole
         # reference (an extra one makes it clone dw on the main stream, before the side kernel ran)
         _pending.append((ev, (j.dyc, j.x, j.ws)))
-    dw, sh, x, dyc, K, R, S, stride, t0 = j.dw, j.sh, j.x, j.dyc, j.K, j.R, j.S, j.stride, j.t0
+    dw, sh, C, K, R, S, stride, t0 = j.dw, j.sh, j.C, j.K, j.R, j.S, j.stride, j.t0
     x3 = j.x3
     j.dw = None
     if _timer:
-        _timer.stop(("x3_" if x3 else "") + "wgrad", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * x.shape[3], t0,
-                    _tag(sh.N, sh.H, sh.W, x.shape[3], K, R, S, stride),
-                    dyc.numel() * dyc.element_size() + x.numel() * x.element_size() + dw.numel() * 4)
+        _timer.stop(("x3_" if x3 else "") + "wgrad", 2.0 * sh.N * sh.Ho * sh.Wo * K * R * S * C, t0,
+                    _tag(sh.N, sh.H, sh.W, C, K, R, S, stride), j.nbytes + dw.numel() * 4)
     return dw
 
 
@@ -863,8 +913,10 @@ class ConvAct(torch.autograd.Function):
         dense = _is_dense(x.shape, w.shape[2], w.shape[3], stride, pad)
         # narrow heads (RPN cls+box 15, predictor 35): the dgrad operand is zero-padded to K8
         wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(K), need_dx, dense, split=is_x3(x))
-        y = conv_fwd(x, wk, stride, pad, bias=b.detach() if b is not None else None, act=act, out_dtype=out_dtype)
-        ctx.save_for_backward(x, y, wt if need_dx else None)
+        xp = _x_planes(x, K, w.shape[2], w.shape[3], dense)
+        y = conv_fwd(x, wk, stride, pad, bias=b.detach() if b is not None else None, act=act, out_dtype=out_dtype,
+                     xp=xp)
+        ctx.save_for_backward(x, y, wt if need_dx else None, xp)
         ctx.cfg = (stride, pad, act, w.shape, b is not None)
         ctx.wref, ctx.uses = weakref.ref(w), _count_use(w)
         ctx.slot = _absorb_take(x) if _absorb else None
@@ -873,13 +925,15 @@ class ConvAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        x, y, wt = ctx.saved_tensors
+        x, y, wt, xp = ctx.saved_tensors
         stride, pad, act, wshape, has_b = ctx.cfg
         K, _, R, S = wshape
         dx = dw = db = None
         K8 = (K + 7) // 8 * 8
         gk, db = act_bias_bwd(gy, y, act, K8, has_b and ctx.needs_input_grad[2], g_dtype=x.dtype)
-        wg = _wgrad_plan(ctx, gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1])  # before the dgrad
+        dense = _is_dense(x.shape, R, S, stride, pad)
+        gp = _dy_planes(gk, x.shape[3], R, S, dense)
+        wg = _wgrad_plan(ctx, gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1], dyp=gp, xp=xp)  # before the dgrad
         if ctx.needs_input_grad[0]:
             if _is_dense(x.shape, R, S, stride, pad):  # 1x1-GEMM form: dX[N, R*S*C] = dY[N, K8] wt
                 N, H, W, C = x.shape
@@ -893,7 +947,7 @@ class ConvAct(torch.autograd.Function):
                 if extra is not None and not (extra.dtype == gk.dtype and extra.shape == x.shape and
                                               extra.is_contiguous()):
                     raise RuntimeError("absorbed gradient needs an input-shaped buffer of the gradient's dtype")
-                dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad, residual=_chain_res(ctx.chain, extra))
+                dx = conv_dgrad(gk, wt, x.shape, R, S, stride, pad, residual=_chain_res(ctx.chain, extra), dyp=gp)
             if ctx.chain is not None:
                 dx = ctx.chain.hand(dx)
         if wg is not None:
@@ -1015,7 +1069,8 @@ class ConvBNAct(torch.autograd.Function):
         ctx.link, ctx.role = link if link is not None else (None, None)
         ctx.bnb_own, ctx.bnb_feed = bnb_own, bnb_feed
         wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(w.shape[0]), need_dx, split=is_x3(x))
-        z, st = conv_fwd(x, wk, stride, pad, stats=True, cin=w.shape[1])
+        xp = _x_planes(x, w.shape[0], w.shape[2], w.shape[3], False)
+        z, st = conv_fwd(x, wk, stride, pad, stats=True, cin=w.shape[1], xp=xp)
         K = w.shape[0]
         M = z.numel() // K
         mean, invstd, scale, shift = bn_train_finalize(st, K, M, gamma, beta, eps, momentum, rmean, rvar)
@@ -1025,7 +1080,7 @@ class ConvBNAct(torch.autograd.Function):
         call("mx_bn_apply", _p(z), dcode(z), M, K, _p(scale), _p(shift), _p(res), int(act), _p(y), dcode(y), _s())
         if _timer:  # bn kinds record algorithmic HBM bytes instead of FLOPs
             _timer.stop("bn_apply", M * K * z.element_size() * (2 + (1 if res is not None else 0)), t0, f"{M}x{K}")
-        ctx.save_for_backward(x, wt if need_dx else None, z, y, mean, invstd, gamma)
+        ctx.save_for_backward(x, wt if need_dx else None, z, y, mean, invstd, gamma, xp)
         ctx.cfg = (stride, pad, act, w.shape, residual is not None)
         if bnb_own is not None:  # the next conv's dgrad will produce this BN's backward partials
             bnb_own.y, bnb_own.z, bnb_own.mean, bnb_own.invstd, bnb_own.act = y, z, mean, invstd, act
@@ -1035,7 +1090,7 @@ class ConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        x, wt, z, y, mean, invstd, gamma = ctx.saved_tensors
+        x, wt, z, y, mean, invstd, gamma, xp = ctx.saved_tensors
         stride, pad, act, wshape, has_res = ctx.cfg
         K, _, R, S = wshape
         M = z.numel() // K
@@ -1064,7 +1119,8 @@ class ConvBNAct(torch.autograd.Function):
         if _timer:
             _timer.stop("bn_bwd_apply", M * K * z.element_size() * (4 + (1 if has_res else 0)), t0, f"{M}x{K}")
         dx = dw = None
-        wg = _wgrad_plan(ctx, dz, x, K, R, S, stride, pad, cin=wshape[1])  # before the dgrad
+        dzp = _dy_planes(dz, x.shape[3], R, S, False)
+        wg = _wgrad_plan(ctx, dz, x, K, R, S, stride, pad, cin=wshape[1], dyp=dzp, xp=xp)  # before the dgrad
         link = ctx.link
         if ctx.role == "sink" and dres is not None:
             link.dres, dres = dres, None  # handed to the block's first conv: added in its dgrad epilogue
@@ -1077,7 +1133,7 @@ class ConvBNAct(torch.autograd.Function):
             # BN-backward partials from this epilogue only when it produces the input's whole gradient
             bnb = feed if (feed is not None and feed.y is not None and tuple(stride) == (1, 1)
                            and feed.y.shape == x.shape and (chain is None or chain.last())) else None
-            dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad, residual=_chain_res(chain, res), bnb=bnb)
+            dx = conv_dgrad(dz, wt, x.shape, R, S, stride, pad, residual=_chain_res(chain, res), bnb=bnb, dyp=dzp)
             if chain is not None:
                 dx = chain.hand(dx)
         if wg is not None:

@@ -47,18 +47,20 @@ def pg():
     conv.set_data_parallel(False)
 
 
-@pytest.mark.parametrize("bounds,order", [("23", ["layer3", "layer2"]),
-                                          ("2345", ["fpn+rpn_head", "layer4", "layer3", "layer2"]),
-                                          ("5", ["fpn+rpn_head", "layer2"]), ("4", ["layer4", "layer2"])])
-def test_segmented_trunk_graphs_match_one_graph(dev, pg, monkeypatch, bounds, order):
-    """Segment boundaries MX_DP_BOUNDS (frcnn._SegGraphs): the hook fires once per segment with its
-    last key; "5" puts the FPN alone, then layer4 + layer3 + layer2 in one pass; "4": FPN + layer4,
-    then layer3 + layer2."""
+# hook order (the last trained key of each segment) per segment-boundary setting (MX_DP_BOUNDS)
+ORDERS = {"23": ["layer3", "layer2"], "2345": ["fpn+rpn_head", "layer4", "layer3", "layer2"],
+          "5": ["fpn+rpn_head", "layer2"], "4": ["layer4", "layer2"]}
+
+
+def test_segmented_trunk_graphs_match_one_graph(dev, pg):
+    """Segment boundaries MX_DP_BOUNDS (frcnn._SegGraphs; the default "23" here, the others through
+    test_segment_bounds_in_child): the hook fires once per segment with its last trained key; "5"
+    puts the FPN alone, then layer4 + layer3 + layer2 in one pass; "4": FPN + layer4, then layer3 +
+    layer2; "2345": one segment per stage."""
     from mx_det import frcnn
     from mx_det.data import synth_batch
     from mx_det.dp import DataParallel
-    monkeypatch.setenv("MX_DP_BOUNDS", bounds)
-    expect = order
+    expect = ORDERS[os.environ.get("MX_DP_BOUNDS", "23")]
     ref = _model(dev)
     m = _model(dev)
     m.load_state_dict(ref.state_dict())
@@ -95,3 +97,19 @@ def test_segmented_trunk_graphs_match_one_graph(dev, pg, monkeypatch, bounds, or
     g = next(iter(m.__dict__["_mx_graphs"].values()))
     assert isinstance(g, frcnn._SegGraphs)
     assert isinstance(next(iter(ref.__dict__["_mx_graphs"].values())), frcnn._Graphs)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("bounds", ["2345", "5"])
+def test_segment_bounds_in_child(bounds):
+    """The other boundary settings, each in a child process: in one process, a second pair of models
+    (one-graph reference + segmented) at the same shapes crashed the host inside hipGraphLaunch at the
+    reference's first replay (r06a, r06b, r06g; profiles/r06_ab.txt) -- one setting per process here."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MX_DP_BOUNDS=bounds, PYTHONUNBUFFERED="1")
+    p = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        "tests/test_gpu_dp.py::test_segmented_trunk_graphs_match_one_graph"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
