@@ -152,7 +152,8 @@ def _cpu_baseline(gpu_model, seconds_hint, cores):
 TRAFFIC_FILE = os.environ.get("MX_TRAFFIC_FILE", os.path.join(ROOT, "profiles", "r04ap_traffic.json"))
 # kernels of one op: outer list = the op's sequential kernels (summed), inner = alternative template
 # instances of one kernel (launch-weighted mean)
-KIND_KERNELS = {"x3_wgrad": [["mx::conv_wgrad_x3_kernel", "mx::conv_wgrad_x3w_kernel"], ["mx::wgrad_reduce_kernel"]],
+KIND_KERNELS = {"x3_wgrad": [["mx::conv_wgrad_x3_kernel", "mx::conv_wgrad_x3w_kernel", "mx::conv_wgrad_x3d_kernel"],
+                             ["mx::wgrad_reduce_kernel"]],
                 "x3_fwd128": [["mx::conv_x3_buf_kernel<128, 0", "mx::conv_x3_kernel<128, 0"]],
                 "x3_fwd64": [["mx::conv_x3_buf_kernel<64, 0", "mx::conv_x3_kernel<64, 0"]],
                 "x3_dgrad": [["mx::conv_x3_buf_kernel<128, 1", "mx::conv_x3_buf_kernel<64, 1",
@@ -162,6 +163,34 @@ KIND_KERNELS = {"x3_wgrad": [["mx::conv_wgrad_x3_kernel", "mx::conv_wgrad_x3w_ke
                 "dgrad": [["mx::conv_igemm_buf_kernel<128, 1", "mx::conv_igemm_buf_kernel<256, 1",
                            "mx::conv_igemm_buf_kernel<64, 1"]],
                 "fwd64": [["mx::conv_igemm_buf_kernel<64, 0"]]}
+
+
+# the graphed headline step's per-kernel table at this HEAD (rocprofv3 kernel trace between bench.py's
+# trace markers, tools/prof_steps.py): in the step the side-stream weight gradients overlap the dgrad
+# chain and run longer than when event-timed alone, so the dominant kind is chosen from it
+STEP_TABLE = os.environ.get("MX_STEP_TABLE", os.path.join(ROOT, "profiles", "r06_in_step_table.txt"))  # CSV; .csv is gpurun-ignored
+IN_STEP_KINDS = {"x3_wgrad": ("mx::conv_wgrad_x3", "mx::wgrad_reduce_kernel"),
+                 "x3_dgrad": ("mx::conv_x3_buf_kernel<128, 1", "mx::conv_x3_buf_kernel<64, 1", "mx::conv_x3_kernel<128, 1",
+                              "mx::conv_x3_kernel<64, 1"),
+                 "x3_fwd": ("mx::conv_x3_buf_kernel<128, 0", "mx::conv_x3_buf_kernel<64, 0", "mx::conv_x3_kernel<128, 0",
+                            "mx::conv_x3_kernel<64, 0", "mx::conv_stem_x3_kernel"),
+                 "x3_split_planes": ("mx::split_planes_kernel",)}
+
+
+def in_step_ms():
+    """{kind: in-step kernel ms per step} from STEP_TABLE, or {} when it is absent."""
+    import csv as _csv
+    try:
+        rows = list(_csv.DictReader(open(STEP_TABLE)))
+    except OSError:
+        return {}
+    out = {}
+    for r in rows:
+        name = r["kernel"].replace("void ", "")
+        for kind, pats in IN_STEP_KINDS.items():
+            if name.startswith(pats):
+                out[kind] = out.get(kind, 0.0) + float(r["ms_per_step"])
+    return out
 
 
 def pmc_traffic(kind):
@@ -205,7 +234,20 @@ def conv_roofline(model, opt, imgs, tg, peak=X3_PEAK_TFLOPS, step_fn=None):
         else:
             os.environ["MX_GRAPHS"] = graphs
     s = {k: v for k, v in t.summary().items() if not k.startswith("bn_")}  # conv kinds only
-    dom = max(s, key=lambda k: s[k]["ms"])
+    # the dominant kind: the largest in-step time of the graphed step (STEP_TABLE, x3 kinds) when the
+    # table exists, else the largest event-timed one
+    ins = in_step_ms() if peak == X3_PEAK_TFLOPS else {}
+    flops = {"x3_wgrad": s.get("x3_wgrad", {}).get("flops", 0.0), "x3_dgrad": s.get("x3_dgrad", {}).get("flops", 0.0),
+             "x3_fwd": s.get("x3_fwd128", {}).get("flops", 0.0) + s.get("x3_fwd64", {}).get("flops", 0.0)}
+    in_step = {k: {"ms": round(ins[k], 3), "tflops": round(flops[k] / (ins[k] * 1e-3) / 1e12, 1),
+                   "frac": round(flops[k] / (ins[k] * 1e-3) / 1e12 / peak, 4)}
+               for k in flops if ins.get(k) and flops[k]}
+    if "x3_split_planes" in ins:
+        in_step["x3_split_planes"] = {"ms": round(ins["x3_split_planes"], 3), "bound": "hbm"}
+    big = max((k for k in in_step if "frac" in in_step[k]), key=lambda k: in_step[k]["ms"], default=None)
+    dom = {"x3_fwd": "x3_fwd128"}.get(big, big) if big in ("x3_wgrad", "x3_dgrad", "x3_fwd") else None
+    if dom not in s:
+        dom = max(s, key=lambda k: s[k]["ms"])
     d = s[dom]
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
     traf = pmc_traffic(dom)
@@ -221,13 +263,15 @@ def conv_roofline(model, opt, imgs, tg, peak=X3_PEAK_TFLOPS, step_fn=None):
                        "x3_fwd128": "conv_x3_buf_kernel<*,0,*> (+ conv_splitk_reduce_kernel<*,float>)",
                        "x3_fwd64": "conv_x3_buf_kernel<64,0,*> (+ conv_splitk_reduce_kernel<*,float>)",
                        "x3_dgrad": "conv_x3_buf_kernel<*,1,*> (+ conv_splitk_reduce_kernel<*,float>)",
-                       "x3_wgrad": "conv_wgrad_x3_kernel / conv_wgrad_x3w_kernel (+ wgrad_reduce_kernel)"}[dom],
+                       "x3_wgrad": "conv_wgrad_x3_kernel / _x3d / _x3w (+ wgrad_reduce_kernel)"}[dom],
             "launches_per_step": d["launches"], "avg_launch_us": round(1000 * d["ms"] / d["launches"], 2),
             "gflop_per_launch": round(d["flops"] / d["launches"] / 1e9, 3),
             # operands read once + output written once, mean over the kind's launches; traffic / this
             # is the re-read factor (L2 misses beyond the algorithmic minimum)
             "algorithmic_mb_per_launch": round(d["bytes"] / d["launches"] / 1e6, 2),
             "traffic_ratio": (round(traf / (d["bytes"] / d["launches"] / 1e6), 2) if traf else None),
+            "in_step": ({"source": os.path.relpath(STEP_TABLE, ROOT), "dominant": big, "by_kind": in_step}
+                        if in_step else None),
             "conv_stack": {"tflops": round(allf / (allms * 1e-3) / 1e12, 2), "gflop_per_step": round(allf / 1e9, 1),
                            "ms_per_step": round(allms, 2),
                            "by_kind": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),

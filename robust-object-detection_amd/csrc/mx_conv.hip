@@ -3902,7 +3902,9 @@ template <int MODE>
 static int launch_igemm_x3(ConvP& p, const Geo& g0, void* ws, size_t ws_bytes, hipStream_t st) {
   const bool buf = g_conv_loader >= 1 && p.IC % 32 == 0 && p.R * p.S <= 64 && p.Kdim % 32 == 0 && p.src_elems > 0 &&
                    p.src_elems * 4 < (1ll << 31) && p.wt_elems > 0 && p.wt_plane + p.wt_elems < (1ll << 30);
-  MX_CHECK_ARG(buf || !p.aplanes, "conv x3p: pre-split A planes need the buffer kernel (channels %% 32 == 0, R*S <= 64)");
+  // (a tap-less stride-parity class of a strided dgrad, Kdim = 0, reads no A: the plain kernel writes its epilogue)
+  MX_CHECK_ARG(buf || !p.aplanes || p.Kdim == 0,
+               "conv x3p: pre-split A planes need the buffer kernel (channels %% 32 == 0, R*S <= 64)");
   Geo g = g0;
   if (g.bmt == 256 && !buf) {  // 256-row tiles exist only as the buffer kernel
     g.bmt = 128;

@@ -534,6 +534,7 @@ def conv_dgrad(dy, wt, x_shape, R, S, stride, pad, residual=None, bnb=None, dyp=
 # the operands stay referenced until then. Single-process only: DDP's reducer reads each gradient
 # from its AccumulateGrad hook on the main stream, so multi-rank runs keep wgrad in order.
 _pending = []
+_pending_task = [None]  # the autograd graph task whose end-of-backward callback joins _pending
 # The side-stream wgrad's dw reaches AccumulateGrad from the side stream; the backward's end-of-pass
 # callback (_join_side) makes the main stream wait for it, so torch's "AccumulateGrad node's stream does
 # not match" warning (printed once per process, then the engine's own stream wait) is expected here.
@@ -737,7 +738,11 @@ def wgrad_launch(j, side=False, fork=None):
     if side:
         ev = torch.cuda.Event()
         ev.record(st)
-        if not _pending:
+        task = torch._C._current_graph_task_id()
+        if not _pending or _pending_task[0] != task:
+            # first side wgrad of this backward (a backward that raised never ran its callback: its
+            # events stay listed and are joined by this one's)
+            _pending_task[0] = task
             torch.autograd.Variable._execution_engine.queue_callback(_join_side)
         # dw itself is NOT held: AccumulateGrad adopts the tensor only while autograd holds the sole
         # reference (an extra one makes it clone dw on the main stream, before the side kernel ran)

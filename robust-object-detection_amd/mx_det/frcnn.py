@@ -1328,13 +1328,14 @@ class _SegGraphs:
     stream while the remaining segments' backward graphs run (mx_det.dp.DataParallel; SURVEY.md §8e:
     bucketed all-reduce overlapped with the backward).
 
-    Segment boundaries sit at stage outputs C2..C5 (MX_DP_BOUNDS, digits 2-5; default "23"): at a
-    boundary the forward detaches the stage output into a leaf that the next stage and the FPN lateral
-    both consume, and the segment below it back-propagates from that leaf's gradient (written by the
-    graphs replayed before it). Without a boundary the next stage and the FPN consume the output
-    itself and the backward flows through in one autograd pass. "2345" gives five segments (FPN + RPN
-    head, layer4, layer3, layer2, stem + layer1); "23" gives FPN + RPN head + layer4 + layer3 (106 MB
-    of gradients, all-reduced while layer2's backward runs), layer2, stem + layer1. Every boundary
+    Segment boundaries sit at stage outputs C2..Cb (MX_DP_BOUNDS "2", "23", "234" or "2345"; default
+    "23"): at a boundary the forward detaches the stage output into a leaf that the next stage and the
+    FPN lateral both consume, and the segment below it back-propagates from that leaf's gradient
+    (written by the graphs replayed before it). Without a boundary the next stage and the FPN consume
+    the output itself and the backward flows through in one autograd pass -- the FPN's, so the
+    boundaries are a prefix C2..Cb. "2345" gives five segments (FPN + RPN head, layer4, layer3, layer2,
+    stem + layer1); "23" gives FPN + RPN head + layer4 + layer3 (106 MB of gradients, all-reduced while
+    layer2's backward runs), layer2, stem + layer1. Every boundary
     costs a join: a segment's graph completes with its side-stream weight gradients, and the next
     segment's dgrad chain waits for them (one-GPU A/B: profiles/r06_ab.txt). Same kernels as the
     one-graph trunk; at a boundary the gradient reaching the stage output is summed over its consumers
@@ -1353,9 +1354,12 @@ class _SegGraphs:
                            "fpn+rpn_head": list(model.backbone.fpn.parameters()) + list(model.rpn.head.parameters())}
         self.seg_params = {k: [p for p in v if p.requires_grad] for k, v in self.seg_params.items()}
         spec = os.environ.get("MX_DP_BOUNDS", "23")
-        if not spec or any(c not in "2345" for c in spec):
-            raise ValueError(f"MX_DP_BOUNDS={spec!r}: digits 2-5 (stage outputs C2..C5 that end a segment)")
-        self.bounds = {int(c) - 2 for c in spec}  # leaf index k <-> C(k+2)
+        self.bounds = {int(c) - 2 for c in spec if c in "2345"}  # leaf index k <-> C(k+2)
+        # the FPN lateral reads every stage output that is not a boundary, so the first (FPN) segment's
+        # pass reaches it: boundaries must be C2..Cb, a prefix ("2", "23", "234", "2345")
+        if not self.bounds or len(spec) != len(self.bounds) or self.bounds != set(range(len(self.bounds))):
+            raise ValueError(f"MX_DP_BOUNDS={spec!r}: one of 2, 23, 234, 2345 (the stage outputs C2..Cb that end a "
+                             "backward segment)")
         # C(k+2) needs a gradient iff some stage below it trains
         up = list(self.LAYER_KEYS)
         self.need = [any(self.seg_params[u] for u in up[:k + 1]) for k in range(4)]

@@ -49,14 +49,14 @@ def pg():
 
 # hook order (the last trained key of each segment) per segment-boundary setting (MX_DP_BOUNDS)
 ORDERS = {"23": ["layer3", "layer2"], "2345": ["fpn+rpn_head", "layer4", "layer3", "layer2"],
-          "5": ["fpn+rpn_head", "layer2"], "4": ["layer4", "layer2"]}
+          "234": ["layer4", "layer3", "layer2"], "2": ["layer2"]}
 
 
 def test_segmented_trunk_graphs_match_one_graph(dev, pg):
     """Segment boundaries MX_DP_BOUNDS (frcnn._SegGraphs; the default "23" here, the others through
-    test_segment_bounds_in_child): the hook fires once per segment with its last trained key; "5"
-    puts the FPN alone, then layer4 + layer3 + layer2 in one pass; "4": FPN + layer4, then layer3 +
-    layer2; "2345": one segment per stage."""
+    test_segment_bounds_in_child): the hook fires once per segment with its last trained key; "2"
+    puts the whole trainable trunk in one pass; "234": FPN + layer4, layer3, layer2; "2345": one
+    segment per stage."""
     from mx_det import frcnn
     from mx_det.data import synth_batch
     from mx_det.dp import DataParallel
@@ -100,7 +100,7 @@ def test_segmented_trunk_graphs_match_one_graph(dev, pg):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("bounds", ["2345", "5"])
+@pytest.mark.parametrize("bounds", ["2345", "2"])
 def test_segment_bounds_in_child(bounds):
     """The other boundary settings, each in a child process: in one process, a second pair of models
     (one-graph reference + segmented) at the same shapes crashed the host inside hipGraphLaunch at the

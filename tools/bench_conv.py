@@ -86,6 +86,8 @@ def main():
     ap.add_argument("--korder", default="1", help="comma list of buffer-kernel K-tile orders (0 tap-, 1 channel-major)")
     ap.add_argument("--debug", default="0", help="comma list of mx_conv_set_debug values (1: no epilogue)")
     ap.add_argument("--graph", action="store_true", help="time launches replayed from a HIP graph")
+    ap.add_argument("--planes", action="store_true",
+                    help="f32: also time the pre-split (x3p) forms and the split passes they need")
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "f32"),
                     help="f32: the precision-faithful bf16x3 kernels (TFLOP/s are f32-equivalent, peak 833)")
     args = ap.parse_args()
@@ -129,13 +131,24 @@ def run(args):
         nb = {"fwd": es * (x.numel() + dy.numel()), "dgrad": es * (x.numel() + dy.numel()),
               "wgrad": es * (x.numel() + dy.numel()) + 4 * w.numel()}  # operands read once, output written once
         res = []
-        for kind, fn in (("fwd", lambda: mc.conv_fwd(x, wk, (st, st), (pd, pd), stats=True)),
-                         ("dgrad", lambda: mc.conv_dgrad(dy, wt, x.shape, k, k, (st, st), (pd, pd))),
-                         ("wgrad", lambda: mc.conv_wgrad(dy, x, K, k, k, (st, st), (pd, pd)))):
+        cases = [("fwd", lambda: mc.conv_fwd(x, wk, (st, st), (pd, pd), stats=True)),
+                 ("dgrad", lambda: mc.conv_dgrad(dy, wt, x.shape, k, k, (st, st), (pd, pd))),
+                 ("wgrad", lambda: mc.conv_wgrad(dy, x, K, k, k, (st, st), (pd, pd)))]
+        if args.planes and args.dtype == "f32" and C % 32 == 0 and K % 32 == 0:
+            xp, dyp = mc.split_planes(x), mc.split_planes(dy)
+            cases += [("split_x", lambda: mc.split_planes(x)), ("split_dy", lambda: mc.split_planes(dy)),
+                      ("fwd_p", lambda: mc.conv_fwd(x, wk, (st, st), (pd, pd), stats=True, xp=xp)),
+                      ("dgrad_p", lambda: mc.conv_dgrad(dy, wt, x.shape, k, k, (st, st), (pd, pd), dyp=dyp)),
+                      ("wgrad_p", lambda: mc.wgrad_launch(mc.wgrad_prepare(dy, x, K, k, k, (st, st), (pd, pd),
+                                                                          dyp=dyp, xp=xp)))]
+        for kind, fn in cases:
+            if kind not in tot:
+                tot[kind] = [0, 0]
             ms = timeit(fn, args.reps)
             tot[kind][0] += fl
             tot[kind][1] += ms
-            res.append(f"{kind} {ms * 1000:8.1f}us {fl / ms / 1e9:7.1f}TF {nb[kind] / ms / 1e6:6.0f}GB/s")
+            nbk = nb.get(kind.replace("_p", ""), 8 * (x.numel() if kind == "split_x" else dy.numel()))
+            res.append(f"{kind} {ms * 1000:8.1f}us {fl / ms / 1e9:7.1f}TF {nbk / ms / 1e6:6.0f}GB/s")
         print(f"{name:34s} {fl / 1e9:7.1f} GF | " + " | ".join(res), flush=True)
     print("aggregate: " + " | ".join(f"{k} {v[0] / v[1] / 1e9:.1f} TF/s" for k, v in tot.items() if v[1]))
 
