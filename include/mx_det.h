@@ -432,6 +432,13 @@ int mx_conv2d_wgrad_x3(const mx_conv_shape* s, const float* dy, const float* x, 
  * kernel) and take the x3 workspaces; wgrad_x3p takes both dy and x as planes and the workspace of
  * mx_conv_workspace_x3p(s, 2) (its split slab only). Same arguments otherwise. */
 int mx_split_planes(const float* src, int64_t n, uint16_t* planes, mx_stream_t stream);
+/* mx_bn_apply / mx_bn_bwd_apply_ex (f32) that also write their output (y, resp. dx) as those planes
+ * [2][M][K]: the producer of a conv operand hands it over pre-split for one extra 4-B write per element
+ * instead of an mx_split_planes pass (a read and a write). */
+int mx_bn_apply_p(const float* x, int64_t M, int64_t K, const float* scale, const float* shift, const float* residual,
+                  int act, float* y, uint16_t* planes, mx_stream_t stream);
+int mx_bn_bwd_apply_p(const float* dy, const float* y, const float* x, int64_t M, int64_t K, int act,
+                      const float* coef, float* dx, float* dres, uint16_t* planes, mx_stream_t stream);
 size_t mx_conv_workspace_x3p(const mx_conv_shape* s, int pass);
 int mx_conv2d_fwd_x3p(const mx_conv_shape* s, const uint16_t* xp, const uint16_t* w, const float* bias,
                       const float* residual, int act, float* y, float* stats, void* ws, size_t ws_bytes,

@@ -189,12 +189,22 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   }
 }
 
+// 8 f32 values (element chunk e of an n-element tensor) -> their split8 hi / lo at planes[e*8] / planes[n + e*8]
+__device__ __forceinline__ void store_planes8(uint16_t* __restrict__ planes, int64_t n, int64_t e, const float (&o)[8]) {
+  uint4 h, l;
+  split8(make_float4(o[0], o[1], o[2], o[3]), make_float4(o[4], o[5], o[6], o[7]), h, l);
+  *(uint4*)(planes + e * 8) = h;
+  *(uint4*)(planes + n + e * 8) = l;
+}
+
 // Thread t owns channel chunk c8 = t % K8 for its whole life (per-channel constants stay in
 // registers) and walks rows r = t / K8 + i * (T / K8): 16-B vector loads/stores, coalesced per row.
+// planes (f32 only, nullable): y also as its bf16x3 planes [2][M][K] (split8: mx_split_planes' values) for
+// a consumer conv that reads pre-split operands -- one 4-B write per element instead of a split pass
 template <typename T, typename TY>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, int64_t M, int64_t K, const float* __restrict__ scale,
                                 const float* __restrict__ shift, const TY* __restrict__ res, int act,
-                                TY* __restrict__ y) {
+                                TY* __restrict__ y, uint16_t* __restrict__ planes = nullptr) {
   const int64_t K8 = K / 8;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t rstride = ((int64_t)gridDim.x * blockDim.x) / K8;
@@ -213,6 +223,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
 #pragma unroll
     for (int q = 0; q < 8; ++q) o[q] = actf(v[q] * sc[q] + sh[q] + rv[q], act);
     st8(y + e * 8, o);
+    if (planes) store_planes8(planes, M * K, e, o);
   }
 }
 
@@ -373,7 +384,7 @@ template <int ACT, typename T>
 __global__ void __launch_bounds__(256) bn_bwd_apply2_kernel(const T* __restrict__ dy, const T* __restrict__ y,
                                                             const T* __restrict__ x, int64_t n8, int K8,
                                                             const float* __restrict__ coef, T* __restrict__ dx,
-                                                            T* __restrict__ dres) {
+                                                            T* __restrict__ dres, uint16_t* __restrict__ planes = nullptr) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= n8) return;
   const int K = K8 * 8;
@@ -396,6 +407,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply2_kernel(const T* __restrict_
   }
   st8(dx + e * 8, o);
   if (dres) st8(dres + e * 8, og);
+  if (planes) store_planes8(planes, n8 * 8, e, o);  // dx as bf16x3 planes too (bn_apply_kernel)
 }
 
 // sums -> coef for the legacy mx_bn_bwd_apply entry
@@ -710,6 +722,16 @@ extern "C" int mx_bn_apply(const void* x, int xdtype, int64_t M, int64_t K, cons
   return MX_OK;
 }
 
+extern "C" int mx_bn_apply_p(const float* x, int64_t M, int64_t K, const float* scale, const float* shift,
+                             const float* residual, int act, float* y, uint16_t* planes, mx_stream_t stream) {
+  MX_CHECK_ARG(K % 8 == 0 && x && y && planes, "bn_apply_p: K %% 8 != 0 or a null operand");
+  if (M == 0) return MX_OK;
+  bn_apply_kernel<float, float><<<grid_rows(M, K / 8), 256, 0, (hipStream_t)stream>>>(x, M, K, scale, shift, residual,
+                                                                                       act, y, planes);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
 extern "C" size_t mx_bn_bwd_workspace(int64_t M, int64_t K) {
   if (M <= 0 || K <= 0 || K % 8) return 0;
   BwdGeo g = bwd_geo(M, K);
@@ -766,6 +788,22 @@ extern "C" int mx_bn_bwd_apply_ex(const void* dy, const void* y, const void* x, 
   if (M == 0) return MX_OK;
   const int64_t n8 = M * (K / 8);
   MX_DT_DISPATCH(dtype, bn_bwd_apply_launch, dy, y, x, n8, (int)(K / 8), act, coef, dx, dres, (hipStream_t)stream);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+extern "C" int mx_bn_bwd_apply_p(const float* dy, const float* y, const float* x, int64_t M, int64_t K, int act,
+                                 const float* coef, float* dx, float* dres, uint16_t* planes, mx_stream_t stream) {
+  MX_CHECK_ARG(K % 8 == 0 && K > 0 && K < (1 << 24) && planes, "bn_bwd_apply_p: K %% 8 != 0 or no planes");
+  MX_CHECK_ARG(act >= 0 && act <= 2 && (act == 0 || y), "bn_bwd_apply_p: act 0/1/2 (y required for 1, 2)");
+  if (M == 0) return MX_OK;
+  const int64_t n8 = M * (K / 8);
+  const unsigned blocks = (unsigned)cdiv(n8, 256);
+  hipStream_t st = (hipStream_t)stream;
+  const int K8 = (int)(K / 8);
+  if (act == 1) bn_bwd_apply2_kernel<1, float><<<blocks, 256, 0, st>>>(dy, y, x, n8, K8, coef, dx, dres, planes);
+  else if (act == 2) bn_bwd_apply2_kernel<2, float><<<blocks, 256, 0, st>>>(dy, y, x, n8, K8, coef, dx, dres, planes);
+  else bn_bwd_apply2_kernel<0, float><<<blocks, 256, 0, st>>>(dy, y, x, n8, K8, coef, dx, dres, planes);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

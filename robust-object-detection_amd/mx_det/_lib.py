@@ -169,6 +169,8 @@ _SIGS = {
     "mx_conv2d_wgrad_x3": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_sz,
                                    c_vp]),
     "mx_split_planes": (c_int, [c_vp, c_i64, c_vp, c_vp]),
+    "mx_bn_apply_p": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
+    "mx_bn_bwd_apply_p": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_conv_workspace_x3p": (c_sz, [ctypes.POINTER(ConvShape), c_int]),
     "mx_conv2d_fwd_x3p": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_sz,
                                   c_vp]),

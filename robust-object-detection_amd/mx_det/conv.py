@@ -457,11 +457,16 @@ def planes_for(n_elems, chans, krs):
             and n_elems >= int(os.environ.get("MX_X3_PLANES_MIN", str(4 << 20))))
 
 
-def _x_planes(x, K, R, S, dense):
-    """x's split_planes when the conv's forward (and its wgrad) should read planes, else None."""
+def _x_planes(x, K, R, S, dense, wgrad):
+    """x's split_planes when the conv's forward (and its wgrad) should read planes, else None: the
+    planes its producer wrote beside it (`x._mx_planes`, ConvBNAct with planes_krs), or -- only when
+    the weight takes a gradient (the wgrad gains most: per-shape timings) -- one split pass."""
     if not is_x3(x) or dense or R * S > 64 or not planes_for(x.numel(), x.shape[3], K * R * S):
         return None
-    return split_planes(x)
+    pl = getattr(x, "_mx_planes", None)
+    if pl is not None and pl.shape[1:] == x.shape:
+        return pl
+    return split_planes(x) if wgrad else None
 
 
 def _dy_planes(dy, C, R, S, dense):
@@ -918,7 +923,7 @@ class ConvAct(torch.autograd.Function):
         dense = _is_dense(x.shape, w.shape[2], w.shape[3], stride, pad)
         # narrow heads (RPN cls+box 15, predictor 35): the dgrad operand is zero-padded to K8
         wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(K), need_dx, dense, split=is_x3(x))
-        xp = _x_planes(x, K, w.shape[2], w.shape[3], dense)
+        xp = _x_planes(x, K, w.shape[2], w.shape[3], dense, ctx.needs_input_grad[1])
         y = conv_fwd(x, wk, stride, pad, bias=b.detach() if b is not None else None, act=act, out_dtype=out_dtype,
                      xp=xp)
         ctx.save_for_backward(x, y, wt if need_dx else None, xp)
@@ -1069,12 +1074,12 @@ class ConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, residual, rmean, rvar, stride, pad, act, eps, momentum, link=None,
-                bnb_own=None, bnb_feed=None):
+                bnb_own=None, bnb_feed=None, planes_krs=0):
         need_dx = ctx.needs_input_grad[0]
         ctx.link, ctx.role = link if link is not None else (None, None)
         ctx.bnb_own, ctx.bnb_feed = bnb_own, bnb_feed
         wk, wt = operands(w, x.shape[3], stride, pad, _ceil8(w.shape[0]), need_dx, split=is_x3(x))
-        xp = _x_planes(x, w.shape[0], w.shape[2], w.shape[3], False)
+        xp = _x_planes(x, w.shape[0], w.shape[2], w.shape[3], False, ctx.needs_input_grad[1])
         z, st = conv_fwd(x, wk, stride, pad, stats=True, cin=w.shape[1], xp=xp)
         K = w.shape[0]
         M = z.numel() // K
@@ -1082,7 +1087,15 @@ class ConvBNAct(torch.autograd.Function):
         y = torch.empty_like(z)
         res = residual.contiguous() if residual is not None else None
         t0 = _timer.start() if _timer else None
-        call("mx_bn_apply", _p(z), dcode(z), M, K, _p(scale), _p(shift), _p(res), int(act), _p(y), dcode(y), _s())
+        # planes_krs: the output channels x taps of the conv this output feeds (frcnn marks the producers
+        # of the P2 / box-head 3x3 inputs): when that conv will read pre-split planes, write them here
+        if planes_krs and is_x3(z) and planes_for(M * K, K, planes_krs):
+            yp = torch.empty((2,) + tuple(z.shape), dtype=torch.bfloat16, device=z.device)
+            call("mx_bn_apply_p", _p(z), M, K, _p(scale), _p(shift), _p(res), int(act), _p(y), _p(yp), _s())
+            y._mx_planes = yp
+        else:
+            call("mx_bn_apply", _p(z), dcode(z), M, K, _p(scale), _p(shift), _p(res), int(act), _p(y), dcode(y),
+                 _s())
         if _timer:  # bn kinds record algorithmic HBM bytes instead of FLOPs
             _timer.stop("bn_apply", M * K * z.element_size() * (2 + (1 if res is not None else 0)), t0, f"{M}x{K}")
         ctx.save_for_backward(x, wt if need_dx else None, z, y, mean, invstd, gamma, xp)
@@ -1120,11 +1133,17 @@ class ConvBNAct(torch.autograd.Function):
         dz = torch.empty_like(z)
         dres = torch.empty_like(z) if has_res else None
         t0 = _timer.start() if _timer else None
-        call("mx_bn_bwd_apply_ex", _p(gy), _p(y), _p(z), dcode(z), M, K, int(act), _p(coef), _p(dz), _p(dres), _s())
+        # dz feeds this conv's dgrad and wgrad: as pre-split planes too when they read them (_dy_planes)
+        dzp = None
+        if is_x3(z) and R * S <= 64 and planes_for(z.numel(), K, x.shape[3] * R * S):
+            dzp = torch.empty((2,) + tuple(z.shape), dtype=torch.bfloat16, device=z.device)
+            call("mx_bn_bwd_apply_p", _p(gy), _p(y), _p(z), M, K, int(act), _p(coef), _p(dz), _p(dres), _p(dzp), _s())
+        else:
+            call("mx_bn_bwd_apply_ex", _p(gy), _p(y), _p(z), dcode(z), M, K, int(act), _p(coef), _p(dz), _p(dres),
+                 _s())
         if _timer:
             _timer.stop("bn_bwd_apply", M * K * z.element_size() * (4 + (1 if has_res else 0)), t0, f"{M}x{K}")
         dx = dw = None
-        dzp = _dy_planes(dz, x.shape[3], R, S, False)
         wg = _wgrad_plan(ctx, dz, x, K, R, S, stride, pad, cin=wshape[1], dyp=dzp, xp=xp)  # before the dgrad
         link = ctx.link
         if ctx.role == "sink" and dres is not None:
@@ -1145,7 +1164,7 @@ class ConvBNAct(torch.autograd.Function):
             dw = _wgrad_run(wg)
         dgamma = sums[1] if ctx.needs_input_grad[2] else None
         dbeta = sums[0] if ctx.needs_input_grad[3] else None
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None
 
 
 class Conv2d(torch.nn.Module):
@@ -1227,7 +1246,8 @@ def conv_bn(x, conv, bn, act, residual=None, link=None, bnb_own=None, bnb_feed=N
         if bn.num_batches_tracked is not None and id(bn) not in _nbt_batched:
             bn.num_batches_tracked.add_(1)
         return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
-                               conv.stride, conv.padding, act, bn.eps, bn.momentum, link, bnb_own, bnb_feed)
+                               conv.stride, conv.padding, act, bn.eps, bn.momentum, link, bnb_own, bnb_feed,
+                               getattr(conv, "planes_krs", 0))
     return eval_conv_bn(x, conv, bn, act, residual)
 
 

@@ -48,6 +48,9 @@ class Bottleneck(nn.Module):
         self.conv3 = Conv2d(planes, planes * 4, 1, bias=False)
         self.bn3 = BatchNorm2d(planes * 4)
         self.downsample = downsample
+        # bn1's output is conv2's (3x3, planes -> planes) input: written as pre-split planes beside it
+        # when conv2 reads them (conv.planes_for)
+        self.conv1.planes_krs = planes * 9
 
     def forward(self, x, be, feed=None, own_out=False):
         """feed: the previous block's bn3 BNBLink (this block's conv1 dgrad, identity gradient included,
@@ -155,6 +158,12 @@ class FeaturePyramidNetwork(nn.Module):
                                            for c in in_channels_list])
         self.layer_blocks = nn.ModuleList([ConvNormAct(out_channels, out_channels, 3, act=ACT_NONE)
                                            for _ in in_channels_list])
+        # producers of 3x3-conv inputs (pre-split planes written beside the output when the consumer
+        # reads them): each inner block feeds its level's 3x3 output block, and the P2 output block
+        # feeds the level-0 RPN head conv (P3..P6 go through the RPN canvas)
+        for blk in self.inner_blocks:
+            blk[0].planes_krs = out_channels * 9
+        self.layer_blocks[0][0].planes_krs = out_channels * 9
         for m in self.modules():
             if isinstance(m, Conv2d):
                 nn.init.kaiming_uniform_(m.weight, a=1)
@@ -175,6 +184,9 @@ class FeaturePyramidNetwork(nn.Module):
                 return self.layer_blocks[idx](t, be)
             side.wait_stream(main)
             t.record_stream(side)
+            pl = getattr(t, "_mx_planes", None)  # its pre-split planes, read there too
+            if pl is not None:
+                pl.record_stream(side)
             with torch.cuda.stream(side):
                 return self.layer_blocks[idx](t, be)
         last_inner = self.inner_blocks[-1](feats[-1], be)
@@ -727,6 +739,8 @@ class FastRCNNConvFCHead(nn.Sequential):
     def __init__(self, in_channels=256, conv_layers=(256, 256, 256, 256), fc_layers=(1024,), hw=7):
         blocks, prev = [], in_channels
         for c in conv_layers:
+            if blocks:  # the previous conv's output is this 3x3 conv's input (pre-split planes)
+                blocks[-1][0].planes_krs = c * 9
             blocks.append(ConvNormAct(prev, c, 3, act=ACT_RELU))
             prev = c
         blocks.append(nn.Flatten())
