@@ -118,3 +118,32 @@ def test_train_step_with_planes_is_bitwise(dev, monkeypatch):
     for (la, ga), (lb, gb) in zip(res["0"], res["1"]):
         assert la == lb, (la, lb)
         assert len(ga) == len(gb) and all(torch.equal(a, b) for a, b in zip(ga, gb))
+
+
+@pytest.mark.parametrize("act", [0, 1])
+def test_bn_apply_and_bwd_apply_planes(dev, act):
+    """mx_bn_apply_p / mx_bn_bwd_apply_p: the same y / dx as the plain entries, and planes equal to
+    split_planes of them."""
+    from mx_det import conv as mc
+    from mx_det._lib import call
+    M, K = 3000, 96
+    g = torch.Generator().manual_seed(1)
+    z, res, gy = (torch.randn(M, K, generator=g).to(dev) for _ in range(3))
+    scale, shift = (torch.randn(K, generator=g).to(dev) for _ in range(2))
+    coef = torch.randn(3, K, generator=g).to(dev)
+    y0, y1 = torch.empty_like(z), torch.empty_like(z)
+    yp = torch.empty((2, M, K), dtype=torch.bfloat16, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    call("mx_bn_apply", z.data_ptr(), 0, M, K, scale.data_ptr(), shift.data_ptr(), res.data_ptr(), act, y0.data_ptr(), 0, s)
+    call("mx_bn_apply_p", z.data_ptr(), M, K, scale.data_ptr(), shift.data_ptr(), res.data_ptr(), act, y1.data_ptr(),
+         yp.data_ptr(), s)
+    d0, d1, r0, r1 = (torch.empty_like(z) for _ in range(4))
+    dp = torch.empty((2, M, K), dtype=torch.bfloat16, device=dev)
+    call("mx_bn_bwd_apply_ex", gy.data_ptr(), y0.data_ptr(), z.data_ptr(), 0, M, K, act, coef.data_ptr(), d0.data_ptr(),
+         r0.data_ptr(), s)
+    call("mx_bn_bwd_apply_p", gy.data_ptr(), y0.data_ptr(), z.data_ptr(), M, K, act, coef.data_ptr(), d1.data_ptr(),
+         r1.data_ptr(), dp.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1) and torch.equal(yp.view(torch.int16), mc.split_planes(y0).view(torch.int16))
+    assert torch.equal(d0, d1) and torch.equal(r0, r1)
+    assert torch.equal(dp.view(torch.int16), mc.split_planes(d0).view(torch.int16))
