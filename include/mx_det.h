@@ -76,6 +76,16 @@ int mx_match_assign_batched(const float* gt, const int64_t* gt_labels, const int
                             void* labels, float* targets, int32_t* counts, void* ws, size_t ws_bytes,
                             mx_stream_t stream);
 
+/* det_utils.BalancedPositiveNegativeSampler in one launch (RegionProposalNetwork.fg_bg_sampler and
+ * RoIHeads.select_training_samples, reached from train_frcnn_baseline.py:171): per row n of labels [N][L]
+ * (ldtype MX_F32: the RPN's float 1 / 0 / -1; 2: int64, the RoI head's class >= 1 / 0 / -1), num_pos =
+ * min(#(label >= 1), int(batch * positive_fraction)) positives and num_neg = min(#(label == 0), batch -
+ * num_pos) negatives, each the num smallest keys [N][L] among its candidates (ties by lowest index: a
+ * uniform draw without replacement for i.i.d. uniform keys). pos / neg uint8 [N][L] masks, sm (nullable)
+ * their union, nums int32 [N][2] = (num_pos, num_neg). One 1024-thread workgroup per row. */
+int mx_sample_draw(const void* labels, int ldtype, const float* keys, int64_t N, int64_t L, int batch,
+                   double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm, int32_t* nums, mx_stream_t stream);
+
 /* torchvision.ops.box_iou -> out[n,m] (test/diagnostic entry). */
 int mx_box_iou(const float* b1, int64_t n, const float* b2, int64_t m, float* out, mx_stream_t stream);
 

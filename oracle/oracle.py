@@ -233,3 +233,25 @@ def jpeg_reconstruct(coefs, info, bgr=False):
     if rc != 0:
         raise MemoryError("orc_jpeg_reconstruct")
     return out
+
+
+def balanced_sample(labels, keys, batch, positive_fraction):
+    """torchvision det_utils.BalancedPositiveNegativeSampler.__call__ (RegionProposalNetwork /
+    RoIHeads.select_training_samples, reached from train_frcnn_baseline.py:171) with the uniform
+    permutation restated as keys: per row num_pos = min(#(label >= 1), int(batch * frac)) and num_neg =
+    min(#(label == 0), batch - num_pos), each class's num smallest keys drawn, ties by lowest index (a
+    stable sort). labels [N, L], keys [N, L] -> (pos, neg bool [N, L], nums int [N, 2])."""
+    labels, keys = np.asarray(labels), np.asarray(keys, np.float32)
+    N, L = labels.shape
+    pos, neg = np.zeros((N, L), bool), np.zeros((N, L), bool)
+    nums = np.zeros((N, 2), np.int64)
+    P = int(batch * positive_fraction)
+    for r in range(N):
+        cp, cn = np.nonzero(labels[r] >= 1)[0], np.nonzero(labels[r] == 0)[0]
+        kp = min(len(cp), P)
+        kn = min(len(cn), batch - kp)
+        for cand, k, out in ((cp, kp, pos), (cn, kn, neg)):
+            order = np.argsort(keys[r, cand], kind="stable")
+            out[r, cand[order[:k]]] = True
+        nums[r] = (kp, kn)
+    return pos, neg, nums

@@ -51,6 +51,7 @@ _SIGS = {
     "mx_match_assign_batched": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_f, c_f, c_int, c_int, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_box_iou": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "mx_sample_draw": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_int, c_d, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_nms_workspace": (c_sz, [c_i64, c_i64]),
     "mx_nms_grouped_workspace": (c_sz, [c_i64, c_i64, c_i64]),
     "mx_batched_nms_grouped_sorted": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_d, c_vp, c_vp, c_i64,

@@ -162,6 +162,9 @@ class HipBackend:
     def level_topk(self, scores, num_per_level, k):
         return ops.level_topk(scores, num_per_level, k)
 
+    def sample_draw(self, labels, keys, batch, positive_fraction, with_union=False):
+        return ops.sample_draw(labels, keys, batch, positive_fraction, with_union)
+
     def proposal_nms(self, boxes, scores, lvl, group, G, L, thr, max_seg):
         return ops.batched_nms_grouped(boxes, scores, lvl, group, G, L, thr, max_seg)
 

@@ -405,6 +405,12 @@ def _compact(mask, total):
     return idx[:total]
 
 
+def _fused_sampler():
+    """MX_FUSED_SAMPLER (default on): both samplers draw with mx_sample_draw; off, the RPN's rows go
+    to torch.topk and the RoI rows to mx_level_topk (the pre-fusion paths, same keys, same picks)."""
+    return os.environ.get("MX_FUSED_SAMPLER", "1") != "0"
+
+
 class BalancedPositiveNegativeSampler:
     """torchvision det_utils.BalancedPositiveNegativeSampler(batch_size_per_image, positive_fraction):
     per image min(#pos, B*frac) positives (label >= 1) and min(#neg, B - num_pos) negatives (label 0),
@@ -417,6 +423,7 @@ class BalancedPositiveNegativeSampler:
     def __init__(self, batch_size_per_image, positive_fraction):
         self.batch, self.frac = batch_size_per_image, positive_fraction
         self.rand = None
+        self.last = None   # (union mask, per-row counts int32 [N, 2]) of the last fused draw
 
     def __call__(self, lab, be=None, counts=None):
         """be: a backend with level_topk draws the k smallest keys with it (used for the RoI sampler's
@@ -424,6 +431,13 @@ class BalancedPositiveNegativeSampler:
         workgroups). counts: per-row (#label >= 1, #label == 0) when the matcher already produced them
         (int [N, 2]), sparing two reductions over the rows."""
         L = lab.shape[1]
+        if be is not None and hasattr(be, "sample_draw") and lab.is_cuda and _fused_sampler():
+            # the whole draw in one launch (mx_sample_draw: counts, per-class radix select, marks);
+            # the union and the per-row counts stay available for the RoI sampler (self.last)
+            r = self.rand(lab.shape, lab.device) if self.rand is not None else torch.rand(lab.shape, device=lab.device)
+            pos, neg, un, nums = be.sample_draw(lab, r, self.batch, self.frac, with_union=True)
+            self.last = (un, nums)
+            return pos, neg
         pos, neg = lab >= 1, lab == 0
         P = int(self.batch * self.frac)
         if counts is not None:
@@ -624,7 +638,7 @@ class RegionProposalNetwork(nn.Module):
                     reg_targets.append(tg)
                 lab = torch.stack(labels)                 # [N, A] 1 / 0 / -1
                 rt = torch.stack(reg_targets)             # [N, A, 4]
-            pm, nm = self.fg_bg_sampler(lab, counts=lcnt)
+            pm, nm = self.fg_bg_sampler(lab, be if _fused_sampler() else None, counts=lcnt)
             return lab, rt, pm, nm
 
         def loss_of(tgt):
@@ -689,7 +703,7 @@ class RegionProposalNetwork(nn.Module):
         gtp, _, gcnt = gt
         _, lab, rt, lcnt = be.match_assign_batched(gtp, gcnt, anchors, self.fg, self.bg, True, 1,
                                                    weights=RPN_WEIGHTS, with_counts=True)
-        pm, nm = self.fg_bg_sampler(lab, counts=lcnt)
+        pm, nm = self.fg_bg_sampler(lab, be if _fused_sampler() else None, counts=lcnt)
         return lab, rt, pm, nm
 
     def join_losses(self):
@@ -858,9 +872,15 @@ class RoIHeads(nn.Module):
                     tg_l.append(tg.to(dev))
                 lab_b, tg_p = torch.stack(lab_l), torch.stack(tg_l)
             lab_p = torch.where(valid, lab_b, -1)
+            self.fg_bg_sampler.last = None
             pos_m, neg_m = self.fg_bg_sampler(lab_p, be)
-            sm = (pos_m | neg_m).flatten()
-            total = int(sm.sum())                         # the stage's one host sync (sizes the RoI head)
+            if self.fg_bg_sampler.last is not None:       # the fused draw's union and per-row counts
+                un, nums = self.fg_bg_sampler.last
+                sm = un.flatten()
+                total = int(nums.sum())                   # the stage's one host sync (sizes the RoI head)
+            else:
+                sm = (pos_m | neg_m).flatten()
+                total = int(sm.sum())                     # the stage's one host sync (sizes the RoI head)
             cm = lab_p.shape[1]
             if hasattr(be, "roi_compact") and os.environ.get("MX_FUSED_ROI_COMPACT", "1") != "0":
                 # per image ascending, as torch.where per image: one launch after the sync

@@ -280,6 +280,25 @@ def roi_compact(mask, total, cm, box, lab, tg):
     return rois, lo, to
 
 
+def sample_draw(labels, keys, batch, positive_fraction, with_union=False):
+    """BalancedPositiveNegativeSampler's draw in one launch (mx_sample_draw): labels [N, L] (float32: the
+    RPN's 1 / 0 / -1, or int64: the RoI head's class / 0 / -1), keys [N, L] uniform -> (pos, neg bool
+    [N, L], union bool [N, L] or None, nums int32 [N, 2] = (num_pos, num_neg)); per row the num smallest
+    keys of each class's candidates, ties by lowest index."""
+    _dev(labels, keys)
+    _check(labels.dim() == 2 and keys.shape == labels.shape and keys.dtype == torch.float32, "sample_draw: shapes")
+    _check(labels.dtype in (torch.float32, torch.int64), "sample_draw: labels must be float32 or int64")
+    N, L = labels.shape
+    dev = labels.device
+    pos = torch.empty((N, L), dtype=torch.uint8, device=dev)
+    neg = torch.empty_like(pos)
+    un = torch.empty_like(pos) if with_union else None
+    nums = torch.empty((N, 2), dtype=torch.int32, device=dev)
+    call("mx_sample_draw", _p(labels.contiguous()), 0 if labels.dtype == torch.float32 else 2, _p(keys.contiguous()), N,
+         L, int(batch), float(positive_fraction), _p(pos), _p(neg), _p(un), _p(nums), _stream())
+    return pos.view(torch.bool), neg.view(torch.bool), (un.view(torch.bool) if un is not None else None), nums
+
+
 def level_topk(scores, num_per_level, k):
     """RegionProposalNetwork._get_top_n_idx (torchvision rpn.py): per image row of scores [N, A] and
     per level, the indices of the min(k, n_l) largest scores (value descending, ties by index) plus
