@@ -46,6 +46,9 @@ int mx_trace_marker(int id, mx_stream_t stream);
  * a process creating more pool streams than that (a model per test, a loader per epoch) would alias
  * two of them -- e.g. a side stream with a graph's capture stream. */
 int mx_stream_create(int device, mx_stream_t* out);
+/* mx_stream_create at the device's highest stream priority (hipDeviceGetStreamPriorityRange's greatest):
+ * the DataParallel NMS-flag read, a 4-B copy that must not wait behind the step's kernels. */
+int mx_stream_create_high_priority(int device, mx_stream_t* out);
 
 /* ---------------------------------------------------------------------------------------------
  * Anchor assignment: torchvision box_iou + Matcher (+ label/target construction), fused.
@@ -85,6 +88,16 @@ int mx_match_assign_batched(const float* gt, const int64_t* gt_labels, const int
  * their union, nums int32 [N][2] = (num_pos, num_neg). One 1024-thread workgroup per row. */
 int mx_sample_draw(const void* labels, int ldtype, const float* keys, int64_t N, int64_t L, int batch,
                    double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm, int32_t* nums, mx_stream_t stream);
+
+/* The same draw for long rows (the RPN's anchors) split over many workgroups: a histogram launch, a
+ * split launch (candidates below each class's boundary bin drawn, the boundary bin's appended to a
+ * per-(row, class) list) and a finishing launch per row (radix select of the (key, index) pairs in the
+ * lists), after a memset of the workspace's counters. ws: mx_sample_draw_workspace(N, L) bytes; rows of
+ * at most 16,384 elements, or ws == NULL, take mx_sample_draw. Results identical to mx_sample_draw. */
+size_t mx_sample_draw_workspace(int64_t N, int64_t L);
+int mx_sample_draw_ws(const void* labels, int ldtype, const float* keys, int64_t N, int64_t L, int batch,
+                      double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm, int32_t* nums, void* ws,
+                      size_t ws_bytes, mx_stream_t stream);
 
 /* torchvision.ops.box_iou -> out[n,m] (test/diagnostic entry). */
 int mx_box_iou(const float* b1, int64_t n, const float* b2, int64_t m, float* out, mx_stream_t stream);

@@ -833,6 +833,23 @@ extern "C" int mx_trace_marker(int id, mx_stream_t stream) {
   return MX_OK;
 }
 
+// the same with the device's highest stream priority (hipStreamCreateWithPriority): a small hand-off that must
+// not queue behind the step's kernels on a shared hardware queue (DataParallel's NMS-flag read)
+extern "C" int mx_stream_create_high_priority(int device, mx_stream_t* out) {
+  MX_CHECK_ARG(out != nullptr, "mx_stream_create_high_priority: null output");
+  int prev = 0;
+  MX_HIP(hipGetDevice(&prev));
+  MX_HIP(hipSetDevice(device));
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  hipStream_t s = nullptr;
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest);
+  MX_HIP(hipSetDevice(prev));
+  MX_HIP(e);
+  *out = (mx_stream_t)s;
+  return MX_OK;
+}
+
 extern "C" int mx_stream_create(int device, mx_stream_t* out) {
   MX_CHECK_ARG(out != nullptr, "mx_stream_create: null output");
   int prev = 0;

@@ -44,6 +44,7 @@ _SIGS = {
     "mx_last_error": (ctypes.c_char_p, []),
     "mx_trace_marker": (c_int, [c_int, c_vp]),
     "mx_stream_create": (c_int, [c_int, c_vp]),
+    "mx_stream_create_high_priority": (c_int, [c_int, c_vp]),
     "mx_match_workspace": (c_sz, [c_i64, c_i64]),
     "mx_match_assign": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_f, c_f, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                 c_vp, c_sz, c_vp]),
@@ -52,6 +53,8 @@ _SIGS = {
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_box_iou": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "mx_sample_draw": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_int, c_d, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mx_sample_draw_workspace": (c_sz, [c_i64, c_i64]),
+    "mx_sample_draw_ws": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_int, c_d, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_nms_workspace": (c_sz, [c_i64, c_i64]),
     "mx_nms_grouped_workspace": (c_sz, [c_i64, c_i64, c_i64]),
     "mx_batched_nms_grouped_sorted": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_d, c_vp, c_vp, c_i64,

@@ -996,7 +996,7 @@ def capture_stream(device):
 _dedicated = {}
 
 
-def dedicated_stream(device, name):
+def dedicated_stream(device, name, high_priority=False):
     """The framework's side stream `name` on `device`: a HIP stream of its own (mx_stream_create),
     created once. torch.cuda.Stream() hands out a round-robin pool of 32 streams per device, so a
     process that creates more (a model per test, a loader per epoch) silently aliases two of them --
@@ -1007,7 +1007,7 @@ def dedicated_stream(device, name):
     s = _dedicated.get((idx, name))
     if s is None:
         h = ctypes.c_void_p()
-        call("mx_stream_create", idx, ctypes.addressof(h))
+        call("mx_stream_create_high_priority" if high_priority else "mx_stream_create", idx, ctypes.addressof(h))
         s = _dedicated[(idx, name)] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
     return s
 

@@ -1500,9 +1500,12 @@ class _SegGraphFn(torch.autograd.Function):
                     if g is not None and p.grad is g:
                         p.grad = g.clone()
         hook = tg.model.__dict__.get("_mx_seg_ready")
+        # the .grad bookkeeping of every segment runs before the first replay: between two replays the
+        # host only fires the hand-off hook (issuing a collective), so the segment graphs queue back
+        # to back; a gradient accumulated onto an existing .grad (add_) must follow its graph
+        plan = []
         for keys, graph in tg.bwd:
-            graph.replay()
-            ps = []
+            ps, acc = [], []
             for key in keys:
                 for p, g in zip(tg.seg_params[key], tg.static_grads[key]):
                     if g is None:
@@ -1511,7 +1514,12 @@ class _SegGraphFn(torch.autograd.Function):
                     if p.grad is None:
                         p.grad = g
                     else:
-                        p.grad.add_(g)
+                        acc.append((p.grad, g))
+            plan.append((keys, graph, ps, acc))
+        for keys, graph, ps, acc in plan:
+            graph.replay()
+            for pg, g in acc:
+                pg.add_(g)
             if hook is not None and ps:  # every group up to the segment's last trained key is final
                 hook([k for k in keys if tg.seg_params[k]][-1], ps)
         return None, None, None

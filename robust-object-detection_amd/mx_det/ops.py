@@ -280,7 +280,10 @@ def roi_compact(mask, total, cm, box, lab, tg):
     return rois, lo, to
 
 
-def sample_draw(labels, keys, batch, positive_fraction, with_union=False):
+SAMPLE_SLICED_MIN = 16384  # mx_sample_draw_ws's threshold (rows at most this long: one workgroup per row)
+
+
+def sample_draw(labels, keys, batch, positive_fraction, with_union=False, sliced=True):
     """BalancedPositiveNegativeSampler's draw in one launch (mx_sample_draw): labels [N, L] (float32: the
     RPN's 1 / 0 / -1, or int64: the RoI head's class / 0 / -1), keys [N, L] uniform -> (pos, neg bool
     [N, L], union bool [N, L] or None, nums int32 [N, 2] = (num_pos, num_neg)); per row the num smallest
@@ -294,8 +297,15 @@ def sample_draw(labels, keys, batch, positive_fraction, with_union=False):
     neg = torch.empty_like(pos)
     un = torch.empty_like(pos) if with_union else None
     nums = torch.empty((N, 2), dtype=torch.int32, device=dev)
-    call("mx_sample_draw", _p(labels.contiguous()), 0 if labels.dtype == torch.float32 else 2, _p(keys.contiguous()), N,
-         L, int(batch), float(positive_fraction), _p(pos), _p(neg), _p(un), _p(nums), _stream())
+    lab, ky, ld = labels.contiguous(), keys.contiguous(), 0 if labels.dtype == torch.float32 else 2
+    if L > SAMPLE_SLICED_MIN and sliced:  # the RPN's long rows: split over many workgroups
+        nb = _lib.load().mx_sample_draw_workspace(N, L)
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        call("mx_sample_draw_ws", _p(lab), ld, _p(ky), N, L, int(batch), float(positive_fraction), _p(pos), _p(neg),
+             _p(un), _p(nums), _p(ws), nb, _stream())
+    else:
+        call("mx_sample_draw", _p(lab), ld, _p(ky), N, L, int(batch), float(positive_fraction), _p(pos), _p(neg),
+             _p(un), _p(nums), _stream())
     return pos.view(torch.bool), neg.view(torch.bool), (un.view(torch.bool) if un is not None else None), nums
 
 

@@ -46,3 +46,23 @@ def test_error_path_without_gpu():
     rc = lib.mx_box_iou(None, -1, None, 5, None, None)
     assert rc == -1 and b"bad sizes" in lib.mx_last_error()
     assert lib.mx_version() == 1
+
+
+def test_binding_arity_matches_header():
+    """Every ctypes signature in mx_det._lib has as many parameters as the header's prototype (ctypes
+    passes surplus arguments through unchecked, so a missing argtype shifts every later argument)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "robust-object-detection_amd"))
+    from mx_det import _lib
+    src = re.sub(r"/\*.*?\*/", "", open(HDR).read(), flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    protos = {m.group(1): m.group(2) for m in re.finditer(r"\b(mx_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", src)}
+    bad = []
+    for name, (_, argtypes) in _lib._SIGS.items():
+        if name not in protos:
+            continue
+        params = protos[name].strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        if n != len(argtypes):
+            bad.append((name, n, len(argtypes)))
+    assert not bad, bad

@@ -109,7 +109,7 @@ def test_dp_issue_order_is_canonical_whatever_the_hooks():
         dp._work, dp.issued, dp.last_issued, dp.world = {}, [], [], 1
         dp.flats = {k: (torch.zeros(1), []) for k in keys + [("bucket", 0)]}
         dp.scale, dp._copied = None, 0
-        dp.rpn, dp._flag_host = None, None
+        dp.rpn, dp._flag_host, dp._adopt = None, None, {}
         dp._start = lambda key: (_Done(), key)
         return dp
 

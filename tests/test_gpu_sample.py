@@ -1,6 +1,6 @@
 """mx_sample_draw, the fused BalancedPositiveNegativeSampler draw: bit-exact masks and counts against
 oracle.balanced_sample (stable sort of each class's keys) on the RPN's float32 1 / 0 / -1 rows at the
-headline anchor count and the RoI head's int64 class / 0 / -1 rows, with key ties, classes short of
+headline anchor count (the sliced three-launch form, checked against the one-workgroup kernel too) and the RoI head's int64 class / 0 / -1 rows, with key ties, classes short of
 their quota, empty classes, rows shorter than one tile and row lengths off the 1,024 grid; and the
 sampler class on both paths (MX_FUSED_SAMPLER=1 / 0) drawing the same masks from the same keys."""
 import numpy as np
@@ -35,6 +35,9 @@ CASES = [  # N, L, p_pos, p_neg, int labels, key levels (0: continuous), batch, 
     (1, 1025, 0.3, 0.3, True, 2, 512, 0.25),           # two key values only
     (2, 0, 0.0, 0.0, True, 0, 512, 0.25),              # empty rows
     (1, 70001, 1.0, 0.0, False, 0, 256, 0.5),          # all positives
+    (2, 50000, 0.3, 0.6, True, 2, 512, 0.25),          # long rows, two key values: whole classes tie
+    (1, 16385, 0.01, 0.5, False, 1, 256, 0.5),         # just past the sliced threshold, every key equal
+    (3, 40000, 0.0, 0.0, False, 0, 256, 0.5),          # long rows without candidates
 ]
 
 
@@ -55,6 +58,9 @@ def test_sample_draw_matches_oracle(dev, case):
     assert np.array_equal(un.cpu().numpy(), rp | rn)
     p2, n2, u2, nums2 = ops.sample_draw(lab.to(dev), keys.to(dev), B, fr)
     assert u2 is None and torch.equal(p2, pos) and torch.equal(n2, neg) and torch.equal(nums2, nums)
+    if L > ops.SAMPLE_SLICED_MIN:  # the one-workgroup-per-row kernel on the same long rows
+        p3, n3, u3, nums3 = ops.sample_draw(lab.to(dev), keys.to(dev), B, fr, with_union=True, sliced=False)
+        assert torch.equal(p3, pos) and torch.equal(n3, neg) and torch.equal(u3, un) and torch.equal(nums3, nums)
 
 
 def test_sample_draw_negative_zero_ties_positive_zero(dev):

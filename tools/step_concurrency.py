@@ -18,7 +18,8 @@ iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for
 
 
 def sh(n):
-    return n.replace("void ", "").replace("at::native::", "").replace("mx::", "").split("(")[0][:48]
+    return (n.replace("void ", "").replace("at::native::", "").replace("(anonymous namespace)::", "")
+            .replace("mx::", "").split("(")[0][:48])
 
 
 def cat(n):
