@@ -45,8 +45,6 @@ first all-reduce of every step carries one extra float, this rank's failure flag
 `sync_gradients()` reads the reduced flag (a wait on that first collective only, long finished by
 then) and raises on every rank before the optimizer step, with the local message where there is one.
 """
-import os
-
 import torch
 import torch.distributed as dist
 
@@ -231,7 +229,7 @@ class DataParallel:
         # the host work after the last collective is issued stays short (the GPU drains meanwhile): the
         # flag read waits on the first collective only; only gradients _start found outside their slot
         # are re-pointed
-        if pending and os.environ.get("MX_DP_NMS_FLAG", "1") != "0":
+        if pending:
             self._check_flag(*pending[0])
         for _, key in pending:
             flat, _ = self.flats[key]
