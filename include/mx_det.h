@@ -84,10 +84,12 @@ int mx_match_assign_batched(const float* gt, const int64_t* gt_labels, const int
  * (ldtype MX_F32: the RPN's float 1 / 0 / -1; 2: int64, the RoI head's class >= 1 / 0 / -1), num_pos =
  * min(#(label >= 1), int(batch * positive_fraction)) positives and num_neg = min(#(label == 0), batch -
  * num_pos) negatives, each the num smallest keys [N][L] among its candidates (ties by lowest index: a
- * uniform draw without replacement for i.i.d. uniform keys). pos / neg uint8 [N][L] masks, sm (nullable)
+ * uniform draw without replacement for i.i.d. uniform keys). valid (nullable) uint8 [N][L]: entries with
+ * valid == 0 are neither class (the RoI head's padding). pos / neg uint8 [N][L] masks, sm (nullable)
  * their union, nums int32 [N][2] = (num_pos, num_neg). One 1024-thread workgroup per row. */
-int mx_sample_draw(const void* labels, int ldtype, const float* keys, int64_t N, int64_t L, int batch,
-                   double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm, int32_t* nums, mx_stream_t stream);
+int mx_sample_draw(const void* labels, int ldtype, const uint8_t* valid, const float* keys, int64_t N, int64_t L,
+                   int batch, double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm, int32_t* nums,
+                   mx_stream_t stream);
 
 /* The same draw for long rows (the RPN's anchors) split over many workgroups: a histogram launch, a
  * split launch (candidates below each class's boundary bin drawn, the boundary bin's appended to a
@@ -95,9 +97,16 @@ int mx_sample_draw(const void* labels, int ldtype, const float* keys, int64_t N,
  * lists), after a memset of the workspace's counters. ws: mx_sample_draw_workspace(N, L) bytes; rows of
  * at most 16,384 elements, or ws == NULL, take mx_sample_draw. Results identical to mx_sample_draw. */
 size_t mx_sample_draw_workspace(int64_t N, int64_t L);
-int mx_sample_draw_ws(const void* labels, int ldtype, const float* keys, int64_t N, int64_t L, int batch,
-                      double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm, int32_t* nums, void* ws,
+int mx_sample_draw_ws(const void* labels, int ldtype, const uint8_t* valid, const float* keys, int64_t N, int64_t L,
+                      int batch, double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm, int32_t* nums, void* ws,
                       size_t ws_bytes, mx_stream_t stream);
+
+/* RoIHeads.select_training_samples' candidate rows (torchvision: cat([proposals, gt]) per image): boxes
+ * [N][post + gm][4] = each image's post padded proposal boxes pb [N][post][4] then its gm padded GT boxes
+ * gtp [N][gm][4], and validity bytes valid [N][post + gm] (pvalid [N][post] for the proposals, slot < gcnt[n]
+ * (int32) for the GT) -- the matcher's and the sampler's rows (mx_sample_draw's valid). One launch. */
+int mx_roi_candidates(const float* pb, const uint8_t* pvalid, const float* gtp, const int32_t* gcnt, int64_t N,
+                      int64_t post, int64_t gm, float* box, uint8_t* valid, mx_stream_t stream);
 
 /* torchvision.ops.box_iou -> out[n,m] (test/diagnostic entry). */
 int mx_box_iou(const float* b1, int64_t n, const float* b2, int64_t m, float* out, mx_stream_t stream);
@@ -511,20 +520,21 @@ size_t mx_rpn_loss_workspace(int64_t n);
 int mx_rpn_loss_fwd(const float* objectness, const float* deltas, const float* labels, const float* targets,
                     const uint8_t* pos, const uint8_t* neg, int64_t n, float beta, float* out, void* ws,
                     size_t ws_bytes, mx_stream_t stream);
-/* Gradients of (out[0], out[1]) scaled by grad[0..1] (device) w.r.t. objectness and deltas. */
+/* Gradients of (out[0], out[1]) scaled by the device scalars *grad0, *grad1 (autograd's upstream
+ * gradients; null = 0, that loss unused) w.r.t. objectness and deltas. */
 int mx_rpn_loss_bwd(const float* objectness, const float* deltas, const float* labels, const float* targets,
-                    const uint8_t* pos, const uint8_t* neg, int64_t n, float beta, const float* out, const float* grad,
-                    float* grad_objectness, float* grad_deltas, mx_stream_t stream);
+                    const uint8_t* pos, const uint8_t* neg, int64_t n, float beta, const float* out, const float* grad0,
+                    const float* grad1, float* grad_objectness, float* grad_deltas, mx_stream_t stream);
 /* fastrcnn_loss over R sampled RoIs: logits [R][ldl] (C classes), box regression [R][ldr] (4 per
  * class), labels [R] int64, targets [R][4]: out[0] = mean cross-entropy, out[1] = smooth-L1(beta) of
  * the labelled class's box over positive RoIs / R. Workspace: mx_rpn_loss_workspace(R). Backward:
- * grad_logits [R][C], grad_reg [R][4C] (dense) for upstream grad[0..1]. */
+ * grad_logits [R][C], grad_reg [R][4C] (dense) for the upstream device scalars *grad0, *grad1 (null = 0). */
 int mx_roi_loss_fwd(const float* logits, int64_t ldl, int C, const float* reg, int64_t ldr, const int64_t* labels,
                     const float* targets, int64_t R, float beta, float* out, void* ws, size_t ws_bytes,
                     mx_stream_t stream);
 int mx_roi_loss_bwd(const float* logits, int64_t ldl, int C, const float* reg, int64_t ldr, const int64_t* labels,
-                    const float* targets, int64_t R, float beta, const float* grad, float* grad_logits,
-                    float* grad_reg, mx_stream_t stream);
+                    const float* targets, int64_t R, float beta, const float* grad0, const float* grad1,
+                    float* grad_logits, float* grad_reg, mx_stream_t stream);
 size_t mx_bn_finalize_workspace(int64_t mblocks, int64_t K);
 int mx_bn_finalize_ex(const float* stats, int64_t mblocks, int64_t K, int64_t count, const float* gamma,
                       const float* beta, float eps, float momentum, float* running_mean, float* running_var,

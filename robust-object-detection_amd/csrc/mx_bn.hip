@@ -503,10 +503,11 @@ __global__ void __launch_bounds__(256) rpn_loss_bwd_kernel(const float* __restri
                                                            const float* __restrict__ y, const float4* __restrict__ t,
                                                            const uint8_t* __restrict__ pm, const uint8_t* __restrict__ nm,
                                                            int64_t n, float beta, const float* __restrict__ stats,
-                                                           const float* __restrict__ g, float* __restrict__ gx,
-                                                           float4* __restrict__ gd) {
+                                                           const float* __restrict__ g0p, const float* __restrict__ g1p,
+                                                           float* __restrict__ gx, float4* __restrict__ gd) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
+  const float g[2] = {g0p ? *g0p : 0.f, g1p ? *g1p : 0.f};  // upstream grads (null: that loss unused)
   const float inv = 1.f / stats[2];
   const bool p = pm[i], s = p || nm[i];
   float gxi = 0.f;
@@ -578,10 +579,11 @@ __global__ void __launch_bounds__(256) roi_loss_bwd_kernel(const float* __restri
                                                            const float* __restrict__ reg, int64_t ldr,
                                                            const int64_t* __restrict__ labels,
                                                            const float* __restrict__ targets, int64_t R, float beta,
-                                                           const float* __restrict__ g, float* __restrict__ gl,
-                                                           float* __restrict__ gr) {
+                                                           const float* __restrict__ g0p, const float* __restrict__ g1p,
+                                                           float* __restrict__ gl, float* __restrict__ gr) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (r >= R) return;
+  const float g[2] = {g0p ? *g0p : 0.f, g1p ? *g1p : 0.f};  // upstream grads (null: that loss unused)
   const float* l = logits + r * ldl;
   const int64_t lab = labels[r];
   const float s0 = g[0] / (float)R, s1 = g[1] / (float)R;
@@ -923,11 +925,12 @@ extern "C" int mx_rpn_loss_fwd(const float* objectness, const float* deltas, con
 
 extern "C" int mx_rpn_loss_bwd(const float* objectness, const float* deltas, const float* labels, const float* targets,
                                const uint8_t* pos, const uint8_t* neg, int64_t n, float beta, const float* out,
-                               const float* grad, float* grad_objectness, float* grad_deltas, mx_stream_t stream) {
-  MX_CHECK_ARG(n > 0 && out && grad && grad_objectness && grad_deltas, "rpn_loss bwd: bad arguments");
+                               const float* grad0, const float* grad1, float* grad_objectness, float* grad_deltas,
+                               mx_stream_t stream) {
+  MX_CHECK_ARG(n > 0 && out && grad_objectness && grad_deltas, "rpn_loss bwd: bad arguments");
   rpn_loss_bwd_kernel<<<(unsigned)cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(
-      objectness, (const float4*)deltas, labels, (const float4*)targets, pos, neg, n, beta, out, grad, grad_objectness,
-      (float4*)grad_deltas);
+      objectness, (const float4*)deltas, labels, (const float4*)targets, pos, neg, n, beta, out, grad0, grad1,
+      grad_objectness, (float4*)grad_deltas);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }
@@ -947,11 +950,12 @@ extern "C" int mx_roi_loss_fwd(const float* logits, int64_t ldl, int C, const fl
 }
 
 extern "C" int mx_roi_loss_bwd(const float* logits, int64_t ldl, int C, const float* reg, int64_t ldr,
-                               const int64_t* labels, const float* targets, int64_t R, float beta, const float* grad,
-                               float* grad_logits, float* grad_reg, mx_stream_t stream) {
-  MX_CHECK_ARG(R > 0 && C > 0 && grad && grad_logits && grad_reg, "roi_loss bwd: bad arguments");
+                               const int64_t* labels, const float* targets, int64_t R, float beta, const float* grad0,
+                               const float* grad1, float* grad_logits, float* grad_reg, mx_stream_t stream) {
+  MX_CHECK_ARG(R > 0 && C > 0 && grad_logits && grad_reg, "roi_loss bwd: bad arguments");
   roi_loss_bwd_kernel<<<(unsigned)cdiv(R, 256), 256, 0, (hipStream_t)stream>>>(logits, ldl, C, reg, ldr, labels, targets,
-                                                                               R, beta, grad, grad_logits, grad_reg);
+                                                                               R, beta, grad0, grad1, grad_logits,
+                                                                               grad_reg);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

@@ -30,7 +30,9 @@ __device__ __forceinline__ uint32_t sp_ord(float f) {  // order-preserving; -0.0
 }
 
 template <typename LT>
-__device__ __forceinline__ int sp_class(LT v) {  // 0 positive, 1 negative, -1 neither
+__device__ __forceinline__ int sp_class(LT v, const uint8_t* __restrict__ valid = nullptr, int64_t i = 0) {
+  // 0 positive, 1 negative, -1 neither (or masked out by the optional validity bytes)
+  if (valid && !valid[i]) return -1;
   if constexpr (sizeof(LT) == 4) {
     const float f = (float)v;
     return f >= 1.f ? 0 : (f == 0.f ? 1 : -1);
@@ -40,7 +42,8 @@ __device__ __forceinline__ int sp_class(LT v) {  // 0 positive, 1 negative, -1 n
 }
 
 template <typename LT>
-__global__ void __launch_bounds__(SP_THREADS) sample_draw_kernel(const LT* __restrict__ lab, const float* __restrict__ keys,
+__global__ void __launch_bounds__(SP_THREADS) sample_draw_kernel(const LT* __restrict__ lab, const uint8_t* __restrict__ valid,
+                                                                const float* __restrict__ keys,
                                                                 int64_t L, int P, int B, uint8_t* __restrict__ pos,
                                                                 uint8_t* __restrict__ neg, uint8_t* __restrict__ sm,
                                                                 int32_t* __restrict__ nums) {
@@ -50,6 +53,7 @@ __global__ void __launch_bounds__(SP_THREADS) sample_draw_kernel(const LT* __res
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, copy = wave & (SP_COPIES - 1);
   const int64_t row = blockIdx.x;
   const LT* lr = lab + row * L;
+  const uint8_t* vr = valid ? valid + row * L : nullptr;
   const float* kr = keys + row * L;
   // digit d covers bits [sh, sh + w) of the key; the bits above it must equal the prefix so far
   const int shs[3] = {21, 10, 0}, ws[3] = {11, 11, 10};
@@ -68,7 +72,7 @@ __global__ void __launch_bounds__(SP_THREADS) sample_draw_kernel(const LT* __res
 #pragma unroll
       for (int u = 0; u < SP_UNROLL; ++u) {
         const int64_t i = i0 + (int64_t)u * SP_THREADS;
-        cl[u] = i < L ? sp_class<LT>(lr[i]) : -1;
+        cl[u] = i < L ? sp_class<LT>(lr[i], vr, i) : -1;
         kk[u] = i < L ? sp_ord(kr[i]) : 0u;
       }
 #pragma unroll
@@ -142,7 +146,7 @@ __global__ void __launch_bounds__(SP_THREADS) sample_draw_kernel(const LT* __res
 #pragma unroll
       for (int u = 0; u < SP_UNROLL; ++u) {
         const int64_t i = i0 + (int64_t)u * SP_THREADS;
-        cl[u] = i < L ? sp_class<LT>(lr[i]) : -1;
+        cl[u] = i < L ? sp_class<LT>(lr[i], vr, i) : -1;
         kk[u] = i < L ? sp_ord(kr[i]) : 0u;
       }
 #pragma unroll
@@ -167,7 +171,7 @@ __global__ void __launch_bounds__(SP_THREADS) sample_draw_kernel(const LT* __res
     int c = -1;
     uint32_t k = 0;
     if (i < L) {
-      c = sp_class<LT>(lr[i]);
+      c = sp_class<LT>(lr[i], vr, i);
       k = sp_ord(kr[i]);
     }
     const bool below0 = c == 0 && k0 > 0 && k < T0, below1 = c == 1 && k1 > 0 && k < T1;
@@ -226,19 +230,21 @@ __device__ __forceinline__ void sp_hist_zero(uint32_t* h, int n) {
 }
 
 template <typename LT>
-__global__ void __launch_bounds__(SH_THREADS) sample_hist_kernel(const LT* __restrict__ lab, const float* __restrict__ keys,
-                                                                int64_t L, uint32_t* __restrict__ ghist) {
+__global__ void __launch_bounds__(SH_THREADS) sample_hist_kernel(const LT* __restrict__ lab, const uint8_t* __restrict__ valid,
+                                                                const float* __restrict__ keys, int64_t L,
+                                                                uint32_t* __restrict__ ghist) {
   __shared__ uint32_t h[2][SP_BINS];
   sp_hist_zero(&h[0][0], 2 * SP_BINS);
   __syncthreads();
   const int64_t row = blockIdx.y, base = (int64_t)blockIdx.x * SH_THREADS * SH_ITEMS;
   const LT* lr = lab + row * L;
+  const uint8_t* vr = valid ? valid + row * L : nullptr;
   const float* kr = keys + row * L;
 #pragma unroll 4
   for (int u = 0; u < SH_ITEMS; ++u) {
     const int64_t i = base + (int64_t)u * SH_THREADS + threadIdx.x;
     if (i < L) {
-      const int c = sp_class<LT>(lr[i]);
+      const int c = sp_class<LT>(lr[i], vr, i);
       if (c >= 0) atomicAdd(&h[c][sp_ord(kr[i]) >> 21], 1u);
     }
   }
@@ -298,7 +304,8 @@ __device__ __forceinline__ void sp_boundaries(const uint32_t* __restrict__ g, in
 }
 
 template <typename LT>
-__global__ void __launch_bounds__(SH_THREADS) sample_split_kernel(const LT* __restrict__ lab, const float* __restrict__ keys,
+__global__ void __launch_bounds__(SH_THREADS) sample_split_kernel(const LT* __restrict__ lab, const uint8_t* __restrict__ valid,
+                                                                 const float* __restrict__ keys,
                                                                  int64_t L, int P, int B, const uint32_t* __restrict__ ghist,
                                                                  uint32_t* __restrict__ lcount, uint64_t* __restrict__ lists,
                                                                  uint8_t* __restrict__ pos, uint8_t* __restrict__ neg,
@@ -308,12 +315,13 @@ __global__ void __launch_bounds__(SH_THREADS) sample_split_kernel(const LT* __re
   sp_boundaries(ghist + row * 2 * SP_BINS, P, B, s_cnt, s_k, s_bin, s_below);
   const uint32_t b0 = s_bin[0], b1 = s_bin[1];
   const LT* lr = lab + row * L;
+  const uint8_t* vr = valid ? valid + row * L : nullptr;
   const float* kr = keys + row * L;
 #pragma unroll 4
   for (int u = 0; u < SH_ITEMS; ++u) {
     const int64_t i = base + (int64_t)u * SH_THREADS + threadIdx.x;
     if (i < L) {
-      const int c = sp_class<LT>(lr[i]);
+      const int c = sp_class<LT>(lr[i], vr, i);
       bool t0 = false, t1 = false;
       if (c >= 0) {
         const uint32_t k = sp_ord(kr[i]), b = k >> 21, bc = c ? b1 : b0;
@@ -427,9 +435,40 @@ __global__ void __launch_bounds__(SP_THREADS) sample_finish_kernel(int64_t L, in
   }
 }
 
+// RoIHeads.select_training_samples' candidate rows: per image its post padded proposal slots (valid where
+// pvalid) then its gm padded GT slots (valid below gcnt), torchvision's cat([proposals, gt]) -- boxes
+// [N][post + gm][4] and validity bytes in one launch (replacing an arange, a compare and two cats)
+__global__ void roi_candidates_kernel(const float4* __restrict__ pb, const uint8_t* __restrict__ pvalid,
+                                      const float4* __restrict__ gtp, const int32_t* __restrict__ gcnt, int64_t N,
+                                      int64_t post, int64_t gm, float4* __restrict__ box, uint8_t* __restrict__ valid) {
+  const int64_t L = post + gm;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * L) return;
+  const int64_t n = e / L, j = e - n * L;
+  if (j < post) {
+    box[e] = pb[n * post + j];
+    valid[e] = pvalid[n * post + j] ? 1 : 0;
+  } else {
+    box[e] = gtp[n * gm + (j - post)];
+    valid[e] = (j - post) < (int64_t)gcnt[n] ? 1 : 0;
+  }
+}
+
 }  // namespace mx
 
 using namespace mx;
+
+extern "C" int mx_roi_candidates(const float* pb, const uint8_t* pvalid, const float* gtp, const int32_t* gcnt, int64_t N,
+                                 int64_t post, int64_t gm, float* box, uint8_t* valid, mx_stream_t stream) {
+  MX_CHECK_ARG(N >= 0 && post >= 0 && gm >= 0, "roi_candidates: negative size");
+  const int64_t n = N * (post + gm);
+  if (n == 0) return MX_OK;
+  MX_CHECK_ARG(box && valid && gcnt && (post == 0 || (pb && pvalid)) && (gm == 0 || gtp), "roi_candidates: null operand");
+  mx::roi_candidates_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      (const float4*)pb, pvalid, (const float4*)gtp, gcnt, N, post, gm, (float4*)box, valid);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
 
 // workspace of mx_sample_draw_ws for N rows of L: histograms, list counts, boundary lists
 static size_t sample_ws_bytes(int64_t N, int64_t L) {
@@ -440,15 +479,15 @@ extern "C" size_t mx_sample_draw_workspace(int64_t N, int64_t L) { return sample
 
 // the sliced three-launch form for rows longer than one workgroup's comfortable share (see above);
 // shorter rows (and ws == NULL) take mx_sample_draw's one-workgroup-per-row kernel. Same results.
-extern "C" int mx_sample_draw(const void* labels, int ldtype, const float* keys, int64_t N, int64_t L, int batch,
-                              double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm, int32_t* nums,
-                              mx_stream_t stream);
+extern "C" int mx_sample_draw(const void* labels, int ldtype, const uint8_t* valid, const float* keys, int64_t N,
+                              int64_t L, int batch, double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm,
+                              int32_t* nums, mx_stream_t stream);
 
-extern "C" int mx_sample_draw_ws(const void* labels, int ldtype, const float* keys, int64_t N, int64_t L, int batch,
-                                 double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm, int32_t* nums,
-                                 void* ws, size_t ws_bytes, mx_stream_t stream) {
+extern "C" int mx_sample_draw_ws(const void* labels, int ldtype, const uint8_t* valid, const float* keys, int64_t N,
+                                 int64_t L, int batch, double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm,
+                                 int32_t* nums, void* ws, size_t ws_bytes, mx_stream_t stream) {
   if (ws == nullptr || L <= SP_SLICED_MIN)
-    return mx_sample_draw(labels, ldtype, keys, N, L, batch, positive_fraction, pos, neg, sm, nums, stream);
+    return mx_sample_draw(labels, ldtype, valid, keys, N, L, batch, positive_fraction, pos, neg, sm, nums, stream);
   MX_CHECK_ARG(N >= 0 && batch >= 0 && labels && keys && pos && neg && nums, "sample_draw: null operand");
   MX_CHECK_ARG(ldtype == MX_F32 || ldtype == 2, "sample_draw: labels must be f32 (0) or int64 (2)");
   MX_CHECK_ARG(N < 65536 && L < (1ll << 31), "sample_draw: sliced rows must be < 2^31 long, < 65536 rows");
@@ -463,13 +502,13 @@ extern "C" int mx_sample_draw_ws(const void* labels, int ldtype, const float* ke
   MX_HIP(hipMemsetAsync(ws, 0, (size_t)N * (2 * SP_BINS + 2) * 4, st));
   const dim3 grid((unsigned)((L + SH_THREADS * SH_ITEMS - 1) / (SH_THREADS * SH_ITEMS)), (unsigned)N);
   if (ldtype == MX_F32) {
-    sample_hist_kernel<float><<<grid, SH_THREADS, 0, st>>>((const float*)labels, keys, L, ghist);
-    sample_split_kernel<float><<<grid, SH_THREADS, 0, st>>>((const float*)labels, keys, L, P, batch, ghist, lcount, lists,
-                                                            pos, neg, sm);
+    sample_hist_kernel<float><<<grid, SH_THREADS, 0, st>>>((const float*)labels, valid, keys, L, ghist);
+    sample_split_kernel<float><<<grid, SH_THREADS, 0, st>>>((const float*)labels, valid, keys, L, P, batch, ghist, lcount,
+                                                            lists, pos, neg, sm);
   } else {
-    sample_hist_kernel<int64_t><<<grid, SH_THREADS, 0, st>>>((const int64_t*)labels, keys, L, ghist);
-    sample_split_kernel<int64_t><<<grid, SH_THREADS, 0, st>>>((const int64_t*)labels, keys, L, P, batch, ghist, lcount,
-                                                              lists, pos, neg, sm);
+    sample_hist_kernel<int64_t><<<grid, SH_THREADS, 0, st>>>((const int64_t*)labels, valid, keys, L, ghist);
+    sample_split_kernel<int64_t><<<grid, SH_THREADS, 0, st>>>((const int64_t*)labels, valid, keys, L, P, batch, ghist,
+                                                              lcount, lists, pos, neg, sm);
   }
   sample_finish_kernel<<<(unsigned)N, SP_THREADS, 0, st>>>(L, P, batch, ghist, lcount, lists, pos, neg, sm, nums);
   MX_LAUNCH_CHECK();
@@ -477,9 +516,9 @@ extern "C" int mx_sample_draw_ws(const void* labels, int ldtype, const float* ke
 }
 
 // labels: ldtype MX_F32 (float, the RPN's 1 / 0 / -1) or 2 (int64, the RoI head's class / 0 / -1)
-extern "C" int mx_sample_draw(const void* labels, int ldtype, const float* keys, int64_t N, int64_t L, int batch,
-                              double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm, int32_t* nums,
-                              mx_stream_t stream) {
+extern "C" int mx_sample_draw(const void* labels, int ldtype, const uint8_t* valid, const float* keys, int64_t N,
+                              int64_t L, int batch, double positive_fraction, uint8_t* pos, uint8_t* neg, uint8_t* sm,
+                              int32_t* nums, mx_stream_t stream) {
   MX_CHECK_ARG(N >= 0 && L >= 0 && batch >= 0, "sample_draw: negative size");
   // empty rows (L == 0) come with null row operands; the launch then only writes nums = (0, 0)
   MX_CHECK_ARG((N == 0 || nums) && (N * L == 0 || (labels && keys && pos && neg)), "sample_draw: null operand");
@@ -489,11 +528,11 @@ extern "C" int mx_sample_draw(const void* labels, int ldtype, const float* keys,
   const int P = (int)(batch * positive_fraction);  // torchvision: int(batch_size_per_image * positive_fraction)
   hipStream_t st = (hipStream_t)stream;
   if (ldtype == MX_F32)
-    sample_draw_kernel<float><<<(unsigned)N, SP_THREADS, 0, st>>>((const float*)labels, keys, L, P, batch, pos, neg, sm,
-                                                                 nums);
+    sample_draw_kernel<float><<<(unsigned)N, SP_THREADS, 0, st>>>((const float*)labels, valid, keys, L, P, batch, pos,
+                                                                 neg, sm, nums);
   else
-    sample_draw_kernel<int64_t><<<(unsigned)N, SP_THREADS, 0, st>>>((const int64_t*)labels, keys, L, P, batch, pos, neg,
-                                                                   sm, nums);
+    sample_draw_kernel<int64_t><<<(unsigned)N, SP_THREADS, 0, st>>>((const int64_t*)labels, valid, keys, L, P, batch, pos,
+                                                                   neg, sm, nums);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

@@ -52,9 +52,11 @@ _SIGS = {
     "mx_match_assign_batched": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_f, c_f, c_int, c_int, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_box_iou": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
-    "mx_sample_draw": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_int, c_d, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mx_sample_draw": (c_int, [c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_d, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_sample_draw_workspace": (c_sz, [c_i64, c_i64]),
-    "mx_sample_draw_ws": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_int, c_d, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "mx_sample_draw_ws": (c_int, [c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_d, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz,
+                                  c_vp]),
+    "mx_roi_candidates": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "mx_nms_workspace": (c_sz, [c_i64, c_i64]),
     "mx_nms_grouped_workspace": (c_sz, [c_i64, c_i64, c_i64]),
     "mx_batched_nms_grouped_sorted": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_d, c_vp, c_vp, c_i64,
@@ -125,9 +127,10 @@ _SIGS = {
                                     c_vp, c_i64, c_vp, c_sz, c_vp]),
     "mx_rpn_loss_workspace": (c_sz, [c_i64]),
     "mx_rpn_loss_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_sz, c_vp]),
-    "mx_rpn_loss_bwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mx_rpn_loss_bwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mx_roi_loss_fwd": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_sz, c_vp]),
-    "mx_roi_loss_bwd": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp]),
+    "mx_roi_loss_bwd": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_vp, c_i64, c_f, c_vp, c_vp, c_vp, c_vp,
+                                c_vp]),
     "mx_bn_bwd_finalize": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_conv2d_dgrad_ex": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mx_conv2d_dgrad_t": (c_int, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),

@@ -162,8 +162,11 @@ class HipBackend:
     def level_topk(self, scores, num_per_level, k):
         return ops.level_topk(scores, num_per_level, k)
 
-    def sample_draw(self, labels, keys, batch, positive_fraction, with_union=False):
-        return ops.sample_draw(labels, keys, batch, positive_fraction, with_union)
+    def sample_draw(self, labels, keys, batch, positive_fraction, with_union=False, valid=None):
+        return ops.sample_draw(labels, keys, batch, positive_fraction, with_union, valid=valid)
+
+    def roi_candidates(self, pb, pvalid, gtp, gcnt):
+        return ops.roi_candidates(pb, pvalid, gtp, gcnt)
 
     def proposal_nms(self, boxes, scores, lvl, group, G, L, thr, max_seg):
         return ops.batched_nms_grouped(boxes, scores, lvl, group, G, L, thr, max_seg)

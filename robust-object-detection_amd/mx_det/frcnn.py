@@ -425,17 +425,21 @@ class BalancedPositiveNegativeSampler:
         self.rand = None
         self.last = None   # (union mask, per-row counts int32 [N, 2]) of the last fused draw
 
-    def __call__(self, lab, be=None, counts=None):
+    def __call__(self, lab, be=None, counts=None, valid=None):
         """be: a backend with level_topk draws the k smallest keys with it (used for the RoI sampler's
         ~2k-wide rows; the RPN's 268k-anchor rows stay on torch.topk, which splits a row over many
         workgroups). counts: per-row (#label >= 1, #label == 0) when the matcher already produced them
-        (int [N, 2]), sparing two reductions over the rows."""
+        (int [N, 2]), sparing two reductions over the rows. valid: bool [N, L], entries where False are
+        neither class (the fused draw reads it; the other paths mask the labels first)."""
         L = lab.shape[1]
+        if valid is not None and not (be is not None and hasattr(be, "sample_draw") and lab.is_cuda and _fused_sampler()):
+            lab = torch.where(valid, lab, -1)  # padding slots belong to neither class
+            valid = None
         if be is not None and hasattr(be, "sample_draw") and lab.is_cuda and _fused_sampler():
             # the whole draw in one launch (mx_sample_draw: counts, per-class radix select, marks);
             # the union and the per-row counts stay available for the RoI sampler (self.last)
             r = self.rand(lab.shape, lab.device) if self.rand is not None else torch.rand(lab.shape, device=lab.device)
-            pos, neg, un, nums = be.sample_draw(lab, r, self.batch, self.frac, with_union=True)
+            pos, neg, un, nums = be.sample_draw(lab, r, self.batch, self.frac, with_union=True, valid=valid)
             self.last = (un, nums)
             return pos, neg
         pos, neg = lab >= 1, lab == 0
@@ -505,9 +509,10 @@ class RegionProposalNetwork(nn.Module):
     def post_nms_top_n(self):
         return self._post["training" if self.training else "testing"]
 
-    def filter_proposals_padded(self, proposals, objectness, image_sizes, num_per_level, be):
+    def filter_proposals_padded(self, proposals, objectness, image_sizes, num_per_level, be, with_scores=True):
         """torchvision's filter_proposals with padded outputs: boxes [N, post, 4], scores [N, post] and
-        a validity mask (each image's survivors in score order form a prefix of its row)."""
+        a validity mask (each image's survivors in score order form a prefix of its row). with_scores=False
+        (the training forward: the RoI head reads boxes and validity only) returns None for the scores."""
         N = proposals.shape[0]
         dev = proposals.device
         ob = objectness.detach()
@@ -548,7 +553,7 @@ class RegionProposalNetwork(nn.Module):
             sel, valid, nk = be.proposal_nms_select(boxes.reshape(-1, 4), prob.reshape(-1), lvl_flat, grp, N,
                                                     len(num_per_level), self.nms_thresh, max(pre, 1000), post)
             self._watch_nms(nk)
-            return boxes.reshape(-1, 4)[sel], prob.reshape(-1)[sel], valid
+            return boxes.reshape(-1, 4)[sel], (prob.reshape(-1)[sel] if with_scores else None), valid
         kk, nk = be.proposal_nms(boxes.reshape(-1, 4), prob.reshape(-1), lvl_flat, grp, N,
                                  len(num_per_level), self.nms_thresh, max(pre, 1000))
         kk, nk = kk.to(dev), nk.to(dev)
@@ -691,7 +696,8 @@ class RegionProposalNetwork(nn.Module):
         proposals = be.box_decode(pred_deltas.detach().reshape(-1, 4), anchors.repeat(N, 1), RPN_WEIGHTS)
         proposals = proposals.view(N, A, 4)
         if self.training:  # padded (boxes, scores, valid): the RoI sampler works on the device
-            boxes = self.filter_proposals_padded(proposals, objectness, images.image_sizes, num_per_level, be)
+            boxes = self.filter_proposals_padded(proposals, objectness, images.image_sizes, num_per_level, be,
+                                                 with_scores=False)
         else:
             boxes, _ = self.filter_proposals(proposals, objectness, images.image_sizes, num_per_level, be)
         return boxes, losses  # the side stream is joined by join_losses(): after the RoI head
@@ -856,9 +862,13 @@ class RoIHeads(nn.Module):
             # draws keys over the same [N, post + gm] rows whichever path builds them
             gtp, glp, gcnt = _gt_batch(targets, dev)
             gm = gtp.shape[1]
-            gslot = torch.arange(gm, device=dev)
-            box_p = torch.cat([pb, gtp], 1)               # [N, post + gm, 4]
-            valid = torch.cat([pvalid, gslot[None, :] < gcnt[:, None]], 1)
+            fused = hasattr(be, "roi_candidates") and _fused_sampler()
+            if fused:  # candidate boxes and validity in one launch; the sampler reads the validity
+                box_p, valid = be.roi_candidates(pb, pvalid, gtp, gcnt)
+            else:
+                gslot = torch.arange(gm, device=dev)
+                box_p = torch.cat([pb, gtp], 1)           # [N, post + gm, 4]
+                valid = torch.cat([pvalid, gslot[None, :] < gcnt[:, None]], 1)
             if hasattr(be, "match_assign_batched"):       # both images in one launch pair
                 _, lab_b, tg_p = be.match_assign_batched(gtp, gcnt, box_p, self.fg, self.bg, False, 2,
                                                          gt_labels=glp, weights=ROI_WEIGHTS)
@@ -871,9 +881,11 @@ class RoIHeads(nn.Module):
                     lab_l.append(lab.to(dev))
                     tg_l.append(tg.to(dev))
                 lab_b, tg_p = torch.stack(lab_l), torch.stack(tg_l)
-            lab_p = torch.where(valid, lab_b, -1)
+            # the sampled entries are valid ones, so the compaction below reads lab_b as it is; the
+            # unfused path masks the padding to -1 first (torchvision's rows hold no padding)
+            lab_p = lab_b if fused else torch.where(valid, lab_b, -1)
             self.fg_bg_sampler.last = None
-            pos_m, neg_m = self.fg_bg_sampler(lab_p, be)
+            pos_m, neg_m = self.fg_bg_sampler(lab_p, be, valid=valid if fused else None)
             if self.fg_bg_sampler.last is not None:       # the fused draw's union and per-row counts
                 un, nums = self.fg_bg_sampler.last
                 sm = un.flatten()
@@ -902,8 +914,8 @@ class RoIHeads(nn.Module):
         else:
             class_logits, box_regression = self.box_predictor(self.box_head(x, be), be)
         if self.training:
-            lab = torch.cat(labels)
-            rt = torch.cat(tgts)
+            lab = labels[0] if len(labels) == 1 else torch.cat(labels)  # (one-entry lists: no copy launch)
+            rt = tgts[0] if len(tgts) == 1 else torch.cat(tgts)
             if hasattr(be, "roi_loss"):  # HIP: one fused launch each way
                 loss_cls, loss_box = be.roi_loss(class_logits, box_regression, lab, rt, 1.0 / 9)
             else:

@@ -283,11 +283,29 @@ def roi_compact(mask, total, cm, box, lab, tg):
 SAMPLE_SLICED_MIN = 16384  # mx_sample_draw_ws's threshold (rows at most this long: one workgroup per row)
 
 
-def sample_draw(labels, keys, batch, positive_fraction, with_union=False, sliced=True):
+def roi_candidates(pb, pvalid, gtp, gcnt):
+    """select_training_samples' candidate rows in one launch (mx_roi_candidates): per image the padded
+    proposals pb [N, post, 4] (valid where pvalid) then the padded GT gtp [N, gm, 4] (valid below gcnt,
+    int32 [N]) -> (boxes [N, post + gm, 4], valid bool [N, post + gm])."""
+    _dev(pb, pvalid, gtp, gcnt)
+    N, post = pvalid.shape
+    gm = gtp.shape[1]
+    _check(pb.shape == (N, post, 4) and gtp.shape == (N, gm, 4) and gcnt.shape == (N,), "roi_candidates: shapes")
+    _check(pb.dtype == torch.float32 and gtp.dtype == torch.float32 and pvalid.dtype == torch.bool
+           and gcnt.dtype == torch.int32, "roi_candidates: dtypes")
+    box = torch.empty((N, post + gm, 4), dtype=torch.float32, device=pb.device)
+    valid = torch.empty((N, post + gm), dtype=torch.uint8, device=pb.device)
+    call("mx_roi_candidates", _p(pb.contiguous()), _p(pvalid.contiguous()), _p(gtp.contiguous()), _p(gcnt.contiguous()),
+         N, post, gm, _p(box), _p(valid), _stream())
+    return box, valid.view(torch.bool)
+
+
+def sample_draw(labels, keys, batch, positive_fraction, with_union=False, sliced=True, valid=None):
     """BalancedPositiveNegativeSampler's draw in one launch (mx_sample_draw): labels [N, L] (float32: the
     RPN's 1 / 0 / -1, or int64: the RoI head's class / 0 / -1), keys [N, L] uniform -> (pos, neg bool
     [N, L], union bool [N, L] or None, nums int32 [N, 2] = (num_pos, num_neg)); per row the num smallest
-    keys of each class's candidates, ties by lowest index."""
+    keys of each class's candidates, ties by lowest index. valid (bool [N, L], optional): entries where it
+    is False belong to neither class (the RoI head's padding slots)."""
     _dev(labels, keys)
     _check(labels.dim() == 2 and keys.shape == labels.shape and keys.dtype == torch.float32, "sample_draw: shapes")
     _check(labels.dtype in (torch.float32, torch.int64), "sample_draw: labels must be float32 or int64")
@@ -298,13 +316,17 @@ def sample_draw(labels, keys, batch, positive_fraction, with_union=False, sliced
     un = torch.empty_like(pos) if with_union else None
     nums = torch.empty((N, 2), dtype=torch.int32, device=dev)
     lab, ky, ld = labels.contiguous(), keys.contiguous(), 0 if labels.dtype == torch.float32 else 2
+    if valid is not None:
+        _check(valid.shape == labels.shape and valid.dtype == torch.bool and valid.device == dev, "sample_draw: valid")
+        valid = valid.contiguous()
+    vp = _p(valid)
     if L > SAMPLE_SLICED_MIN and sliced:  # the RPN's long rows: split over many workgroups
         nb = _lib.load().mx_sample_draw_workspace(N, L)
         ws = torch.empty(nb, dtype=torch.uint8, device=dev)
-        call("mx_sample_draw_ws", _p(lab), ld, _p(ky), N, L, int(batch), float(positive_fraction), _p(pos), _p(neg),
-             _p(un), _p(nums), _p(ws), nb, _stream())
+        call("mx_sample_draw_ws", _p(lab), ld, vp, _p(ky), N, L, int(batch), float(positive_fraction), _p(pos),
+             _p(neg), _p(un), _p(nums), _p(ws), nb, _stream())
     else:
-        call("mx_sample_draw", _p(lab), ld, _p(ky), N, L, int(batch), float(positive_fraction), _p(pos), _p(neg),
+        call("mx_sample_draw", _p(lab), ld, vp, _p(ky), N, L, int(batch), float(positive_fraction), _p(pos), _p(neg),
              _p(un), _p(nums), _stream())
     return pos.view(torch.bool), neg.view(torch.bool), (un.view(torch.bool) if un is not None else None), nums
 
@@ -701,12 +723,11 @@ class _RPNLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g0, g1):
         x, d, y, t, pm, nm, out = ctx.saved_tensors
-        z = torch.zeros((), dtype=torch.float32, device=x.device)
-        g = torch.stack([g0 if g0 is not None else z, g1 if g1 is not None else z]).float().contiguous()
+        g0, g1 = _loss_grad(g0), _loss_grad(g1)  # read by the kernel in place: no stack / zeros launches
         gx = torch.empty_like(x)
         gd = torch.empty_like(d)
         call("mx_rpn_loss_bwd", _p(x), _p(d), _p(y), _p(t), _p(pm), _p(nm), x.numel(), float(ctx.beta), _p(out),
-             _p(g), _p(gx), _p(gd), _stream())
+             _p(g0), _p(g1), _p(gx), _p(gd), _stream())
         return gx.view(ctx.shapes[0]), gd.view(ctx.shapes[1]), None, None, None, None, None
 
 
@@ -715,6 +736,14 @@ def rpn_loss(objectness, deltas, labels, targets, pos, neg, beta=1.0 / 9):
     the sampler's masks; objectness [N, A], deltas / targets [N, A, 4], labels [N, A] (1/0/-1)."""
     _dev(objectness, deltas)
     return _RPNLoss.apply(objectness, deltas, labels, targets, pos, neg, beta)
+
+
+def _loss_grad(g):
+    """A loss's upstream gradient as the f32 device scalar the fused loss backward reads (None: that
+    loss is unused, the kernel takes 0)."""
+    if g is None:
+        return None
+    return g if g.dtype == torch.float32 and g.is_contiguous() else g.float().contiguous()
 
 
 class _RoILoss(torch.autograd.Function):
@@ -744,12 +773,11 @@ class _RoILoss(torch.autograd.Function):
     def backward(ctx, g0, g1):
         lg, rg, lab, t = ctx.saved_tensors
         R, C = lg.shape
-        z = torch.zeros((), dtype=torch.float32, device=lg.device)
-        g = torch.stack([g0 if g0 is not None else z, g1 if g1 is not None else z]).float().contiguous()
+        g0, g1 = _loss_grad(g0), _loss_grad(g1)
         gl = torch.empty((R, C), dtype=torch.float32, device=lg.device)
         gr = torch.empty((R, 4 * C), dtype=torch.float32, device=lg.device)
         call("mx_roi_loss_bwd", _p(lg), lg.stride(0), C, _p(rg), rg.stride(0), _p(lab), _p(t), R, float(ctx.beta),
-             _p(g), _p(gl), _p(gr), _stream())
+             _p(g0), _p(g1), _p(gl), _p(gr), _stream())
         return gl, gr, None, None, None
 
 

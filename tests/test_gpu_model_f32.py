@@ -154,13 +154,13 @@ def _pin_proposals():
     orig = frcnn.RegionProposalNetwork.filter_proposals_padded
     cap = {}
 
-    def fp(self, proposals, objectness, image_sizes, num_per_level, be):
+    def fp(self, proposals, objectness, image_sizes, num_per_level, be, **kw):
         if "p" not in cap and proposals.device.type == "cpu":
-            cap["p"] = orig(self, proposals, objectness, image_sizes, num_per_level, be)
+            cap["p"] = orig(self, proposals, objectness, image_sizes, num_per_level, be, **kw)
             return cap["p"]
         if "p" not in cap:
-            return orig(self, proposals, objectness, image_sizes, num_per_level, be)
-        return tuple(t.to(proposals.device) for t in cap["p"])
+            return orig(self, proposals, objectness, image_sizes, num_per_level, be, **kw)
+        return tuple(t.to(proposals.device) if t is not None else None for t in cap["p"])
     return fp
 
 
@@ -230,8 +230,8 @@ def test_f32_rpn_proposal_drift_bounded(dev):
     orig = frcnn.RegionProposalNetwork.filter_proposals_padded
     cap = {}
 
-    def fp(self, proposals, objectness, image_sizes, num_per_level, be):
-        out = orig(self, proposals, objectness, image_sizes, num_per_level, be)
+    def fp(self, proposals, objectness, image_sizes, num_per_level, be, **kw):
+        out = orig(self, proposals, objectness, image_sizes, num_per_level, be, **kw)
         cap.setdefault(proposals.device.type, out)
         return out
     frcnn.RegionProposalNetwork.filter_proposals_padded = fp

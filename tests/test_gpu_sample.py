@@ -95,3 +95,38 @@ def test_sampler_paths_agree(dev, monkeypatch, int_labels):
         use = be if (fused == "1" or int_labels) else None
         out[fused] = s(lab, use)
     assert torch.equal(out["1"][0], out["0"][0]) and torch.equal(out["1"][1], out["0"][1])
+
+
+@pytest.mark.parametrize("L", [2011, 40000])
+def test_sample_draw_valid_mask_is_label_masking(dev, L):
+    """valid=False entries belong to neither class: the same draw as on labels set to -1 there (both
+    kernel forms: the RoI rows' one-workgroup kernel and the sliced one)."""
+    from mx_det import ops
+    g = torch.Generator().manual_seed(L)
+    lab = _rows(g, 2, L, 0.1, 0.8, True)
+    keys = torch.rand(2, L, generator=g)
+    valid = torch.rand(2, L, generator=g) < 0.7
+    masked = torch.where(valid, lab, -1)
+    p0, n0, u0, c0 = ops.sample_draw(masked.to(dev), keys.to(dev), 512, 0.25, with_union=True)
+    p1, n1, u1, c1 = ops.sample_draw(lab.to(dev), keys.to(dev), 512, 0.25, with_union=True, valid=valid.to(dev))
+    rp, rn, rnums = orc.balanced_sample(masked.numpy(), keys.numpy(), 512, 0.25)
+    assert np.array_equal(p1.cpu().numpy(), rp) and np.array_equal(n1.cpu().numpy(), rn)
+    assert np.array_equal(c1.cpu().numpy(), rnums)
+    assert torch.equal(p0, p1) and torch.equal(n0, n1) and torch.equal(u0, u1) and torch.equal(c0, c1)
+
+
+@pytest.mark.parametrize("gm,counts", [(32, [5, 0]), (64, [64, 33]), (0, [0, 0])])
+def test_roi_candidates_matches_cat(dev, gm, counts):
+    """mx_roi_candidates = torchvision's cat([proposals, gt]) on the padded rows, with the validity the
+    sampler masks by: proposals valid where pvalid, GT slots below the per-image count."""
+    from mx_det import ops
+    g = torch.Generator().manual_seed(gm + 1)
+    N, post = 2, 2000
+    pb = torch.rand(N, post, 4, generator=g) * 800
+    pvalid = torch.arange(post)[None, :] < torch.tensor([1500, 2000])[:, None]
+    gtp = torch.rand(N, gm, 4, generator=g) * 800
+    gcnt = torch.tensor(counts, dtype=torch.int32)
+    box, valid = ops.roi_candidates(pb.to(dev), pvalid.to(dev), gtp.to(dev), gcnt.to(dev))
+    want_box = torch.cat([pb, gtp], 1)
+    want_valid = torch.cat([pvalid, torch.arange(gm)[None, :] < gcnt[:, None].long()], 1)
+    assert torch.equal(box.cpu(), want_box) and torch.equal(valid.cpu(), want_valid)

@@ -33,11 +33,53 @@ def main():
     for ev in prof.key_averages(group_by_stack_n=6):
         if ev.key in ("aten::copy_", "aten::clone", "aten::_to_copy", "aten::cat", "aten::index", "aten::nonzero",
                       "aten::item", "aten::_local_scalar_dense", "aten::mul", "aten::mul_", "aten::add_",
-                      "aten::add"):
+                      "aten::add", "aten::fill_", "aten::zero_", "aten::arange", "aten::where", "aten::lt",
+                      "aten::uniform_", "aten::sum", "aten::scatter_", "aten::index_put_", "aten::stack",
+                      "aten::sigmoid", "aten::_foreach_add_", "aten::div", "aten::sub"):
             print(f"{ev.key} x{ev.count}")
             for fr in ev.stack[:6]:
                 print("    ", fr)
 
 
+def call_sites():
+    """Every device-launching aten op of one steady-state train step with the framework frames that
+    issued it (a TorchDispatchMode records the Python stack at dispatch)."""
+    import traceback
+    from collections import Counter
+    from torch.utils._python_dispatch import TorchDispatchMode
+    skip = ("aten::view", "aten::detach", "aten::empty", "aten::as_strided", "aten::reshape", "aten::_unsafe_view",
+            "aten::expand", "aten::select", "aten::slice", "aten::unsqueeze", "aten::t", "aten::alias",
+            "aten::empty_strided", "aten::empty_like", "aten::narrow", "aten::squeeze", "aten::permute",
+            "aten::transpose", "aten::lift_fresh", "aten::_to_copy", "aten::is_nonzero", "aten::set_")
+    seen = Counter()
+
+    class Log(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            name = str(func.overloadpacket).replace("aten.", "aten::")
+            if name not in skip:
+                fr = [f for f in traceback.extract_stack()[:-1] if "mx_det" in f.filename or "bench.py" in f.filename]
+                where = " <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}" for f in fr[-3:][::-1])
+                seen[(name, where)] += 1
+            return func(*args, **(kwargs or {}))
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    m = bench.build_model(dev).train()
+    opt = bench.make_optimizer(m)
+    imgs, tg = synth_batch(0, 2, device=dev)
+    for _ in range(4):
+        bench.train_step(m, opt, imgs, tg)
+    torch.cuda.synchronize()
+    with Log():
+        bench.train_step(m, opt, imgs, tg)
+    torch.cuda.synchronize()
+    print("aten ops dispatched in one step (count, op, call site):")
+    for (name, where), n in sorted(seen.items(), key=lambda kv: kv[0][1]):
+        print(f"  {n:3d}  {name:28s} {where}")
+
+
 if __name__ == "__main__":
-    main()
+    if "--sites" in sys.argv:
+        call_sites()
+    else:
+        main()
