@@ -149,7 +149,7 @@ def _cpu_baseline(gpu_model, seconds_hint, cores):
             "sample": f"{n} train step(s) x 2 images 1333x800 on {cores} CPU threads ({dt:.1f} s)"}
 
 
-TRAFFIC_FILE = os.environ.get("MX_TRAFFIC_FILE", os.path.join(ROOT, "profiles", "r04ap_traffic.json"))
+TRAFFIC_FILE = os.environ.get("MX_TRAFFIC_FILE", os.path.join(ROOT, "profiles", "r06_traffic.json"))
 # kernels of one op: outer list = the op's sequential kernels (summed), inner = alternative template
 # instances of one kernel (launch-weighted mean)
 KIND_KERNELS = {"x3_wgrad": [["mx::conv_wgrad_x3_kernel", "mx::conv_wgrad_x3w_kernel", "mx::conv_wgrad_x3d_kernel"],

@@ -36,7 +36,9 @@ buffer), so the all-reduce runs on the gradients in place: no flatten copy in, n
 A gradient that arrives elsewhere (BatchNorm affine, biases, the RPN head's weights summed over five
 levels, a parameter unused on this rank) is copied into its slot (one multi-tensor launch per group)
 and the parameter's `.grad` becomes the slot view. Over RCCL the average is `ReduceOp.AVG` (ncclAvg:
-no separate 1/N pass); gloo has no AVG, so it sums and scales.
+no separate 1/N pass); gloo has no AVG, so it sums and scales. In a one-rank group the average is the
+sum (RCCL's in-place one-rank sum moves no data, where its AVG rewrites every bucket: ~0.3 ms per
+step), unless one_rank_sum=False.
 
 Failing together: a rank whose proposal NMS reports a failure (RegionProposalNetwork.check_nms,
 num_keep < 0) must not raise alone -- the other ranks would block in the next all-reduce until the
@@ -62,7 +64,7 @@ def _in_slot(g, ptr):
 
 
 class DataParallel:
-    def __init__(self, model, bucket_mb=64, group=None):
+    def __init__(self, model, bucket_mb=64, group=None, one_rank_sum=True):
         self.model = model
         self.group = group
         self.world = dist.get_world_size(group)
@@ -133,6 +135,8 @@ class DataParallel:
         self.op, self.scale = dist.ReduceOp.SUM, 1.0 / self.world
         if dist.get_backend(group) == "nccl":  # RCCL: ncclAvg, the 1/N folded into the reduction
             self.op, self.scale = dist.ReduceOp.AVG, None
+        if self.world == 1 and one_rank_sum:  # one rank's average is its sum: in place, RCCL moves no data
+            self.op, self.scale = dist.ReduceOp.SUM, None
         self.copied = 0  # gradients copied into their slot in the last synced step (diagnostics)
         self._copied = 0
         for m in model.modules():  # graphs and side-stream wgrad stay enabled under this wrapper

@@ -49,7 +49,7 @@ def main():
     ref.__dict__["_mx_seg_ready"] = lambda key, ps: None  # same segmented trunk graphs, no exchange
     m = _model(dev)
     m.load_state_dict(ref.state_dict())
-    dp = DataParallel(m)
+    dp = DataParallel(m, one_rank_sum=False)  # exercise ncclAvg, the N>1 reduction, in the one-rank group
     res["reduce_op"] = str(dp.op)
     hook = m.__dict__["_mx_seg_ready"]
     m.__dict__["_mx_seg_ready"] = lambda key, ps: (res["order"].append(key), hook(key, ps))
