@@ -59,6 +59,10 @@ def call_sites():
             if name not in skip:
                 fr = [f for f in traceback.extract_stack()[:-1] if "mx_det" in f.filename or "bench.py" in f.filename]
                 where = " <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}" for f in fr[-3:][::-1])
+                if name in ("aten::copy_", "aten::zero_", "aten::fill_", "aten::zeros", "aten::cat") and args:
+                    a0 = args[0][0] if isinstance(args[0], (list, tuple)) and args[0] else args[0]
+                    if isinstance(a0, torch.Tensor):
+                        where += f"  {tuple(a0.shape)} {str(a0.dtype).replace('torch.', '')}"
                 seen[(name, where)] += 1
             return func(*args, **(kwargs or {}))
 
