@@ -569,6 +569,10 @@ int mx_bn_bwd_apply_ex(const void* dy, const void* y, const void* x, int dtype, 
 size_t mx_act_bias_bwd_workspace(int64_t M, int64_t K);
 int mx_act_bias_bwd(const void* gy, const void* y, int dtype, int64_t M, int64_t K, int64_t K8, int act,
                     void* g, int gdtype, float* db, void* ws, size_t ws_bytes, mx_stream_t stream);
+/* The f32 form with g's bf16x3 planes [2][M][K8] written beside g (the x3p dgrad / wgrad operand of the conv
+ * this backward head belongs to; bitwise what mx_split_planes of g writes). */
+int mx_act_bias_bwd_p(const float* gy, const float* y, int64_t M, int64_t K, int64_t K8, int act, float* g, float* db,
+                      void* ws, size_t ws_bytes, uint16_t* planes, mx_stream_t stream);
 /* Convenience forms (allocate per call): sums[2][K] is overwritten. */
 int mx_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, int64_t M, int64_t K, int act,
                      const float* mean, const float* invstd, float* sums, mx_stream_t stream);

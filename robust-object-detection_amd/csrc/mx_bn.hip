@@ -331,7 +331,7 @@ template <typename T, int ACT, typename TG>
 __global__ void __launch_bounds__(256) act_bias_bwd_kernel(const T* __restrict__ gy, const T* __restrict__ y, int64_t M,
                                                            int K, int K8, int64_t rows_per_block, TG* __restrict__ g,
                                                            float* __restrict__ db, unsigned* __restrict__ ctr,
-                                                           float* __restrict__ part) {
+                                                           float* __restrict__ part, uint16_t* __restrict__ planes) {
   __shared__ float red[32][65];
   const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
   const int c0 = blockIdx.y * 64 + cl * 8;
@@ -359,6 +359,7 @@ __global__ void __launch_bounds__(256) act_bias_bwd_kernel(const T* __restrict__
 #pragma unroll
       for (int t = 0; t < 8; ++t) s[t] += v[t];
       st8(g + r * K8 + c0, v);
+      if (planes) store_planes8(planes, M * (int64_t)K8, (r * K8 + c0) >> 3, v);  // f32 g's bf16x3 planes
     }
   }
   if (!db) return;
@@ -861,15 +862,18 @@ extern "C" size_t mx_act_bias_bwd_workspace(int64_t M, int64_t K) {
 
 template <typename T, typename TG>
 static void launch_act_bias(const void* gy, const void* y, int64_t M, int K, int K8, int act, const BwdGeo& g,
-                            void* out_, float* db, unsigned* ctr, float* part, hipStream_t st) {
+                            void* out_, float* db, unsigned* ctr, float* part, hipStream_t st, uint16_t* planes = nullptr) {
   dim3 grid((unsigned)g.RB, (unsigned)g.gy);
   TG* out = (TG*)out_;
   if (act == 1)
-    act_bias_bwd_kernel<T, 1, TG><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr, part);
+    act_bias_bwd_kernel<T, 1, TG><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr,
+                                                        part, planes);
   else if (act == 2)
-    act_bias_bwd_kernel<T, 2, TG><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr, part);
+    act_bias_bwd_kernel<T, 2, TG><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr,
+                                                        part, planes);
   else
-    act_bias_bwd_kernel<T, 0, TG><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr, part);
+    act_bias_bwd_kernel<T, 0, TG><<<grid, 256, 0, st>>>((const T*)gy, (const T*)y, M, K, K8, g.rows_per_block, out, db, ctr,
+                                                        part, planes);
 }
 
 extern "C" int mx_act_bias_bwd(const void* gy, const void* y, int dtype, int64_t M, int64_t K, int64_t K8, int act,
@@ -901,6 +905,28 @@ extern "C" int mx_act_bias_bwd(const void* gy, const void* y, int dtype, int64_t
     launch_act_bias<float, float>(gy, y, M, (int)K, (int)K8, act, g_, g, db, ctr, part, st);
   else
     MX_CHECK_ARG(false, "act_bias_bwd: bf16 input with f32 gradient output is not a supported combination");
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
+// mx_act_bias_bwd for f32 (the bf16x3 path) that also writes g's bf16x3 planes [2][M][K8] (split8: what
+// mx_split_planes would write) for the convs' x3p dgrad / wgrad -- no separate split pass over g
+extern "C" int mx_act_bias_bwd_p(const float* gy, const float* y, int64_t M, int64_t K, int64_t K8, int act, float* g,
+                                 float* db, void* ws, size_t ws_bytes, uint16_t* planes, mx_stream_t stream) {
+  MX_CHECK_ARG(planes != nullptr && M > 0, "act_bias_bwd_p: planes and M > 0 required");
+  MX_CHECK_ARG(K > 0 && K8 >= K && K8 % 8 == 0 && K8 < (1 << 24), "act_bias_bwd: need 0 < K <= K8, K8 %% 8 == 0");
+  MX_CHECK_ARG(act >= 0 && act <= 2 && (act == 0 || y), "act_bias_bwd: act 0/1/2 (y required for 1/2)");
+  BwdGeo g_ = act_geo(M, K8);
+  MX_CHECK_ARG(g_.gy <= MAX_CHUNKS, "act_bias_bwd: K8 > %d", MAX_CHUNKS * 64);
+  unsigned* ctr = nullptr;
+  float* part = nullptr;
+  if (db) {
+    const size_t need = mx_act_bias_bwd_workspace(M, K);
+    MX_CHECK_ARG(ws && ws_bytes >= need, "act_bias_bwd: workspace of %zu bytes required (mx_act_bias_bwd_workspace)", need);
+    ctr = (unsigned*)ws;
+    part = (float*)((char*)ws + CTR_BYTES);
+  }
+  launch_act_bias<float, float>(gy, y, M, (int)K, (int)K8, act, g_, g, db, ctr, part, (hipStream_t)stream, planes);
   MX_LAUNCH_CHECK();
   return MX_OK;
 }

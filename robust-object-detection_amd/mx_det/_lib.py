@@ -152,6 +152,7 @@ _SIGS = {
     "mx_bn_finalize_ex": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                   c_vp, ctypes.c_size_t, c_vp]),
     "mx_act_bias_bwd_workspace": (ctypes.c_size_t, [c_i64, c_i64]),
+    "mx_act_bias_bwd_p": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_sz, c_vp, c_vp]),
     "mx_act_bias_bwd": (c_int, [c_vp, c_vp, c_int, c_i64, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp,
                                 ctypes.c_size_t, c_vp]),
     "mx_sgd_step": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_f, c_f, c_int, c_vp]),

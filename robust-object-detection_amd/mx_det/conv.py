@@ -469,9 +469,15 @@ def _x_planes(x, K, R, S, dense, wgrad):
     return split_planes(x) if wgrad else None
 
 
+def _dy_planes_wanted(n_elems, chans, x3, C, R, S, dense):
+    """Whether a conv's dy (n_elems values, chans channels) is read as planes by its dgrad (and, with x's
+    planes, its wgrad)."""
+    return x3 and not dense and R * S <= 64 and planes_for(n_elems, chans, C * R * S)
+
+
 def _dy_planes(dy, C, R, S, dense):
     """dy's split_planes for the dgrad (and, with x's planes, the wgrad), or None."""
-    if not is_x3(dy) or dense or R * S > 64 or not planes_for(dy.numel(), dy.shape[-1], C * R * S):
+    if not _dy_planes_wanted(dy.numel(), dy.shape[-1], is_x3(dy), C, R, S, dense):
         return None
     return split_planes(dy)
 
@@ -769,10 +775,11 @@ def conv_wgrad(dy, x, K, R, S, stride, pad, kout=None, cin=None, side=False, out
     return wgrad_launch(wgrad_prepare(dy, x, K, R, S, stride, pad, kout, cin, out), side)
 
 
-def act_bias_bwd(gy, y, act, K8, need_db, g_dtype=torch.bfloat16):
+def act_bias_bwd(gy, y, act, K8, need_db, g_dtype=torch.bfloat16, planes=False):
     """(g, db): g = gy * act'(y) as g_dtype [..., K8] (zero-padded columns; the dgrad/wgrad operand:
     bf16, or f32 for the bf16x3 path), db = sum of g over all but the last dim (f32, or None) --
-    one launch (mx_act_bias_bwd)."""
+    one launch (mx_act_bias_bwd). planes=True (f32): (g, db, g's bf16x3 planes) from the same launch
+    (mx_act_bias_bwd_p)."""
     K = gy.shape[-1]
     gy = gy.contiguous()
     M = gy.numel() // K
@@ -782,6 +789,12 @@ def act_bias_bwd(gy, y, act, K8, need_db, g_dtype=torch.bfloat16):
     ws = None
     if need_db:
         ws = bn_scratch(_lib.load().mx_act_bias_bwd_workspace(M, K), gy.device)
+    if planes:
+        assert gy.dtype == torch.float32 and g_dtype == torch.float32 and M > 0
+        gp = torch.empty((2,) + tuple(g.shape), dtype=torch.bfloat16, device=gy.device)
+        call("mx_act_bias_bwd_p", _p(gy), _p(y.contiguous()) if act else None, M, K, K8, int(act), _p(g), _p(db),
+             _p(ws), ws.numel() if ws is not None else 0, _p(gp), _s())
+        return g, db, gp
     call("mx_act_bias_bwd", _p(gy), _p(y.contiguous()) if act else None, dcode(gy), M, K, K8, int(act), _p(g),
          dcode(g), _p(db), _p(ws), ws.numel() if ws is not None else 0, _s())
     return g, db
@@ -940,9 +953,14 @@ class ConvAct(torch.autograd.Function):
         K, _, R, S = wshape
         dx = dw = db = None
         K8 = (K + 7) // 8 * 8
-        gk, db = act_bias_bwd(gy, y, act, K8, has_b and ctx.needs_input_grad[2], g_dtype=x.dtype)
         dense = _is_dense(x.shape, R, S, stride, pad)
-        gp = _dy_planes(gk, x.shape[3], R, S, dense)
+        need_db = has_b and ctx.needs_input_grad[2]
+        if _dy_planes_wanted(gy.numel() // K * K8, K8, is_x3(x), x.shape[3], R, S, dense) and gy.numel():
+            # the backward head writes dy's planes beside it (no split pass over the gradient)
+            gk, db, gp = act_bias_bwd(gy, y, act, K8, need_db, g_dtype=x.dtype, planes=True)
+        else:
+            gk, db = act_bias_bwd(gy, y, act, K8, need_db, g_dtype=x.dtype)
+            gp = None
         wg = _wgrad_plan(ctx, gk, x, K8, R, S, stride, pad, kout=K, cin=wshape[1], dyp=gp, xp=xp)  # before the dgrad
         if ctx.needs_input_grad[0]:
             if _is_dense(x.shape, R, S, stride, pad):  # 1x1-GEMM form: dX[N, R*S*C] = dY[N, K8] wt

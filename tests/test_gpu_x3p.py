@@ -147,3 +147,18 @@ def test_bn_apply_and_bwd_apply_planes(dev, act):
     assert torch.equal(y0, y1) and torch.equal(yp.view(torch.int16), mc.split_planes(y0).view(torch.int16))
     assert torch.equal(d0, d1) and torch.equal(r0, r1)
     assert torch.equal(dp.view(torch.int16), mc.split_planes(d0).view(torch.int16))
+
+
+@pytest.mark.parametrize("act,K,K8", [(1, 256, 256), (0, 15, 16), (1, 96, 96)])
+def test_act_bias_bwd_planes(dev, act, K, K8):
+    """mx_act_bias_bwd_p (the ConvAct backward head with the gradient's planes): the same g and bias
+    gradient as mx_act_bias_bwd, and planes equal to split_planes(g)."""
+    from mx_det import conv as mc
+    g = torch.Generator().manual_seed(K)
+    gy = torch.randn(2, 37, 41, K, generator=g).to(dev)
+    y = torch.relu(torch.randn(2, 37, 41, K, generator=g)).to(dev)
+    g0, db0 = mc.act_bias_bwd(gy, y, act, K8, True, g_dtype=torch.float32)
+    g1, db1, gp = mc.act_bias_bwd(gy, y, act, K8, True, g_dtype=torch.float32, planes=True)
+    torch.cuda.synchronize()
+    assert torch.equal(g0, g1) and torch.equal(db0, db1)
+    assert torch.equal(gp.view(torch.int16), mc.split_planes(g0).view(torch.int16))
