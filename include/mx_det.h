@@ -287,6 +287,11 @@ int mx_canvas_pack(const void* const* maps, const int32_t* rects, int n, int64_t
                    int dtype, void* cv, mx_stream_t stream);
 int mx_canvas_unpack(const void* gcv, const int32_t* rects, int n, int64_t N, int64_t Hc, int64_t Wc, int64_t C,
                      int dtype, const void* const* add, void* const* grads, mx_stream_t stream);
+/* RPNHead's canvas frame mask between its convs (t * mask): y [N][HW][C] = x * mask[pixel] (mask f32 [HW] of
+ * 0 / 1; the same IEEE products as the broadcast multiply), dtype MX_F32 or MX_BF16, C % 8 == 0; planes
+ * (nullable, f32 only): y's bf16x3 hi / lo planes [2][N*HW*C] for the next conv's x3p operand. */
+int mx_mask_pixels(const void* x, int dtype, const float* mask, int64_t N, int64_t HW, int64_t C, void* y,
+                   uint16_t* planes, mx_stream_t stream);
 /* The same for the reference loader's own image tensors: ToDtype(float32, scale=True) output, f32 CHW
  * [3, Hs[b], Ws[b]] contiguous (train_frcnn_baseline.py:50-54 build_transforms, fed to the model at :171).
  * A float image equal to u8 * (float)(1/255) gives the bit-identical batch of mx_resize_normalize_pad;

@@ -823,6 +823,47 @@ extern "C" int mx_canvas_unpack(const void* gcv, const int32_t* rects, int n, in
   return MX_OK;
 }
 
+// RPN canvas frame mask between the head's convs (frcnn RPNHead.raw: t * mask, mask [Hc][Wc] of 0 / 1 per
+// pixel): y = x * mask[pixel] in f32 (the same IEEE products as torch's broadcast multiply: x * 1 = x,
+// x * 0 = +-0 or NaN), 8 channels per thread with 16-B accesses; planes (f32 only, nullable): y's bf16x3
+// hi / lo planes [2][N*HW*C] for the next conv's x3p operand. Used both ways (the backward is g * mask).
+template <typename T>
+__global__ void mask_pixels_kernel(const T* __restrict__ x, const float* __restrict__ mask, int64_t HW, int64_t C8,
+                                   int64_t n8, T* __restrict__ y, uint16_t* __restrict__ planes) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n8) return;
+  const float m = mask[(e / C8) % HW];
+  float v[8];
+  ld8(x + e * 8, v);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) v[t] *= m;
+  st8(y + e * 8, v);
+  if (planes) {
+    uint4 h, l;
+    split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), h, l);
+    *(uint4*)(planes + e * 8) = h;
+    *(uint4*)(planes + n8 * 8 + e * 8) = l;
+  }
+}
+
+extern "C" int mx_mask_pixels(const void* x, int dtype, const float* mask, int64_t N, int64_t HW, int64_t C, void* y,
+                              uint16_t* planes, mx_stream_t stream) {
+  MX_CHECK_ARG(N >= 0 && HW >= 0 && C > 0 && C % 8 == 0, "mask_pixels: C must be a positive multiple of 8");
+  MX_CHECK_ARG(dtype == MX_F32 || (dtype == MX_BF16 && !planes), "mask_pixels: f32, or bf16 without planes");
+  const int64_t n8 = N * HW * (C / 8);
+  if (n8 == 0) return MX_OK;
+  MX_CHECK_ARG(x && mask && y, "mask_pixels: null operand");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MX_F32)
+    mask_pixels_kernel<float><<<(unsigned)cdiv(n8, 256), 256, 0, st>>>((const float*)x, mask, HW, C / 8, n8, (float*)y,
+                                                                      planes);
+  else
+    mask_pixels_kernel<uint16_t><<<(unsigned)cdiv(n8, 256), 256, 0, st>>>((const uint16_t*)x, mask, HW, C / 8, n8,
+                                                                         (uint16_t*)y, nullptr);
+  MX_LAUNCH_CHECK();
+  return MX_OK;
+}
+
 // Empty kernel that marks a point in a rocprofv3 kernel trace (bench.py brackets its timed steps with
 // ids 1 and 2, tools/prof_steps.py keeps only the dispatches between them).
 __global__ void trace_marker_kernel(int id) { (void)id; }

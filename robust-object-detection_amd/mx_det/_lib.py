@@ -89,6 +89,7 @@ _SIGS = {
     "mx_resize_normalize_pad": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_int,
                                         c_vp, c_vp]),
     "mx_canvas_pack": (c_int, [c_vp, c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, c_vp]),
+    "mx_mask_pixels": (c_int, [c_vp, c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "mx_canvas_unpack": (c_int, [c_vp, c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp]),
     "mx_rpn_head_split": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_vp]),
     "mx_rpn_head_merge": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_vp]),

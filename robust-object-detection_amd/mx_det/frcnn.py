@@ -264,8 +264,22 @@ class RPNHead(nn.Module):
         for ci, c in enumerate(self.conv):
             t = c(t, be)
             if mask is not None and ci + 1 < len(self.conv):
-                t = t * mask  # zero frame between levels: the next 3x3 conv reads it as padding
+                # zero frame between levels: the next 3x3 conv reads it as padding
+                if t.is_cuda and getattr(be, "name", "") == "hip" and t.shape[3] % 8 == 0:
+                    # one launch each way, with the next conv's operand planes (mx_mask_pixels)
+                    wn = self.conv[ci + 1][0].weight  # [K, C, R, S] of the next conv
+                    t = ops.mask_pixels(t, self._maskf(mask), planes_krs=wn.shape[0] * wn.shape[2] * wn.shape[3])
+                else:
+                    t = t * mask
         return be.conv(t, w, b, (1, 1), (0, 0), ACT_NONE, out_dtype=torch.float32)  # [N,H,W,A*5]
+
+    def _maskf(self, mask):
+        """The canvas mask as f32 [Hc * Wc] (mx_mask_pixels' operand), built once per mask."""
+        cache = self.__dict__.setdefault("_maskf_cache", {})
+        m = cache.get(id(mask))
+        if m is None or m[0] is not mask:
+            m = cache[id(mask)] = (mask, mask.reshape(-1).float().contiguous())
+        return m[1]
 
     def layout(self, feats):
         """Static per input shape: (canvas?, level (h, w)s, canvas rectangles (y, x, h, w) of levels 1..,

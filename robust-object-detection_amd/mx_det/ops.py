@@ -478,6 +478,43 @@ def canvas_pack(maps, rects, Hc, Wc, slots=None):
                              *[m.contiguous() for m in maps])
 
 
+class _MaskPixels(torch.autograd.Function):
+    """t * mask for a per-pixel 0 / 1 mask (mx_mask_pixels both ways); planes_krs > 0: the output's bf16x3
+    planes for the next conv (f32, policy conv.planes_for), attached as y._mx_planes."""
+
+    @staticmethod
+    def forward(ctx, x, maskf, planes_krs):
+        from . import conv as mc
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        y = torch.empty_like(x)
+        pl = None
+        if planes_krs and x.dtype == torch.float32 and mc.planes_for(x.numel(), C, planes_krs):
+            pl = torch.empty((2,) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
+        call("mx_mask_pixels", _p(x), _dtype_code(x), _p(maskf), N, H * W, C, _p(y), _p(pl), _stream())
+        if pl is not None:
+            y._mx_planes = pl
+        ctx.save_for_backward(maskf)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (maskf,) = ctx.saved_tensors
+        g = g.contiguous()
+        N, H, W, C = g.shape
+        gx = torch.empty_like(g)
+        call("mx_mask_pixels", _p(g), _dtype_code(g), _p(maskf), N, H * W, C, _p(gx), None, _stream())
+        return gx, None, None
+
+
+def mask_pixels(x, maskf, planes_krs=0):
+    """RPNHead's canvas frame mask: x [N, H, W, C] * maskf [H, W] (f32 0 / 1), one launch each way."""
+    _dev(x, maskf)
+    _check(x.dim() == 4 and x.shape[3] % 8 == 0 and maskf.numel() == x.shape[1] * x.shape[2]
+           and maskf.dtype == torch.float32 and x.dtype in (torch.float32, torch.bfloat16), "mask_pixels: shapes")
+    return _MaskPixels.apply(x, maskf.contiguous(), int(planes_krs))
+
+
 class _RPNHeadSplit(torch.autograd.Function):
     @staticmethod
     def forward(ctx, o0, ocv, rects, A):
