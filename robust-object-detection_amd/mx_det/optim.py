@@ -100,9 +100,14 @@ class SGD(torch.optim.SGD):
             grads = [p.grad for p in ps]
             if any(g is None for g in grads):
                 return False
-            st = self.state
+            # the plan holds the parameters' and momentum buffers' addresses: still theirs? (per-parameter
+            # state dicts cached by identity: no tensor hashing on this host-critical path -- the GPU
+            # idles while the optimizer is issued after the backward's last graph launch returns;
+            # load_state_dict replaces self.state, which drops this cache)
+            if c.get("state") is not self.state or c.get("sdicts") is None:
+                c["state"], c["sdicts"] = self.state, [self.state[p] for p in ps]
             if ([p.data_ptr() for p in ps] != c["pptr"] or
-                    any(st[p].get("momentum_buffer") is not b for p, b in zip(ps, c["bufs"]))):
+                    any(d.get("momentum_buffer") is not b for d, b in zip(c["sdicts"], c["bufs"]))):
                 c = None
         if c is None or c["ps"] is not ps or c["packer"] is not pk or not c["ready"]:
             if (not ps or group.get("maximize") or group["momentum"] == 0 or
