@@ -350,6 +350,7 @@ class WeightPacker:
         e.version = None
         self.entries[k] = e
         self.order.append(k)
+        self._elist = None  # (rebuilt by refresh)
 
     @staticmethod
     def desc(e):
@@ -383,7 +384,10 @@ class WeightPacker:
                 e.version = e.w._version
 
     def refresh(self):
-        dirty = [k for k in self.order if self.entries[k].version != self.entries[k].w._version]
+        el = self.__dict__.get("_elist")
+        if el is None:  # (key, entry) in registration order; the per-step check below runs right after
+            el = self._elist = [(k, self.entries[k]) for k in self.order]  # loss.item(): GPU idle time
+        dirty = [k for k, e in el if e.version != e.w._version]
         if not dirty:
             return
         upload = tuple(dirty) != self._plan_key
@@ -1221,14 +1225,23 @@ class BatchNorm2d(torch.nn.Module):
 _nbt_batched = set()
 
 
+_nbt_cache = [None, None, None]  # (modules, their counters, their ids) of the last call
+
+
 def count_batches(bns):
     """num_batches_tracked += 1 for every module in `bns` in one foreach launch (called once per
-    training forward by the model); conv_bn then skips its own per-layer increment for them."""
+    training forward by the model); conv_bn then skips its own per-layer increment for them. The
+    counter list and id set are reused while the same modules (and counters) come back: this runs
+    right after the previous step's loss.item(), so its host time is GPU idle."""
     global _nbt_batched
-    t = [b.num_batches_tracked for b in bns if b.num_batches_tracked is not None]
-    if t:
-        torch._foreach_add_(t, 1)
-    _nbt_batched = {id(b) for b in bns}
+    c = _nbt_cache
+    if (c[0] is None or len(c[0]) != len(bns) or any(a is not b for a, b in zip(c[0], bns))
+            or any(x is not b.num_batches_tracked for x, b in zip(c[1][0], c[1][1]))):
+        mods = [b for b in bns if b.num_batches_tracked is not None]
+        c[0], c[1], c[2] = list(bns), ([b.num_batches_tracked for b in mods], mods), {id(b) for b in bns}
+    if c[1][0]:
+        torch._foreach_add_(c[1][0], 1)
+    _nbt_batched = c[2]
 
 
 class ResLink:
