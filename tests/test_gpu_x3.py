@@ -450,3 +450,22 @@ def test_x3_wgrad_presplit_is_bitwise_default(dev, monkeypatch, case):
         finally:
             call("mx_conv_set_wgrad_variant", 3)
     assert torch.equal(out[3], out[7])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,with_add", [((2, 100, 168, 256, 200, 336), False), ((2, 13, 21, 256, 25, 42), True),
+                                            ((1, 7, 5, 64, 100, 77), True)])
+def test_upsample_rows_kernel_matches_torch(dev, dtype, shape, with_add):
+    """The row-grid upsample kernel (FPN top-down, configs[1]'s P3 -> P2 shape): F.interpolate(nearest)
+    (+ add) bit for bit, any scale."""
+    from mx_det.backend import HipBackend
+    be = HipBackend("f32" if dtype == torch.float32 else "bf16")
+    N, H, W, C, Ho, Wo = shape
+    g = torch.Generator().manual_seed(H + Wo)
+    s = torch.randn(N, H, W, C, generator=g).to(dtype)
+    a = torch.randn(N, Ho, Wo, C, generator=g).to(dtype) if with_add else None
+    u = be.upsample_add(s.to(dev), a.to(dev) if a is not None else None, (Ho, Wo))
+    ur = F.interpolate(s.float().permute(0, 3, 1, 2), size=(Ho, Wo), mode="nearest").permute(0, 2, 3, 1)
+    if a is not None:
+        ur = ur + a.float()
+    assert torch.equal(u.cpu(), ur.to(dtype))
