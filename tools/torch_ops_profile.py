@@ -68,15 +68,29 @@ def call_sites():
 
     dev = torch.device("cuda")
     torch.manual_seed(0)
+    from mx_det import conv as mc
+    orig_split = mc.split_planes
+    splits = Counter()
+
+    def logged_split(t, *a, **k):  # captured graphs replay these: log them while the steps capture
+        fr = [f for f in traceback.extract_stack()[:-1] if "mx_det" in f.filename or "bench.py" in f.filename]
+        where = " <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}" for f in fr[-4:][::-1])
+        splits[(where, tuple(t.shape), torch.cuda.is_current_stream_capturing())] += 1
+        return orig_split(t, *a, **k)
+    mc.split_planes = logged_split
     m = bench.build_model(dev).train()
     opt = bench.make_optimizer(m)
     imgs, tg = synth_batch(0, 2, device=dev)
     for _ in range(4):
         bench.train_step(m, opt, imgs, tg)
     torch.cuda.synchronize()
+    print("mx_split_planes calls during the warm-up steps (site, shape, inside a capture):")
+    for (where, shp, cap), n in sorted(splits.items()):
+        print(f"  {n:3d}  {'graph' if cap else 'eager'}  {shp}  {where}")
     with Log():
         bench.train_step(m, opt, imgs, tg)
     torch.cuda.synchronize()
+    mc.split_planes = orig_split
     print("aten ops dispatched in one step (count, op, call site):")
     for (name, where), n in sorted(seen.items(), key=lambda kv: kv[0][1]):
         print(f"  {n:3d}  {name:28s} {where}")
