@@ -525,6 +525,8 @@ def _time_eval(precision, args, world, rank, dev, imgs, restored):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    from mx_det import _lib
+    _lib.trace_marker(1)  # timed-region markers (tools/prof_steps.py, tools/step_concurrency.py)
     t0 = time.perf_counter()
     for i in range(args.steps):
         eval_step(model, imgs[(args.warmup + i) % n], unet)
@@ -532,6 +534,7 @@ def _time_eval(precision, args, world, rank, dev, imgs, restored):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    _lib.trace_marker(2)
     if world > 1:
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

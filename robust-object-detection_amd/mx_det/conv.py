@@ -1315,8 +1315,31 @@ def fold_bn(conv, bn):
     return w, b.float().contiguous()
 
 
+def cached_operand(owner, key, tensors, make):
+    """make()'s value, kept in owner.__dict__ while every tensor of `tensors` keeps its storage and version
+    counter: eval-mode BN folding + packing ran ~5 torch ops and a pack launch per conv per image. A
+    BatchNorm's running statistics are written in place by the HIP kernels without a version bump, so the
+    folding callers list the module's num_batches_tracked, which every training forward bumps (torch
+    in-place add); without it (track_running_stats=False) nothing is cached."""
+    if any(t is None for t in tensors):
+        return make()
+    sig = tuple((t.data_ptr(), t._version) for t in tensors)
+    cache = owner.__dict__.setdefault("_mx_opcache", {})
+    e = cache.get(key)
+    if e is None or e[0] != sig:
+        e = cache[key] = (sig, make())
+    return e[1]
+
+
+def _fold_tensors(conv, bn):
+    ts = [conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked]
+    return ts + ([conv.bias] if conv.bias is not None else [])
+
+
 def eval_conv_bn(x, conv, bn, act, residual=None):
-    w, b = fold_bn(conv, bn)
-    wk, _ = pack_weight(w, x.shape[3], conv.stride, conv.padding, split=is_x3(x))
+    def make():
+        w, b = fold_bn(conv, bn)
+        return pack_weight(w, x.shape[3], conv.stride, conv.padding, split=is_x3(x))[0], b
+    wk, b = cached_operand(conv, ("fold", id(bn), x.shape[3], is_x3(x)), _fold_tensors(conv, bn), make)
     return conv_fwd(x.contiguous(), wk, conv.stride, conv.padding, bias=b, residual=residual, act=act,
                     cin=conv.weight.shape[1])

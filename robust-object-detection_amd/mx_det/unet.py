@@ -85,8 +85,12 @@ class ConvBlock(nn.Module):
             return x
         for ci, bi in ((0, 1), (3, 4)):
             c, b = self.block[ci], self.block[bi]
-            w, bias = mc.fold_bn(c, b)
-            x = mc.conv_fwd(x, _wk(w, x.shape[3], x), c.stride, c.padding, bias=bias, act=mc.ACT_LEAKY)
+
+            def make(c=c, b=b, x=x):
+                w, bias = mc.fold_bn(c, b)
+                return _wk(w, x.shape[3], x), bias
+            wk, bias = mc.cached_operand(c, ("fold", id(b), x.shape[3], x.dtype), mc._fold_tensors(c, b), make)
+            x = mc.conv_fwd(x, wk, c.stride, c.padding, bias=bias, act=mc.ACT_LEAKY)
         return x
 
 

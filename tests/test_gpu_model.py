@@ -235,3 +235,36 @@ def test_strict_targets_raise_before_forward(dev, monkeypatch):
         m(imgs, tg)
     after = m.state_dict()
     assert all(torch.equal(v, after[k]) for k, v in before.items())
+
+
+def test_eval_folded_operands_follow_training(dev):
+    """Eval-mode BN folding + packing is cached per conv (conv.cached_operand): after a training step
+    (new weights, new running statistics written by the HIP kernels) the next eval forward must fold
+    again -- equal, bit for bit, to a fresh model loaded with the trained state -- and differ from the
+    eval before the step."""
+    from mx_det.data import synth_batch
+    from mx_det.optim import SGD
+    torch.manual_seed(4)
+    m = _model(dev)
+    imgs, tg = synth_batch(0, 2, H=320, W=480, device=dev)
+    m.eval()
+    with torch.no_grad():
+        before = m(imgs[:1])[0]
+    m.train()
+    opt = SGD([p for p in m.parameters() if p.requires_grad], lr=0.05, momentum=0.9)
+    loss = sum(m(imgs, tg).values())
+    opt.zero_grad(set_to_none=True)
+    loss.backward()
+    opt.step()
+    m.eval()
+    with torch.no_grad():
+        after = m(imgs[:1])[0]
+        again = m(imgs[:1])[0]  # served from the cache
+    fresh = _model(dev)
+    fresh.load_state_dict(m.state_dict())
+    fresh.eval()
+    with torch.no_grad():
+        ref = fresh(imgs[:1])[0]
+    for k in ("boxes", "scores", "labels"):
+        assert torch.equal(after[k], ref[k]) and torch.equal(again[k], ref[k]), k
+    assert not (before["scores"].shape == after["scores"].shape and torch.equal(before["scores"], after["scores"]))
