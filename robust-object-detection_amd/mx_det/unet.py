@@ -134,11 +134,14 @@ class UpBlock(nn.Module):
             up = F.interpolate(up.permute(0, 3, 1, 2), size=tuple(skip.shape[1:3]), mode="bilinear",
                                align_corners=False).permute(0, 2, 3, 1)
             return self.conv(torch.cat([up, skip], dim=3).contiguous())
-        wt = self.up.weight.detach()                     # [Cin, Cout, 2, 2]
-        Cout = wt.shape[1]
-        w1 = wt.permute(2, 3, 1, 0).reshape(4 * Cout, C, 1, 1)  # output channel = (i, j, co)
-        b1 = self.up.bias.detach().repeat(4).float().contiguous()
-        u = mc.conv_fwd(x, _wk(w1, C, x), (1, 1), (0, 0), bias=b1)   # [N, H, W, 4*Cout]
+        Cout = self.up.weight.shape[1]
+
+        def make():  # the transposed conv as one 1x1 GEMM: weight rows = (i, j, co)
+            wt = self.up.weight.detach()                 # [Cin, Cout, 2, 2]
+            w1 = wt.permute(2, 3, 1, 0).reshape(4 * Cout, C, 1, 1)
+            return _wk(w1, C, x), self.up.bias.detach().repeat(4).float().contiguous()
+        wk1, b1 = mc.cached_operand(self.up, ("up", C, x.dtype), [self.up.weight, self.up.bias], make)
+        u = mc.conv_fwd(x, wk1, (1, 1), (0, 0), bias=b1)   # [N, H, W, 4*Cout]
         if (2 * H, 2 * W) == (skip.shape[1], skip.shape[2]):
             cat = torch.empty((N, 2 * H, 2 * W, Cout + skip.shape[3]), dtype=x.dtype, device=x.device)
             call("mx_up_concat", _p(u), _p(skip.contiguous()), mc.dcode(x), N, H, W, Cout, skip.shape[3], _p(cat),
@@ -182,8 +185,9 @@ class RestorationUNet(nn.Module):
         oc = self.out_conv
         if _training(self):
             return mc.ConvAct.apply(u, oc.weight, oc.bias, (1, 1), (0, 0), mc.ACT_NONE, torch.float32)
-        return mc.conv_fwd(u, _wk(oc.weight.detach(), u.shape[3], u), (1, 1), (0, 0), bias=oc.bias.detach().float(),
-                           out_dtype=torch.float32)
+        wk, b = mc.cached_operand(oc, ("out", u.shape[3], u.dtype), [oc.weight, oc.bias],
+                                  lambda: (_wk(oc.weight.detach(), u.shape[3], u), oc.bias.detach().float()))
+        return mc.conv_fwd(u, wk, (1, 1), (0, 0), bias=b, out_dtype=torch.float32)
 
     def _prepare(self):
         """Training: every 3x3 / 1x1 conv weight repacked (hi/lo planes in f32 mode) in one launch."""
