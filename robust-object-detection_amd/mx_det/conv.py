@@ -424,13 +424,33 @@ def get_packer():
     return _packer
 
 
+_nograd_ops = WeakIdKeyDictionary()  # weight tensor -> {layout: (version, (wk, wt))}, no-grad use only
+
+
 def operands(w, cin_pad, stride, pad, kpad, dgrad, dense=False, split=False):
     """(wk, wt) for a conv weight: from the model's WeightPacker when registered and current, else
-    packed now (one launch; the dense dgrad layout by a transpose of wk)."""
+    packed now (one launch; the dense dgrad layout by a transpose of wk). An unregistered weight used
+    without autograd (eval: the heads' concatenated cls + box weights, cached by their modules) keeps
+    its operands while the tensor object and its version counter stay the same; never inside a graph
+    capture (a replay must repack what the captured step recomputes)."""
     if _packer is not None:
         r = _packer.lookup(w, cin_pad, kpad, stride, pad, dgrad, dense, split)
         if r is not None:
             return r
+    if (not torch.is_grad_enabled() and not w.requires_grad and w.is_cuda
+            and not torch.cuda.is_current_stream_capturing()):
+        per = _nograd_ops.get(w)
+        if per is None:
+            per = _nograd_ops[w] = {}
+        lk = (cin_pad, kpad, tuple(stride), tuple(pad), bool(dgrad), bool(dense), bool(split))
+        e = per.get(lk)
+        if e is None or e[0] != w._version:
+            e = per[lk] = (w._version, _operands_now(w, cin_pad, stride, pad, kpad, dgrad, dense, split))
+        return e[1]
+    return _operands_now(w, cin_pad, stride, pad, kpad, dgrad, dense, split)
+
+
+def _operands_now(w, cin_pad, stride, pad, kpad, dgrad, dense, split):
     if dense and dgrad:
         wk, _ = pack_weight(w, cin_pad, stride, pad, split=split)
         K = w.shape[0]

@@ -299,8 +299,7 @@ class RPNHead(nn.Module):
         element as per-level convs, in 2 launches per conv instead of 5 (the P4..P6 maps are too small
         to fill the GPU alone). The shared weights' gradients then sum the canvas pixels in one wgrad
         (frame pixels add exact zeros). Without the canvas: one map per level."""
-        w = torch.cat([self.cls_logits.weight, self.bbox_pred.weight])
-        b = torch.cat([self.cls_logits.bias, self.bbox_pred.bias])
+        w, b = _head_cat(self, (self.cls_logits, self.bbox_pred), 4)
         canvas, hws, rects, (Hc, Wc) = self.layout(feats)
         hip = feats[0].is_cuda and getattr(be, "name", "") == "hip"
         # inside a trunk-graph capture (HIP): the levels' root gradients (RoIAlign's) are taken by the
@@ -748,6 +747,20 @@ class Linear(nn.Module):
             nn.init.uniform_(self.bias, -bound, bound)
 
 
+def _head_cat(owner, mods, wdim):
+    """The fused cls + box GEMM operands: (cat of the modules' weights as a [K, C, 1, 1] conv weight, cat
+    of their biases). Without autograd (eval) the same tensors are returned while the parameters are
+    unchanged (mc.cached_operand), so conv.operands keeps their packed form too; with autograd (training,
+    graph captures) they are recomputed every call."""
+    def make():
+        w = torch.cat([m.weight for m in mods])
+        return (w if wdim == 4 else w[:, :, None, None]), torch.cat([m.bias for m in mods])
+    if torch.is_grad_enabled() or (mods[0].weight.is_cuda and torch.cuda.is_current_stream_capturing()):
+        return make()
+    ts = [m.weight for m in mods] + [m.bias for m in mods]
+    return mc.cached_operand(owner, ("head_cat",), ts, make)
+
+
 class FastRCNNPredictor(nn.Module):
     """torchvision FastRCNNPredictor(in_channels, num_classes): cls_score + bbox_pred, fused in one
     MFMA GEMM (N = num_classes*5) with f32 output."""
@@ -759,8 +772,7 @@ class FastRCNNPredictor(nn.Module):
 
     def forward(self, x, be):
         nc = self.cls_score.out_features
-        w = torch.cat([self.cls_score.weight, self.bbox_pred.weight])[:, :, None, None]
-        b = torch.cat([self.cls_score.bias, self.bbox_pred.bias])
+        w, b = _head_cat(self, (self.cls_score, self.bbox_pred), 2)
         o = be.conv(x, w, b, (1, 1), (0, 0), ACT_NONE, out_dtype=torch.float32).reshape(x.shape[0], -1)
         return o[:, :nc], o[:, nc:]
 
