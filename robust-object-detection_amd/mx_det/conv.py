@@ -438,7 +438,7 @@ def operands(w, cin_pad, stride, pad, kpad, dgrad, dense=False, split=False):
         if r is not None:
             return r
     if (not torch.is_grad_enabled() and not w.requires_grad and w.is_cuda
-            and not torch.cuda.is_current_stream_capturing()):
+            and os.environ.get("MX_EVAL_OPCACHE", "1") != "0" and not torch.cuda.is_current_stream_capturing()):
         per = _nograd_ops.get(w)
         if per is None:
             per = _nograd_ops[w] = {}
@@ -1341,7 +1341,7 @@ def cached_operand(owner, key, tensors, make):
     BatchNorm's running statistics are written in place by the HIP kernels without a version bump, so the
     folding callers list the module's num_batches_tracked, which every training forward bumps (torch
     in-place add); without it (track_running_stats=False) nothing is cached."""
-    if any(t is None for t in tensors):
+    if any(t is None for t in tensors) or os.environ.get("MX_EVAL_OPCACHE", "1") == "0":
         return make()
     sig = tuple((t.data_ptr(), t._version) for t in tensors)
     cache = owner.__dict__.setdefault("_mx_opcache", {})
