@@ -967,10 +967,10 @@ class RoIHeads(nn.Module):
                                  boxes[..., 2].clamp(0, w), boxes[..., 3].clamp(0, h)), -1)
             labels = torch.arange(nc, device=dev).view(1, -1).expand_as(sc)
             boxes, sc, labels = boxes[:, 1:].reshape(-1, 4), sc[:, 1:].reshape(-1), labels[:, 1:].reshape(-1)
-            k = torch.where(sc > self.score_thresh)[0]
-            boxes, sc, labels = boxes[k], sc[k], labels[k]
+            # torchvision's score threshold, then remove_small_boxes(1e-2) on the survivors: the same set in
+            # the same order as one mask over both conditions (one nonzero -- one host sync -- not two)
             ws, hs = boxes[:, 2] - boxes[:, 0], boxes[:, 3] - boxes[:, 1]
-            k = torch.where((ws >= 1e-2) & (hs >= 1e-2))[0]
+            k = torch.where((sc > self.score_thresh) & (ws >= 1e-2) & (hs >= 1e-2))[0]
             boxes, sc, labels = boxes[k], sc[k], labels[k]
             k = be.batched_nms(boxes, sc, labels, self.nms_thresh, max_seg=max(per) if per else None)
             k = k[: self.detections_per_img]
