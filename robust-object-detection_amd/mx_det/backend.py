@@ -130,6 +130,8 @@ class HipBackend:
         return mc.BNBLink()
 
     def conv(self, x, weight, bias, stride, pad, act, out_dtype=None):
+        if not torch.is_grad_enabled():  # eval: no autograd bookkeeping, no planes for an unused wgrad
+            return mc.conv_act_nograd(x, weight, bias, stride, pad, act, out_dtype)
         return mc.ConvAct.apply(x, weight, bias, stride, pad, act, out_dtype)
 
     def maxpool(self, x, k, stride, pad):

@@ -949,6 +949,18 @@ def _absorb_take(t):
     return e[1].claim()
 
 
+def conv_act_nograd(x, w, b, stride, pad, act, out_dtype):
+    """ConvAct's forward without autograd (eval, torch.no_grad): no saved tensors, no dgrad operand, and
+    no split of x into planes for a weight gradient nobody takes (planes x's producer wrote are still
+    read); bitwise the same y."""
+    K = w.shape[0]
+    dense = _is_dense(x.shape, w.shape[2], w.shape[3], stride, pad)
+    wk, _ = operands(w, x.shape[3], stride, pad, _ceil8(K), False, dense, split=is_x3(x))
+    xp = _x_planes(x, K, w.shape[2], w.shape[3], dense, False)
+    return conv_fwd(x, wk, stride, pad, bias=b.detach() if b is not None else None, act=act, out_dtype=out_dtype,
+                    xp=xp)
+
+
 class ConvAct(torch.autograd.Function):
     """y = act(conv(x, w) + b). x NHWC (bf16, or f32: bf16x3); w [K,C,R,S] f32 parameter; b f32 [K]
     or None."""
